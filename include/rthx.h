@@ -1,0 +1,192 @@
+/*
+ * rthx.h — C ABI of the MI355X-native Monte Carlo exchange-factor tracer.
+ *
+ * This is the drop-in boundary for `mesh(N_rays; method=:exchange)` of
+ * RayTraceHeatTransfer.jl.  The seam in the reference is the Julia function
+ *
+ *   computeExchangeFactorsBin(rtm, rays_per_emitter, nudge, spectral_bin,
+ *                             surface_mapping, volume_mapping, num_surfaces,
+ *                             num_volumes, num_emitters, verbose, rec)
+ *       -> SparseMatrixCSC{Float64,Int64}
+ *   (src/RayTracing/RayTracing2D/ExchangeFactors2D/parallelRayTracing.jl:64-159)
+ *
+ * which is called from the three sites parallelRayTracing.jl:22, :34 and :54.
+ * A Julia shim (raytraceheattransfer.jl_amd/julia/RTHX.jl) flattens the
+ * RayTracingDomain2D once (rthx_domain_create), calls rthx_trace_exchange per
+ * traced spectral bin, copies the per-emitter absorber counts back
+ * (rthx_result_copy_csr) and rebuilds the SparseMatrixCSC exactly as the
+ * reference does (V = count / R, then row_normalize!, parallelRayTracing.jl:145,
+ * :154-158, :161-169).  Everything above the seam (bin grouping, surfaces_only
+ * truncation, smooth_F, solveEquilibrium!) stays unchanged.
+ *
+ * Conventions
+ *   - All indices are 0-based.  Global element index g: surfaces 0..Ns-1 in
+ *     (coarse, fine, wall) order, then volumes Ns..Ns+Nv-1 in (coarse, fine)
+ *     order (createIndexMapping2D.jl:1-21, RayTracingDomain2D.jl:57-76).
+ *   - Caller-owned descriptor arrays are copied during rthx_domain_create; the
+ *     library keeps no caller pointer.  Result buffers are library-owned until
+ *     copied into caller-allocated arrays (size query, then copy).
+ *   - Every function returns 0 on success or a negative RTHX_E* code; the
+ *     message is available from rthx_last_error() (thread-local).  No C++
+ *     exception crosses the ABI.
+ *   - One in-flight call per domain handle.  Calls block until the requested
+ *     outputs are complete.
+ */
+#ifndef RTHX_H
+#define RTHX_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RTHX_ABI_VERSION 1
+
+/* status codes */
+#define RTHX_OK 0
+#define RTHX_EINVAL -1      /* invalid argument / geometry */
+#define RTHX_ENOMEM -2      /* host or device allocation failed */
+#define RTHX_EDEVICE -3     /* HIP runtime error / no device */
+#define RTHX_ERANGE -4      /* a size limit of this build was exceeded */
+#define RTHX_ESTATE -5      /* call order violated (e.g. copy before trace) */
+
+/* rthx_trace_args.flags */
+#define RTHX_FLAG_FAITHFUL_SAMPLING 0x1u /* acos/sin/cos emission exactly as the
+                                            reference (emitVolumeRay2D.jl:26-31);
+                                            default: algebraic sin(acos(x)) */
+#define RTHX_FLAG_DEVICE_ONLY 0x2u       /* leave the CSR on the device; copy
+                                            calls then fetch it on demand */
+
+/* Uniform grid over a set of polygons (UniformGrid,
+ * src/Domains/domains/DomainStructs.jl:79-86; built by
+ * spatialAccelerations.jl:2-59).  Cell (i, j), 0-based, is stored at
+ * cell_start[j * nx + i] .. cell_start[j * nx + i + 1] in cell_items, and lists
+ * polygon indices (0-based, local to the set) in ascending order. */
+typedef struct rthx_grid_desc {
+  double origin_x;
+  double origin_y;
+  double inv_cell_size;
+  int32_t nx;
+  int32_t ny;
+  const int32_t* cell_start; /* [nx*ny + 1] */
+  const int32_t* cell_items; /* [cell_start[nx*ny]] */
+} rthx_grid_desc;
+
+/* Flattened RayTracingDomain2D (DomainStructs.jl:89-130).  Polygons have 3 or
+ * 4 vertices; per-polygon arrays are padded to 4 vertices / 4 walls. */
+typedef struct rthx_domain_desc {
+  int32_t abi_version;   /* = RTHX_ABI_VERSION */
+  int32_t n_coarse;      /* length(rtm.coarse_mesh) */
+  int32_t n_fine;        /* sum(length.(rtm.fine_mesh)) = Nv */
+  int32_t n_surfaces;    /* Ns = number of solid fine walls */
+  int32_t n_bins;        /* rtm.n_spectral_bins (>= 1) */
+  int32_t reserved0;
+
+  /* coarse polygons (rtm.coarse_face_cache) */
+  const int32_t* coarse_nv;      /* [n_coarse]  3 or 4 */
+  const double* coarse_xy;       /* [n_coarse*8] (x0,y0,x1,y1,..) */
+  const double* coarse_normal;   /* [n_coarse*8] unit inward normal of wall w
+                                    (calculateInwardNormal.jl:1-12) */
+  const uint8_t* coarse_solid;   /* [n_coarse*4] solidWalls */
+  const double* coarse_bbox;     /* [n_coarse*4] min_x,max_x,min_y,max_y */
+  rthx_grid_desc coarse_grid;    /* rtm.coarse_grid_opt */
+
+  /* fine polygons, grouped by coarse polygon (rtm.fine_mesh) */
+  const int32_t* fine_offset;    /* [n_coarse+1] first fine polygon of coarse c */
+  const int32_t* fine_nv;        /* [n_fine] */
+  const double* fine_xy;         /* [n_fine*8] */
+  const double* fine_normal;     /* [n_fine*8] */
+  const double* fine_mid;        /* [n_fine*2] vertex mean (PolyVolume2D.jl:9,103) */
+  const double* fine_volume;     /* [n_fine] signed shoelace area (PolyVolume2D.jl:20-21,112) */
+  const double* fine_bbox;       /* [n_fine*4] */
+  const int32_t* fine_surface;   /* [n_fine*4] global surface index of wall w,
+                                    -1 where the fine wall is not solid */
+  const rthx_grid_desc* fine_grid; /* [n_coarse] rtm.fine_grids_opt */
+
+  /* extinction, per bin */
+  const double* beta;            /* [n_bins*n_fine] kappa_g[b] + sigma_s_g[b] */
+  const double* uniform_beta;    /* [n_bins] rtm.uniform_across_bin: beta if the
+                                    bin is spatially uniform, -1 otherwise
+                                    (validateDomainUniformity.jl:57-85) */
+} rthx_domain_desc;
+
+/* One traced bin: the arguments of computeExchangeFactorsBin
+ * (parallelRayTracing.jl:64-67) plus the device/RNG controls the Julia
+ * version does not have. */
+typedef struct rthx_trace_args {
+  int32_t bin;               /* 0-based spectral bin (Julia spectral_bin - 1) */
+  uint32_t flags;            /* RTHX_FLAG_* */
+  int64_t rays_per_emitter;  /* R = div(rays_total, N), parallelRayTracing.jl:6 */
+  double nudge;              /* eta; reference default 1e4*eps(Float64),
+                                multiDispatchRayTrace2D.jl:10 */
+  uint64_t seed;             /* Philox-4x32-10 key */
+  int64_t emitter_begin;     /* trace emitters g = begin + k*stride < end */
+  int64_t emitter_end;
+  int64_t emitter_stride;    /* >= 1 (1 = contiguous block) */
+  int32_t device;            /* HIP device ordinal (ignored by the CPU oracle) */
+  int32_t n_record;          /* RayRecorder: number of recorded emitter ids */
+  const int64_t* record_ids; /* [n_record] 0-based global ids (RayRecorder.ids - 1) */
+  int32_t record_bin;        /* 0-based RayRecorder.bin */
+  int32_t reserved0;
+} rthx_trace_args;
+
+typedef struct rthx_result_info {
+  int64_t n_emitters;      /* N = Ns + Nv (rows and columns of F) */
+  int64_t rows_traced;     /* emitters traced by this call */
+  int64_t rays_per_emitter;
+  int64_t rays_traced;     /* rows_traced * rays_per_emitter (lost rays included) */
+  int64_t nnz;             /* stored (row, absorber) pairs */
+  int64_t lost_total;      /* rays that were not tallied */
+  int64_t lost_max_row;    /* max lost rays of one emitter (row_normalize! print) */
+  int64_t n_recorded;      /* recorded (origin, endpoint) pairs */
+  double trace_ms;         /* device time of the trace kernel (hipEvents) */
+  double pack_ms;          /* device time of scan + CSR pack kernels */
+  double total_ms;         /* host wall time of the whole call */
+} rthx_result_info;
+
+typedef struct rthx_domain rthx_domain;
+typedef struct rthx_result rthx_result;
+
+/* Library / device queries. */
+int rthx_abi_version(void);
+const char* rthx_last_error(void);
+int rthx_device_count(int32_t* count);
+int rthx_device_synchronize(int32_t device);
+
+/* Upload the flattened domain to `device`. */
+int rthx_domain_create(const rthx_domain_desc* desc, int32_t device,
+                       rthx_domain** out);
+void rthx_domain_destroy(rthx_domain* dom);
+
+/* Result objects are reusable: tracing into an existing result reuses its
+ * device buffers when they are large enough. */
+int rthx_result_create(rthx_result** out);
+void rthx_result_destroy(rthx_result* res);
+
+/* Trace one bin (the body of computeExchangeFactorsBin,
+ * parallelRayTracing.jl:69-152): every emitter in the selected range launches
+ * R rays; absorber counts are tallied per row.  Row order is the global
+ * emitter order; within a row, absorbers are ascending. */
+int rthx_trace_exchange(rthx_domain* dom, const rthx_trace_args* args,
+                        rthx_result* res);
+
+int rthx_result_get_info(const rthx_result* res, rthx_result_info* info);
+
+/* Copy the count matrix as CSR over all N rows (rows that were not traced are
+ * empty): row_ptr[N+1], cols[nnz], counts[nnz].  F_raw(i,j) of the reference
+ * is counts / R followed by row normalisation. */
+int rthx_result_copy_csr(const rthx_result* res, int64_t* row_ptr,
+                         int32_t* cols, uint32_t* counts);
+
+/* Copy the recorded rays (RayRecorder origins / endpoints,
+ * parallelRayTracing.jl:120-123,135-138): xy pairs, plus the emitter of each
+ * ray.  At most `cap` rays are written; *n_out receives the count written. */
+int rthx_result_copy_rays(const rthx_result* res, double* origins_xy,
+                          double* endpoints_xy, int64_t* emitter, int64_t cap,
+                          int64_t* n_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RTHX_H */

@@ -1,0 +1,134 @@
+"""TEST INFRASTRUCTURE ONLY — ctypes wrapper of the CPU restatement.
+
+Loaded by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg,
+never by the product package (raytraceheattransfer.jl_amd/rthx).  See the
+header of rthx_oracle.c for what it restates and how it is pinned.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+import sys
+from typing import Optional
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_ROOT = os.path.dirname(_HERE)
+sys.path.insert(0, os.path.join(_ROOT, "raytraceheattransfer.jl_amd"))
+
+from rthx import abi  # noqa: E402
+from rthx._lib import make_args  # noqa: E402  (argument struct builder only; loads nothing)
+
+LIB_PATH = os.path.join(_HERE, "_build", "librthx_oracle.so")
+_lib: Optional[C.CDLL] = None
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return LIB_PATH
+
+
+def load() -> C.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        build()
+    lib = C.CDLL(LIB_PATH)
+    lib.oracle_philox4x32_10.argtypes = [C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
+    lib.oracle_philox4x32_10.restype = None
+    lib.oracle_uniform.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]
+    lib.oracle_uniform.restype = C.c_double
+    lib.oracle_trace_exchange.argtypes = [C.POINTER(abi.DomainDesc), C.POINTER(abi.TraceArgs), C.c_int,
+                                          C.POINTER(C.c_void_p)]
+    lib.oracle_result_get_info.argtypes = [C.c_void_p, C.POINTER(abi.ResultInfo)]
+    lib.oracle_result_threads.argtypes = [C.c_void_p]
+    lib.oracle_result_copy_csr.argtypes = [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int32),
+                                           C.POINTER(C.c_uint32)]
+    lib.oracle_result_copy_rays.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double),
+                                            C.POINTER(C.c_int64), C.c_int64, C.POINTER(C.c_int64)]
+    lib.oracle_result_free.argtypes = [C.c_void_p]
+    lib.oracle_result_free.restype = None
+    lib.oracle_trace_ray.argtypes = [C.POINTER(abi.DomainDesc), C.POINTER(abi.TraceArgs), C.c_int64, C.c_int64,
+                                     C.POINTER(C.c_int64), C.POINTER(C.c_double), C.POINTER(C.c_double)]
+    lib.oracle_last_error.restype = C.c_char_p
+    _lib = lib
+    return lib
+
+
+def philox(ctr, key):
+    lib = load()
+    c = (C.c_uint32 * 4)(*ctr)
+    k = (C.c_uint32 * 2)(*key)
+    o = (C.c_uint32 * 4)()
+    lib.oracle_philox4x32_10(c, k, o)
+    return list(o)
+
+
+def uniform(seed, bin0, g, r, k) -> float:
+    return load().oracle_uniform(seed, bin0, g, r, k)
+
+
+def trace_ray(flat, args, g, r):
+    lib = load()
+    a = C.c_int64()
+    o = (C.c_double * 2)()
+    e = (C.c_double * 2)()
+    rc = lib.oracle_trace_ray(C.byref(flat.desc), C.byref(args), g, r, C.byref(a), o, e)
+    assert rc == 0
+    return a.value, (o[0], o[1]), (e[0], e[1])
+
+
+def trace_exchange(flat, args, nthreads: int = 0):
+    """Run the oracle on a FlatDomain.  Returns (row_ptr, cols, counts, info, rays)."""
+    lib = load()
+    h = C.c_void_p()
+    rc = lib.oracle_trace_exchange(C.byref(flat.desc), C.byref(args), nthreads, C.byref(h))
+    if rc != 0:
+        raise RuntimeError(f"oracle error {rc}: {lib.oracle_last_error().decode()}")
+    try:
+        inf = abi.ResultInfo()
+        lib.oracle_result_get_info(h, C.byref(inf))
+        info = inf.as_dict()
+        info["threads"] = lib.oracle_result_threads(h)
+        n, nnz = info["n_emitters"], info["nnz"]
+        row_ptr = np.zeros(n + 1, dtype=np.int64)
+        cols = np.zeros(max(nnz, 1), dtype=np.int32)
+        counts = np.zeros(max(nnz, 1), dtype=np.uint32)
+        lib.oracle_result_copy_csr(h, abi.ptr(row_ptr, C.c_int64), abi.ptr(cols, C.c_int32),
+                                   abi.ptr(counts, C.c_uint32))
+        rays = None
+        if info["n_recorded"] > 0:
+            cap = info["n_recorded"]
+            o = np.zeros((cap, 2))
+            e = np.zeros((cap, 2))
+            g = np.zeros(cap, dtype=np.int64)
+            nout = C.c_int64()
+            lib.oracle_result_copy_rays(h, abi.ptr(o, C.c_double), abi.ptr(e, C.c_double),
+                                        abi.ptr(g, C.c_int64), cap, C.byref(nout))
+            rays = (o, e, g)
+        return row_ptr, cols[:nnz], counts[:nnz], info, rays
+    finally:
+        lib.oracle_result_free(h)
+
+
+class OracleBackend:
+    """Backend object for rthx.exchange's host logic, for CPU tests only."""
+
+    name = "oracle"
+
+    def __init__(self, nthreads: int = 0):
+        self.nthreads = nthreads
+
+    def trace(self, dom, bin0, rays_per_emitter, nudge, seed, device, faithful, record_ids=None,
+              record_bin0=0, emitter_begin=0, emitter_end=None, emitter_stride=1):
+        flat = dom.flat()
+        end = flat.n_emitters if emitter_end is None else emitter_end
+        flags = abi.RTHX_FLAG_FAITHFUL_SAMPLING if faithful else 0
+        args, keep = make_args(bin0, rays_per_emitter, nudge, seed, emitter_begin, end, emitter_stride,
+                               device, flags, record_ids, record_bin0)
+        out = trace_exchange(flat, args, self.nthreads)
+        del keep
+        return out

@@ -1,0 +1,808 @@
+/*
+ * rthx_oracle.c — TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement (plain C, pthreads) of the reference's exchange-factor
+ * tracer, `mesh(N_rays; method=:exchange)` of RayTraceHeatTransfer.jl v0.11.2.
+ * It is the checker for the HIP product path and the CPU baseline of bench.py
+ * ("port": the reference is Julia and no Julia toolchain exists on either
+ * machine).  Only tests/, __graft_entry__.smoke() and
+ * bench.py's cpu_baseline leg may load it; the product never links it.
+ *
+ * Parity status: pinned by analytic known answers and the reference test
+ * suite's own tables (tests/golden/, tests/test_oracle_known_answers.py):
+ * crossed-strings view factors, reciprocity, Crosbie & Schrenker centreline
+ * (test/test_2d_grey.jl:25-33), the 840.896 K wedge limit
+ * (test/test_triangle_mesh.jl:48-74).  Bit-for-bit stream parity with the
+ * Julia reference is impossible (it calls the unseeded global rand(),
+ * SURVEY.md §0.6); this restatement uses a counter-based Philox-4x32-10
+ * stream that the HIP kernel shares, so GPU and CPU counts can be compared
+ * exactly.
+ *
+ * Every function cites the reference file:line it restates (paths relative
+ * to src/ of the reference).  Structure of the multithreaded driver follows
+ * parallelRayTracing.jl:64-159: a static contiguous partition of the emitter
+ * list over threads, a per-thread hash tally that is flushed per emitter into
+ * per-thread COO buffers, then one sparse assembly.
+ */
+#define _GNU_SOURCE
+#include <math.h>
+#include <pthread.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+#include <unistd.h>
+
+#include "../include/rthx.h"
+
+#define ORACLE_API __attribute__((visibility("default")))
+
+/* ------------------------------------------------------------------------ */
+/* Philox-4x32-10 (Salmon et al., SC'11; Random123 reference constants).     */
+/* The Julia reference uses the unseeded task-local Xoshiro `rand()`         */
+/* (traceRay.jl:25, emitSurfaceRay2D.jl:5 ...), which no test pins.          */
+/* ------------------------------------------------------------------------ */
+#define PHILOX_M0 0xD2511F53u
+#define PHILOX_M1 0xCD9E8D57u
+#define PHILOX_W0 0x9E3779B9u
+#define PHILOX_W1 0xBB67AE85u
+
+ORACLE_API void oracle_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2],
+                                     uint32_t out[4]) {
+  uint32_t c0 = ctr[0], c1 = ctr[1], c2 = ctr[2], c3 = ctr[3];
+  uint32_t k0 = key[0], k1 = key[1];
+  for (int round = 0; round < 10; ++round) {
+    uint64_t p0 = (uint64_t)PHILOX_M0 * c0;
+    uint64_t p1 = (uint64_t)PHILOX_M1 * c2;
+    uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+    uint32_t n1 = (uint32_t)p1;
+    uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+    uint32_t n3 = (uint32_t)p0;
+    c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+    k0 += PHILOX_W0;
+    k1 += PHILOX_W1;
+  }
+  out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+/* 53-bit uniform in [0, 1) from two 32-bit words (hi word first). */
+static inline double u53(uint32_t hi, uint32_t lo) {
+  uint64_t x = ((uint64_t)hi << 32) | lo;
+  return (double)(x >> 11) * 0x1.0p-53;
+}
+
+/* Draw k of ray (g, r) in bin b: block k/2 of the Philox stream with
+ * counter (r, g, k/2, b) and key (seed_lo, seed_hi). */
+typedef struct {
+  uint32_t key[2];
+  uint32_t g, r, bin;
+  uint32_t block;
+  double cache[2];
+  int avail; /* draws left in cache */
+} rng_t;
+
+static void rng_init(rng_t* s, uint64_t seed, uint32_t bin, uint32_t g, uint32_t r) {
+  s->key[0] = (uint32_t)seed;
+  s->key[1] = (uint32_t)(seed >> 32);
+  s->g = g; s->r = r; s->bin = bin; s->block = 0; s->avail = 0;
+}
+
+static double rng_next(rng_t* s) {
+  if (s->avail == 0) {
+    uint32_t ctr[4] = {s->r, s->g, s->block, s->bin};
+    uint32_t o[4];
+    oracle_philox4x32_10(ctr, s->key, o);
+    s->cache[0] = u53(o[0], o[1]);
+    s->cache[1] = u53(o[2], o[3]);
+    s->block++;
+    s->avail = 2;
+  }
+  double v = s->cache[2 - s->avail];
+  s->avail--;
+  return v;
+}
+
+ORACLE_API double oracle_uniform(uint64_t seed, uint32_t bin, uint32_t g, uint32_t r,
+                                 uint32_t k) {
+  rng_t s;
+  rng_init(&s, seed, bin, g, r);
+  double v = 0;
+  for (uint32_t i = 0; i <= k; ++i) v = rng_next(&s);
+  return v;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Domain view (read-only pointers into the caller's descriptor).           */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+  const rthx_domain_desc* d;
+  int64_t n_emitters;
+  int32_t* surf_face;  /* [Ns] global fine face of surface s */
+  int8_t* surf_wall;   /* [Ns] wall index 0..3 */
+  int32_t* coarse_of;  /* [n_fine] */
+} dom_t;
+
+/* distToSurface2D.jl:2-17.  Returns the smallest positive distance parameter
+ * along `d` to the walls of polygon (xy, nrm, n) and the first wall attaining
+ * it; walls with |d.n| < 1e-10 or a non-positive parameter are +Inf.  All
+ * +Inf returns (Inf, 0) like Julia's findmin. */
+static inline double dist_to_polygon(double px, double py, double dx, double dy,
+                                     const double* xy, const double* nrm, int n,
+                                     int* widx) {
+  double best = INFINITY;
+  int bi = 0;
+  int have_nan = 0;
+  for (int i = 0; i < n; ++i) {
+    double nx = nrm[2 * i], ny = nrm[2 * i + 1];
+    double den = dx * nx + dy * ny;
+    double u;
+    if (fabs(den) < 1e-10) {
+      u = INFINITY;
+    } else {
+      u = ((xy[2 * i] - px) * nx + (xy[2 * i + 1] - py) * ny) / den;
+    }
+    if (u <= 0.0) u = INFINITY; /* u[u .<= 0] .= Inf */
+    if (isnan(u)) {             /* findmin propagates NaN (first one) */
+      if (!have_nan) { have_nan = 1; best = u; bi = i; }
+      continue;
+    }
+    if (!have_nan && u < best) { best = u; bi = i; }
+  }
+  *widx = bi;
+  return best;
+}
+
+/* pointInPolygonFast2D, findFace2D.jl:77-101 (crossing test, j = previous). */
+static inline int point_in_polygon(double px, double py, const double* xy, int n) {
+  int inside = 0;
+  int j = n - 1;
+  for (int i = 0; i < n; ++i) {
+    double xi = xy[2 * i], yi = xy[2 * i + 1];
+    double xj = xy[2 * j], yj = xy[2 * j + 1];
+    if ((yi > py) != (yj > py)) {
+      double slope = (xj - xi) / (yj - yi);
+      double ix = xi + slope * (py - yi);
+      if (px < ix) inside = !inside;
+    }
+    j = i;
+  }
+  return inside;
+}
+
+/* findFace2D, findFace2D.jl:48-68: uniform grid first (findFaceUniformGrid2D,
+ * :2-27), then the bbox-prefiltered linear scan (findFaceWithBboxPrefilter2D,
+ * :30-45, pointInBbox2D :71-74).  Polygons [first, first+count) of the flat
+ * arrays; returns the local index or -1 (`nothing`). */
+static int locate(const rthx_grid_desc* g, const int32_t* nv, const double* xy,
+                  const double* bbox, int first, int count, double px, double py) {
+  double fi = floor((px - g->origin_x) * g->inv_cell_size);
+  double fj = floor((py - g->origin_y) * g->inv_cell_size);
+  if (fi >= 0.0 && fi < (double)g->nx && fj >= 0.0 && fj < (double)g->ny) {
+    int cell = (int)fj * g->nx + (int)fi;
+    for (int k = g->cell_start[cell]; k < g->cell_start[cell + 1]; ++k) {
+      int f = g->cell_items[k];
+      if (point_in_polygon(px, py, xy + 8 * (size_t)(first + f), nv[first + f])) return f;
+    }
+  }
+  for (int f = 0; f < count; ++f) {
+    const double* b = bbox + 4 * (size_t)(first + f);
+    if (b[0] <= px && px <= b[1] && b[2] <= py && py <= b[3]) {
+      if (point_in_polygon(px, py, xy + 8 * (size_t)(first + f), nv[first + f])) return f;
+    }
+  }
+  return -1;
+}
+
+static inline int locate_fine(const dom_t* D, int c, double px, double py) {
+  const rthx_domain_desc* d = D->d;
+  int first = d->fine_offset[c];
+  int count = d->fine_offset[c + 1] - first;
+  return locate(&d->fine_grid[c], d->fine_nv, d->fine_xy, d->fine_bbox, first, count, px, py);
+}
+
+static inline int locate_coarse(const dom_t* D, double px, double py) {
+  const rthx_domain_desc* d = D->d;
+  return locate(&d->coarse_grid, d->coarse_nv, d->coarse_xy, d->coarse_bbox, 0, d->n_coarse,
+                px, py);
+}
+
+#define TWO_PI 6.283185307179586 /* Float64(2pi), Julia's 2*pi / 2π */
+
+/* emitSurfaceRay2D.jl:1-26 with lambertSample2D.jl:1-10.  Emission point
+ * uniform on wall w, nudged relatively toward the fine midpoint; cosine-law
+ * direction in the (tangent, left normal) frame, with the Float32-rounded
+ * draws of lambertSample2D.  The direction is left un-normalised (its length
+ * is the in-plane projection of a 3D unit vector). */
+static void emit_surface(const rthx_domain_desc* d, int f, int w, double eta, int faithful,
+                         rng_t* rng, double* p, double* dir) {
+  const double* xy = d->fine_xy + 8 * (size_t)f;
+  int n = d->fine_nv[f];
+  int w2 = (w + 1) % n;
+  double p1x = xy[2 * w], p1y = xy[2 * w + 1];
+  double p2x = xy[2 * w2], p2y = xy[2 * w2 + 1];
+  double R = rng_next(rng);
+  double px = p1x + (p2x - p1x) * R;
+  double py = p1y + (p2y - p1y) * R;
+  const double* m = d->fine_mid + 2 * (size_t)f;
+  px = px + (m[0] - px) * eta;
+  py = py + (m[1] - py) * eta;
+
+  /* lambertSample2D: R_angle1 = Float32(rand()); cosTheta = sqrt(R_angle1)
+   * (Float32); sinTheta = sqrt(1.0 - cosTheta^2) (cosTheta^2 in Float32);
+   * psi = 2*pi*Float32(rand()) (Float64). */
+  float r1 = (float)rng_next(rng);
+  float ct = (float)sqrt((double)r1); /* correctly rounded Float32 sqrt */
+  float ct2 = ct * ct;
+  double st = sqrt(1.0 - (double)ct2);
+  float r2 = (float)rng_next(rng);
+  double cpsi;
+  if (faithful) {
+    double psi = TWO_PI * (double)r2;
+    cpsi = cos(psi);
+  } else {
+    cpsi = cos(TWO_PI * (double)r2);
+  }
+  double xl = st * cpsi;
+  double zl = (double)ct;
+
+  /* xVecLocal = normalize(p2 - p1); yVecLocal = (-x[2], x[1]) */
+  double ex = p2x - p1x, ey = p2y - p1y;
+  double len = sqrt(ex * ex + ey * ey);
+  double tx = ex / len, ty = ey / len;
+  double nx = -ty, ny = tx;
+  /* RotationMatrix * i1_loc (emitSurfaceRay2D.jl:21-23) */
+  dir[0] = tx * xl + nx * zl;
+  dir[1] = ty * xl + ny * zl;
+  p[0] = px;
+  p[1] = py;
+}
+
+/* emitVolumeRay2D.jl:1-33: uniform point (quad = two triangles ABC / CDA
+ * chosen by area, triangle formula (1-sqrt u1)A + sqrt u1 (1-u2) B +
+ * sqrt u1 u2 C), nudged toward the midpoint, isotropic 3D direction
+ * projected onto the plane: (sin(theta) cos(phi), cos(theta)). */
+static void emit_volume(const rthx_domain_desc* d, int f, double eta, int faithful, rng_t* rng,
+                        double* p, double* dir) {
+  const double* v = d->fine_xy + 8 * (size_t)f;
+  int n = d->fine_nv[f];
+  double px, py;
+  if (n == 4) {
+    double Ax = v[0], Ay = v[1], Bx = v[2], By = v[3], Cx = v[4], Cy = v[5], Dx = v[6], Dy = v[7];
+    double R1 = rng_next(rng), R2 = rng_next(rng);
+    double sel = rng_next(rng);
+    double a1 = 0.5 * (Ax * (By - Cy) + Bx * (Cy - Ay) + Cx * (Ay - By)) / d->fine_volume[f];
+    double s1 = sqrt(R1);
+    double wa = 1.0 - s1, wb = s1 * (1.0 - R2), wc = s1 * R2;
+    if (sel < a1) {
+      px = wa * Ax + wb * Bx + wc * Cx;
+      py = wa * Ay + wb * By + wc * Cy;
+    } else {
+      px = wa * Cx + wb * Dx + wc * Ax;
+      py = wa * Cy + wb * Dy + wc * Ay;
+    }
+  } else {
+    double Ax = v[0], Ay = v[1], Bx = v[2], By = v[3], Cx = v[4], Cy = v[5];
+    double R1 = rng_next(rng), R2 = rng_next(rng);
+    double s1 = sqrt(R1);
+    double wa = 1.0 - s1, wb = s1 * (1.0 - R2), wc = s1 * R2;
+    px = wa * Ax + wb * Bx + wc * Cx;
+    py = wa * Ay + wb * By + wc * Cy;
+  }
+  const double* m = d->fine_mid + 2 * (size_t)f;
+  px = px + (m[0] - px) * eta;
+  py = py + (m[1] - py) * eta;
+
+  double u4 = rng_next(rng), u5 = rng_next(rng);
+  double st, ct;
+  if (faithful) {
+    double theta = acos(1.0 - 2.0 * u4);
+    st = sin(theta);
+    ct = cos(theta);
+  } else {
+    ct = 1.0 - 2.0 * u4;               /* cos(acos(x)) = x */
+    st = 2.0 * sqrt(u4 * (1.0 - u4));  /* sin(acos(x)) = sqrt((1-x)(1+x)) */
+  }
+  double cphi = cos(TWO_PI * u5);
+  dir[0] = st * cphi;
+  dir[1] = ct;
+  p[0] = px;
+  p[1] = py;
+}
+
+/* Result of one traced ray (the tuple returned by traceRay*, traceRay.jl:40,52,
+ * then getGlobalIndex2D.jl:1-15).  absorber = -1 means the ray is lost. */
+typedef struct {
+  int64_t absorber;
+  double end[2];
+} hit_t;
+
+/* traceRayUniform, traceRay.jl:20-70 (free path S = -ln u / beta). */
+static hit_t trace_uniform(const dom_t* D, double px, double py, double dx, double dy,
+                           double beta, double eta, int c, rng_t* rng) {
+  const rthx_domain_desc* d = D->d;
+  hit_t h = {-1, {px, py}};
+  double S = beta > 0 ? -log(rng_next(rng)) / beta : INFINITY;
+  for (int it = 0; it < 10000; ++it) {
+    int k;
+    double u = dist_to_polygon(px, py, dx, dy, d->coarse_xy + 8 * (size_t)c,
+                               d->coarse_normal + 8 * (size_t)c, d->coarse_nv[c], &k);
+    if (S < u) {
+      double t = S - eta;
+      px = px + t * dx;
+      py = py + t * dy;
+      int f = locate_fine(D, c, px, py);
+      if (f < 0) return h;
+      h.absorber = d->n_surfaces + d->fine_offset[c] + f;
+      h.end[0] = px; h.end[1] = py;
+      return h;
+    } else if (d->coarse_solid[4 * (size_t)c + k]) {
+      double t = u - eta;
+      px = px + t * dx;
+      py = py + t * dy;
+      int f = locate_fine(D, c, px, py);
+      if (f < 0) return h;
+      int fg = d->fine_offset[c] + f;
+      int w;
+      dist_to_polygon(px, py, dx, dy, d->fine_xy + 8 * (size_t)fg, d->fine_normal + 8 * (size_t)fg,
+                      d->fine_nv[fg], &w);
+      h.absorber = d->fine_surface[4 * (size_t)fg + w]; /* -1 if not solid */
+      h.end[0] = px; h.end[1] = py;
+      return h;
+    } else {
+      double t = u + eta;
+      px = px + t * dx;
+      py = py + t * dy;
+      S -= u;
+      c = locate_coarse(D, px, py);
+      if (c < 0) return h;
+    }
+  }
+  return h;
+}
+
+/* traceRayVariable, traceRay.jl:73-147 (optical-depth sampling; beta taken
+ * from the fine cell containing each segment's start point). */
+static hit_t trace_variable(const dom_t* D, double px, double py, double dx, double dy, int bin,
+                            double eta, int c, rng_t* rng) {
+  const rthx_domain_desc* d = D->d;
+  hit_t h = {-1, {px, py}};
+  const double* beta_bin = d->beta + (size_t)bin * d->n_fine;
+  double target = -log(rng_next(rng));
+  double acc = 0.0;
+  for (int it = 0; it < 10000; ++it) {
+    int k;
+    double u = dist_to_polygon(px, py, dx, dy, d->coarse_xy + 8 * (size_t)c,
+                               d->coarse_normal + 8 * (size_t)c, d->coarse_nv[c], &k);
+    int f0 = locate_fine(D, c, px, py);
+    if (f0 < 0) return h;
+    double beta = beta_bin[d->fine_offset[c] + f0];
+    double tau_b = beta * u;
+    if (acc + tau_b >= target) {
+      double S = (target - acc) / beta;
+      double t = S - eta;
+      px = px + t * dx;
+      py = py + t * dy;
+      int f = locate_fine(D, c, px, py);
+      if (f < 0) return h;
+      h.absorber = d->n_surfaces + d->fine_offset[c] + f;
+      h.end[0] = px; h.end[1] = py;
+      return h;
+    } else if (d->coarse_solid[4 * (size_t)c + k]) {
+      double t = u - eta;
+      px = px + t * dx;
+      py = py + t * dy;
+      int f = locate_fine(D, c, px, py);
+      if (f < 0) return h;
+      int fg = d->fine_offset[c] + f;
+      int w;
+      dist_to_polygon(px, py, dx, dy, d->fine_xy + 8 * (size_t)fg, d->fine_normal + 8 * (size_t)fg,
+                      d->fine_nv[fg], &w);
+      h.absorber = d->fine_surface[4 * (size_t)fg + w];
+      h.end[0] = px; h.end[1] = py;
+      return h;
+    } else {
+      double t = u + eta;
+      px = px + t * dx;
+      py = py + t * dy;
+      acc += tau_b;
+      c = locate_coarse(D, px, py);
+      if (c < 0) return h;
+    }
+  }
+  return h;
+}
+
+/* One ray of emitter g: emit (surface or volume) then traceRay dispatch
+ * (traceRay.jl:1-17: uniform path when uniform_across_bin[bin] > -0.1, with
+ * beta of fine_mesh[1][1]). */
+static hit_t trace_one(const dom_t* D, const rthx_trace_args* a, int64_t g, int64_t r,
+                       double* origin) {
+  const rthx_domain_desc* d = D->d;
+  int faithful = (a->flags & RTHX_FLAG_FAITHFUL_SAMPLING) != 0;
+  rng_t rng;
+  rng_init(&rng, a->seed, (uint32_t)a->bin, (uint32_t)g, (uint32_t)r);
+  double p[2], dir[2];
+  int f;
+  if (g < d->n_surfaces) {
+    f = D->surf_face[g];
+    emit_surface(d, f, D->surf_wall[g], a->nudge, faithful, &rng, p, dir);
+  } else {
+    f = (int)(g - d->n_surfaces);
+    emit_volume(d, f, a->nudge, faithful, &rng, p, dir);
+  }
+  origin[0] = p[0];
+  origin[1] = p[1];
+  int c = D->coarse_of[f];
+  if (d->uniform_beta[a->bin] > -0.1) {
+    double beta = d->beta[(size_t)a->bin * d->n_fine + 0];
+    return trace_uniform(D, p[0], p[1], dir[0], dir[1], beta, a->nudge, c, &rng);
+  }
+  return trace_variable(D, p[0], p[1], dir[0], dir[1], a->bin, a->nudge, c, &rng);
+}
+
+/* ------------------------------------------------------------------------ */
+/* Per-thread hash tally (the reference's Dict{Int,Int} row,                 */
+/* parallelRayTracing.jl:104,124,139) and COO buffers (:94-96,143-146).      */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+  int64_t* keys;
+  uint32_t* vals;
+  int64_t* used;
+  size_t n_used, cap, mask;
+} hmap_t;
+
+static void hmap_init(hmap_t* h, size_t expect) {
+  size_t cap = 16;
+  while (cap < 2 * expect) cap <<= 1;
+  h->cap = cap;
+  h->mask = cap - 1;
+  h->keys = (int64_t*)malloc(cap * sizeof(int64_t));
+  h->vals = (uint32_t*)malloc(cap * sizeof(uint32_t));
+  h->used = (int64_t*)malloc(cap * sizeof(int64_t));
+  for (size_t i = 0; i < cap; ++i) h->keys[i] = -1;
+  h->n_used = 0;
+}
+
+static void hmap_free(hmap_t* h) {
+  free(h->keys); free(h->vals); free(h->used);
+}
+
+static inline void hmap_add(hmap_t* h, int64_t key) {
+  size_t i = ((uint64_t)key * 0x9E3779B97F4A7C15ull) >> 20 & h->mask;
+  while (1) {
+    if (h->keys[i] == key) { h->vals[i]++; return; }
+    if (h->keys[i] < 0) {
+      h->keys[i] = key;
+      h->vals[i] = 1;
+      h->used[h->n_used++] = (int64_t)i;
+      return;
+    }
+    i = (i + 1) & h->mask;
+  }
+}
+
+static void hmap_clear(hmap_t* h) {
+  for (size_t k = 0; k < h->n_used; ++k) h->keys[h->used[k]] = -1;
+  h->n_used = 0;
+}
+
+typedef struct {
+  int64_t* row;
+  int64_t* col;
+  uint32_t* cnt;
+  size_t n, cap;
+} coo_t;
+
+static int coo_push(coo_t* c, int64_t i, int64_t j, uint32_t v) {
+  if (c->n == c->cap) {
+    size_t nc = c->cap ? 2 * c->cap : 1024;
+    int64_t* r = (int64_t*)realloc(c->row, nc * sizeof(int64_t));
+    if (!r) return -1;
+    c->row = r;
+    int64_t* cc = (int64_t*)realloc(c->col, nc * sizeof(int64_t));
+    if (!cc) return -1;
+    c->col = cc;
+    uint32_t* vv = (uint32_t*)realloc(c->cnt, nc * sizeof(uint32_t));
+    if (!vv) return -1;
+    c->cnt = vv;
+    c->cap = nc;
+  }
+  c->row[c->n] = i; c->col[c->n] = j; c->cnt[c->n] = v; c->n++;
+  return 0;
+}
+
+typedef struct {
+  double* orig;
+  double* end;
+  int64_t* emitter;
+  size_t n, cap;
+} recbuf_t;
+
+static int rec_push(recbuf_t* b, const double* o, const double* e, int64_t g) {
+  if (b->n == b->cap) {
+    size_t nc = b->cap ? 2 * b->cap : 1024;
+    double* no = (double*)realloc(b->orig, 2 * nc * sizeof(double));
+    if (!no) return -1;
+    b->orig = no;
+    double* ne = (double*)realloc(b->end, 2 * nc * sizeof(double));
+    if (!ne) return -1;
+    b->end = ne;
+    int64_t* ng = (int64_t*)realloc(b->emitter, nc * sizeof(int64_t));
+    if (!ng) return -1;
+    b->emitter = ng;
+    b->cap = nc;
+  }
+  b->orig[2 * b->n] = o[0]; b->orig[2 * b->n + 1] = o[1];
+  b->end[2 * b->n] = e[0]; b->end[2 * b->n + 1] = e[1];
+  b->emitter[b->n] = g;
+  b->n++;
+  return 0;
+}
+
+typedef struct oracle_result {
+  int64_t n_emitters;
+  int64_t rows_traced;
+  int64_t R;
+  int64_t nnz;
+  int64_t lost_total;
+  int64_t lost_max_row;
+  int64_t* row_ptr;  /* [N+1] */
+  int32_t* cols;
+  uint32_t* counts;
+  recbuf_t rec;
+  double wall_ms;
+  int threads;
+} oracle_result;
+
+typedef struct {
+  const dom_t* D;
+  const rthx_trace_args* a;
+  const int64_t* emitters;
+  int64_t e_begin, e_end;  /* slice of `emitters` */
+  coo_t coo;
+  recbuf_t rec;
+  int64_t lost_total, lost_max;
+  int err;
+} worker_t;
+
+static int is_recorded(const rthx_trace_args* a, int64_t g) {
+  if (a->n_record <= 0 || a->record_bin != a->bin) return 0;
+  for (int i = 0; i < a->n_record; ++i)
+    if (a->record_ids[i] == g) return 1;
+  return 0;
+}
+
+static void* worker_main(void* arg) {
+  worker_t* W = (worker_t*)arg;
+  const dom_t* D = W->D;
+  const rthx_trace_args* a = W->a;
+  int64_t R = a->rays_per_emitter;
+  int64_t expect = R < D->n_emitters ? R : D->n_emitters;
+  hmap_t row;
+  hmap_init(&row, (size_t)(expect > 0 ? expect : 1));
+  for (int64_t e = W->e_begin; e < W->e_end; ++e) {
+    int64_t g = W->emitters[e];
+    int rec = is_recorded(a, g);
+    hmap_clear(&row);
+    int64_t tallied = 0;
+    for (int64_t r = 0; r < R; ++r) {
+      double origin[2];
+      hit_t h = trace_one(D, a, g, r, origin);
+      if (h.absorber < 0) continue; /* `result === nothing` / `a == -1` */
+      if (rec && rec_push(&W->rec, origin, h.end, g)) { W->err = 1; break; }
+      hmap_add(&row, h.absorber);
+      tallied++;
+    }
+    int64_t lost = R - tallied;
+    W->lost_total += lost;
+    if (lost > W->lost_max) W->lost_max = lost;
+    for (size_t k = 0; k < row.n_used; ++k) {
+      size_t slot = (size_t)row.used[k];
+      if (coo_push(&W->coo, g, row.keys[slot], row.vals[slot])) { W->err = 1; break; }
+    }
+  }
+  hmap_free(&row);
+  return NULL;
+}
+
+static __thread char g_err[512];
+
+ORACLE_API const char* oracle_last_error(void) { return g_err; }
+
+static int cmp_u64(const void* x, const void* y) {
+  uint64_t a = *(const uint64_t*)x, b = *(const uint64_t*)y;
+  return (a > b) - (a < b);
+}
+
+static double now_ms(void) {
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec * 1e3 + ts.tv_nsec * 1e-6;
+}
+
+ORACLE_API int oracle_trace_exchange(const rthx_domain_desc* d, const rthx_trace_args* a,
+                                     int nthreads, oracle_result** out) {
+  double t0 = now_ms();
+  *out = NULL;
+  if (!d || !a || a->rays_per_emitter < 0 || a->bin < 0 || a->bin >= d->n_bins ||
+      a->emitter_stride < 1) {
+    snprintf(g_err, sizeof g_err, "invalid arguments");
+    return RTHX_EINVAL;
+  }
+  dom_t D;
+  D.d = d;
+  D.n_emitters = (int64_t)d->n_surfaces + d->n_fine;
+  D.surf_face = (int32_t*)malloc(sizeof(int32_t) * (d->n_surfaces + 1));
+  D.surf_wall = (int8_t*)malloc(d->n_surfaces + 1);
+  D.coarse_of = (int32_t*)malloc(sizeof(int32_t) * (d->n_fine + 1));
+  for (int c = 0; c < d->n_coarse; ++c)
+    for (int f = d->fine_offset[c]; f < d->fine_offset[c + 1]; ++f) D.coarse_of[f] = c;
+  for (int f = 0; f < d->n_fine; ++f)
+    for (int w = 0; w < 4; ++w) {
+      int s = d->fine_surface[4 * (size_t)f + w];
+      if (s >= 0) { D.surf_face[s] = f; D.surf_wall[s] = (int8_t)w; }
+    }
+
+  /* Emitter list in ascending global order (parallelRayTracing.jl:69-77). */
+  int64_t end = a->emitter_end < D.n_emitters ? a->emitter_end : D.n_emitters;
+  int64_t n_list = 0;
+  for (int64_t g = a->emitter_begin; g < end; g += a->emitter_stride) n_list++;
+  int64_t* emitters = (int64_t*)malloc(sizeof(int64_t) * (n_list + 1));
+  n_list = 0;
+  for (int64_t g = a->emitter_begin; g < end; g += a->emitter_stride) emitters[n_list++] = g;
+
+  if (nthreads <= 0) nthreads = (int)sysconf(_SC_NPROCESSORS_ONLN);
+  if (nthreads < 1) nthreads = 1;
+  /* Static contiguous partition (parallelRayTracing.jl:81-91). */
+  worker_t* W = (worker_t*)calloc((size_t)nthreads, sizeof(worker_t));
+  pthread_t* th = (pthread_t*)calloc((size_t)nthreads, sizeof(pthread_t));
+  int64_t per = n_list / nthreads, rem = n_list % nthreads, start = 0;
+  for (int t = 0; t < nthreads; ++t) {
+    int64_t sz = per + (t < rem ? 1 : 0);
+    W[t].D = &D; W[t].a = a; W[t].emitters = emitters;
+    W[t].e_begin = start; W[t].e_end = start + sz;
+    start += sz;
+  }
+  for (int t = 1; t < nthreads; ++t) pthread_create(&th[t], NULL, worker_main, &W[t]);
+  worker_main(&W[0]);
+  for (int t = 1; t < nthreads; ++t) pthread_join(th[t], NULL);
+
+  oracle_result* res = (oracle_result*)calloc(1, sizeof(oracle_result));
+  res->n_emitters = D.n_emitters;
+  res->rows_traced = n_list;
+  res->R = a->rays_per_emitter;
+  res->threads = nthreads;
+  int err = 0;
+  size_t nnz = 0;
+  for (int t = 0; t < nthreads; ++t) {
+    nnz += W[t].coo.n;
+    res->lost_total += W[t].lost_total;
+    if (W[t].lost_max > res->lost_max_row) res->lost_max_row = W[t].lost_max;
+    err |= W[t].err;
+  }
+  /* sparse(I, J, V) assembly (parallelRayTracing.jl:154-155), CSR here. */
+  res->nnz = (int64_t)nnz;
+  res->row_ptr = (int64_t*)calloc((size_t)D.n_emitters + 1, sizeof(int64_t));
+  res->cols = (int32_t*)malloc(sizeof(int32_t) * (nnz + 1));
+  res->counts = (uint32_t*)malloc(sizeof(uint32_t) * (nnz + 1));
+  for (int t = 0; t < nthreads; ++t)
+    for (size_t k = 0; k < W[t].coo.n; ++k) res->row_ptr[W[t].coo.row[k] + 1]++;
+  for (int64_t i = 0; i < D.n_emitters; ++i) res->row_ptr[i + 1] += res->row_ptr[i];
+  int64_t* fill = (int64_t*)malloc(sizeof(int64_t) * ((size_t)D.n_emitters + 1));
+  memcpy(fill, res->row_ptr, sizeof(int64_t) * (size_t)D.n_emitters);
+  for (int t = 0; t < nthreads; ++t)
+    for (size_t k = 0; k < W[t].coo.n; ++k) {
+      int64_t pos = fill[W[t].coo.row[k]]++;
+      res->cols[pos] = (int32_t)W[t].coo.col[k];
+      res->counts[pos] = W[t].coo.cnt[k];
+    }
+  free(fill);
+  /* sort each row by column (pairs sorted through a packed 64-bit key) */
+  for (int64_t i = 0; i < D.n_emitters; ++i) {
+    int64_t b = res->row_ptr[i], e = res->row_ptr[i + 1];
+    if (e - b < 2) continue;
+    uint64_t* tmp = (uint64_t*)malloc(sizeof(uint64_t) * (size_t)(e - b));
+    for (int64_t k = b; k < e; ++k)
+      tmp[k - b] = ((uint64_t)(uint32_t)res->cols[k] << 32) | res->counts[k];
+    qsort(tmp, (size_t)(e - b), sizeof(uint64_t), cmp_u64);
+    for (int64_t k = b; k < e; ++k) {
+      res->cols[k] = (int32_t)(tmp[k - b] >> 32);
+      res->counts[k] = (uint32_t)tmp[k - b];
+    }
+    free(tmp);
+  }
+  /* recorder: concatenate per-thread buffers (collect_rays, :199-200) */
+  for (int t = 0; t < nthreads; ++t) {
+    for (size_t k = 0; k < W[t].rec.n; ++k)
+      if (rec_push(&res->rec, W[t].rec.orig + 2 * k, W[t].rec.end + 2 * k, W[t].rec.emitter[k]))
+        err = 1;
+    free(W[t].rec.orig); free(W[t].rec.end); free(W[t].rec.emitter);
+    free(W[t].coo.row); free(W[t].coo.col); free(W[t].coo.cnt);
+  }
+  free(W); free(th); free(emitters);
+  free(D.surf_face); free(D.surf_wall); free(D.coarse_of);
+  res->wall_ms = now_ms() - t0;
+  if (err) {
+    snprintf(g_err, sizeof g_err, "out of host memory");
+    free(res->row_ptr); free(res->cols); free(res->counts);
+    free(res->rec.orig); free(res->rec.end); free(res->rec.emitter);
+    free(res);
+    return RTHX_ENOMEM;
+  }
+  *out = res;
+  return RTHX_OK;
+}
+
+ORACLE_API int oracle_result_get_info(const oracle_result* r, rthx_result_info* info) {
+  if (!r || !info) return RTHX_EINVAL;
+  memset(info, 0, sizeof *info);
+  info->n_emitters = r->n_emitters;
+  info->rows_traced = r->rows_traced;
+  info->rays_per_emitter = r->R;
+  info->rays_traced = r->rows_traced * r->R;
+  info->nnz = r->nnz;
+  info->lost_total = r->lost_total;
+  info->lost_max_row = r->lost_max_row;
+  info->n_recorded = (int64_t)r->rec.n;
+  info->trace_ms = r->wall_ms;
+  info->total_ms = r->wall_ms;
+  return RTHX_OK;
+}
+
+ORACLE_API int oracle_result_threads(const oracle_result* r) { return r ? r->threads : 0; }
+
+ORACLE_API int oracle_result_copy_csr(const oracle_result* r, int64_t* row_ptr, int32_t* cols,
+                                      uint32_t* counts) {
+  if (!r) return RTHX_EINVAL;
+  if (row_ptr) memcpy(row_ptr, r->row_ptr, sizeof(int64_t) * (size_t)(r->n_emitters + 1));
+  if (cols) memcpy(cols, r->cols, sizeof(int32_t) * (size_t)r->nnz);
+  if (counts) memcpy(counts, r->counts, sizeof(uint32_t) * (size_t)r->nnz);
+  return RTHX_OK;
+}
+
+ORACLE_API int oracle_result_copy_rays(const oracle_result* r, double* orig, double* end,
+                                       int64_t* emitter, int64_t cap, int64_t* n_out) {
+  if (!r) return RTHX_EINVAL;
+  int64_t n = (int64_t)r->rec.n < cap ? (int64_t)r->rec.n : cap;
+  if (n > 0) {
+    if (orig) memcpy(orig, r->rec.orig, sizeof(double) * 2 * (size_t)n);
+    if (end) memcpy(end, r->rec.end, sizeof(double) * 2 * (size_t)n);
+    if (emitter) memcpy(emitter, r->rec.emitter, sizeof(int64_t) * (size_t)n);
+  }
+  if (n_out) *n_out = n;
+  return RTHX_OK;
+}
+
+ORACLE_API void oracle_result_free(oracle_result* r) {
+  if (!r) return;
+  free(r->row_ptr); free(r->cols); free(r->counts);
+  free(r->rec.orig); free(r->rec.end); free(r->rec.emitter);
+  free(r);
+}
+
+/* Single-ray probe for debugging parity: absorber (-1 = lost), emission point
+ * and end point of ray (g, r). */
+ORACLE_API int oracle_trace_ray(const rthx_domain_desc* d, const rthx_trace_args* a, int64_t g,
+                                int64_t r, int64_t* absorber, double* origin, double* end) {
+  dom_t D;
+  D.d = d;
+  D.n_emitters = (int64_t)d->n_surfaces + d->n_fine;
+  if (g < 0 || g >= D.n_emitters) return RTHX_EINVAL;
+  D.surf_face = (int32_t*)malloc(sizeof(int32_t) * (d->n_surfaces + 1));
+  D.surf_wall = (int8_t*)malloc(d->n_surfaces + 1);
+  D.coarse_of = (int32_t*)malloc(sizeof(int32_t) * (d->n_fine + 1));
+  for (int c = 0; c < d->n_coarse; ++c)
+    for (int f = d->fine_offset[c]; f < d->fine_offset[c + 1]; ++f) D.coarse_of[f] = c;
+  for (int f = 0; f < d->n_fine; ++f)
+    for (int w = 0; w < 4; ++w) {
+      int s = d->fine_surface[4 * (size_t)f + w];
+      if (s >= 0) { D.surf_face[s] = f; D.surf_wall[s] = (int8_t)w; }
+    }
+  hit_t h = trace_one(&D, a, g, r, origin);
+  *absorber = h.absorber;
+  end[0] = h.end[0];
+  end[1] = h.end[1];
+  free(D.surf_face); free(D.surf_wall); free(D.coarse_of);
+  return RTHX_OK;
+}

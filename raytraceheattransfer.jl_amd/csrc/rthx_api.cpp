@@ -1,0 +1,555 @@
+// rthx_api.cpp — the C ABI declared in include/rthx.h (host side, HIP runtime).
+//
+// Replaces the body of computeExchangeFactorsBin
+// (src/RayTracing/RayTracing2D/ExchangeFactors2D/parallelRayTracing.jl:64-159):
+// the domain is validated and uploaded once (rthx_domain_create), each traced
+// bin is one rthx_trace_exchange call (trace -> scan -> CSR pack on one HIP
+// stream), and the count matrix comes back as CSR for the host to turn into
+// SparseMatrixCSC (V = c/R, row_normalize!).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/rthx.h"
+#include "rthx_kernels.h"
+
+#define RTHX_EXPORT extern "C" __attribute__((visibility("default")))
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+  return fail(RTHX_EDEVICE, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define HIP_TRY(expr, what)                 \
+  do {                                      \
+    hipError_t _e = (expr);                 \
+    if (_e != hipSuccess) return hip_fail(_e, what); \
+  } while (0)
+
+// Device buffer with grow-only capacity.
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  hipError_t reserve(size_t bytes) {
+    if (bytes <= cap && p) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = bytes < 256 ? 256 : bytes;
+    hipError_t e = hipMalloc(&p, want);
+    if (e == hipSuccess) cap = want;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  template <class T>
+  T* as() const { return static_cast<T*>(p); }
+};
+
+double now_ms() {
+  using namespace std::chrono;
+  return duration<double, std::milli>(steady_clock::now().time_since_epoch()).count();
+}
+
+}  // namespace
+
+struct rthx_domain {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  rthx::DevDomain D{};
+  std::vector<void*> allocs;
+  int64_t n_emitters = 0;
+  int32_t n_bins = 1;
+  std::vector<double> uniform_beta;  // per bin
+  std::vector<double> beta_first;    // beta of fine face 0 per bin (traceRay.jl:6-11)
+  ~rthx_domain() {
+    for (void* p : allocs) (void)hipFree(p);
+    for (auto& e : ev)
+      if (e) (void)hipEventDestroy(e);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+};
+
+struct rthx_result {
+  int device = -1;
+  DevBuf stage_cols, stage_cnt, row_nnz, row_tallied, row_off, totals, cols, cnt;
+  DevBuf rec_ids, rec_ok, rec_orig, rec_end;
+  bool valid = false;
+  bool host_csr = false;
+  int64_t N = 0, R = 0, n_rows = 0, begin = 0, stride = 1;
+  std::vector<int64_t> h_row_off;
+  std::vector<uint32_t> h_cols, h_cnt;
+  std::vector<int64_t> rec_g;  // recorded emitters (ascending)
+  std::vector<uint8_t> h_ok;
+  std::vector<double> h_orig, h_end;
+  bool host_rec = false;
+  rthx_result_info info{};
+  ~rthx_result() {
+    if (device >= 0) (void)hipSetDevice(device);
+    DevBuf* all[] = {&stage_cols, &stage_cnt, &row_nnz, &row_tallied, &row_off, &totals,
+                     &cols,       &cnt,       &rec_ids, &rec_ok,      &rec_orig, &rec_end};
+    for (DevBuf* b : all) b->release();
+  }
+};
+
+namespace {
+
+template <class T>
+int upload(rthx_domain* d, const T* src, size_t n, const T** dst, const char* what) {
+  if (n == 0) {
+    *dst = nullptr;
+    return RTHX_OK;
+  }
+  if (!src) return fail(RTHX_EINVAL, std::string("null descriptor array: ") + what);
+  void* p = nullptr;
+  hipError_t e = hipMalloc(&p, n * sizeof(T));
+  if (e != hipSuccess) return fail(RTHX_ENOMEM, std::string("hipMalloc failed for ") + what);
+  d->allocs.push_back(p);
+  e = hipMemcpy(p, src, n * sizeof(T), hipMemcpyHostToDevice);
+  if (e != hipSuccess) return hip_fail(e, what);
+  *dst = static_cast<const T*>(p);
+  return RTHX_OK;
+}
+
+int check_grid(const rthx_grid_desc& g, int32_t count, const char* what) {
+  if (g.nx < 1 || g.ny < 1 || !g.cell_start || !(std::isfinite(g.inv_cell_size)) || g.inv_cell_size <= 0)
+    return fail(RTHX_EINVAL, std::string("invalid grid: ") + what);
+  int64_t cells = (int64_t)g.nx * g.ny;
+  if (cells > (1ll << 30)) return fail(RTHX_ERANGE, std::string("grid too large: ") + what);
+  if (g.cell_start[0] != 0) return fail(RTHX_EINVAL, std::string("grid cell_start[0] != 0: ") + what);
+  for (int64_t c = 0; c < cells; ++c)
+    if (g.cell_start[c + 1] < g.cell_start[c]) return fail(RTHX_EINVAL, std::string("grid cell_start not monotone: ") + what);
+  int64_t n_items = g.cell_start[cells];
+  if (n_items > 0 && !g.cell_items) return fail(RTHX_EINVAL, std::string("null grid items: ") + what);
+  for (int64_t k = 0; k < n_items; ++k)
+    if (g.cell_items[k] < 0 || g.cell_items[k] >= count)
+      return fail(RTHX_EINVAL, std::string("grid item out of range: ") + what);
+  return RTHX_OK;
+}
+
+}  // namespace
+
+RTHX_EXPORT int rthx_abi_version(void) { return RTHX_ABI_VERSION; }
+
+RTHX_EXPORT const char* rthx_last_error(void) { return g_last_error.c_str(); }
+
+RTHX_EXPORT int rthx_device_count(int32_t* count) {
+  if (!count) return fail(RTHX_EINVAL, "null count");
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) {
+    *count = 0;
+    return hip_fail(e, "hipGetDeviceCount");
+  }
+  *count = n;
+  return RTHX_OK;
+}
+
+RTHX_EXPORT int rthx_device_synchronize(int32_t device) {
+  HIP_TRY(hipSetDevice(device), "hipSetDevice");
+  HIP_TRY(hipDeviceSynchronize(), "hipDeviceSynchronize");
+  return RTHX_OK;
+}
+
+RTHX_EXPORT int rthx_domain_create(const rthx_domain_desc* desc, int32_t device, rthx_domain** out) {
+  if (!out) return fail(RTHX_EINVAL, "null out");
+  *out = nullptr;
+  if (!desc) return fail(RTHX_EINVAL, "null descriptor");
+  if (desc->abi_version != RTHX_ABI_VERSION) return fail(RTHX_EINVAL, "descriptor ABI version mismatch");
+  const rthx_domain_desc& s = *desc;
+  if (s.n_coarse < 1 || s.n_fine < 1 || s.n_surfaces < 0 || s.n_bins < 1)
+    return fail(RTHX_EINVAL, "empty or negative domain sizes");
+  if ((int64_t)s.n_surfaces + s.n_fine >= (1ll << 31)) return fail(RTHX_ERANGE, "too many elements");
+  if (!s.coarse_nv || !s.coarse_xy || !s.coarse_normal || !s.coarse_solid || !s.coarse_bbox || !s.fine_offset ||
+      !s.fine_nv || !s.fine_xy || !s.fine_normal || !s.fine_mid || !s.fine_volume || !s.fine_bbox ||
+      !s.fine_surface || !s.fine_grid || !s.beta || !s.uniform_beta)
+    return fail(RTHX_EINVAL, "null descriptor array");
+  for (int c = 0; c < s.n_coarse; ++c)
+    if (s.coarse_nv[c] != 3 && s.coarse_nv[c] != 4) return fail(RTHX_EINVAL, "coarse polygon with n not in {3,4}");
+  if (s.fine_offset[0] != 0 || s.fine_offset[s.n_coarse] != s.n_fine)
+    return fail(RTHX_EINVAL, "fine_offset must run from 0 to n_fine");
+  for (int c = 0; c < s.n_coarse; ++c)
+    if (s.fine_offset[c + 1] <= s.fine_offset[c]) return fail(RTHX_EINVAL, "coarse polygon without fine polygons");
+  for (int f = 0; f < s.n_fine; ++f)
+    if (s.fine_nv[f] != 3 && s.fine_nv[f] != 4) return fail(RTHX_EINVAL, "fine polygon with n not in {3,4}");
+  std::vector<int32_t> s_face(s.n_surfaces, -1), s_wall(s.n_surfaces, -1);
+  for (int f = 0; f < s.n_fine; ++f)
+    for (int w = 0; w < 4; ++w) {
+      int32_t sidx = s.fine_surface[4 * (size_t)f + w];
+      if (sidx < -1 || sidx >= s.n_surfaces || (sidx >= 0 && w >= s.fine_nv[f]))
+        return fail(RTHX_EINVAL, "fine_surface index out of range");
+      if (sidx >= 0) {
+        if (s_face[sidx] != -1) return fail(RTHX_EINVAL, "surface index used twice");
+        s_face[sidx] = f;
+        s_wall[sidx] = w;
+      }
+    }
+  for (int i = 0; i < s.n_surfaces; ++i)
+    if (s_face[i] < 0) return fail(RTHX_EINVAL, "surface index without a solid fine wall");
+  for (int64_t k = 0; k < (int64_t)s.n_bins * s.n_fine; ++k)
+    if (!std::isfinite(s.beta[k]) || s.beta[k] < 0) return fail(RTHX_EINVAL, "non-finite or negative extinction");
+  for (int64_t k = 0; k < 8ll * s.n_fine; ++k)
+    if (!std::isfinite(s.fine_xy[k]) || !std::isfinite(s.fine_normal[k]))
+      return fail(RTHX_EINVAL, "non-finite fine geometry");
+  int rc = check_grid(s.coarse_grid, s.n_coarse, "coarse grid");
+  if (rc) return rc;
+  for (int c = 0; c < s.n_coarse; ++c) {
+    rc = check_grid(s.fine_grid[c], s.fine_offset[c + 1] - s.fine_offset[c], "fine grid");
+    if (rc) return rc;
+  }
+
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) return fail(RTHX_EDEVICE, "no HIP device visible");
+  if (device < 0 || device >= ndev) return fail(RTHX_EINVAL, "device ordinal out of range");
+  HIP_TRY(hipSetDevice(device), "hipSetDevice");
+
+  rthx_domain* d = new (std::nothrow) rthx_domain();
+  if (!d) return fail(RTHX_ENOMEM, "host allocation failed");
+  d->device = device;
+  d->n_emitters = (int64_t)s.n_surfaces + s.n_fine;
+  d->n_bins = s.n_bins;
+  d->uniform_beta.assign(s.uniform_beta, s.uniform_beta + s.n_bins);
+  d->beta_first.resize(s.n_bins);
+  for (int b = 0; b < s.n_bins; ++b) d->beta_first[b] = s.beta[(size_t)b * s.n_fine];
+
+  auto bail = [&](int code) {
+    delete d;
+    return code;
+  };
+  if (hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess) return bail(fail(RTHX_EDEVICE, "hipStreamCreate"));
+  for (auto& e : d->ev)
+    if (hipEventCreate(&e) != hipSuccess) return bail(fail(RTHX_EDEVICE, "hipEventCreate"));
+
+  rthx::DevDomain& D = d->D;
+  D.n_coarse = s.n_coarse;
+  D.n_fine = s.n_fine;
+  D.n_surfaces = s.n_surfaces;
+  D.n_bins = s.n_bins;
+  std::vector<uint32_t> csolid(s.n_coarse, 0u);
+  for (int c = 0; c < s.n_coarse; ++c)
+    for (int w = 0; w < 4; ++w)
+      if (s.coarse_solid[4 * c + w]) csolid[c] |= 1u << w;
+  std::vector<int32_t> fcoarse(s.n_fine);
+  for (int c = 0; c < s.n_coarse; ++c)
+    for (int f = s.fine_offset[c]; f < s.fine_offset[c + 1]; ++f) fcoarse[f] = c;
+
+  // concatenate grids: coarse first, then fine grids in coarse order
+  std::vector<int32_t> cell_start, items;
+  auto add_grid = [&](const rthx_grid_desc& g) {
+    rthx::DevGrid dg;
+    dg.ox = g.origin_x;
+    dg.oy = g.origin_y;
+    dg.inv = g.inv_cell_size;
+    dg.nx = g.nx;
+    dg.ny = g.ny;
+    dg.cell_base = (int32_t)cell_start.size();
+    dg.item_base = (int32_t)items.size();
+    int64_t cells = (int64_t)g.nx * g.ny;
+    cell_start.insert(cell_start.end(), g.cell_start, g.cell_start + cells + 1);
+    items.insert(items.end(), g.cell_items, g.cell_items + g.cell_start[cells]);
+    return dg;
+  };
+  D.c_grid = add_grid(s.coarse_grid);
+  std::vector<rthx::DevGrid> fgrids(s.n_coarse);
+  for (int c = 0; c < s.n_coarse; ++c) fgrids[c] = add_grid(s.fine_grid[c]);
+  if (cell_start.size() >= (1ull << 31) || items.size() >= (1ull << 31)) return bail(fail(RTHX_ERANGE, "grids too large"));
+
+  const size_t nc = s.n_coarse, nf = s.n_fine;
+#define UP(src, n, dst)                                          \
+  do {                                                           \
+    int _r = upload(d, (src), (n), &(dst), #dst);                \
+    if (_r) return bail(_r);                                     \
+  } while (0)
+  UP(s.coarse_nv, nc, D.c_nv);
+  UP(s.coarse_xy, 8 * nc, D.c_xy);
+  UP(s.coarse_normal, 8 * nc, D.c_nrm);
+  UP(csolid.data(), nc, D.c_solid);
+  UP(s.coarse_bbox, 4 * nc, D.c_bbox);
+  UP(s.fine_offset, nc + 1, D.f_offset);
+  UP(s.fine_nv, nf, D.f_nv);
+  UP(s.fine_xy, 8 * nf, D.f_xy);
+  UP(s.fine_normal, 8 * nf, D.f_nrm);
+  UP(s.fine_mid, 2 * nf, D.f_mid);
+  UP(s.fine_volume, nf, D.f_vol);
+  UP(s.fine_bbox, 4 * nf, D.f_bbox);
+  UP(s.fine_surface, 4 * nf, D.f_surf);
+  UP(fcoarse.data(), nf, D.f_coarse);
+  UP(fgrids.data(), nc, D.f_grid);
+  UP(cell_start.data(), cell_start.size(), D.grid_cell_start);
+  UP(items.data(), items.size(), D.grid_items);
+  UP(s.beta, (size_t)s.n_bins * nf, D.beta);
+  UP(s.uniform_beta, (size_t)s.n_bins, D.uniform_beta);
+  UP(s_face.data(), s_face.size(), D.s_face);
+  UP(s_wall.data(), s_wall.size(), D.s_wall);
+#undef UP
+  if (!D.grid_items) {  // an all-empty grid still needs a valid pointer
+    int32_t zero = 0;
+    int r2 = upload(d, &zero, 1, &D.grid_items, "grid_items");
+    if (r2) return bail(r2);
+  }
+  *out = d;
+  return RTHX_OK;
+}
+
+RTHX_EXPORT void rthx_domain_destroy(rthx_domain* dom) {
+  if (!dom) return;
+  (void)hipSetDevice(dom->device);
+  (void)hipStreamSynchronize(dom->stream);
+  delete dom;
+}
+
+RTHX_EXPORT int rthx_result_create(rthx_result** out) {
+  if (!out) return fail(RTHX_EINVAL, "null out");
+  *out = new (std::nothrow) rthx_result();
+  return *out ? RTHX_OK : fail(RTHX_ENOMEM, "host allocation failed");
+}
+
+RTHX_EXPORT void rthx_result_destroy(rthx_result* res) { delete res; }
+
+RTHX_EXPORT int rthx_trace_exchange(rthx_domain* dom, const rthx_trace_args* a, rthx_result* res) {
+  const double t0 = now_ms();
+  if (!dom || !a || !res) return fail(RTHX_EINVAL, "null argument");
+  if (a->bin < 0 || a->bin >= dom->n_bins) return fail(RTHX_EINVAL, "bin out of range");
+  if (a->rays_per_emitter < 0 || a->rays_per_emitter > 0xFFFFFFFFll)
+    return fail(RTHX_ERANGE, "rays_per_emitter must be in [0, 2^32)");
+  if (a->emitter_stride < 1 || a->emitter_begin < 0) return fail(RTHX_EINVAL, "bad emitter range");
+  if (!std::isfinite(a->nudge)) return fail(RTHX_EINVAL, "non-finite nudge");
+  if (a->device != dom->device) return fail(RTHX_EINVAL, "args.device differs from the domain's device");
+  if (a->n_record < 0 || (a->n_record > 0 && !a->record_ids)) return fail(RTHX_EINVAL, "bad record ids");
+  HIP_TRY(hipSetDevice(dom->device), "hipSetDevice");
+  if (res->device >= 0 && res->device != dom->device) return fail(RTHX_EINVAL, "result bound to another device");
+  res->device = dom->device;
+
+  const int64_t N = dom->n_emitters;
+  const int64_t R = a->rays_per_emitter;
+  const int64_t end = std::min<int64_t>(a->emitter_end, N);
+  const int64_t n_rows = end > a->emitter_begin ? (end - a->emitter_begin + a->emitter_stride - 1) / a->emitter_stride : 0;
+  if (n_rows >= (1ll << 31)) return fail(RTHX_ERANGE, "too many rows in one call");
+  const bool pack16 = R < 65536;
+  const int64_t words = pack16 ? (N + 1) / 2 : N;
+  const size_t lds_bytes = (size_t)words * 4;
+  if (lds_bytes + 1024 > rthx::kMaxLdsBytes)
+    return fail(RTHX_ERANGE, "N too large for the LDS row histogram of this build (N <= 81408 when R < 65536, N <= 40704 otherwise)");
+  const int64_t row_cap = std::max<int64_t>(1, std::min<int64_t>(N, R));
+
+  res->valid = false;
+  res->host_csr = false;
+  res->host_rec = false;
+  res->N = N;
+  res->R = R;
+  res->n_rows = n_rows;
+  res->begin = a->emitter_begin;
+  res->stride = a->emitter_stride;
+  res->info = rthx_result_info{};
+  res->info.n_emitters = N;
+  res->info.rows_traced = n_rows;
+  res->info.rays_per_emitter = R;
+  res->info.rays_traced = n_rows * R;
+
+  // recorded emitters traced by this call (ascending, unique)
+  res->rec_g.clear();
+  if (a->n_record > 0 && a->record_bin == a->bin) {
+    for (int i = 0; i < a->n_record; ++i) {
+      int64_t g = a->record_ids[i];
+      if (g >= a->emitter_begin && g < end && (g - a->emitter_begin) % a->emitter_stride == 0) res->rec_g.push_back(g);
+    }
+    std::sort(res->rec_g.begin(), res->rec_g.end());
+    res->rec_g.erase(std::unique(res->rec_g.begin(), res->rec_g.end()), res->rec_g.end());
+  }
+  const size_t n_rec = res->rec_g.size();
+
+  HIP_TRY(res->stage_cols.reserve((size_t)n_rows * row_cap * 4), "hipMalloc stage_cols");
+  HIP_TRY(res->stage_cnt.reserve((size_t)n_rows * row_cap * 4), "hipMalloc stage_cnt");
+  HIP_TRY(res->row_nnz.reserve((size_t)n_rows * 4), "hipMalloc row_nnz");
+  HIP_TRY(res->row_tallied.reserve((size_t)n_rows * 4), "hipMalloc row_tallied");
+  HIP_TRY(res->row_off.reserve((size_t)(n_rows + 1) * 8), "hipMalloc row_off");
+  HIP_TRY(res->totals.reserve(4 * 8), "hipMalloc totals");
+  HIP_TRY(res->cols.reserve((size_t)n_rows * row_cap * 4), "hipMalloc cols");
+  HIP_TRY(res->cnt.reserve((size_t)n_rows * row_cap * 4), "hipMalloc cnt");
+  rthx::RecordParams rec{};
+  if (n_rec > 0) {
+    HIP_TRY(res->rec_ids.reserve(n_rec * 8), "hipMalloc rec_ids");
+    HIP_TRY(res->rec_ok.reserve(n_rec * (size_t)R), "hipMalloc rec_ok");
+    HIP_TRY(res->rec_orig.reserve(n_rec * (size_t)R * 16), "hipMalloc rec_orig");
+    HIP_TRY(res->rec_end.reserve(n_rec * (size_t)R * 16), "hipMalloc rec_end");
+    HIP_TRY(hipMemcpyAsync(res->rec_ids.p, res->rec_g.data(), n_rec * 8, hipMemcpyHostToDevice, dom->stream),
+            "hipMemcpy rec ids");
+    rec.n = (int32_t)n_rec;
+    rec.ids = res->rec_ids.as<int64_t>();
+    rec.ok = res->rec_ok.as<uint8_t>();
+    rec.orig = res->rec_orig.as<double>();
+    rec.end = res->rec_end.as<double>();
+  }
+
+  rthx::TraceParams P{};
+  P.R = R;
+  P.g_begin = a->emitter_begin;
+  P.g_stride = a->emitter_stride;
+  P.eta = a->nudge;
+  P.key0 = (uint32_t)a->seed;
+  P.key1 = (uint32_t)(a->seed >> 32);
+  P.bin = a->bin;
+  P.faithful = (a->flags & RTHX_FLAG_FAITHFUL_SAMPLING) ? 1 : 0;
+  P.beta_uniform = dom->beta_first[a->bin];
+  const bool uniform = dom->uniform_beta[a->bin] > -0.1;  // traceRay.jl:4
+
+  hipStream_t st = dom->stream;
+  HIP_TRY(hipEventRecord(dom->ev[0], st), "hipEventRecord");
+  if (n_rows > 0) {
+    HIP_TRY(rthx::launch_trace(dom->D, P, uniform, pack16, N, n_rows, res->stage_cols.as<uint32_t>(),
+                               res->stage_cnt.as<uint32_t>(), row_cap, res->row_nnz.as<uint32_t>(),
+                               res->row_tallied.as<uint32_t>(), rec, lds_bytes, st),
+            "trace_exchange_kernel launch");
+  }
+  HIP_TRY(hipEventRecord(dom->ev[1], st), "hipEventRecord");
+  if (n_rows > 0) {
+    HIP_TRY(rthx::launch_scan(res->row_nnz.as<uint32_t>(), res->row_tallied.as<uint32_t>(), n_rows, R,
+                              res->row_off.as<int64_t>(), res->totals.as<int64_t>(), st),
+            "row_scan_kernel launch");
+    HIP_TRY(rthx::launch_pack(res->stage_cols.as<uint32_t>(), res->stage_cnt.as<uint32_t>(), row_cap,
+                              res->row_off.as<int64_t>(), n_rows, res->cols.as<uint32_t>(), res->cnt.as<uint32_t>(), st),
+            "csr_pack_kernel launch");
+  } else {
+    HIP_TRY(hipMemsetAsync(res->row_off.p, 0, 8, st), "hipMemset");
+    HIP_TRY(hipMemsetAsync(res->totals.p, 0, 32, st), "hipMemset");
+  }
+  HIP_TRY(hipEventRecord(dom->ev[2], st), "hipEventRecord");
+
+  int64_t totals[3] = {0, 0, 0};
+  HIP_TRY(hipMemcpyAsync(totals, res->totals.p, 24, hipMemcpyDeviceToHost, st), "hipMemcpy totals");
+  res->h_row_off.resize(n_rows + 1);
+  HIP_TRY(hipMemcpyAsync(res->h_row_off.data(), res->row_off.p, (n_rows + 1) * 8, hipMemcpyDeviceToHost, st),
+          "hipMemcpy row_off");
+  HIP_TRY(hipStreamSynchronize(st), "trace kernels");
+  float ms_trace = 0.f, ms_pack = 0.f;
+  HIP_TRY(hipEventElapsedTime(&ms_trace, dom->ev[0], dom->ev[1]), "hipEventElapsedTime");
+  HIP_TRY(hipEventElapsedTime(&ms_pack, dom->ev[1], dom->ev[2]), "hipEventElapsedTime");
+
+  res->info.nnz = totals[0];
+  res->info.lost_total = totals[1];
+  res->info.lost_max_row = totals[2];
+  res->info.trace_ms = ms_trace;
+  res->info.pack_ms = ms_pack;
+  res->valid = true;
+
+  if (!(a->flags & RTHX_FLAG_DEVICE_ONLY)) {
+    const size_t nnz = (size_t)totals[0];
+    res->h_cols.resize(nnz);
+    res->h_cnt.resize(nnz);
+    if (nnz) {
+      HIP_TRY(hipMemcpy(res->h_cols.data(), res->cols.p, nnz * 4, hipMemcpyDeviceToHost), "hipMemcpy cols");
+      HIP_TRY(hipMemcpy(res->h_cnt.data(), res->cnt.p, nnz * 4, hipMemcpyDeviceToHost), "hipMemcpy counts");
+    }
+    res->host_csr = true;
+    if (n_rec > 0) {
+      res->h_ok.resize(n_rec * (size_t)R);
+      res->h_orig.resize(n_rec * (size_t)R * 2);
+      res->h_end.resize(n_rec * (size_t)R * 2);
+      HIP_TRY(hipMemcpy(res->h_ok.data(), res->rec_ok.p, n_rec * (size_t)R, hipMemcpyDeviceToHost), "hipMemcpy rec");
+      HIP_TRY(hipMemcpy(res->h_orig.data(), res->rec_orig.p, n_rec * (size_t)R * 16, hipMemcpyDeviceToHost), "hipMemcpy rec");
+      HIP_TRY(hipMemcpy(res->h_end.data(), res->rec_end.p, n_rec * (size_t)R * 16, hipMemcpyDeviceToHost), "hipMemcpy rec");
+      res->host_rec = true;
+    }
+  }
+  int64_t nrec = 0;
+  if (n_rec > 0) {
+    if (!res->host_rec) {
+      res->h_ok.resize(n_rec * (size_t)R);
+      HIP_TRY(hipMemcpy(res->h_ok.data(), res->rec_ok.p, n_rec * (size_t)R, hipMemcpyDeviceToHost), "hipMemcpy rec");
+    }
+    for (uint8_t v : res->h_ok) nrec += v;
+  }
+  res->info.n_recorded = nrec;
+  res->info.total_ms = now_ms() - t0;
+  return RTHX_OK;
+}
+
+RTHX_EXPORT int rthx_result_get_info(const rthx_result* res, rthx_result_info* info) {
+  if (!res || !info) return fail(RTHX_EINVAL, "null argument");
+  if (!res->valid) return fail(RTHX_ESTATE, "result holds no trace");
+  *info = res->info;
+  return RTHX_OK;
+}
+
+RTHX_EXPORT int rthx_result_copy_csr(const rthx_result* cres, int64_t* row_ptr, int32_t* cols, uint32_t* counts) {
+  if (!cres) return fail(RTHX_EINVAL, "null result");
+  if (!cres->valid) return fail(RTHX_ESTATE, "result holds no trace");
+  rthx_result* res = const_cast<rthx_result*>(cres);
+  const size_t nnz = (size_t)res->info.nnz;
+  if (!res->host_csr) {
+    HIP_TRY(hipSetDevice(res->device), "hipSetDevice");
+    res->h_cols.resize(nnz);
+    res->h_cnt.resize(nnz);
+    if (nnz) {
+      HIP_TRY(hipMemcpy(res->h_cols.data(), res->cols.p, nnz * 4, hipMemcpyDeviceToHost), "hipMemcpy cols");
+      HIP_TRY(hipMemcpy(res->h_cnt.data(), res->cnt.p, nnz * 4, hipMemcpyDeviceToHost), "hipMemcpy counts");
+    }
+    res->host_csr = true;
+  }
+  if (row_ptr) {
+    // rows g = begin + k*stride hold slot k; all other rows are empty
+    row_ptr[0] = 0;
+    int64_t k = 0;
+    for (int64_t g = 0; g < res->N; ++g) {
+      int64_t n = 0;
+      if (k < res->n_rows && g == res->begin + k * res->stride) {
+        n = res->h_row_off[k + 1] - res->h_row_off[k];
+        ++k;
+      }
+      row_ptr[g + 1] = row_ptr[g] + n;
+    }
+  }
+  if (cols && nnz) std::memcpy(cols, res->h_cols.data(), nnz * 4);
+  if (counts && nnz) std::memcpy(counts, res->h_cnt.data(), nnz * 4);
+  return RTHX_OK;
+}
+
+RTHX_EXPORT int rthx_result_copy_rays(const rthx_result* cres, double* origins_xy, double* endpoints_xy,
+                                      int64_t* emitter, int64_t cap, int64_t* n_out) {
+  if (!cres) return fail(RTHX_EINVAL, "null result");
+  if (!cres->valid) return fail(RTHX_ESTATE, "result holds no trace");
+  rthx_result* res = const_cast<rthx_result*>(cres);
+  const size_t n_rec = res->rec_g.size();
+  const size_t R = (size_t)res->R;
+  if (n_rec > 0 && !res->host_rec) {
+    HIP_TRY(hipSetDevice(res->device), "hipSetDevice");
+    res->h_ok.resize(n_rec * R);
+    res->h_orig.resize(n_rec * R * 2);
+    res->h_end.resize(n_rec * R * 2);
+    HIP_TRY(hipMemcpy(res->h_ok.data(), res->rec_ok.p, n_rec * R, hipMemcpyDeviceToHost), "hipMemcpy rec");
+    HIP_TRY(hipMemcpy(res->h_orig.data(), res->rec_orig.p, n_rec * R * 16, hipMemcpyDeviceToHost), "hipMemcpy rec");
+    HIP_TRY(hipMemcpy(res->h_end.data(), res->rec_end.p, n_rec * R * 16, hipMemcpyDeviceToHost), "hipMemcpy rec");
+    res->host_rec = true;
+  }
+  int64_t n = 0;
+  for (size_t i = 0; i < n_rec; ++i)
+    for (size_t r = 0; r < R; ++r) {
+      size_t k = i * R + r;
+      if (!res->h_ok[k]) continue;
+      if (n >= cap) break;
+      if (origins_xy) { origins_xy[2 * n] = res->h_orig[2 * k]; origins_xy[2 * n + 1] = res->h_orig[2 * k + 1]; }
+      if (endpoints_xy) { endpoints_xy[2 * n] = res->h_end[2 * k]; endpoints_xy[2 * n + 1] = res->h_end[2 * k + 1]; }
+      if (emitter) emitter[n] = res->rec_g[i];
+      ++n;
+    }
+  if (n_out) *n_out = n;
+  return RTHX_OK;
+}

@@ -1,0 +1,34 @@
+// rthx_kernels.h — launcher interface between the C ABI (rthx_api.cpp) and
+// the gfx950 kernels (rthx_kernels.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rthx_device.h"
+
+namespace rthx {
+
+constexpr int kTraceThreads = 256;               // 4 waves of 64 per emitter row
+constexpr size_t kMaxLdsBytes = 160 * 1024;      // gfx950 LDS per CU
+
+struct RecordParams {
+  int32_t n;            // recorded emitters in this call
+  const int64_t* ids;   // [n] global emitter ids (device)
+  uint8_t* ok;          // [n*R] 1 if the ray was tallied
+  double* orig;         // [n*R*2]
+  double* end;          // [n*R*2]
+};
+
+hipError_t launch_trace(const DevDomain& D, const TraceParams& P, bool uniform, bool pack16, int64_t n_emitters,
+                        int64_t n_rows, uint32_t* stage_cols, uint32_t* stage_cnt, int64_t row_cap,
+                        uint32_t* row_nnz, uint32_t* row_tallied, const RecordParams& rec, size_t lds_bytes,
+                        hipStream_t stream);
+
+hipError_t launch_scan(const uint32_t* row_nnz, const uint32_t* row_tallied, int64_t n_rows, int64_t R,
+                       int64_t* row_off, int64_t* totals, hipStream_t stream);
+
+hipError_t launch_pack(const uint32_t* stage_cols, const uint32_t* stage_cnt, int64_t row_cap, const int64_t* row_off,
+                       int64_t n_rows, uint32_t* cols, uint32_t* cnt, hipStream_t stream);
+
+}  // namespace rthx

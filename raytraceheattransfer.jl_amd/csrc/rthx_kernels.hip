@@ -1,0 +1,222 @@
+// rthx_kernels.hip — exchange-factor trace kernels for gfx950 (MI355X).
+//
+// trace_exchange_kernel: one workgroup per emitter row (computeExchangeFactorsBin's
+//   per-emitter loop, parallelRayTracing.jl:102-150).  The workgroup's 256 lanes
+//   trace the row's R rays, tally absorbers into an LDS histogram (uint16
+//   counters packed two per dword when R < 65536 — the Dict{Int,Int} row of
+//   the reference), then compact the histogram in ascending absorber order into
+//   a fixed-stride staging slot of min(N, R) entries (no global atomics, so the
+//   output is deterministic).
+// row_scan_kernel: exclusive scan of per-row nnz + lost-ray reductions.
+// csr_pack_kernel: copies every row's staging slot into the dense CSR arrays.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rthx_device.h"
+#include "rthx_kernels.h"
+
+namespace rthx {
+
+__device__ __forceinline__ uint32_t lane_id() {
+  return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+}
+
+template <bool UNIFORM, bool PACK16>
+__global__ __launch_bounds__(kTraceThreads) void trace_exchange_kernel(DevDomain D, TraceParams P, int64_t n_emitters,
+                                                                     uint32_t* __restrict__ stage_cols,
+                                                                     uint32_t* __restrict__ stage_cnt,
+                                                                     int64_t row_cap, uint32_t* __restrict__ row_nnz,
+                                                                     uint32_t* __restrict__ row_tallied,
+                                                                     RecordParams rec) {
+  extern __shared__ uint32_t hist[];
+  __shared__ uint32_t wave_sum[kTraceThreads / 64];
+  __shared__ uint32_t s_running;
+  __shared__ uint32_t s_tallied;
+
+  const int64_t slot = blockIdx.x;
+  const int64_t g = P.g_begin + slot * P.g_stride;
+  const int tid = threadIdx.x;
+  const int64_t n_words = PACK16 ? (n_emitters + 1) / 2 : n_emitters;
+
+  for (int64_t w = tid; w < n_words; w += kTraceThreads) hist[w] = 0u;
+  if (tid == 0) { s_running = 0u; s_tallied = 0u; }
+
+  // recorded emitter?  (RayRecorder ids, parallelRayTracing.jl:108)
+  int rec_slot = -1;
+  for (int i = 0; i < rec.n; ++i)
+    if (rec.ids[i] == g) { rec_slot = i; break; }
+  __syncthreads();
+
+  uint32_t tallied = 0;
+  for (int64_t r = tid; r < P.R; r += kTraceThreads) {
+    double ox, oy, px, py;
+    int64_t a = trace_one<UNIFORM>(D, P, g, r, ox, oy, px, py);
+    if (a >= 0) {
+      if (PACK16)
+        atomicAdd(&hist[a >> 1], 1u << ((uint32_t)(a & 1) << 4));
+      else
+        atomicAdd(&hist[a], 1u);
+      ++tallied;
+    }
+    if (rec_slot >= 0) {
+      size_t k = (size_t)rec_slot * (size_t)P.R + (size_t)r;
+      rec.ok[k] = a >= 0 ? 1 : 0;
+      rec.orig[2 * k] = ox; rec.orig[2 * k + 1] = oy;
+      rec.end[2 * k] = px; rec.end[2 * k + 1] = py;
+    }
+  }
+  // wave reduce the tallied count, one LDS atomic per wave
+  for (int off = 32; off > 0; off >>= 1) tallied += __shfl_xor(tallied, off);
+  if (lane_id() == 0) atomicAdd(&s_tallied, tallied);
+  __syncthreads();
+
+  // Compaction: ascending absorber order (the reference's sparse() sorts
+  // columns, parallelRayTracing.jl:154).
+  const uint32_t lane = lane_id();
+  const int wave = tid >> 6;
+  const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  uint32_t* out_c = stage_cols + slot * row_cap;
+  uint32_t* out_n = stage_cnt + slot * row_cap;
+  for (int64_t w0 = 0; w0 < n_words; w0 += kTraceThreads) {
+    int64_t w = w0 + tid;
+    uint32_t v = (w < n_words) ? hist[w] : 0u;
+    uint32_t lo = PACK16 ? (v & 0xFFFFu) : v;
+    uint32_t hi = PACK16 ? (v >> 16) : 0u;
+    uint64_t m_lo = __ballot(lo != 0u);
+    uint64_t m_hi = PACK16 ? __ballot(hi != 0u) : 0ull;
+    uint32_t pre = __popcll(m_lo & lt_mask) + __popcll(m_hi & lt_mask);
+    if (lane == 0) wave_sum[wave] = __popcll(m_lo) + __popcll(m_hi);
+    __syncthreads();
+    uint32_t base = s_running;
+    for (int i = 0; i < wave; ++i) base += wave_sum[i];
+    uint32_t pos = base + pre;
+    if (lo) { out_c[pos] = PACK16 ? (uint32_t)(2 * w) : (uint32_t)w; out_n[pos] = lo; ++pos; }
+    if (PACK16 && hi) { out_c[pos] = (uint32_t)(2 * w + 1); out_n[pos] = hi; }
+    __syncthreads();
+    if (tid == 0) {
+      uint32_t tot = 0;
+      for (int i = 0; i < kTraceThreads / 64; ++i) tot += wave_sum[i];
+      s_running += tot;
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    row_nnz[slot] = s_running;
+    row_tallied[slot] = s_tallied;
+  }
+}
+
+// Exclusive scan of row_nnz -> row_off[n_rows+1]; totals of lost rays.
+// One workgroup of 1024 lanes (rows <= a few 1e5).
+__global__ __launch_bounds__(1024) void row_scan_kernel(const uint32_t* __restrict__ row_nnz,
+                                                      const uint32_t* __restrict__ row_tallied, int64_t n_rows,
+                                                      int64_t R, int64_t* __restrict__ row_off,
+                                                      int64_t* __restrict__ totals) {
+  __shared__ int64_t part[1024];
+  __shared__ int64_t lost_sum[1024];
+  __shared__ int64_t lost_max[1024];
+  const int tid = threadIdx.x;
+  const int64_t chunk = (n_rows + 1023) / 1024;
+  const int64_t b = tid * chunk;
+  const int64_t e = (b + chunk < n_rows) ? b + chunk : n_rows;
+  int64_t s = 0, ls = 0, lm = 0;
+  for (int64_t i = b; i < e; ++i) {
+    s += row_nnz[i];
+    int64_t lost = R - (int64_t)row_tallied[i];
+    ls += lost;
+    lm = lost > lm ? lost : lm;
+  }
+  part[tid] = s;
+  lost_sum[tid] = ls;
+  lost_max[tid] = lm;
+  __syncthreads();
+  // Hillis-Steele inclusive scan over 1024 partials
+  for (int off = 1; off < 1024; off <<= 1) {
+    int64_t v = (tid >= off) ? part[tid - off] : 0;
+    int64_t a = (tid >= off) ? lost_sum[tid - off] : 0;
+    int64_t m = (tid >= off) ? lost_max[tid - off] : 0;
+    __syncthreads();
+    part[tid] += v;
+    lost_sum[tid] += a;
+    lost_max[tid] = lost_max[tid] > m ? lost_max[tid] : m;
+    __syncthreads();
+  }
+  int64_t run = (tid == 0) ? 0 : part[tid - 1];
+  for (int64_t i = b; i < e; ++i) {
+    row_off[i] = run;
+    run += row_nnz[i];
+  }
+  if (tid == 1023) {
+    row_off[n_rows] = part[1023];
+    totals[0] = part[1023];
+    totals[1] = lost_sum[1023];
+    totals[2] = lost_max[1023];
+  }
+}
+
+// Copy each row's staging slot to its CSR position (HBM streaming copy).
+__global__ __launch_bounds__(256) void csr_pack_kernel(const uint32_t* __restrict__ stage_cols,
+                                                      const uint32_t* __restrict__ stage_cnt, int64_t row_cap,
+                                                      const int64_t* __restrict__ row_off,
+                                                      uint32_t* __restrict__ cols, uint32_t* __restrict__ cnt) {
+  const int64_t row = blockIdx.x;
+  const int64_t b = row_off[row];
+  const int64_t n = row_off[row + 1] - b;
+  const uint32_t* sc = stage_cols + row * row_cap;
+  const uint32_t* sn = stage_cnt + row * row_cap;
+  for (int64_t i = threadIdx.x; i < n; i += 256) {
+    cols[b + i] = sc[i];
+    cnt[b + i] = sn[i];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------
+template <bool UNIFORM, bool PACK16>
+static hipError_t launch_trace_t(const DevDomain& D, const TraceParams& P, int64_t n_emitters, int64_t n_rows,
+                                 uint32_t* stage_cols, uint32_t* stage_cnt, int64_t row_cap, uint32_t* row_nnz,
+                                 uint32_t* row_tallied, const RecordParams& rec, size_t lds_bytes,
+                                 hipStream_t stream) {
+  auto kern = trace_exchange_kernel<UNIFORM, PACK16>;
+  if (lds_bytes > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds_bytes);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(kern, dim3((unsigned)n_rows), dim3(kTraceThreads), lds_bytes, stream, D, P, n_emitters,
+                     stage_cols, stage_cnt, row_cap, row_nnz, row_tallied, rec);
+  return hipGetLastError();
+}
+
+hipError_t launch_trace(const DevDomain& D, const TraceParams& P, bool uniform, bool pack16, int64_t n_emitters,
+                        int64_t n_rows, uint32_t* stage_cols, uint32_t* stage_cnt, int64_t row_cap,
+                        uint32_t* row_nnz, uint32_t* row_tallied, const RecordParams& rec, size_t lds_bytes,
+                        hipStream_t stream) {
+  if (uniform) {
+    return pack16 ? launch_trace_t<true, true>(D, P, n_emitters, n_rows, stage_cols, stage_cnt, row_cap, row_nnz,
+                                               row_tallied, rec, lds_bytes, stream)
+                  : launch_trace_t<true, false>(D, P, n_emitters, n_rows, stage_cols, stage_cnt, row_cap, row_nnz,
+                                                row_tallied, rec, lds_bytes, stream);
+  }
+  return pack16 ? launch_trace_t<false, true>(D, P, n_emitters, n_rows, stage_cols, stage_cnt, row_cap, row_nnz,
+                                              row_tallied, rec, lds_bytes, stream)
+                : launch_trace_t<false, false>(D, P, n_emitters, n_rows, stage_cols, stage_cnt, row_cap, row_nnz,
+                                               row_tallied, rec, lds_bytes, stream);
+}
+
+hipError_t launch_scan(const uint32_t* row_nnz, const uint32_t* row_tallied, int64_t n_rows, int64_t R,
+                       int64_t* row_off, int64_t* totals, hipStream_t stream) {
+  hipLaunchKernelGGL(row_scan_kernel, dim3(1), dim3(1024), 0, stream, row_nnz, row_tallied, n_rows, R, row_off,
+                     totals);
+  return hipGetLastError();
+}
+
+hipError_t launch_pack(const uint32_t* stage_cols, const uint32_t* stage_cnt, int64_t row_cap, const int64_t* row_off,
+                       int64_t n_rows, uint32_t* cols, uint32_t* cnt, hipStream_t stream) {
+  hipLaunchKernelGGL(csr_pack_kernel, dim3((unsigned)n_rows), dim3(256), 0, stream, stage_cols, stage_cnt, row_cap,
+                     row_off, cols, cnt);
+  return hipGetLastError();
+}
+
+}  // namespace rthx

@@ -1,0 +1,216 @@
+"""Loader for ``librthx.so`` (HIP kernels + C ABI) and thin handle classes.
+
+The product path has no CPU fallback: if the library is missing or no MI355X
+is visible, every call raises ``RthxError`` (loudly), it never substitutes
+another implementation.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Optional, Sequence
+
+import numpy as np
+
+from . import abi
+
+_PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_PKG_DIR), "csrc", "_build", "librthx.so")
+
+_lib: Optional[C.CDLL] = None
+
+
+class RthxError(RuntimeError):
+    pass
+
+
+def _prefer_single_hip_runtime() -> None:
+    """If PyTorch is importable, import it before librthx so that both share
+    torch's already-loaded libamdhip64.so.7 (same SONAME) instead of mapping a
+    second HIP runtime into the process."""
+    try:
+        import torch  # noqa: F401
+    except Exception:  # pragma: no cover - torch absent
+        pass
+
+
+def load(path: Optional[str] = None) -> C.CDLL:
+    """Load librthx.so (raises RthxError when it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    p = path or os.environ.get("RTHX_LIB", LIB_PATH)
+    if not os.path.exists(p):
+        raise RthxError(f"librthx.so not found at {p}: build it with `python __graft_entry__.py build` "
+                        "(the HIP extension is required; there is no CPU fallback)")
+    _prefer_single_hip_runtime()
+    lib = C.CDLL(p, mode=C.RTLD_GLOBAL)
+    lib.rthx_abi_version.restype = C.c_int
+    lib.rthx_last_error.restype = C.c_char_p
+    lib.rthx_device_count.argtypes = [C.POINTER(C.c_int32)]
+    lib.rthx_device_synchronize.argtypes = [C.c_int32]
+    lib.rthx_domain_create.argtypes = [C.POINTER(abi.DomainDesc), C.c_int32, C.POINTER(C.c_void_p)]
+    lib.rthx_domain_destroy.argtypes = [C.c_void_p]
+    lib.rthx_domain_destroy.restype = None
+    lib.rthx_result_create.argtypes = [C.POINTER(C.c_void_p)]
+    lib.rthx_result_destroy.argtypes = [C.c_void_p]
+    lib.rthx_result_destroy.restype = None
+    lib.rthx_trace_exchange.argtypes = [C.c_void_p, C.POINTER(abi.TraceArgs), C.c_void_p]
+    lib.rthx_result_get_info.argtypes = [C.c_void_p, C.POINTER(abi.ResultInfo)]
+    lib.rthx_result_copy_csr.argtypes = [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int32),
+                                         C.POINTER(C.c_uint32)]
+    lib.rthx_result_copy_rays.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double),
+                                          C.POINTER(C.c_int64), C.c_int64, C.POINTER(C.c_int64)]
+    if lib.rthx_abi_version() != abi.RTHX_ABI_VERSION:
+        raise RthxError("librthx ABI version mismatch")
+    _lib = lib
+    return lib
+
+
+def check(rc: int) -> None:
+    if rc != 0:
+        msg = _lib.rthx_last_error().decode() if _lib is not None else "?"
+        raise RthxError(f"rthx error {rc}: {msg}")
+
+
+def device_count() -> int:
+    lib = load()
+    n = C.c_int32(0)
+    check(lib.rthx_device_count(C.byref(n)))
+    return n.value
+
+
+def synchronize(device: int = 0) -> None:
+    check(load().rthx_device_synchronize(device))
+
+
+def make_args(bin0: int, rays_per_emitter: int, nudge: float, seed: int, emitter_begin: int,
+              emitter_end: int, emitter_stride: int = 1, device: int = 0, flags: int = 0,
+              record_ids: Optional[Sequence[int]] = None, record_bin0: int = 0):
+    """Build an ``rthx_trace_args`` (0-based bin / ids).  Returns (args, keepalive)."""
+    a = abi.TraceArgs()
+    a.bin = bin0
+    a.flags = flags
+    a.rays_per_emitter = rays_per_emitter
+    a.nudge = nudge
+    a.seed = seed
+    a.emitter_begin = emitter_begin
+    a.emitter_end = emitter_end
+    a.emitter_stride = emitter_stride
+    a.device = device
+    keep = None
+    if record_ids:
+        keep = np.ascontiguousarray(np.asarray(record_ids, dtype=np.int64))
+        a.n_record = len(keep)
+        a.record_ids = abi.ptr(keep, C.c_int64)
+        a.record_bin = record_bin0
+    else:
+        a.n_record = 0
+        a.record_ids = C.cast(None, C.POINTER(C.c_int64))
+        a.record_bin = 0
+    return a, keep
+
+
+class DeviceDomain:
+    """An uploaded domain (``rthx_domain*``) on one device."""
+
+    def __init__(self, flat, device: int = 0):
+        self._lib = load()
+        self.device = device
+        self.n_emitters = flat.n_emitters
+        h = C.c_void_p()
+        check(self._lib.rthx_domain_create(C.byref(flat.desc), device, C.byref(h)))
+        self.handle = h
+
+    def close(self) -> None:
+        if getattr(self, "handle", None):
+            self._lib.rthx_domain_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class DeviceResult:
+    """A reusable ``rthx_result*``."""
+
+    def __init__(self):
+        self._lib = load()
+        h = C.c_void_p()
+        check(self._lib.rthx_result_create(C.byref(h)))
+        self.handle = h
+
+    def trace(self, dom: DeviceDomain, args) -> "DeviceResult":
+        check(self._lib.rthx_trace_exchange(dom.handle, C.byref(args), self.handle))
+        return self
+
+    def info(self) -> dict:
+        inf = abi.ResultInfo()
+        check(self._lib.rthx_result_get_info(self.handle, C.byref(inf)))
+        return inf.as_dict()
+
+    def csr(self):
+        inf = self.info()
+        n = inf["n_emitters"]
+        nnz = inf["nnz"]
+        row_ptr = np.zeros(n + 1, dtype=np.int64)
+        cols = np.zeros(max(nnz, 1), dtype=np.int32)
+        counts = np.zeros(max(nnz, 1), dtype=np.uint32)
+        check(self._lib.rthx_result_copy_csr(self.handle, abi.ptr(row_ptr, C.c_int64),
+                                             abi.ptr(cols, C.c_int32), abi.ptr(counts, C.c_uint32)))
+        return row_ptr, cols[:nnz], counts[:nnz]
+
+    def rays(self):
+        inf = self.info()
+        cap = inf["n_recorded"]
+        o = np.zeros((max(cap, 1), 2))
+        e = np.zeros((max(cap, 1), 2))
+        g = np.zeros(max(cap, 1), dtype=np.int64)
+        n = C.c_int64(0)
+        check(self._lib.rthx_result_copy_rays(self.handle, abi.ptr(o, C.c_double), abi.ptr(e, C.c_double),
+                                              abi.ptr(g, C.c_int64), cap, C.byref(n)))
+        k = n.value
+        return o[:k], e[:k], g[:k]
+
+    def close(self) -> None:
+        if getattr(self, "handle", None):
+            self._lib.rthx_result_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class HipBackend:
+    """The product backend: trace one bin on an MI355X through librthx."""
+
+    name = "hip"
+
+    def trace(self, dom, bin0: int, rays_per_emitter: int, nudge: float, seed: int, device: int,
+              faithful: bool, record_ids=None, record_bin0: int = 0, emitter_begin: int = 0,
+              emitter_end: Optional[int] = None, emitter_stride: int = 1):
+        flat = dom.flat()
+        dd = dom._device_domains.get(device)
+        if dd is None:
+            dd = DeviceDomain(flat, device)
+            dom._device_domains[device] = dd
+        end = flat.n_emitters if emitter_end is None else emitter_end
+        flags = abi.RTHX_FLAG_FAITHFUL_SAMPLING if faithful else 0
+        args, keep = make_args(bin0, rays_per_emitter, nudge, seed, emitter_begin, end, emitter_stride,
+                               device, flags, record_ids, record_bin0)
+        res = DeviceResult()
+        try:
+            res.trace(dd, args)
+            row_ptr, cols, counts = res.csr()
+            info = res.info()
+            rays = res.rays() if info["n_recorded"] > 0 else None
+        finally:
+            res.close()
+        del keep
+        return row_ptr, cols, counts, info, rays

@@ -1,0 +1,126 @@
+"""ctypes mirror of ``include/rthx.h`` (the C ABI of the exchange tracer).
+
+Only data layouts live here; loading the HIP library is ``rthx._lib``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+RTHX_ABI_VERSION = 1
+
+RTHX_OK = 0
+RTHX_EINVAL = -1
+RTHX_ENOMEM = -2
+RTHX_EDEVICE = -3
+RTHX_ERANGE = -4
+RTHX_ESTATE = -5
+
+RTHX_FLAG_FAITHFUL_SAMPLING = 0x1
+RTHX_FLAG_DEVICE_ONLY = 0x2
+
+_p_i32 = C.POINTER(C.c_int32)
+_p_f64 = C.POINTER(C.c_double)
+_p_u8 = C.POINTER(C.c_uint8)
+_p_i64 = C.POINTER(C.c_int64)
+
+
+class GridDesc(C.Structure):
+    _fields_ = [
+        ("origin_x", C.c_double),
+        ("origin_y", C.c_double),
+        ("inv_cell_size", C.c_double),
+        ("nx", C.c_int32),
+        ("ny", C.c_int32),
+        ("cell_start", _p_i32),
+        ("cell_items", _p_i32),
+    ]
+
+
+class DomainDesc(C.Structure):
+    _fields_ = [
+        ("abi_version", C.c_int32),
+        ("n_coarse", C.c_int32),
+        ("n_fine", C.c_int32),
+        ("n_surfaces", C.c_int32),
+        ("n_bins", C.c_int32),
+        ("reserved0", C.c_int32),
+        ("coarse_nv", _p_i32),
+        ("coarse_xy", _p_f64),
+        ("coarse_normal", _p_f64),
+        ("coarse_solid", _p_u8),
+        ("coarse_bbox", _p_f64),
+        ("coarse_grid", GridDesc),
+        ("fine_offset", _p_i32),
+        ("fine_nv", _p_i32),
+        ("fine_xy", _p_f64),
+        ("fine_normal", _p_f64),
+        ("fine_mid", _p_f64),
+        ("fine_volume", _p_f64),
+        ("fine_bbox", _p_f64),
+        ("fine_surface", _p_i32),
+        ("fine_grid", C.POINTER(GridDesc)),
+        ("beta", _p_f64),
+        ("uniform_beta", _p_f64),
+    ]
+
+
+class TraceArgs(C.Structure):
+    _fields_ = [
+        ("bin", C.c_int32),
+        ("flags", C.c_uint32),
+        ("rays_per_emitter", C.c_int64),
+        ("nudge", C.c_double),
+        ("seed", C.c_uint64),
+        ("emitter_begin", C.c_int64),
+        ("emitter_end", C.c_int64),
+        ("emitter_stride", C.c_int64),
+        ("device", C.c_int32),
+        ("n_record", C.c_int32),
+        ("record_ids", _p_i64),
+        ("record_bin", C.c_int32),
+        ("reserved0", C.c_int32),
+    ]
+
+
+class ResultInfo(C.Structure):
+    _fields_ = [
+        ("n_emitters", C.c_int64),
+        ("rows_traced", C.c_int64),
+        ("rays_per_emitter", C.c_int64),
+        ("rays_traced", C.c_int64),
+        ("nnz", C.c_int64),
+        ("lost_total", C.c_int64),
+        ("lost_max_row", C.c_int64),
+        ("n_recorded", C.c_int64),
+        ("trace_ms", C.c_double),
+        ("pack_ms", C.c_double),
+        ("total_ms", C.c_double),
+    ]
+
+    def as_dict(self) -> dict:
+        return {name: getattr(self, name) for name, _ in self._fields_}
+
+
+# Every symbol include/rthx.h declares (checked by tests/test_abi_symbols.py).
+EXPORTED_SYMBOLS = (
+    "rthx_abi_version",
+    "rthx_last_error",
+    "rthx_device_count",
+    "rthx_device_synchronize",
+    "rthx_domain_create",
+    "rthx_domain_destroy",
+    "rthx_result_create",
+    "rthx_result_destroy",
+    "rthx_trace_exchange",
+    "rthx_result_get_info",
+    "rthx_result_copy_csr",
+    "rthx_result_copy_rays",
+)
+
+
+def ptr(arr, ctype):
+    """Pointer to the data of a C-contiguous numpy array (kept alive by caller)."""
+    if arr is None:
+        return C.cast(None, C.POINTER(ctype))
+    assert arr.flags["C_CONTIGUOUS"], "array must be C-contiguous"
+    return arr.ctypes.data_as(C.POINTER(ctype))

@@ -1,0 +1,168 @@
+"""Host logic of ``method=:exchange`` above the C-ABI seam.
+
+Mirrors src/RayTracing/RayTracing2D/ExchangeFactors2D/ of the reference:
+
+* ``exchange_ray_tracing``      — exchangeRayTracing!, exchangeRayTracing.jl:1-74
+  (tracing + surfaces_only truncation; the smoothing half stays with the
+  reference's host ``smooth_F``, out of scope here);
+* ``parallel_ray_tracing``      — parallelRayTracing, parallelRayTracing.jl:1-62;
+* ``compute_exchange_factors_bin`` — computeExchangeFactorsBin, :64-159 — the
+  seam: its body is one ``rthx_trace_exchange`` call on the MI355X;
+* ``row_normalize``             — row_normalize!, :161-169;
+* ``group_uniform_bins``        — :171-191;
+* ``RayRecorder`` / ``collect_rays`` — :194-200 (ids and bin are 1-based, like
+  the reference).
+"""
+from __future__ import annotations
+
+import math
+from typing import List, Optional, Sequence
+
+import numpy as np
+import scipy.sparse as sp
+
+
+class RayRecorder:
+    """RayRecorder(ids; bin=1) (DomainStructs.jl:176-181, parallelRayTracing.jl:194-197)."""
+
+    def __init__(self, ids: Sequence[int], bin: int = 1):
+        self.ids = [int(i) for i in ids]
+        self.bin = int(bin)
+        self.origins: List[np.ndarray] = []
+        self.endpoints: List[np.ndarray] = []
+        self.emitters: List[np.ndarray] = []
+
+
+def collect_rays(rec: RayRecorder):
+    """collect_rays (parallelRayTracing.jl:199-200): (origins, endpoints) as [n,2] arrays."""
+    if not rec.origins:
+        return np.zeros((0, 2)), np.zeros((0, 2))
+    return np.concatenate(rec.origins), np.concatenate(rec.endpoints)
+
+
+def _isapprox(a: float, b: float, atol: float, rtol: float) -> bool:
+    return abs(a - b) <= max(atol, rtol * max(abs(a), abs(b)))
+
+
+def group_uniform_bins(uniform_across_bin: Sequence[float], atol: float = 1e-8, rtol: float = 1e-8):
+    """group_uniform_bins, parallelRayTracing.jl:171-191 (1-based bin numbers)."""
+    groups: List[List[int]] = []
+    reps: List[float] = []
+    nonuniform: List[int] = []
+    for i, v in enumerate(uniform_across_bin, start=1):
+        if v < -0.1:
+            nonuniform.append(i)
+            continue
+        idx = next((k for k, r in enumerate(reps) if _isapprox(r, v, atol, rtol)), None)
+        if idx is None:
+            reps.append(v)
+            groups.append([i])
+        else:
+            groups[idx].append(i)
+    return groups, reps, nonuniform
+
+
+def row_normalize(F: sp.csr_matrix, rays_per_emitter: int, verbose: bool = True) -> sp.csr_matrix:
+    """row_normalize!, parallelRayTracing.jl:161-169: divide each row by its sum.
+
+    Lost rays are thereby redistributed over the row's absorbers; the largest
+    loss is reported as in the reference.
+    """
+    rs = np.asarray(F.sum(axis=1)).ravel()
+    if verbose:
+        loss = int(round(rays_per_emitter * float(np.max(np.abs(1.0 - rs))))) if rs.size else 0
+        print(f"Maximum ray tracing ray loss per emitter: {loss}/{rays_per_emitter}")
+    row_of = np.repeat(np.arange(F.shape[0]), np.diff(F.indptr))
+    with np.errstate(divide="ignore", invalid="ignore"):
+        F.data /= rs[row_of]
+    return F
+
+
+def counts_to_F(row_ptr, cols, counts, n: int, rays_per_emitter: int) -> sp.csr_matrix:
+    """V = c / R (parallelRayTracing.jl:145) assembled as an N x N CSR matrix."""
+    inv = 1.0 / rays_per_emitter if rays_per_emitter > 0 else math.inf
+    data = counts.astype(np.float64) * inv
+    return sp.csr_matrix((data, cols.astype(np.int64), row_ptr.astype(np.int64)), shape=(n, n))
+
+
+def _default_backend():
+    from ._lib import HipBackend
+
+    return HipBackend()
+
+
+def compute_exchange_factors_bin(dom, rays_per_emitter: int, nudge: float, spectral_bin: int,
+                                 verbose: bool, rec: Optional[RayRecorder], seed: int = 1,
+                                 device: int = 0, faithful: bool = False, backend=None):
+    """computeExchangeFactorsBin, parallelRayTracing.jl:64-159 (``spectral_bin`` 1-based).
+
+    The whole per-emitter loop (:69-152) is one device call; the host keeps
+    the sparse assembly and row normalisation (:154-158).
+    """
+    backend = backend or _default_backend()
+    rec_ids = None
+    rec_bin0 = 0
+    if rec is not None and rec.bin == spectral_bin:
+        rec_ids = [i - 1 for i in rec.ids]
+        rec_bin0 = rec.bin - 1
+    row_ptr, cols, counts, info, rays = backend.trace(
+        dom, spectral_bin - 1, rays_per_emitter, nudge, seed, device, faithful,
+        record_ids=rec_ids, record_bin0=rec_bin0)
+    info = dict(info)
+    info["bin"] = spectral_bin
+    info["backend"] = getattr(backend, "name", type(backend).__name__)
+    dom.last_trace_info.append(info)
+    if verbose:
+        print(f"  bin {spectral_bin}: {info['rays_traced']} rays, nnz {info['nnz']}, "
+              f"trace {info['trace_ms']:.3f} ms")
+    if rec is not None and rays is not None:
+        o, e, _g = rays
+        rec.origins.append(o)
+        rec.endpoints.append(e)
+        rec.emitters.append(_g + 1)
+    F = counts_to_F(row_ptr, cols, counts, dom.num_emitters, rays_per_emitter)
+    return row_normalize(F, rays_per_emitter, verbose=verbose)
+
+
+def parallel_ray_tracing(dom, rays_total: int, nudge: float, verbose: bool, rec=None, seed: int = 1,
+                         device: int = 0, faithful: bool = False, backend=None):
+    """parallelRayTracing, parallelRayTracing.jl:1-62."""
+    num_emitters = dom.num_emitters
+    rays_per_emitter = rays_total // num_emitters
+    n_bins = dom.n_spectral_bins
+    dom.last_trace_info = []
+    kw = dict(seed=seed, device=device, faithful=faithful, backend=backend)
+    if dom.spectral_mode == "spectral_variable":
+        F_vec: List[Optional[sp.csr_matrix]] = [None] * n_bins
+        groups, _reps, nonuniform = group_uniform_bins(dom.uniform_across_bin)
+        for b in nonuniform:
+            if verbose:
+                print(f"Computing F matrix for nonuniform spectral bin {b}/{n_bins}")
+            F_vec[b - 1] = compute_exchange_factors_bin(dom, rays_per_emitter, nudge, b, verbose, rec, **kw)
+        for grp in groups:
+            rep = grp[0]
+            if verbose:
+                print(f"Computing F matrix for uniform spectral bin {rep}/{n_bins}")
+            Fb = compute_exchange_factors_bin(dom, rays_per_emitter, nudge, rep, verbose, rec, **kw)
+            for j in grp:
+                F_vec[j - 1] = Fb
+        return F_vec, rays_per_emitter
+    F = compute_exchange_factors_bin(dom, rays_per_emitter, nudge, 1, verbose, rec, **kw)
+    return F, rays_per_emitter
+
+
+def exchange_ray_tracing(dom, rays_tot: int, nudge: float, verbose: bool, rec=None, seed: int = 1,
+                         device: int = 0, faithful: bool = False, backend=None):
+    """exchangeRayTracing!, exchangeRayTracing.jl:1-11 and :73 (tracing half)."""
+    F_raw, rpe = parallel_ray_tracing(dom, rays_tot, nudge, verbose, rec, seed=seed, device=device,
+                                      faithful=faithful, backend=backend)
+    ns = dom.num_surfaces
+    if dom.surfaces_only:
+        if isinstance(F_raw, list):
+            seen = {}
+            F_raw = [seen.setdefault(id(F), F[:ns, :ns].tocsr()) for F in F_raw]
+        else:
+            F_raw = F_raw[:ns, :ns].tocsr()
+    dom.F_raw = F_raw
+    dom.rays_per_emitter = rpe
+    return F_raw

@@ -1,0 +1,169 @@
+"""Test helpers: reference test geometries and a numpy restatement of the grey
+GERT solve used to pin the tracer against the reference's own known answers.
+
+Test infrastructure only (the solver is the reference's host code, which stays
+on the host and out of this package's scope: SURVEY.md §2 row 8).
+"""
+from __future__ import annotations
+
+import json
+import math
+import os
+import sys
+
+import numpy as np
+import scipy.sparse as sp
+import scipy.sparse.linalg as spla
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "raytraceheattransfer.jl_amd")
+for p in (PKG, ROOT):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+from rthx import PolyVolume2D, RayTracingDomain2D  # noqa: E402
+
+STEFAN_BOLTZMANN = 5.670374419e-8  # src/RayTraceHeatTransfer.jl:20
+NUDGE = 10_000 * np.finfo(np.float64).eps  # multiDispatchRayTrace2D.jl:10
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def golden(name: str):
+    with open(os.path.join(GOLDEN, name)) as fh:
+        return json.load(fh)
+
+
+def square_face(kappa=1.0, sigma_s=0.0, rotation=0.0, T_walls=(1000.0, 0.0, 0.0, 0.0), epsilon=1.0,
+                n_bins=1):
+    """createSquareDomain2D's face (test/test_2d_grey.jl:41-92)."""
+    base = [(0.0, 0.0), (1.0, 0.0), (1.0, 1.0), (0.0, 1.0)]
+    if rotation != 0.0:
+        c, s = math.cos(rotation), math.sin(rotation)
+        verts = [((x - 0.5) * c - (y - 0.5) * s + 0.5, (x - 0.5) * s + (y - 0.5) * c + 0.5) for x, y in base]
+    else:
+        verts = base
+    face = PolyVolume2D(verts, [True] * 4, n_bins, kappa, sigma_s)
+    face.T_in_w = list(T_walls)
+    face.epsilon = [epsilon] * 4
+    face.T_in_g = -1.0
+    face.q_in_g = 0.0
+    return face
+
+
+def square_domain(ndim=11, **kw) -> RayTracingDomain2D:
+    return RayTracingDomain2D([square_face(**kw)], [(ndim, ndim)])
+
+
+def wedge_domain(n_wedges=16, ndim=2, kappa=1.0, T_half=(1000.0, 0.0)):
+    """Circle of triangle wedges around the origin (test/test_triangle_mesh.jl:1-46).
+
+    Outer walls solid, spokes open; the first half of the wedges' outer walls
+    at T_half[0], the rest at T_half[1].
+    """
+    faces = []
+    for k in range(n_wedges):
+        a0 = 2 * math.pi * k / n_wedges
+        a1 = 2 * math.pi * (k + 1) / n_wedges
+        verts = [(0.0, 0.0), (math.cos(a0), math.sin(a0)), (math.cos(a1), math.sin(a1))]
+        f = PolyVolume2D(verts, [False, True, False], 1, kappa, 0.0)
+        T = T_half[0] if k < n_wedges // 2 else T_half[1]
+        f.T_in_w = [0.0, T, 0.0]
+        f.epsilon = [1.0, 1.0, 1.0]
+        f.T_in_g = -1.0
+        f.q_in_g = 0.0
+        faces.append(f)
+    return RayTracingDomain2D(faces, [(ndim, ndim)] * n_wedges)
+
+
+def element_arrays(dom):
+    """Per-element (global order) properties as populateWorkspace! gathers them
+    (src/HeatTransfer/equilibrium/WorkspaceStructs.jl:68-118), bin 1."""
+    ns, nv = dom.num_surfaces, dom.num_volumes
+    area = np.zeros(ns); eps = np.zeros(ns); Tw = np.zeros(ns); qw = np.zeros(ns)
+    vol = np.zeros(nv); kap = np.zeros(nv); omg = np.zeros(nv); Tg = np.zeros(nv); qg = np.zeros(nv)
+    for (c, f, w), s in dom.surface_mapping.items():
+        face = dom.fine_mesh[c - 1][f - 1]
+        e = face.epsilon[w - 1]
+        area[s - 1] = face.area[w - 1]
+        eps[s - 1] = float(np.atleast_1d(e)[0])
+        Tw[s - 1] = face.T_in_w[w - 1]
+        qw[s - 1] = face.q_in_w[w - 1]
+    for (c, f), v in dom.volume_mapping.items():
+        face = dom.fine_mesh[c - 1][f - 1]
+        k = float(np.atleast_1d(face.kappa_g)[0]); s_ = float(np.atleast_1d(face.sigma_s_g)[0])
+        vol[v - 1] = face.volume
+        kap[v - 1] = k
+        omg[v - 1] = s_ / (k + s_) if k + s_ > 0 else 0.0
+        Tg[v - 1] = face.T_in_g
+        qg[v - 1] = face.q_in_g
+    return dict(area=area, eps=eps, Tw=Tw, qw=qw, vol=vol, kappa=kap, omega=omg, Tg=Tg, qg=qg)
+
+
+def solve_grey(dom, F):
+    """equilibriumGrey2D!, src/HeatTransfer/equilibrium/equilibriumGrey2D.jl:80-211
+    (dense/sparse direct solve of (I - diag(coeff) F^T) j = h).  Returns
+    (T_surfaces, T_volumes, energy_error)."""
+    a = element_arrays(dom)
+    ns = dom.num_surfaces
+    nv = 0 if dom.surfaces_only else dom.num_volumes
+    n = ns + nv
+    F = sp.csr_matrix(F)[:n, :n]
+    q_known = np.concatenate([(a["Tw"] < 0).astype(int), (a["Tg"][:nv] < 0).astype(int)])
+    E = np.zeros(n); Q = np.zeros(n)
+    for i in range(ns):
+        if q_known[i] == 0:
+            E[i] = a["eps"][i] * STEFAN_BOLTZMANN * a["area"][i] * a["Tw"][i] ** 4
+        else:
+            Q[i] = a["qw"][i]
+    for v in range(nv):
+        i = ns + v
+        if q_known[i] == 0:
+            E[i] = 4 * a["kappa"][v] * STEFAN_BOLTZMANN * a["vol"][v] * a["Tg"][v] ** 4
+        else:
+            Q[i] = a["qg"][v]
+    b = np.zeros(n)
+    if np.any(a["omega"][:nv] > 1e-6) or np.sum(a["eps"]) < n:
+        b[:ns] = 1.0 - a["eps"]
+        b[ns:] = a["omega"][:nv]
+    h = np.where(q_known == 1, Q, E)
+    coeff = np.where(q_known == 1, 1.0, b)
+    M = sp.identity(n, format="csr") - sp.diags(coeff) @ F.T.tocsr()
+    j = spla.spsolve(M.tocsc(), h)
+    g = F.T @ j
+    r = b * g
+    absorbed = (1.0 - b) * g
+    T = np.zeros(n)
+    for i in range(ns):
+        e = max(j[i] - r[i], 0.0)
+        T[i] = (e / (a["eps"][i] * STEFAN_BOLTZMANN * a["area"][i])) ** 0.25 if a["eps"][i] > 0 else 0.0
+    for v in range(nv):
+        i = ns + v
+        e = max(j[i] - r[i], 0.0)
+        if a["kappa"][v] > 0 and a["vol"][v] > 0:
+            T[i] = (e / (4 * a["kappa"][v] * a["vol"][v] * STEFAN_BOLTZMANN)) ** 0.25
+    energy_error = float(np.sum(j - r - absorbed))
+    return T[:ns], T[ns:], energy_error
+
+
+def centerline_source_function(dom, ndim, T_hot=1000.0):
+    """extractCenterlineTemperatures + dimensionlessSourceFunction (test/test_2d_grey.jl:94-118)."""
+    _, Tg, _ = solve_grey(dom, dom.F_raw)
+    grid = Tg.reshape(ndim, ndim)  # row m (y) major, n (x) fastest
+    col = (ndim + 1) // 2 - 1
+    return (grid[:, col] / T_hot) ** 4
+
+
+def line_interpolation(xd, yd, x):
+    """lineInterpolation (test/test_2d_grey.jl:124-162), constant extrapolation."""
+    return np.interp(x, xd, yd)
+
+
+def reciprocity_weights(dom, bin0=0):
+    """w = [wall length; 4 beta V] (smoothExchangeFactors.jl:320-341, get_w)."""
+    flat = dom.flat()
+    ns = dom.num_surfaces
+    w = np.zeros(dom.num_emitters)
+    w[:ns] = dom.surface_areas
+    beta = flat.beta.reshape(flat.n_bins, flat.n_fine)[bin0]
+    w[ns:] = 4.0 * beta * flat.fine_volume
+    return w
