@@ -1,0 +1,244 @@
+"""Benchmark: exchange-factor trace throughput (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1]): 1x1 m square, 101x101 fine cells, grey
+kappa = 1, sigma_s = 0, all walls solid -> N = 404 + 10201 = 10605 emitters,
+1e8 rays per GPU (R = div(rays, N) rays per emitter).  One "step" is one pass
+of the hot path -- computeExchangeFactorsBin's body, i.e. one
+rthx_trace_exchange call: trace kernel + row scan + CSR pack on the device,
+inputs resident in HBM, output left on the device (the PCIe copy of the CSR
+is reported separately, never as `value`).
+
+Multi-GPU (one process per GPU, launched by torch.distributed.run): emitter
+rows are independent, so rank k traces rows g = k, k+W, k+2W, ... of the same
+enclosure with W x 1e8 rays in total (weak scaling: 1e8 rays per GPU).  There
+is no data-path collective; a gloo barrier brackets the timed region and the
+elapsed time is max-reduced over ranks.
+
+Prints one JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "raytraceheattransfer.jl_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+METRIC = "Mrays/sec (exchange-factor trace), 101×101 grey κ=1 enclosure, 1/2/4/8 GPUs"
+RAYS_PER_GPU = 100_000_000
+NDIM = 101
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md)
+FP64_VECTOR_PEAK_TFLOPS = 78.6  # MI355X fp64 vector (AMD spec)
+TRACE_KERNEL = "trace_exchange_kernel"
+
+
+def build_domain(ndim=NDIM):
+    from rthx import PolyVolume2D, RayTracingDomain2D
+
+    face = PolyVolume2D([(0.0, 0.0), (1.0, 0.0), (1.0, 1.0), (0.0, 1.0)], [True] * 4, 1, 1.0, 0.0)
+    face.T_in_w = [1000.0, 0.0, 0.0, 0.0]
+    face.epsilon = [1.0] * 4
+    face.T_in_g = -1.0
+    return RayTracingDomain2D([face], [(ndim, ndim)])
+
+
+def cpu_baseline(dom, R, nudge, seed, budget_s=12.0, threads=16):
+    """Time the CPU restatement (oracle, test infrastructure) on a bounded
+    strided sample of the same emitters with the same R."""
+    from oracle import oracle
+    from rthx import _lib
+
+    flat = dom.flat()
+    N = flat.n_emitters
+    threads = max(1, min(threads, os.cpu_count() or 1))
+    # probe on 1/256 of the rows, then size the sample to the budget
+    stride = 256
+    args, _k = _lib.make_args(0, R, nudge, seed, 0, N, stride)
+    t = time.perf_counter()
+    oracle.trace_exchange(flat, args, threads)
+    dt = time.perf_counter() - t
+    rows_probe = len(range(0, N, stride))
+    rate_rows = rows_probe / max(dt, 1e-6)
+    want_rows = max(rows_probe, int(rate_rows * budget_s))
+    stride = max(1, N // want_rows)
+    args, _k = _lib.make_args(0, R, nudge, seed, 0, N, stride)
+    t = time.perf_counter()
+    _rp, _c, _n, info, _ = oracle.trace_exchange(flat, args, threads)
+    dt = time.perf_counter() - t
+    rays = info["rays_traced"]
+    return {
+        "value": rays / dt / 1e6,
+        "unit": "Mrays/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": (f"CPU restatement of the reference algorithm (oracle/rthx_oracle.c: pthreads, static emitter "
+                   f"partition, per-thread hash tallies, COO->CSR) on every {stride}-th emitter row of the same "
+                   f"101x101 workload: {info['rows_traced']} rows x R={R} = {rays} rays in {dt:.2f} s, "
+                   f"{threads} threads"),
+    }
+
+
+def read_pmc_traffic():
+    """HBM bytes per trace launch from the committed rocprofv3 --pmc summary
+    (profiles/round1_pmc_trace.json, written by tools/pmc_summary.py), or None."""
+    p = os.path.join(ROOT, "profiles", "round1_pmc_trace.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        with open(p) as fh:
+            return json.load(fh).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--rays-per-gpu", type=int, default=RAYS_PER_GPU)
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", str(args.gpus)))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and "WORLD_SIZE" in os.environ:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # noqa: F811
+
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    from rthx import _lib
+    from rthx import abi
+
+    nudge = 10_000 * np.finfo(np.float64).eps
+    dom = build_domain()
+    flat = dom.flat()
+    N = flat.n_emitters
+    total_rays = args.rays_per_gpu * world
+    R = total_rays // N
+    device = local_rank
+    dd = _lib.DeviceDomain(flat, device)
+    targs, _keep = _lib.make_args(0, R, nudge, args.seed, rank, N, world, device=device,
+                                  flags=abi.RTHX_FLAG_DEVICE_ONLY)
+    res = _lib.DeviceResult()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        res.trace(dd, targs)
+    _lib.synchronize(device)
+    barrier()
+    _lib.synchronize(device)
+    t0 = time.perf_counter()
+    trace_ms = []
+    pack_ms = []
+    info = None
+    for _ in range(args.steps):
+        res.trace(dd, targs)
+        info = res.info()
+        trace_ms.append(info["trace_ms"])
+        pack_ms.append(info["pack_ms"])
+    _lib.synchronize(device)
+    elapsed = time.perf_counter() - t0
+    barrier()
+
+    rays_rank = info["rays_traced"]
+    nnz_rank = info["nnz"]
+    if dist is not None:
+        import torch
+
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        r = torch.tensor([rays_rank, nnz_rank], dtype=torch.int64)
+        dist.all_reduce(r, op=dist.ReduceOp.SUM)
+        rays_all, nnz_all = int(r[0]), int(r[1])
+    else:
+        rays_all, nnz_all = rays_rank, nnz_rank
+
+    # PCIe-inclusive end-to-end pass (CSR copied to the host), reported aside
+    e2e = None
+    if rank == 0:
+        args_h, _kh = _lib.make_args(0, R, nudge, args.seed, rank, N, world, device=device)
+        t = time.perf_counter()
+        res.trace(dd, args_h)
+        res.csr()
+        e2e_s = time.perf_counter() - t
+        e2e = rays_rank / e2e_s / 1e6
+
+    out = None
+    if rank == 0:
+        ms_per_step = elapsed / args.steps * 1e3
+        value = rays_all * args.steps / elapsed / 1e6
+        avg_trace_ms = float(np.mean(trace_ms))
+        # B_alg = 8 B/ray + 12 B x nnz/(N R)
+        b_alg = 8.0 * rays_rank + 12.0 * nnz_rank
+        achieved = b_alg / (avg_trace_ms * 1e-3) / 1e9
+        traffic = read_pmc_traffic()
+        out = {
+            "metric": METRIC,
+            "value": round(value, 3),
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic",
+            "config": {
+                "workload": (f"101x101 grey kappa=1 sigma_s=0 unit-square enclosure (BASELINE configs[1]); "
+                             f"{args.rays_per_gpu:.0e} rays per GPU, emitter rows sharded over {world} rank(s)"),
+                "n_emitters": N,
+                "rays_per_emitter": R,
+                "rays_per_step": rays_all,
+                "nnz_per_step": nnz_all,
+                "parallelism": f"emitter-rows x{world}",
+                "seed": args.seed,
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 3),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 6),
+                "traffic": traffic,
+                "kernel": TRACE_KERNEL,
+                "avg_kernel_ms": round(avg_trace_ms, 4),
+                "alg_bytes_per_launch": b_alg,
+                "note": "latency/fp64-VALU bound path; HBM fraction reported as mandated (DESIGN.md)",
+            },
+            "pack_ms": round(float(np.mean(pack_ms)), 4),
+            "e2e_with_d2h_mrays_s": round(e2e, 3) if e2e else None,
+        }
+        if world == 1 and not args.no_cpu:
+            out["cpu_baseline"] = cpu_baseline(dom, R, nudge, args.seed, args.cpu_budget)
+        else:
+            out["cpu_baseline"] = None
+        print(json.dumps(out), flush=True)
+    res.close()
+    dd.close()
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,96 @@
+"""Generate the committed golden fixtures (run in the build container only).
+
+reference_tables.json — known answers transcribed from the reference's own
+test files (parsed from /root/reference/test when it is present):
+  * Crosbie & Schrenker (1984) centreline table, test/test_2d_grey.jl:25-33,
+    tolerance test/test_2d_grey.jl:35 (rtol 0.05, norm-wise isapprox);
+  * wedge centre limit ((T^4 + 0)/2)^(1/4) and its 2 K tolerance,
+    test/test_triangle_mesh.jl:66-69;
+  * Stefan-Boltzmann constant, src/RayTraceHeatTransfer.jl:20;
+  * Philox-4x32-10 known-answer vectors (Random123 kat_vectors; the RNG
+    is this build's, the reference's rand() is unseeded);
+  * Hottel crossed-strings view factors of the unit square.
+
+oracle_c1_seed1.npz — CPU-restatement absorber counts for README Ex.1
+(11x11, kappa=1, 1e6 rays, seed 1): a regression fixture that the HIP path
+must reproduce exactly.
+"""
+import json
+import math
+import os
+import re
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(ROOT, "raytraceheattransfer.jl_amd"))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+
+def parse_julia_vector(text, name):
+    m = re.search(name + r"\s*=\s*\[(.*?)\]", text, re.S)
+    return [float(x) for x in m.group(1).replace("\n", " ").split(",") if x.strip()]
+
+
+def main():
+    ref = "/root/reference/test/test_2d_grey.jl"
+    tables = {}
+    if os.path.exists(ref):
+        txt = open(ref).read()
+        tables["crosbie_schrenker"] = {
+            "source": "test/test_2d_grey.jl:25-33",
+            "relative_tau_z": parse_julia_vector(txt, "RELATIVE_TAU_Z"),
+            "source_func_center": parse_julia_vector(txt, "SOURCE_FUNC_CENTER"),
+            "rtol": 0.05,
+            "rtol_source": "test/test_2d_grey.jl:35 (isapprox on vectors: norm-wise)",
+        }
+    else:  # keep the committed values
+        with open(os.path.join(HERE, "reference_tables.json")) as fh:
+            tables = json.load(fh)
+    tables["wedge_center_limit"] = {
+        "source": "test/test_triangle_mesh.jl:48-74",
+        "T_hot": 1000.0,
+        "T_limit": ((1000.0 ** 4 + 0.0) / 2) ** 0.25,
+        "tol_K": 2.0,
+        "n_wedges": 16,
+        "ndiv": 11,
+        "rays": 10_000_000,
+    }
+    tables["stefan_boltzmann"] = {"source": "src/RayTraceHeatTransfer.jl:20", "value": 5.670374419e-8}
+    tables["philox4x32_10_kat"] = {
+        "source": "Random123 kat_vectors (Salmon et al. SC'11)",
+        "vectors": [
+            {"ctr": [0, 0, 0, 0], "key": [0, 0], "out": [0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8]},
+            {"ctr": [0xFFFFFFFF] * 4, "key": [0xFFFFFFFF] * 2,
+             "out": [0x408F276D, 0x41C83B0E, 0xA20BC7C6, 0x6D5451FD]},
+            {"ctr": [0x243F6A88, 0x85A308D3, 0x13198A2E, 0x03707344], "key": [0xA4093822, 0x299F31D0],
+             "out": [0xD16CFE09, 0x94FDCCEB, 0x5001E420, 0x24126EA1]},
+        ],
+    }
+    tables["crossed_strings_unit_square"] = {
+        "source": "Hottel crossed strings (SURVEY.md §8(c))",
+        "adjacent": (2 - math.sqrt(2)) / 2,
+        "opposite": math.sqrt(2) - 1,
+    }
+    with open(os.path.join(HERE, "reference_tables.json"), "w") as fh:
+        json.dump(tables, fh, indent=1)
+
+    import helpers as H
+    from oracle import oracle
+    from rthx import _lib
+
+    dom = H.square_domain(11)
+    flat = dom.flat()
+    R = 1_000_000 // flat.n_emitters
+    args, _k = _lib.make_args(0, R, H.NUDGE, 1, 0, flat.n_emitters)
+    rp, cols, cnt, info, _ = oracle.trace_exchange(flat, args, 8)
+    np.savez_compressed(os.path.join(HERE, "oracle_c1_seed1.npz"), row_ptr=rp, cols=cols, counts=cnt,
+                        R=np.int64(R), seed=np.int64(1))
+    print("wrote fixtures; C1 nnz", info["nnz"])
+
+
+if __name__ == "__main__":
+    main()

@@ -167,3 +167,97 @@ def reciprocity_weights(dom, bin0=0):
     beta = flat.beta.reshape(flat.n_bins, flat.n_fine)[bin0]
     w[ns:] = 4.0 * beta * flat.fine_volume
     return w
+
+
+# --------------------------------------------------------------------------
+# statistical / analytic checks
+# --------------------------------------------------------------------------
+def counts_matrix(row_ptr, cols, counts, n):
+    return sp.csr_matrix((counts.astype(np.float64), cols.astype(np.int64), row_ptr.astype(np.int64)), shape=(n, n))
+
+
+def surface_segments(dom):
+    """[(a, b)] end points of every surface element, CCW along its polygon."""
+    segs = [None] * dom.num_surfaces
+    for (c, f, w), s in dom.surface_mapping.items():
+        face = dom.fine_mesh[c - 1][f - 1]
+        a = face.vertices[w - 1]
+        b = face.vertices[w % face.n]
+        segs[s - 1] = (np.array(a), np.array(b))
+    return segs
+
+
+def crossed_strings(seg1, seg2):
+    """View factor between two CCW boundary segments of a convex enclosure
+    (Hottel crossed strings); 0 for collinear segments."""
+    a1, b1 = seg1
+    a2, b2 = seg2
+    d1 = b1 - a1
+    cross = lambda u, v: u[0] * v[1] - u[1] * v[0]
+    if abs(cross(d1, a2 - a1)) < 1e-12 and abs(cross(d1, b2 - a1)) < 1e-12:
+        return 0.0
+    L = np.linalg.norm
+    crossed = L(a1 - a2) + L(b1 - b2)
+    uncrossed = L(a1 - b2) + L(b1 - a2)
+    return (crossed - uncrossed) / (2 * L(d1))
+
+
+def reciprocity_z(C, R, w, min_count=50):
+    """z-scores of w_i F_ij - w_j F_ji for pairs where both counts >= min_count
+    (F = C/R, binomial variances).  Reciprocity holds only if emission uses the
+    un-normalised in-plane directions of the reference."""
+    C = sp.csr_matrix(C, dtype=np.float64)
+    C.data[C.data < min_count] = 0
+    C.eliminate_zeros()
+    Ct = C.T.tocsr()
+    A = C.multiply(Ct.astype(bool)).tocsr()
+    B = Ct.multiply(C.astype(bool)).tocsr()
+    A.sort_indices()
+    B.sort_indices()
+    assert np.array_equal(A.indptr, B.indptr) and np.array_equal(A.indices, B.indices)
+    i = np.repeat(np.arange(A.shape[0]), np.diff(A.indptr))
+    j = A.indices
+    m = i < j
+    i, j, c, cji = i[m], j[m], A.data[m], B.data[m]
+    Fij, Fji = c / R, cji / R
+    a, b = w[i] * Fij, w[j] * Fji
+    var = w[i] ** 2 * Fij * (1 - Fij) / R + w[j] ** 2 * Fji * (1 - Fji) / R
+    return (a - b) / np.sqrt(var)
+
+
+def element_keys(dom, nd=9):
+    """Geometric key per global element (wall midpoint / cell midpoint), for
+    matching elements of two meshings of the same region."""
+    keys = [None] * dom.num_emitters
+    for (c, f, w), s in dom.surface_mapping.items():
+        face = dom.fine_mesh[c - 1][f - 1]
+        m = face.wallMidPoints[w - 1]
+        keys[s - 1] = ("s", round(m[0], nd), round(m[1], nd))
+    ns = dom.num_surfaces
+    for (c, f), v in dom.volume_mapping.items():
+        m = dom.fine_mesh[c - 1][f - 1].midPoint
+        keys[ns + v - 1] = ("v", round(m[0], nd), round(m[1], nd))
+    return keys
+
+
+def greenhouse_domain(n_layers=67, nx=201, ny=3, n_bins=8, scale_height=15_900.0 / 100_000.0,
+                      kappa_vis=0.01, kappa_ir=100.0):
+    """BASELINE configs[4] geometry: a 1x1 stack of coarse
+    layers, side walls solid, bottom of layer 1 and top of the last layer
+    solid, interfaces open; per-band kappa(y) = rho(y_mid) (k_ir s_b + k_vis
+    (1 - s_b)), s_b = 1/(1 + (4 um / lambda_b)^6) (readme.md:227-247),
+    log-spaced bands between 1 nm and 1 m (readme.md:202-204)."""
+    edges = 10 ** np.linspace(-9, 0, n_bins + 1)
+    centers = np.sqrt(edges[:-1] * edges[1:])
+    sig = 1 / (1 + (4e-6 / centers) ** 6)
+    faces = []
+    for j in range(n_layers):
+        y0, y1 = j / n_layers, (j + 1) / n_layers
+        rho = math.exp(-((y0 + y1) / 2) / scale_height)
+        kap = rho * (kappa_ir * sig + kappa_vis * (1 - sig))
+        f = PolyVolume2D([(0.0, y0), (1.0, y0), (1.0, y1), (0.0, y1)], [j == 0, True, j == n_layers - 1, True],
+                         n_bins, kap, np.zeros(n_bins))
+        f.epsilon = [np.ones(n_bins) for _ in range(4)]
+        f.T_in_g = -1.0
+        faces.append(f)
+    return RayTracingDomain2D(faces, [(nx, ny)] * n_layers)

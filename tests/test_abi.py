@@ -1,0 +1,85 @@
+"""The C-ABI library loads and exports every symbol include/rthx.h declares;
+argument validation works without a GPU; the product fails loudly without it."""
+import ctypes as C
+import os
+import re
+import subprocess
+import sys
+
+import pytest
+
+import helpers as H
+from rthx import abi, _lib
+
+HEADER = os.path.join(H.ROOT, "include", "rthx.h")
+
+
+def declared_functions():
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"\b(rthx_[a-z_]+)\s*\(", txt)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    if not os.path.exists(_lib.LIB_PATH):
+        subprocess.run(["make", "-s", "-C", os.path.dirname(os.path.dirname(_lib.LIB_PATH))], check=True)
+    return _lib.load()
+
+
+def test_header_and_python_mirror_agree():
+    assert declared_functions() == sorted(abi.EXPORTED_SYMBOLS)
+    txt = open(HEADER).read()
+    assert f"#define RTHX_ABI_VERSION {abi.RTHX_ABI_VERSION}" in txt
+
+
+def test_every_declared_symbol_is_exported(lib):
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r"\b(rthx_[a-z_]+)\b", out))
+    missing = [s for s in declared_functions() if s not in exported]
+    assert not missing, missing
+    for s in declared_functions():
+        getattr(lib, s)
+
+
+def test_struct_sizes_match_header():
+    # offsets fixed by the header's field order (x86-64 SysV)
+    assert C.sizeof(abi.GridDesc) == 48
+    assert C.sizeof(abi.TraceArgs) == 80
+    assert C.sizeof(abi.ResultInfo) == 88
+
+
+def test_validation_without_gpu(lib):
+    assert lib.rthx_abi_version() == abi.RTHX_ABI_VERSION
+    h = C.c_void_p()
+    assert lib.rthx_domain_create(None, 0, C.byref(h)) == abi.RTHX_EINVAL
+    assert b"null descriptor" in lib.rthx_last_error()
+    d = H.square_domain(3).flat().desc
+    d.abi_version = 99
+    assert lib.rthx_domain_create(C.byref(d), 0, C.byref(h)) == abi.RTHX_EINVAL
+    r = C.c_void_p()
+    assert lib.rthx_result_create(C.byref(r)) == 0
+    info = abi.ResultInfo()
+    assert lib.rthx_result_get_info(r, C.byref(info)) == abi.RTHX_ESTATE
+    assert lib.rthx_result_copy_csr(r, None, None, None) == abi.RTHX_ESTATE
+    assert lib.rthx_trace_exchange(None, None, r) == abi.RTHX_EINVAL
+    lib.rthx_result_destroy(r)
+
+
+def test_bad_geometry_rejected(lib):
+    flat = H.square_domain(3).flat()
+    bad = flat.fine_surface.copy()
+    flat.fine_surface[0] = 10_000  # surface index out of range
+    h = C.c_void_p()
+    assert lib.rthx_domain_create(C.byref(flat.desc), 0, C.byref(h)) == abi.RTHX_EINVAL
+    flat.fine_surface[:] = bad
+    flat.fine_grid_descs[0].cell_items[0] = 999  # grid item out of range
+    assert lib.rthx_domain_create(C.byref(flat.desc), 0, C.byref(h)) == abi.RTHX_EINVAL
+
+
+def test_missing_library_fails_loudly(tmp_path):
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "from rthx import _lib\n"
+            "try:\n    _lib.load()\nexcept _lib.RthxError as e:\n    print('LOUD', e)\n") % H.PKG
+    env = dict(os.environ, RTHX_LIB=str(tmp_path / "nope.so"))
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=120)
+    assert "LOUD" in out.stdout and "no CPU fallback" in out.stdout

@@ -1,0 +1,275 @@
+"""HIP path (librthx through the C ABI) against the CPU restatement.
+
+Both sides draw every ray from the same Philox-4x32-10 stream, so absorber
+counts are compared exactly (row pointers, columns, counts).  At sizes the
+oracle finishes in seconds the comparison covers every row; at BASELINE's
+full sizes it covers a strided sample of rows plus size-independent
+properties (conservation, determinism, shard invariance, reciprocity).
+
+Tolerance: exact equality is required everywhere except on the full-size
+sampled comparisons, which allow at most 1e-6 of the sampled rays to change
+absorber (the GPU evaluates log/cos/sqrt with ROCm's ocml and the CPU with
+glibc, which can differ by an ulp; a ray changes cell only if it ends within
+~1e-16 of a cell edge).  No case has needed that allowance so far.
+"""
+import math
+
+import numpy as np
+import pytest
+
+import helpers as H
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _args(_lib, flat, R, seed=1, bin0=0, flags=0, begin=0, end=None, stride=1, rec=None, rec_bin0=0):
+    return _lib.make_args(bin0, R, H.NUDGE, seed, begin, flat.n_emitters if end is None else end, stride,
+                          flags=flags, record_ids=rec, record_bin0=rec_bin0)
+
+
+def gpu_trace(_lib, flat, args):
+    dd = _lib.DeviceDomain(flat, 0)
+    res = _lib.DeviceResult()
+    try:
+        res.trace(dd, args)
+        info = res.info()
+        rp, cols, cnt = res.csr()
+        rays = res.rays() if info["n_recorded"] else None
+    finally:
+        res.close()
+        dd.close()
+    return rp, cols, cnt, info, rays
+
+
+def assert_same(g, o, allow_frac=0.0):
+    rp, cols, cnt, info = g[:4]
+    orp, ocols, ocnt, oinfo = o[:4]
+    assert info["rays_traced"] == oinfo["rays_traced"]
+    if allow_frac == 0.0:
+        assert np.array_equal(rp, orp), "row pointers differ"
+        assert np.array_equal(cols, ocols), "columns differ"
+        assert np.array_equal(cnt, ocnt), f"{int(np.sum(cnt != ocnt))} counts differ"
+        assert info["lost_total"] == oinfo["lost_total"]
+        return
+    n = len(rp) - 1
+    A = H.counts_matrix(rp, cols, cnt, n)
+    B = H.counts_matrix(orp, ocols, ocnt, n)
+    moved = abs(A - B).sum() / 2
+    assert moved <= allow_frac * oinfo["rays_traced"], f"{moved} rays changed absorber"
+
+
+@pytest.mark.parametrize("flags", [0, 1])
+def test_c1_exact(hip, flags):
+    dom = H.square_domain(11)
+    flat = dom.flat()
+    args, _k = _args(hip, flat, 1_000_000 // flat.n_emitters, flags=flags)
+    assert_same(gpu_trace(hip, flat, args), oracle.trace_exchange(flat, args, 16))
+
+
+def test_c1_matches_committed_golden(hip):
+    g = np.load(H.os.path.join(H.GOLDEN, "oracle_c1_seed1.npz"))
+    dom = H.square_domain(11)
+    flat = dom.flat()
+    args, _k = _args(hip, flat, int(g["R"]), seed=int(g["seed"]))
+    rp, cols, cnt, _i, _ = gpu_trace(hip, flat, args)
+    assert np.array_equal(rp, g["row_ptr"]) and np.array_equal(cols, g["cols"]) and np.array_equal(cnt, g["counts"])
+
+
+@pytest.mark.parametrize("rotation", [0.3, math.pi / 4, 2.0])
+def test_rotated_square_exact(hip, rotation):
+    dom = H.square_domain(9, rotation=rotation)
+    flat = dom.flat()
+    args, _k = _args(hip, flat, 3000, seed=2)
+    assert_same(gpu_trace(hip, flat, args), oracle.trace_exchange(flat, args, 16))
+
+
+def test_wedges_multi_coarse_exact(hip):
+    """16 triangle wedges with open spokes: coarse crossings + triangle cells."""
+    dom = H.wedge_domain(16, 4)
+    flat = dom.flat()
+    args, _k = _args(hip, flat, 4000, seed=3)
+    assert_same(gpu_trace(hip, flat, args), oracle.trace_exchange(flat, args, 16))
+
+
+def test_scattering_beta6_exact(hip):
+    """C3 physics at 11x11 (kappa = 1, sigma_s = 5: beta = 6, no re-scatter on :exchange)."""
+    dom = H.square_domain(11, sigma_s=5.0)
+    flat = dom.flat()
+    args, _k = _args(hip, flat, 5000, seed=4)
+    assert_same(gpu_trace(hip, flat, args), oracle.trace_exchange(flat, args, 16))
+
+
+def test_transparent_surfaces_only_exact(hip):
+    dom = H.square_domain(6, kappa=0.0)
+    assert dom.surfaces_only
+    flat = dom.flat()
+    args, _k = _args(hip, flat, 5000, seed=5)
+    assert_same(gpu_trace(hip, flat, args), oracle.trace_exchange(flat, args, 16))
+
+
+def test_spectral_variable_bins_exact(hip):
+    """traceRayVariable (beta from each segment's start cell) on a layered
+    8-band domain; every band is spatially non-uniform."""
+    dom = H.greenhouse_domain(n_layers=6, nx=9, ny=3, n_bins=8)
+    assert dom.spectral_mode == "spectral_variable"
+    flat = dom.flat()
+    for b in range(8):
+        args, _k = _args(hip, flat, 1500, seed=6, bin0=b)
+        assert_same(gpu_trace(hip, flat, args), oracle.trace_exchange(flat, args, 16))
+
+
+def test_recorder_exact(hip):
+    dom = H.wedge_domain(8, 3)
+    flat = dom.flat()
+    ids = [0, 5, flat.n_emitters - 1]
+    args, _k = _args(hip, flat, 700, seed=7, rec=ids)
+    g = gpu_trace(hip, flat, args)
+    o = oracle.trace_exchange(flat, args, 16)
+    assert_same(g, o)
+    (go, ge, gg), (oo, oe, og) = g[4], o[4]
+    order = np.lexsort((np.arange(len(og)), og))  # oracle: per-thread order; compare by emitter then ray
+    assert np.array_equal(gg, og[order])
+    assert np.allclose(go, oo[order], rtol=0, atol=1e-12)
+    assert np.allclose(ge, oe[order], rtol=0, atol=1e-9)
+
+
+def test_shards_union_equals_full(hip):
+    from rthx.distributed import merge_csr
+
+    dom = H.square_domain(13)
+    flat = dom.flat()
+    args, _k = _args(hip, flat, 2000, seed=8)
+    full = gpu_trace(hip, flat, args)
+    pieces = []
+    for rank in range(3):
+        a, _k2 = _args(hip, flat, 2000, seed=8, begin=rank, stride=3)
+        pieces.append(gpu_trace(hip, flat, a)[:3])
+    rp, c, v = merge_csr(pieces, flat.n_emitters)
+    assert np.array_equal(rp, full[0]) and np.array_equal(c, full[1]) and np.array_equal(v, full[2])
+
+
+def test_edge_cases(hip):
+    dom = H.square_domain(5)
+    flat = dom.flat()
+    # R = 0 (rays_total < N): empty result
+    args, _k = _args(hip, flat, 0)
+    rp, cols, cnt, info, _ = gpu_trace(hip, flat, args)
+    assert info["nnz"] == 0 and rp[-1] == 0
+    # empty emitter range
+    args, _k = _args(hip, flat, 100, begin=flat.n_emitters, end=flat.n_emitters)
+    assert gpu_trace(hip, flat, args)[3]["rows_traced"] == 0
+    # R >= 65536 switches the row histogram to 32-bit counters
+    args, _k = _args(hip, flat, 70_000, seed=9, begin=0, end=flat.n_emitters, stride=7)
+    assert_same(gpu_trace(hip, flat, args), oracle.trace_exchange(flat, args, 16))
+
+
+def test_errors_do_not_crash(hip):
+    import ctypes as C
+
+    from rthx import abi
+
+    dom = H.square_domain(3)
+    flat = dom.flat()
+    dd = hip.DeviceDomain(flat, 0)
+    res = hip.DeviceResult()
+    lib = hip.load()
+    a, _k = _args(hip, flat, 10, bin0=3)
+    assert lib.rthx_trace_exchange(dd.handle, C.byref(a), res.handle) == abi.RTHX_EINVAL
+    a, _k = _args(hip, flat, 10)
+    a.device = 5
+    assert lib.rthx_trace_exchange(dd.handle, C.byref(a), res.handle) == abi.RTHX_EINVAL
+    a, _k = _args(hip, flat, 1 << 33)
+    assert lib.rthx_trace_exchange(dd.handle, C.byref(a), res.handle) == abi.RTHX_ERANGE
+    res.close()
+    dd.close()
+
+
+def test_lds_limit_reports_erange(hip):
+    """N above the LDS row-histogram limit is refused, not faulted."""
+    import ctypes as C
+
+    from rthx import abi
+
+    dom = H.square_domain(286)  # N = 1144 + 81796 > 81408
+    flat = dom.flat()
+    dd = hip.DeviceDomain(flat, 0)
+    res = hip.DeviceResult()
+    a, _k = _args(hip, flat, 10, end=1)
+    assert hip.load().rthx_trace_exchange(dd.handle, C.byref(a), res.handle) == abi.RTHX_ERANGE
+    res.close()
+    dd.close()
+
+
+# ---------------------------------------------------------------------------
+# BASELINE full sizes
+# ---------------------------------------------------------------------------
+def _full_size_checks(hip, dom, rays, seed, sample_stride, bin0=0, recip=True):
+    flat = dom.flat()
+    N = flat.n_emitters
+    R = rays // N
+    args, _k = _args(hip, flat, R, seed=seed, bin0=bin0)
+    g1 = gpu_trace(hip, flat, args)
+    g2 = gpu_trace(hip, flat, args)
+    for x, y in zip(g1[:3], g2[:3]):
+        assert np.array_equal(x, y), "not deterministic"
+    rp, cols, cnt, info, _ = g1
+    assert info["rays_traced"] == N * R
+    assert int(cnt.sum(dtype=np.int64)) + info["lost_total"] == N * R
+    assert np.all(np.diff(rp) <= min(N, R))
+    assert np.all(cnt > 0)
+    for r in range(N):  # strictly ascending columns in every row
+        seg = cols[rp[r]:rp[r + 1]]
+        if seg.size > 1:
+            assert np.all(np.diff(seg) > 0)
+            break
+    # sampled rows against the oracle
+    sargs, _k2 = _args(hip, flat, R, seed=seed, bin0=bin0, stride=sample_stride)
+    sg = gpu_trace(hip, flat, sargs)
+    so = oracle.trace_exchange(flat, sargs, 16)
+    assert_same(sg, so, allow_frac=1e-6)
+    if recip:
+        C = H.counts_matrix(rp, cols, cnt, N)
+        z = H.reciprocity_z(C, R, H.reciprocity_weights(dom, bin0), min_count=40)
+        assert z.size > 100
+        assert np.max(np.abs(z)) < 7.0
+        assert 0.8 < float(np.mean(z ** 2)) < 1.25
+    return info
+
+
+def test_c2_full_size(hip):
+    """BASELINE configs[1]: 101x101 grey kappa = 1, 1e8 rays on one GPU."""
+    info = _full_size_checks(hip, H.square_domain(101), 100_000_000, seed=1, sample_stride=97)
+    assert info["lost_total"] == 0
+
+
+def test_c3_full_size(hip):
+    """BASELINE configs[2]: 51x51, kappa = 1, sigma_s = 5, 1e8 rays."""
+    info = _full_size_checks(hip, H.square_domain(51, sigma_s=5.0), 100_000_000, seed=2, sample_stride=53)
+    assert info["lost_total"] == 0
+
+
+def test_c5_greenhouse_band(hip):
+    """BASELINE configs[4] geometry (201x201 over 67 layers, 8 bands, variable
+    beta) at 2e7 rays for two bands (visible and infrared)."""
+    dom = H.greenhouse_domain()
+    assert dom.num_emitters == 41205
+    for b in (0, 7):
+        _full_size_checks(hip, dom, 20_000_000, seed=3, sample_stride=211, bin0=b, recip=False)
+
+
+def test_host_path_crosbie_schrenker_on_gpu(hip):
+    """mesh(1e7; method=:exchange) through the product path reproduces the
+    Crosbie & Schrenker centreline (test/test_2d_grey.jl:169-225)."""
+    from rthx.exchange import exchange_ray_tracing
+
+    cs = H.golden("reference_tables.json")["crosbie_schrenker"]
+    nd = 11
+    tau = np.linspace(1 / (2 * nd), 1 - 1 / (2 * nd), nd)
+    ana = H.line_interpolation(cs["relative_tau_z"], cs["source_func_center"], tau)
+    dom = H.square_domain(nd)
+    F = exchange_ray_tracing(dom, 10_000_000, H.NUDGE, False, None, seed=11)
+    assert dom.last_trace_info[0]["backend"] == "hip"
+    assert np.allclose(np.asarray(F.sum(axis=1)).ravel(), 1.0)
+    sf = H.centerline_source_function(dom, nd)
+    assert np.linalg.norm(sf - ana) <= 0.02 * np.linalg.norm(ana)
