@@ -145,6 +145,149 @@ int check_grid(const rthx_grid_desc& g, int32_t count, const char* what) {
   return RTHX_OK;
 }
 
+// ---------------------------------------------------------------------------
+// Device point-location grid (DESIGN.md "Point location").
+//
+// The reference locates a point with a uniform grid of cell size
+// 2*sqrt(mean area) whose cells list, in ascending order, every polygon whose
+// bbox meets the cell (spatialAccelerations.jl:2-59), then tests candidates in
+// order until the first point-in-polygon hit (findFace2D.jl:2-27).  With
+// ~9 candidates per cell that is the single largest cost of a ray on the GPU.
+// The device grid keeps the rule "every polygon whose bbox meets the cell is
+// a candidate" but uses cells of about half a polygon (per axis, from the mean
+// bbox extent), and orders each cell's candidates by the area of the polygon
+// inside the cell (largest first, ties by index), so that the first
+// point-in-polygon test nearly always hits.  Only a point that lies inside two
+// polygons at once -- within an ulp of a shared edge -- can resolve
+// differently from the reference's order.
+// ---------------------------------------------------------------------------
+constexpr double kGridCellsPerPolygon = 2.0;  // cells per mean polygon extent, per axis
+constexpr int64_t kGridMaxCellsPerPolygon = 64;
+
+// area of polygon (n <= 4 vertices) clipped to [x0,x1]x[y0,y1] (Sutherland-Hodgman)
+double clipped_area(const double* xy, int n, double x0, double x1, double y0, double y1) {
+  double a[16][2], b[16][2];
+  int na = n;
+  for (int i = 0; i < n; ++i) { a[i][0] = xy[2 * i]; a[i][1] = xy[2 * i + 1]; }
+  for (int edge = 0; edge < 4 && na > 0; ++edge) {
+    int nb = 0;
+    for (int i = 0; i < na; ++i) {
+      const double* P = a[i];
+      const double* Q = a[(i + 1) % na];
+      auto inside = [&](const double* v) {
+        switch (edge) {
+          case 0: return v[0] >= x0;
+          case 1: return v[0] <= x1;
+          case 2: return v[1] >= y0;
+          default: return v[1] <= y1;
+        }
+      };
+      auto cut = [&](double* out) {
+        double t;
+        switch (edge) {
+          case 0: t = (x0 - P[0]) / (Q[0] - P[0]); break;
+          case 1: t = (x1 - P[0]) / (Q[0] - P[0]); break;
+          case 2: t = (y0 - P[1]) / (Q[1] - P[1]); break;
+          default: t = (y1 - P[1]) / (Q[1] - P[1]); break;
+        }
+        out[0] = P[0] + t * (Q[0] - P[0]);
+        out[1] = P[1] + t * (Q[1] - P[1]);
+      };
+      bool pin = inside(P), qin = inside(Q);
+      if (pin && nb < 16) { b[nb][0] = P[0]; b[nb][1] = P[1]; ++nb; }
+      if (pin != qin && nb < 16) { cut(b[nb]); ++nb; }
+    }
+    for (int i = 0; i < nb; ++i) { a[i][0] = b[i][0]; a[i][1] = b[i][1]; }
+    na = nb;
+  }
+  double A = 0.0;
+  for (int i = 0; i < na; ++i) {
+    int j = (i + 1) % na;
+    A += a[i][0] * a[j][1] - a[j][0] * a[i][1];
+  }
+  return std::fabs(0.5 * A);
+}
+
+// Build one device grid over polygons [first, first+count) and append its
+// cells / items to the shared arrays.
+rthx::DevGrid build_device_grid(const int32_t* nv, const double* xy, int first, int count,
+                                std::vector<int32_t>& cell_start_all, std::vector<int32_t>& items_all) {
+  double minx = INFINITY, maxx = -INFINITY, miny = INFINITY, maxy = -INFINITY, sw = 0.0, sh = 0.0;
+  std::vector<double> bb(4 * (size_t)count);
+  for (int f = 0; f < count; ++f) {
+    const double* v = xy + 8 * (size_t)(first + f);
+    double a = INFINITY, b = -INFINITY, c = INFINITY, d = -INFINITY;
+    for (int i = 0; i < nv[first + f]; ++i) {
+      a = std::min(a, v[2 * i]); b = std::max(b, v[2 * i]);
+      c = std::min(c, v[2 * i + 1]); d = std::max(d, v[2 * i + 1]);
+    }
+    bb[4 * f] = a; bb[4 * f + 1] = b; bb[4 * f + 2] = c; bb[4 * f + 3] = d;
+    minx = std::min(minx, a); maxx = std::max(maxx, b); miny = std::min(miny, c); maxy = std::max(maxy, d);
+    sw += b - a;
+    sh += d - c;
+  }
+  double ext = std::max(maxx - minx, maxy - miny);
+  double sx = std::max(sw / count / kGridCellsPerPolygon, 1e-12 * ext);
+  double sy = std::max(sh / count / kGridCellsPerPolygon, 1e-12 * ext);
+  double padx = 0.01 * sx, pady = 0.01 * sy;
+  auto dims = [&](double& nxd, double& nyd) {
+    nxd = std::max(1.0, std::ceil((maxx - minx + 2 * padx) / sx));
+    nyd = std::max(1.0, std::ceil((maxy - miny + 2 * pady) / sy));
+  };
+  double nxd, nyd;
+  dims(nxd, nyd);
+  const double cap = (double)std::max<int64_t>(64, kGridMaxCellsPerPolygon * (int64_t)count);
+  if (nxd * nyd > cap) {
+    double k = std::sqrt(nxd * nyd / cap);
+    sx *= k; sy *= k; padx = 0.01 * sx; pady = 0.01 * sy;
+    dims(nxd, nyd);
+  }
+  rthx::DevGrid g{};
+  g.ox = minx - padx;
+  g.oy = miny - pady;
+  g.inv_x = 1.0 / sx;
+  g.inv_y = 1.0 / sy;
+  g.nx = (int32_t)nxd;
+  g.ny = (int32_t)nyd;
+  g.cell_base = (int32_t)cell_start_all.size();
+  g.item_base = (int32_t)items_all.size();
+  const int64_t ncell = (int64_t)g.nx * g.ny;
+  struct Cand { int64_t cell; int32_t f; double area; };
+  std::vector<Cand> cand;
+  cand.reserve((size_t)count * 9);
+  for (int f = 0; f < count; ++f) {
+    // same expression as the device lookup, so a point of f maps into [i0, i1]
+    int64_t i0 = (int64_t)std::floor((bb[4 * f] - g.ox) * g.inv_x);
+    int64_t i1 = (int64_t)std::floor((bb[4 * f + 1] - g.ox) * g.inv_x);
+    int64_t j0 = (int64_t)std::floor((bb[4 * f + 2] - g.oy) * g.inv_y);
+    int64_t j1 = (int64_t)std::floor((bb[4 * f + 3] - g.oy) * g.inv_y);
+    i0 = std::max<int64_t>(0, i0); j0 = std::max<int64_t>(0, j0);
+    i1 = std::min<int64_t>(g.nx - 1, i1); j1 = std::min<int64_t>(g.ny - 1, j1);
+    const double* v = xy + 8 * (size_t)(first + f);
+    for (int64_t j = j0; j <= j1; ++j)
+      for (int64_t i = i0; i <= i1; ++i) {
+        double cx0 = g.ox + i * sx, cy0 = g.oy + j * sy;
+        double area = clipped_area(v, nv[first + f], cx0, cx0 + sx, cy0, cy0 + sy);
+        cand.push_back({j * g.nx + i, f, area});
+      }
+  }
+  std::sort(cand.begin(), cand.end(), [](const Cand& a, const Cand& b) {
+    if (a.cell != b.cell) return a.cell < b.cell;
+    if (a.area != b.area) return a.area > b.area;
+    return a.f < b.f;
+  });
+  size_t k = 0;
+  for (int64_t c = 0; c < ncell; ++c) {
+    cell_start_all.push_back((int32_t)(k));
+    while (k < cand.size() && cand[k].cell == c) {
+      items_all.push_back(cand[k].f);
+      ++k;
+    }
+  }
+  cell_start_all.push_back((int32_t)k);
+  return g;
+}
+
 }  // namespace
 
 RTHX_EXPORT int rthx_abi_version(void) { return RTHX_ABI_VERSION; }
@@ -251,25 +394,13 @@ RTHX_EXPORT int rthx_domain_create(const rthx_domain_desc* desc, int32_t device,
   for (int c = 0; c < s.n_coarse; ++c)
     for (int f = s.fine_offset[c]; f < s.fine_offset[c + 1]; ++f) fcoarse[f] = c;
 
-  // concatenate grids: coarse first, then fine grids in coarse order
+  // device point-location grids: coarse first, then one per coarse polygon
   std::vector<int32_t> cell_start, items;
-  auto add_grid = [&](const rthx_grid_desc& g) {
-    rthx::DevGrid dg;
-    dg.ox = g.origin_x;
-    dg.oy = g.origin_y;
-    dg.inv = g.inv_cell_size;
-    dg.nx = g.nx;
-    dg.ny = g.ny;
-    dg.cell_base = (int32_t)cell_start.size();
-    dg.item_base = (int32_t)items.size();
-    int64_t cells = (int64_t)g.nx * g.ny;
-    cell_start.insert(cell_start.end(), g.cell_start, g.cell_start + cells + 1);
-    items.insert(items.end(), g.cell_items, g.cell_items + g.cell_start[cells]);
-    return dg;
-  };
-  D.c_grid = add_grid(s.coarse_grid);
+  D.c_grid = build_device_grid(s.coarse_nv, s.coarse_xy, 0, s.n_coarse, cell_start, items);
   std::vector<rthx::DevGrid> fgrids(s.n_coarse);
-  for (int c = 0; c < s.n_coarse; ++c) fgrids[c] = add_grid(s.fine_grid[c]);
+  for (int c = 0; c < s.n_coarse; ++c)
+    fgrids[c] = build_device_grid(s.fine_nv, s.fine_xy, s.fine_offset[c], s.fine_offset[c + 1] - s.fine_offset[c],
+                                  cell_start, items);
   if (cell_start.size() >= (1ull << 31) || items.size() >= (1ull << 31)) return bail(fail(RTHX_ERANGE, "grids too large"));
 
   const size_t nc = s.n_coarse, nf = s.n_fine;
@@ -407,14 +538,13 @@ RTHX_EXPORT int rthx_trace_exchange(rthx_domain* dom, const rthx_trace_args* a, 
   P.key0 = (uint32_t)a->seed;
   P.key1 = (uint32_t)(a->seed >> 32);
   P.bin = a->bin;
-  P.faithful = (a->flags & RTHX_FLAG_FAITHFUL_SAMPLING) ? 1 : 0;
   P.beta_uniform = dom->beta_first[a->bin];
   const bool uniform = dom->uniform_beta[a->bin] > -0.1;  // traceRay.jl:4
 
   hipStream_t st = dom->stream;
   HIP_TRY(hipEventRecord(dom->ev[0], st), "hipEventRecord");
   if (n_rows > 0) {
-    HIP_TRY(rthx::launch_trace(dom->D, P, uniform, pack16, N, n_rows, res->stage_cols.as<uint32_t>(),
+    HIP_TRY(rthx::launch_trace(dom->D, P, uniform, pack16, (a->flags & RTHX_FLAG_FAITHFUL_SAMPLING) != 0, N, n_rows, res->stage_cols.as<uint32_t>(),
                                res->stage_cnt.as<uint32_t>(), row_cap, res->row_nnz.as<uint32_t>(),
                                res->row_tallied.as<uint32_t>(), rec, lds_bytes, st),
             "trace_exchange_kernel launch");

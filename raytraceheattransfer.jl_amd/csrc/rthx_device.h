@@ -14,7 +14,8 @@ namespace rthx {
 // as a kernel argument; every pointer is device memory.
 // ---------------------------------------------------------------------------
 struct DevGrid {
-  double ox, oy, inv;   // origin, 1/cell_size
+  double ox, oy;        // origin
+  double inv_x, inv_y;  // 1/cell size in x and y
   int32_t nx, ny;
   int32_t cell_base;    // offset of this grid's cell_start in grid_cell_start
   int32_t item_base;    // offset of this grid's items in grid_items
@@ -57,7 +58,7 @@ struct TraceParams {
   double eta;              // nudge
   uint32_t key0, key1;     // Philox key (seed)
   int32_t bin;
-  int32_t faithful;
+  int32_t reserved;
   double beta_uniform;     // beta of fine face 0 in `bin` (uniform path)
 };
 
@@ -110,38 +111,38 @@ struct RayRng {
 // distToSurface2D.jl:2-17: smallest positive parameter along d to the walls
 // of a polygon (inward unit normals), first index on ties, walls with
 // |d.n| < 1e-10 or parameter <= 0 are +Inf; all +Inf -> (Inf, 0).
+// The reference divides every wall's numerator by its denominator and takes
+// findmin; here the candidates (num/den > 0, i.e. num and den of one sign) are
+// compared by cross-multiplication |num_a| |den_b| < |num_b| |den_a| and only
+// the winner is divided: the same minimum and index except for walls whose
+// parameters tie to within an ulp (a ray through a corner).
 __device__ __forceinline__ double dist_to_polygon(double px, double py, double dx, double dy,
                                                   const double* __restrict__ xy,
                                                   const double* __restrict__ nrm, int n, int& widx) {
-  double best = __builtin_inf();
+  double bn = 1.0, bd = 0.0;  // best |num|, |den|; bd == 0 means "none yet"
   int bi = 0;
-  bool have_nan = false;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     if (i < n) {
       double nx = nrm[2 * i], ny = nrm[2 * i + 1];
       double den = __dmul_rn(dx, nx) + __dmul_rn(dy, ny);
-      double u;
-      if (fabs(den) < 1e-10) {
-        u = __builtin_inf();
-      } else {
-        double num = __dmul_rn(xy[2 * i] - px, nx) + __dmul_rn(xy[2 * i + 1] - py, ny);
-        u = num / den;
-      }
-      if (u <= 0.0) u = __builtin_inf();
-      if (u != u) {
-        if (!have_nan) { have_nan = true; best = u; bi = i; }
-      } else if (!have_nan && u < best) {
-        best = u;
-        bi = i;
-      }
+      double num = __dmul_rn(xy[2 * i] - px, nx) + __dmul_rn(xy[2 * i + 1] - py, ny);
+      double an = fabs(num), ad = fabs(den);
+      bool ok = (ad >= 1e-10) && ((num > 0.0 && den > 0.0) || (num < 0.0 && den < 0.0));
+      bool better = ok && (bd == 0.0 || __dmul_rn(an, bd) < __dmul_rn(bn, ad));
+      if (better) { bn = an; bd = ad; bi = i; }
     }
   }
   widx = bi;
-  return best;
+  if (bd == 0.0) return __builtin_inf();
+  double u = bn / bd;
+  return u > 0.0 ? u : __builtin_inf();
 }
 
-// pointInPolygonFast2D, findFace2D.jl:77-101.
+// pointInPolygonFast2D, findFace2D.jl:77-101 (crossing test, j = previous
+// vertex).  The reference's  px < xi + (xj-xi)/(yj-yi) (py-yi)  is evaluated
+// without the division as  sign((xj-xi)(py-yi) - (px-xi)(yj-yi)) == sign(yj-yi),
+// which decides identically except for points within an ulp of the edge.
 __device__ __forceinline__ bool point_in_polygon(double px, double py, const double* __restrict__ xy, int n) {
   bool inside = false;
   double xj = xy[2 * (n - 1)], yj = xy[2 * (n - 1) + 1];
@@ -149,11 +150,11 @@ __device__ __forceinline__ bool point_in_polygon(double px, double py, const dou
   for (int i = 0; i < 4; ++i) {
     if (i < n) {
       double xi = xy[2 * i], yi = xy[2 * i + 1];
-      if ((yi > py) != (yj > py)) {
-        double slope = (xj - xi) / (yj - yi);
-        double ix = xi + __dmul_rn(slope, py - yi);
-        if (px < ix) inside = !inside;
-      }
+      double ey = yj - yi;
+      double cr = __dmul_rn(xj - xi, py - yi) - __dmul_rn(px - xi, ey);
+      bool crossing = (yi > py) != (yj > py);
+      bool left = ey > 0.0 ? (cr > 0.0) : (cr < 0.0);
+      inside ^= (crossing && left);
       xj = xi;
       yj = yi;
     }
@@ -163,12 +164,18 @@ __device__ __forceinline__ bool point_in_polygon(double px, double py, const dou
 
 // findFace2D, findFace2D.jl:48-68 (grid :2-27, bbox fallback :30-45).
 // Polygons [first, first+count) of (nv, xy, bbox); returns local index or -1.
+// The grid is the device acceleration grid built by rthx_domain_create
+// (DESIGN.md "Point location"): finer than the reference's, with each cell's
+// candidates ordered by overlap area so the first test usually hits.  Every
+// polygon whose bbox meets a cell is listed in it, so the polygon that
+// contains a point is always a candidate of the point's cell; the bbox scan
+// in index order remains the fallback exactly as in the reference.
 __device__ __forceinline__ int locate(const DevGrid& g, const int32_t* __restrict__ cell_start,
-                                   const int32_t* __restrict__ items, const int32_t* __restrict__ nv,
-                                   const double* __restrict__ xy, const double* __restrict__ bbox,
-                                   int first, int count, double px, double py) {
-  double fi = floor(__dmul_rn(px - g.ox, g.inv));
-  double fj = floor(__dmul_rn(py - g.oy, g.inv));
+                                      const int32_t* __restrict__ items, const int32_t* __restrict__ nv,
+                                      const double* __restrict__ xy, const double* __restrict__ bbox,
+                                      int first, int count, double px, double py) {
+  double fi = floor(__dmul_rn(px - g.ox, g.inv_x));
+  double fj = floor(__dmul_rn(py - g.oy, g.inv_y));
   if (fi >= 0.0 && fi < (double)g.nx && fj >= 0.0 && fj < (double)g.ny) {
     int cell = g.cell_base + (int)fj * g.nx + (int)fi;
     int k0 = cell_start[cell], k1 = cell_start[cell + 1];
@@ -202,7 +209,8 @@ __device__ __forceinline__ int locate_coarse(const DevDomain& D, double px, doub
 
 // emitSurfaceRay2D.jl:1-26 + lambertSample2D.jl:1-10 (Float32-rounded
 // Lambert draws; un-normalised in-plane direction).
-__device__ __forceinline__ void emit_surface(const DevDomain& D, int f, int w, double eta, bool faithful,
+template <bool faithful>
+__device__ __forceinline__ void emit_surface(const DevDomain& D, int f, int w, double eta,
                                              RayRng& rng, double& px, double& py, double& dx,
                                              double& dy) {
   const double* xy = D.f_xy + 8 * (size_t)f;
@@ -232,7 +240,8 @@ __device__ __forceinline__ void emit_surface(const DevDomain& D, int f, int w, d
 }
 
 // emitVolumeRay2D.jl:1-33.
-__device__ __forceinline__ void emit_volume(const DevDomain& D, int f, double eta, bool faithful, RayRng& rng,
+template <bool faithful>
+__device__ __forceinline__ void emit_volume(const DevDomain& D, int f, double eta, RayRng& rng,
                                             double& px, double& py, double& dx, double& dy) {
   const double* v = D.f_xy + 8 * (size_t)f;
   int n = D.f_nv[f];
@@ -270,22 +279,10 @@ __device__ __forceinline__ void emit_volume(const DevDomain& D, int f, double et
   dy = ct;
 }
 
-// Wall hit: p += (u - eta) d, locate the fine cell, find the fine wall
-// (traceRay.jl:42-52 / :118-128).  Returns global absorber or -1.
-__device__ __forceinline__ int64_t wall_hit(const DevDomain& D, int c, double& px, double& py, double dx,
-                                            double dy, double u, double eta) {
-  double t = u - eta;
-  px = px + __dmul_rn(t, dx);
-  py = py + __dmul_rn(t, dy);
-  int f = locate_fine(D, c, px, py);
-  if (f < 0) return -1;
-  int fg = D.f_offset[c] + f;
-  int w;
-  dist_to_polygon(px, py, dx, dy, D.f_xy + 8 * (size_t)fg, D.f_nrm + 8 * (size_t)fg, D.f_nv[fg], w);
-  return D.f_surf[4 * fg + w];
-}
-
 // traceRayUniform (traceRay.jl:20-70) and traceRayVariable (:73-147).
+// The gas branch (:31-40 / :105-116) and the solid-wall branch (:42-52 /
+// :118-128) both move the point and locate its fine cell; they are merged so
+// that the wave runs one point location for both kinds of lanes.
 template <bool UNIFORM>
 __device__ __forceinline__ int64_t trace_ray(const DevDomain& D, const TraceParams& P, int c, double& px,
                                              double& py, double dx, double dy, RayRng& rng) {
@@ -312,24 +309,25 @@ __device__ __forceinline__ int64_t trace_ray(const DevDomain& D, const TracePara
       tau_b = __dmul_rn(beta, u);
       gas = acc + tau_b >= target;
     }
-    if (gas) {
-      double Sg = UNIFORM ? S : (target - acc) / beta;
-      double t = Sg - eta;
+    bool wall = !gas && ((D.c_solid[c] >> k) & 1u);
+    if (gas || wall) {
+      double t = gas ? (UNIFORM ? S : (target - acc) / beta) - eta : u - eta;
       px = px + __dmul_rn(t, dx);
       py = py + __dmul_rn(t, dy);
       int f = locate_fine(D, c, px, py);
       if (f < 0) return -1;
-      return (int64_t)D.n_surfaces + D.f_offset[c] + f;
-    } else if ((D.c_solid[c] >> k) & 1u) {
-      return wall_hit(D, c, px, py, dx, dy, u, eta);
-    } else {
-      double t = u + eta;
-      px = px + __dmul_rn(t, dx);
-      py = py + __dmul_rn(t, dy);
-      if (UNIFORM) S -= u; else acc += tau_b;
-      c = locate_coarse(D, px, py);
-      if (c < 0) return -1;
+      int fg = D.f_offset[c] + f;
+      if (gas) return (int64_t)D.n_surfaces + fg;
+      int w;
+      dist_to_polygon(px, py, dx, dy, D.f_xy + 8 * (size_t)fg, D.f_nrm + 8 * (size_t)fg, D.f_nv[fg], w);
+      return D.f_surf[4 * fg + w];  // -1 if the fine wall is not solid
     }
+    double t = u + eta;
+    px = px + __dmul_rn(t, dx);
+    py = py + __dmul_rn(t, dy);
+    if (UNIFORM) S -= u; else acc += tau_b;
+    c = locate_coarse(D, px, py);
+    if (c < 0) return -1;
   }
   return -1;
 }
@@ -337,19 +335,18 @@ __device__ __forceinline__ int64_t trace_ray(const DevDomain& D, const TracePara
 // One ray (g, r): emit then trace (traceRay.jl:1-17 dispatch done by the
 // caller through UNIFORM).  Returns absorber (-1 = lost); (ox, oy) emission
 // point, (px, py) end point.
-template <bool UNIFORM>
+template <bool UNIFORM, bool FAITHFUL>
 __device__ __forceinline__ int64_t trace_one(const DevDomain& D, const TraceParams& P, int64_t g, int64_t r,
                                              double& ox, double& oy, double& px, double& py) {
   RayRng rng((uint32_t)r, (uint32_t)g, (uint32_t)P.bin, P.key0, P.key1);
   double dx, dy;
   int f;
-  bool faithful = P.faithful != 0;
   if (g < D.n_surfaces) {
     f = D.s_face[g];
-    emit_surface(D, f, D.s_wall[g], P.eta, faithful, rng, px, py, dx, dy);
+    emit_surface<FAITHFUL>(D, f, D.s_wall[g], P.eta, rng, px, py, dx, dy);
   } else {
     f = (int)(g - D.n_surfaces);
-    emit_volume(D, f, P.eta, faithful, rng, px, py, dx, dy);
+    emit_volume<FAITHFUL>(D, f, P.eta, rng, px, py, dx, dy);
   }
   ox = px;
   oy = py;

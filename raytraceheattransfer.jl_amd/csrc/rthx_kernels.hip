@@ -21,7 +21,7 @@ __device__ __forceinline__ uint32_t lane_id() {
   return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
 }
 
-template <bool UNIFORM, bool PACK16>
+template <bool UNIFORM, bool PACK16, bool FAITHFUL>
 __global__ __launch_bounds__(kTraceThreads) void trace_exchange_kernel(DevDomain D, TraceParams P, int64_t n_emitters,
                                                                      uint32_t* __restrict__ stage_cols,
                                                                      uint32_t* __restrict__ stage_cnt,
@@ -50,7 +50,7 @@ __global__ __launch_bounds__(kTraceThreads) void trace_exchange_kernel(DevDomain
   uint32_t tallied = 0;
   for (int64_t r = tid; r < P.R; r += kTraceThreads) {
     double ox, oy, px, py;
-    int64_t a = trace_one<UNIFORM>(D, P, g, r, ox, oy, px, py);
+    int64_t a = trace_one<UNIFORM, FAITHFUL>(D, P, g, r, ox, oy, px, py);
     if (a >= 0) {
       if (PACK16)
         atomicAdd(&hist[a >> 1], 1u << ((uint32_t)(a & 1) << 4));
@@ -173,12 +173,12 @@ __global__ __launch_bounds__(256) void csr_pack_kernel(const uint32_t* __restric
 // ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
-template <bool UNIFORM, bool PACK16>
+template <bool UNIFORM, bool PACK16, bool FAITHFUL>
 static hipError_t launch_trace_t(const DevDomain& D, const TraceParams& P, int64_t n_emitters, int64_t n_rows,
                                  uint32_t* stage_cols, uint32_t* stage_cnt, int64_t row_cap, uint32_t* row_nnz,
                                  uint32_t* row_tallied, const RecordParams& rec, size_t lds_bytes,
                                  hipStream_t stream) {
-  auto kern = trace_exchange_kernel<UNIFORM, PACK16>;
+  auto kern = trace_exchange_kernel<UNIFORM, PACK16, FAITHFUL>;
   if (lds_bytes > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)lds_bytes);
@@ -189,20 +189,20 @@ static hipError_t launch_trace_t(const DevDomain& D, const TraceParams& P, int64
   return hipGetLastError();
 }
 
-hipError_t launch_trace(const DevDomain& D, const TraceParams& P, bool uniform, bool pack16, int64_t n_emitters,
-                        int64_t n_rows, uint32_t* stage_cols, uint32_t* stage_cnt, int64_t row_cap,
-                        uint32_t* row_nnz, uint32_t* row_tallied, const RecordParams& rec, size_t lds_bytes,
-                        hipStream_t stream) {
-  if (uniform) {
-    return pack16 ? launch_trace_t<true, true>(D, P, n_emitters, n_rows, stage_cols, stage_cnt, row_cap, row_nnz,
-                                               row_tallied, rec, lds_bytes, stream)
-                  : launch_trace_t<true, false>(D, P, n_emitters, n_rows, stage_cols, stage_cnt, row_cap, row_nnz,
-                                                row_tallied, rec, lds_bytes, stream);
+hipError_t launch_trace(const DevDomain& D, const TraceParams& P, bool uniform, bool pack16, bool faithful,
+                        int64_t n_emitters, int64_t n_rows, uint32_t* stage_cols, uint32_t* stage_cnt,
+                        int64_t row_cap, uint32_t* row_nnz, uint32_t* row_tallied, const RecordParams& rec,
+                        size_t lds_bytes, hipStream_t stream) {
+#define RTHX_LAUNCH(U, P16, F)                                                                                  \
+  return launch_trace_t<U, P16, F>(D, P, n_emitters, n_rows, stage_cols, stage_cnt, row_cap, row_nnz, row_tallied, \
+                                   rec, lds_bytes, stream)
+  if (faithful) {
+    if (uniform) { if (pack16) RTHX_LAUNCH(true, true, true); else RTHX_LAUNCH(true, false, true); }
+    if (pack16) RTHX_LAUNCH(false, true, true); else RTHX_LAUNCH(false, false, true);
   }
-  return pack16 ? launch_trace_t<false, true>(D, P, n_emitters, n_rows, stage_cols, stage_cnt, row_cap, row_nnz,
-                                              row_tallied, rec, lds_bytes, stream)
-                : launch_trace_t<false, false>(D, P, n_emitters, n_rows, stage_cols, stage_cnt, row_cap, row_nnz,
-                                               row_tallied, rec, lds_bytes, stream);
+  if (uniform) { if (pack16) RTHX_LAUNCH(true, true, false); else RTHX_LAUNCH(true, false, false); }
+  if (pack16) RTHX_LAUNCH(false, true, false); else RTHX_LAUNCH(false, false, false);
+#undef RTHX_LAUNCH
 }
 
 hipError_t launch_scan(const uint32_t* row_nnz, const uint32_t* row_tallied, int64_t n_rows, int64_t R,
