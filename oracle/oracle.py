@@ -39,8 +39,8 @@ def load() -> C.CDLL:
     lib = C.CDLL(LIB_PATH)
     lib.oracle_philox4x32_10.argtypes = [C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
     lib.oracle_philox4x32_10.restype = None
-    lib.oracle_uniform.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]
-    lib.oracle_uniform.restype = C.c_double
+    lib.oracle_ray_draws.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(C.c_double)]
+    lib.oracle_ray_draws.restype = None
     lib.oracle_trace_exchange.argtypes = [C.POINTER(abi.DomainDesc), C.POINTER(abi.TraceArgs), C.c_int,
                                           C.POINTER(C.c_void_p)]
     lib.oracle_result_get_info.argtypes = [C.c_void_p, C.POINTER(abi.ResultInfo)]
@@ -67,8 +67,14 @@ def philox(ctr, key):
     return list(o)
 
 
-def uniform(seed, bin0, g, r, k) -> float:
-    return load().oracle_uniform(seed, bin0, g, r, k)
+DRAW_NAMES = ("R1", "R2", "path", "sel", "th", "ph", "l1", "l2")
+
+
+def ray_draws(seed, bin0, g, r) -> dict:
+    """The eight uniforms of ray (g, r) (layout: rthx_oracle.c ray_draws)."""
+    out = (C.c_double * 8)()
+    load().oracle_ray_draws(seed, bin0, g, r, out)
+    return dict(zip(DRAW_NAMES, list(out)))
 
 
 def trace_ray(flat, args, g, r):

@@ -66,50 +66,55 @@ ORACLE_API void oracle_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2
   out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
 }
 
-/* 53-bit uniform in [0, 1) from two 32-bit words (hi word first). */
-static inline double u53(uint32_t hi, uint32_t lo) {
+/* Uniform in [0, 1) with 52 random bits, built like Julia's rand() (a
+ * double in [1, 2) from the top 52 bits of hi:lo, minus 1). */
+static inline double u52(uint32_t hi, uint32_t lo) {
   uint64_t x = ((uint64_t)hi << 32) | lo;
-  return (double)(x >> 11) * 0x1.0p-53;
+  uint64_t bits = 0x3FF0000000000000ull | (x >> 12);
+  double d;
+  memcpy(&d, &bits, sizeof d);
+  return d - 1.0;
 }
 
-/* Draw k of ray (g, r) in bin b: block k/2 of the Philox stream with
- * counter (r, g, k/2, b) and key (seed_lo, seed_hi). */
+/* Uniform in [0, 1) with 32 random bits (exact in double). */
+static inline double u32(uint32_t w) { return (double)w * 0x1.0p-32; }
+
+/* The random draws of ray (g, r) in bin b: two Philox blocks, counters
+ * (r, g, 0, b) -> a[0..3] and (r, g, 1, b) -> c[0..3], key (seed lo, seed hi).
+ *   R1   = u52(a0, a1)  surface position / volume sqrt-weight
+ *   R2   = u52(a2, a3)  volume second barycentric draw
+ *   path = u52(c0, c1)  free path (-ln u)
+ *   sel  = u32(c2)      quad triangle selection
+ *   th   = u32(c3)      volume cos(theta) draw
+ *   ph   = u32(a1[11:0] << 20 | a3[11:0] << 8 | c1[11:4])  volume phi draw
+ *   l1   = u32(a2), l2 = u32(a3)   surface Lambert draws (rounded to Float32)
+ * Draws that feed positions and free paths keep 52 bits like Julia's rand();
+ * angle and selection draws use 32 bits (then rounded or compared). */
 typedef struct {
-  uint32_t key[2];
-  uint32_t g, r, bin;
-  uint32_t block;
-  double cache[2];
-  int avail; /* draws left in cache */
-} rng_t;
+  double R1, R2, path, sel, th, ph, l1, l2;
+} draws_t;
 
-static void rng_init(rng_t* s, uint64_t seed, uint32_t bin, uint32_t g, uint32_t r) {
-  s->key[0] = (uint32_t)seed;
-  s->key[1] = (uint32_t)(seed >> 32);
-  s->g = g; s->r = r; s->bin = bin; s->block = 0; s->avail = 0;
+static void ray_draws(uint64_t seed, uint32_t bin, uint32_t g, uint32_t r, draws_t* d) {
+  uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+  uint32_t ca[4] = {r, g, 0u, bin}, cc[4] = {r, g, 1u, bin};
+  uint32_t a[4], c[4];
+  oracle_philox4x32_10(ca, key, a);
+  oracle_philox4x32_10(cc, key, c);
+  d->R1 = u52(a[0], a[1]);
+  d->R2 = u52(a[2], a[3]);
+  d->path = u52(c[0], c[1]);
+  d->sel = u32(c[2]);
+  d->th = u32(c[3]);
+  d->ph = u32(((a[1] & 0xFFFu) << 20) | ((a[3] & 0xFFFu) << 8) | ((c[1] & 0xFFFu) >> 4));
+  d->l1 = u32(a[2]);
+  d->l2 = u32(a[3]);
 }
 
-static double rng_next(rng_t* s) {
-  if (s->avail == 0) {
-    uint32_t ctr[4] = {s->r, s->g, s->block, s->bin};
-    uint32_t o[4];
-    oracle_philox4x32_10(ctr, s->key, o);
-    s->cache[0] = u53(o[0], o[1]);
-    s->cache[1] = u53(o[2], o[3]);
-    s->block++;
-    s->avail = 2;
-  }
-  double v = s->cache[2 - s->avail];
-  s->avail--;
-  return v;
-}
-
-ORACLE_API double oracle_uniform(uint64_t seed, uint32_t bin, uint32_t g, uint32_t r,
-                                 uint32_t k) {
-  rng_t s;
-  rng_init(&s, seed, bin, g, r);
-  double v = 0;
-  for (uint32_t i = 0; i <= k; ++i) v = rng_next(&s);
-  return v;
+ORACLE_API void oracle_ray_draws(uint64_t seed, uint32_t bin, uint32_t g, uint32_t r, double out[8]) {
+  draws_t d;
+  ray_draws(seed, bin, g, r, &d);
+  out[0] = d.R1; out[1] = d.R2; out[2] = d.path; out[3] = d.sel;
+  out[4] = d.th; out[5] = d.ph; out[6] = d.l1; out[7] = d.l2;
 }
 
 /* ------------------------------------------------------------------------ */
@@ -215,13 +220,13 @@ static inline int locate_coarse(const dom_t* D, double px, double py) {
  * draws of lambertSample2D.  The direction is left un-normalised (its length
  * is the in-plane projection of a 3D unit vector). */
 static void emit_surface(const rthx_domain_desc* d, int f, int w, double eta, int faithful,
-                         rng_t* rng, double* p, double* dir) {
+                         const draws_t* rd, double* p, double* dir) {
   const double* xy = d->fine_xy + 8 * (size_t)f;
   int n = d->fine_nv[f];
   int w2 = (w + 1) % n;
   double p1x = xy[2 * w], p1y = xy[2 * w + 1];
   double p2x = xy[2 * w2], p2y = xy[2 * w2 + 1];
-  double R = rng_next(rng);
+  double R = rd->R1;
   double px = p1x + (p2x - p1x) * R;
   double py = p1y + (p2y - p1y) * R;
   const double* m = d->fine_mid + 2 * (size_t)f;
@@ -231,11 +236,11 @@ static void emit_surface(const rthx_domain_desc* d, int f, int w, double eta, in
   /* lambertSample2D: R_angle1 = Float32(rand()); cosTheta = sqrt(R_angle1)
    * (Float32); sinTheta = sqrt(1.0 - cosTheta^2) (cosTheta^2 in Float32);
    * psi = 2*pi*Float32(rand()) (Float64). */
-  float r1 = (float)rng_next(rng);
+  float r1 = (float)rd->l1;
   float ct = (float)sqrt((double)r1); /* correctly rounded Float32 sqrt */
   float ct2 = ct * ct;
   double st = sqrt(1.0 - (double)ct2);
-  float r2 = (float)rng_next(rng);
+  float r2 = (float)rd->l2;
   double cpsi;
   if (faithful) {
     double psi = TWO_PI * (double)r2;
@@ -262,15 +267,15 @@ static void emit_surface(const rthx_domain_desc* d, int f, int w, double eta, in
  * chosen by area, triangle formula (1-sqrt u1)A + sqrt u1 (1-u2) B +
  * sqrt u1 u2 C), nudged toward the midpoint, isotropic 3D direction
  * projected onto the plane: (sin(theta) cos(phi), cos(theta)). */
-static void emit_volume(const rthx_domain_desc* d, int f, double eta, int faithful, rng_t* rng,
+static void emit_volume(const rthx_domain_desc* d, int f, double eta, int faithful, const draws_t* rd,
                         double* p, double* dir) {
   const double* v = d->fine_xy + 8 * (size_t)f;
   int n = d->fine_nv[f];
   double px, py;
   if (n == 4) {
     double Ax = v[0], Ay = v[1], Bx = v[2], By = v[3], Cx = v[4], Cy = v[5], Dx = v[6], Dy = v[7];
-    double R1 = rng_next(rng), R2 = rng_next(rng);
-    double sel = rng_next(rng);
+    double R1 = rd->R1, R2 = rd->R2;
+    double sel = rd->sel;
     double a1 = 0.5 * (Ax * (By - Cy) + Bx * (Cy - Ay) + Cx * (Ay - By)) / d->fine_volume[f];
     double s1 = sqrt(R1);
     double wa = 1.0 - s1, wb = s1 * (1.0 - R2), wc = s1 * R2;
@@ -283,7 +288,7 @@ static void emit_volume(const rthx_domain_desc* d, int f, double eta, int faithf
     }
   } else {
     double Ax = v[0], Ay = v[1], Bx = v[2], By = v[3], Cx = v[4], Cy = v[5];
-    double R1 = rng_next(rng), R2 = rng_next(rng);
+    double R1 = rd->R1, R2 = rd->R2;
     double s1 = sqrt(R1);
     double wa = 1.0 - s1, wb = s1 * (1.0 - R2), wc = s1 * R2;
     px = wa * Ax + wb * Bx + wc * Cx;
@@ -293,7 +298,7 @@ static void emit_volume(const rthx_domain_desc* d, int f, double eta, int faithf
   px = px + (m[0] - px) * eta;
   py = py + (m[1] - py) * eta;
 
-  double u4 = rng_next(rng), u5 = rng_next(rng);
+  double u4 = rd->th, u5 = rd->ph;
   double st, ct;
   if (faithful) {
     double theta = acos(1.0 - 2.0 * u4);
@@ -319,10 +324,10 @@ typedef struct {
 
 /* traceRayUniform, traceRay.jl:20-70 (free path S = -ln u / beta). */
 static hit_t trace_uniform(const dom_t* D, double px, double py, double dx, double dy,
-                           double beta, double eta, int c, rng_t* rng) {
+                           double beta, double eta, int c, const draws_t* rd) {
   const rthx_domain_desc* d = D->d;
   hit_t h = {-1, {px, py}};
-  double S = beta > 0 ? -log(rng_next(rng)) / beta : INFINITY;
+  double S = beta > 0 ? -log(rd->path) / beta : INFINITY;
   for (int it = 0; it < 10000; ++it) {
     int k;
     double u = dist_to_polygon(px, py, dx, dy, d->coarse_xy + 8 * (size_t)c,
@@ -364,11 +369,11 @@ static hit_t trace_uniform(const dom_t* D, double px, double py, double dx, doub
 /* traceRayVariable, traceRay.jl:73-147 (optical-depth sampling; beta taken
  * from the fine cell containing each segment's start point). */
 static hit_t trace_variable(const dom_t* D, double px, double py, double dx, double dy, int bin,
-                            double eta, int c, rng_t* rng) {
+                            double eta, int c, const draws_t* rd) {
   const rthx_domain_desc* d = D->d;
   hit_t h = {-1, {px, py}};
   const double* beta_bin = d->beta + (size_t)bin * d->n_fine;
-  double target = -log(rng_next(rng));
+  double target = -log(rd->path);
   double acc = 0.0;
   for (int it = 0; it < 10000; ++it) {
     int k;
@@ -420,25 +425,25 @@ static hit_t trace_one(const dom_t* D, const rthx_trace_args* a, int64_t g, int6
                        double* origin) {
   const rthx_domain_desc* d = D->d;
   int faithful = (a->flags & RTHX_FLAG_FAITHFUL_SAMPLING) != 0;
-  rng_t rng;
-  rng_init(&rng, a->seed, (uint32_t)a->bin, (uint32_t)g, (uint32_t)r);
+  draws_t rd;
+  ray_draws(a->seed, (uint32_t)a->bin, (uint32_t)g, (uint32_t)r, &rd);
   double p[2], dir[2];
   int f;
   if (g < d->n_surfaces) {
     f = D->surf_face[g];
-    emit_surface(d, f, D->surf_wall[g], a->nudge, faithful, &rng, p, dir);
+    emit_surface(d, f, D->surf_wall[g], a->nudge, faithful, &rd, p, dir);
   } else {
     f = (int)(g - d->n_surfaces);
-    emit_volume(d, f, a->nudge, faithful, &rng, p, dir);
+    emit_volume(d, f, a->nudge, faithful, &rd, p, dir);
   }
   origin[0] = p[0];
   origin[1] = p[1];
   int c = D->coarse_of[f];
   if (d->uniform_beta[a->bin] > -0.1) {
     double beta = d->beta[(size_t)a->bin * d->n_fine + 0];
-    return trace_uniform(D, p[0], p[1], dir[0], dir[1], beta, a->nudge, c, &rng);
+    return trace_uniform(D, p[0], p[1], dir[0], dir[1], beta, a->nudge, c, &rd);
   }
-  return trace_variable(D, p[0], p[1], dir[0], dir[1], a->bin, a->nudge, c, &rng);
+  return trace_variable(D, p[0], p[1], dir[0], dir[1], a->bin, a->nudge, c, &rd);
 }
 
 /* ------------------------------------------------------------------------ */

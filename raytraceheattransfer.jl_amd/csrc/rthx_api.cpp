@@ -6,6 +6,8 @@
 // bin is one rthx_trace_exchange call (trace -> scan -> CSR pack on one HIP
 // stream), and the count matrix comes back as CSR for the host to turn into
 // SparseMatrixCSC (V = c/R, row_normalize!).
+// host-only translation unit: device pointers are plain pointers here
+#define RTHX_HOST_ONLY_TU 1
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -75,11 +77,13 @@ struct rthx_domain {
   hipStream_t stream = nullptr;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   rthx::DevDomain D{};
+  const rthx::DevDomain* d_dom = nullptr;  // copy of D in device memory (kernel argument)
   std::vector<void*> allocs;
   int64_t n_emitters = 0;
   int32_t n_bins = 1;
   std::vector<double> uniform_beta;  // per bin
   std::vector<double> beta_first;    // beta of fine face 0 per bin (traceRay.jl:6-11)
+  bool single_convex = false;        // one convex coarse polygon (SINGLE kernels)
   ~rthx_domain() {
     for (void* p : allocs) (void)hipFree(p);
     for (auto& e : ev)
@@ -161,7 +165,7 @@ int check_grid(const rthx_grid_desc& g, int32_t count, const char* what) {
 // polygons at once -- within an ulp of a shared edge -- can resolve
 // differently from the reference's order.
 // ---------------------------------------------------------------------------
-constexpr double kGridCellsPerPolygon = 2.0;  // cells per mean polygon extent, per axis
+constexpr double kGridCellsPerPolygon = 4.0;  // cells per mean polygon extent, per axis
 constexpr int64_t kGridMaxCellsPerPolygon = 64;
 
 // area of polygon (n <= 4 vertices) clipped to [x0,x1]x[y0,y1] (Sutherland-Hodgman)
@@ -276,9 +280,43 @@ rthx::DevGrid build_device_grid(const int32_t* nv, const double* xy, int first, 
     if (a.area != b.area) return a.area > b.area;
     return a.f < b.f;
   });
+  // A cell whose first candidate is convex and contains the whole cell (all
+  // four corners strictly inside every wall's half-plane) is flagged in bit 31
+  // of its cell_start entry: the device returns that polygon without a
+  // point-in-polygon test.
+  auto covers = [&](int f, int64_t cell) {
+    const double* v = xy + 8 * (size_t)(first + f);
+    int n = nv[first + f];
+    int pos = 0, neg = 0;
+    for (int i = 0; i < n; ++i) {
+      int j = (i + 1) % n, k2 = (i + 2) % n;
+      double cr = (v[2 * j] - v[2 * i]) * (v[2 * k2 + 1] - v[2 * j + 1]) -
+                  (v[2 * j + 1] - v[2 * i + 1]) * (v[2 * k2] - v[2 * j]);
+      pos += cr > 0;
+      neg += cr < 0;
+    }
+    if (pos != 0 && neg != 0) return false;  // not convex
+    double sgn = pos > 0 ? 1.0 : -1.0;       // CCW: interior on the left of each edge
+    int64_t i = cell % g.nx, j = cell / g.nx;
+    double cx[4] = {g.ox + i * sx, g.ox + (i + 1) * sx, g.ox + (i + 1) * sx, g.ox + i * sx};
+    double cy[4] = {g.oy + j * sy, g.oy + j * sy, g.oy + (j + 1) * sy, g.oy + (j + 1) * sy};
+    double margin = 1e-9 * std::max(sx, sy);
+    for (int e2 = 0; e2 < n; ++e2) {
+      int e3 = (e2 + 1) % n;
+      double ex = v[2 * e3] - v[2 * e2], ey = v[2 * e3 + 1] - v[2 * e2 + 1];
+      double len = std::sqrt(ex * ex + ey * ey);
+      for (int q = 0; q < 4; ++q) {
+        double side = sgn * (ex * (cy[q] - v[2 * e2 + 1]) - ey * (cx[q] - v[2 * e2])) / len;
+        if (!(side > margin)) return false;
+      }
+    }
+    return true;
+  };
   size_t k = 0;
   for (int64_t c = 0; c < ncell; ++c) {
-    cell_start_all.push_back((int32_t)(k));
+    uint32_t start = (uint32_t)k;
+    if (k < cand.size() && cand[k].cell == c && covers(cand[k].f, c)) start |= 0x80000000u;
+    cell_start_all.push_back((int32_t)start);
     while (k < cand.size() && cand[k].cell == c) {
       items_all.push_back(cand[k].f);
       ++k;
@@ -390,6 +428,26 @@ RTHX_EXPORT int rthx_domain_create(const rthx_domain_desc* desc, int32_t device,
   for (int c = 0; c < s.n_coarse; ++c)
     for (int w = 0; w < 4; ++w)
       if (s.coarse_solid[4 * c + w]) csolid[c] |= 1u << w;
+  // area(ABC)/V of every quad (emitVolumeRay2D.jl:7), evaluated exactly as the
+  // reference's expression (no contraction: -ffp-contract=off)
+  std::vector<double> trifrac(s.n_fine, 0.0);
+  for (int f = 0; f < s.n_fine; ++f) {
+    if (s.fine_nv[f] != 4) continue;
+    const double* v = s.fine_xy + 8 * (size_t)f;
+    trifrac[f] = 0.5 * (v[0] * (v[3] - v[5]) + v[2] * (v[5] - v[1]) + v[4] * (v[1] - v[3])) / s.fine_volume[f];
+  }
+  // one convex coarse polygon -> SINGLE kernels (a ray that leaves it is lost)
+  if (s.n_coarse == 1) {
+    const double* v = s.coarse_xy;
+    int n = s.coarse_nv[0], pos = 0, neg = 0;
+    for (int i = 0; i < n; ++i) {
+      int j = (i + 1) % n, k = (i + 2) % n;
+      double cr = (v[2 * j] - v[2 * i]) * (v[2 * k + 1] - v[2 * j + 1]) - (v[2 * j + 1] - v[2 * i + 1]) * (v[2 * k] - v[2 * j]);
+      pos += cr > 0;
+      neg += cr < 0;
+    }
+    d->single_convex = (pos == 0 || neg == 0);
+  }
   std::vector<int32_t> fcoarse(s.n_fine);
   for (int c = 0; c < s.n_coarse; ++c)
     for (int f = s.fine_offset[c]; f < s.fine_offset[c + 1]; ++f) fcoarse[f] = c;
@@ -419,7 +477,7 @@ RTHX_EXPORT int rthx_domain_create(const rthx_domain_desc* desc, int32_t device,
   UP(s.fine_xy, 8 * nf, D.f_xy);
   UP(s.fine_normal, 8 * nf, D.f_nrm);
   UP(s.fine_mid, 2 * nf, D.f_mid);
-  UP(s.fine_volume, nf, D.f_vol);
+  UP(trifrac.data(), nf, D.f_trifrac);
   UP(s.fine_bbox, 4 * nf, D.f_bbox);
   UP(s.fine_surface, 4 * nf, D.f_surf);
   UP(fcoarse.data(), nf, D.f_coarse);
@@ -427,7 +485,6 @@ RTHX_EXPORT int rthx_domain_create(const rthx_domain_desc* desc, int32_t device,
   UP(cell_start.data(), cell_start.size(), D.grid_cell_start);
   UP(items.data(), items.size(), D.grid_items);
   UP(s.beta, (size_t)s.n_bins * nf, D.beta);
-  UP(s.uniform_beta, (size_t)s.n_bins, D.uniform_beta);
   UP(s_face.data(), s_face.size(), D.s_face);
   UP(s_wall.data(), s_wall.size(), D.s_wall);
 #undef UP
@@ -435,6 +492,10 @@ RTHX_EXPORT int rthx_domain_create(const rthx_domain_desc* desc, int32_t device,
     int32_t zero = 0;
     int r2 = upload(d, &zero, 1, &D.grid_items, "grid_items");
     if (r2) return bail(r2);
+  }
+  {
+    int r3 = upload(d, &d->D, 1, &d->d_dom, "domain record");
+    if (r3) return bail(r3);
   }
   *out = d;
   return RTHX_OK;
@@ -539,12 +600,13 @@ RTHX_EXPORT int rthx_trace_exchange(rthx_domain* dom, const rthx_trace_args* a, 
   P.key1 = (uint32_t)(a->seed >> 32);
   P.bin = a->bin;
   P.beta_uniform = dom->beta_first[a->bin];
+  P.inv_beta_uniform = P.beta_uniform > 0 ? 1.0 / P.beta_uniform : 0.0;
   const bool uniform = dom->uniform_beta[a->bin] > -0.1;  // traceRay.jl:4
 
   hipStream_t st = dom->stream;
   HIP_TRY(hipEventRecord(dom->ev[0], st), "hipEventRecord");
   if (n_rows > 0) {
-    HIP_TRY(rthx::launch_trace(dom->D, P, uniform, pack16, (a->flags & RTHX_FLAG_FAITHFUL_SAMPLING) != 0, N, n_rows, res->stage_cols.as<uint32_t>(),
+    HIP_TRY(rthx::launch_trace(dom->d_dom, P, uniform, pack16, (a->flags & RTHX_FLAG_FAITHFUL_SAMPLING) != 0, dom->single_convex, N, n_rows, res->stage_cols.as<uint32_t>(),
                                res->stage_cnt.as<uint32_t>(), row_cap, res->row_nnz.as<uint32_t>(),
                                res->row_tallied.as<uint32_t>(), rec, lds_bytes, st),
             "trace_exchange_kernel launch");

@@ -1,5 +1,5 @@
 // rthx_device.h — device-side ray physics of the exchange-factor tracer
-// (gfx950 / CDNA4, wave64).  One ray per lane; fp64 geometry, one Philox
+// (gfx950 / CDNA4, wave64).  One ray per lane; fp64 geometry; one Philox
 // stream per ray.  Every function cites the reference file:line it follows
 // (paths relative to src/ of RayTraceHeatTransfer.jl v0.11.2).
 #pragma once
@@ -7,11 +7,27 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// Device code sees the domain arrays as global-address-space pointers, so the
+// compiler emits global_load (not flat_load) and can use SGPR base addressing;
+// host code sees plain pointers (same layout).
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(RTHX_HOST_ONLY_TU)
+#define RTHX_GLOBAL __attribute__((address_space(1)))
+#else
+#define RTHX_GLOBAL
+#endif
+
+// Diagnostic builds only (tools/ablate.sh): RTHX_ABLATE replaces parts of the
+// ray with cheap stand-ins to price them.  Results are wrong in such builds;
+// the product build has RTHX_ABLATE == 0.
+#ifndef RTHX_ABLATE
+#define RTHX_ABLATE 0
+#endif
+
 namespace rthx {
 
 // ---------------------------------------------------------------------------
-// Flattened domain in HBM (DESIGN.md "Data layout in HBM").  Passed by value
-// as a kernel argument; every pointer is device memory.
+// Flattened domain in HBM (DESIGN.md "Data layout in HBM").  One copy of this
+// record lives in device memory; kernels get its address.
 // ---------------------------------------------------------------------------
 struct DevGrid {
   double ox, oy;        // origin
@@ -24,32 +40,31 @@ struct DevGrid {
 struct DevDomain {
   int32_t n_coarse, n_fine, n_surfaces, n_bins;
   // coarse polygons
-  const int32_t* c_nv;
-  const double* c_xy;      // [n_coarse][4][2]
-  const double* c_nrm;     // [n_coarse][4][2]
-  const uint32_t* c_solid; // [n_coarse] bit w = wall w solid
-  const double* c_bbox;    // [n_coarse][4]
+  const int32_t RTHX_GLOBAL* c_nv;
+  const double RTHX_GLOBAL* c_xy;      // [n_coarse][4][2]
+  const double RTHX_GLOBAL* c_nrm;     // [n_coarse][4][2] unit inward normals
+  const uint32_t RTHX_GLOBAL* c_solid; // [n_coarse] bit w = wall w solid
+  const double RTHX_GLOBAL* c_bbox;    // [n_coarse][4]
   DevGrid c_grid;
   // fine polygons
-  const int32_t* f_offset; // [n_coarse+1]
-  const int32_t* f_nv;     // [n_fine]
-  const double* f_xy;      // [n_fine][4][2]
-  const double* f_nrm;     // [n_fine][4][2]
-  const double* f_mid;     // [n_fine][2]
-  const double* f_vol;     // [n_fine]
-  const double* f_bbox;    // [n_fine][4]
-  const int32_t* f_surf;   // [n_fine][4]  global surface index or -1
-  const int32_t* f_coarse; // [n_fine]
-  const DevGrid* f_grid;   // [n_coarse]
+  const int32_t RTHX_GLOBAL* f_offset; // [n_coarse+1]
+  const int32_t RTHX_GLOBAL* f_nv;     // [n_fine]
+  const double RTHX_GLOBAL* f_xy;      // [n_fine][4][2]
+  const double RTHX_GLOBAL* f_nrm;     // [n_fine][4][2]
+  const double RTHX_GLOBAL* f_mid;     // [n_fine][2]
+  const double RTHX_GLOBAL* f_trifrac; // [n_fine] area(ABC)/V of quads (emitVolumeRay2D.jl:7)
+  const double RTHX_GLOBAL* f_bbox;    // [n_fine][4]
+  const int32_t RTHX_GLOBAL* f_surf;   // [n_fine][4]  global surface index or -1
+  const int32_t RTHX_GLOBAL* f_coarse; // [n_fine]
+  const DevGrid RTHX_GLOBAL* f_grid;   // [n_coarse]
   // grid storage (all grids concatenated)
-  const int32_t* grid_cell_start;
-  const int32_t* grid_items;
+  const int32_t RTHX_GLOBAL* grid_cell_start;
+  const int32_t RTHX_GLOBAL* grid_items;
   // extinction
-  const double* beta;      // [n_bins][n_fine]
-  const double* uniform_beta; // [n_bins]
+  const double RTHX_GLOBAL* beta;      // [n_bins][n_fine]
   // surface emitters
-  const int32_t* s_face;   // [Ns]
-  const int32_t* s_wall;   // [Ns]
+  const int32_t RTHX_GLOBAL* s_face;   // [Ns]
+  const int32_t RTHX_GLOBAL* s_wall;   // [Ns]
 };
 
 struct TraceParams {
@@ -59,49 +74,64 @@ struct TraceParams {
   uint32_t key0, key1;     // Philox key (seed)
   int32_t bin;
   int32_t reserved;
-  double beta_uniform;     // beta of fine face 0 in `bin` (uniform path)
+  double beta_uniform;     // beta of fine face 0 in `bin` (uniform path, traceRay.jl:6-11)
+  double inv_beta_uniform; // 1 / beta_uniform (0 when beta_uniform <= 0)
 };
 
 // ---------------------------------------------------------------------------
 // Philox-4x32-10 counter RNG (Salmon et al. SC'11).  Counter (r, g, block,
-// bin), key (seed lo, seed hi); each block yields two 53-bit uniforms.
+// bin), key (seed lo, seed hi).
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
 #pragma unroll
-  for (int i = 0; i < 10; ++i) {
-    uint32_t hi0 = __umulhi(0xD2511F53u, c[0]);
-    uint32_t lo0 = 0xD2511F53u * c[0];
-    uint32_t hi1 = __umulhi(0xCD9E8D57u, c[2]);
-    uint32_t lo1 = 0xCD9E8D57u * c[2];
-    uint32_t n0 = hi1 ^ c[1] ^ k0;
-    uint32_t n2 = hi0 ^ c[3] ^ k1;
-    c[0] = n0; c[1] = lo1; c[2] = n2; c[3] = lo0;
+  for (int i = 0; i < ((RTHX_ABLATE & 1) ? 1 : 10); ++i) {
+    // one 32x32->64 multiply per product (v_mad_u64_u32) instead of mul_lo + mul_hi
+    uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
+    uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
+    uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0;
+    uint32_t n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1;
+    c[0] = n0; c[1] = (uint32_t)p1; c[2] = n2; c[3] = (uint32_t)p0;
     k0 += 0x9E3779B9u;
     k1 += 0xBB67AE85u;
   }
 }
 
-__device__ __forceinline__ double u53(uint32_t hi, uint32_t lo) {
-  uint64_t x = ((uint64_t)hi << 32) | lo;
-  return (double)(x >> 11) * 0x1.0p-53;
+// Uniform in [0, 1) with 52 random bits, built like Julia's rand(): the top
+// 52 bits of (hi:lo) as the mantissa of a double in [1, 2), minus 1.
+__device__ __forceinline__ double u52(uint32_t hi, uint32_t lo) {
+  uint32_t mhi = 0x3FF00000u | (hi >> 12);
+  uint32_t mlo = (hi << 20) | (lo >> 12);
+  return __hiloint2double((int)mhi, (int)mlo) - 1.0;
 }
 
-struct RayRng {
-  uint32_t r, g, bin, block;
-  uint32_t k0, k1;
-  double d1;
-  bool have;
-  __device__ __forceinline__ RayRng(uint32_t r_, uint32_t g_, uint32_t bin_, uint32_t k0_, uint32_t k1_)
-      : r(r_), g(g_), bin(bin_), block(0), k0(k0_), k1(k1_), d1(0.0), have(false) {}
-  __device__ __forceinline__ double next() {
-    if (have) { have = false; return d1; }
-    uint32_t c[4] = {r, g, block, bin};
+__device__ __forceinline__ double u32(uint32_t w) { return (double)w * 0x1.0p-32; }
+
+// The random draws of ray (g, r) in bin b: two Philox blocks, counters
+// (r, g, 0, b) -> a[0..3] and (r, g, 1, b) -> c[0..3] (same layout as the CPU
+// restatement, oracle/rthx_oracle.c ray_draws):
+//   R1 = u52(a0,a1)  R2 = u52(a2,a3)  path = u52(c0,c1)
+//   sel = u32(c2)    th = u32(c3)     ph = u32(a1[11:0]<<20 | a3[11:0]<<8 | c1[11:4])
+//   l1 = u32(a2)     l2 = u32(a3)     (surface Lambert draws, rounded to Float32)
+// Positions and free paths keep 52 bits like Julia's rand(); angles and the
+// triangle selection use 32 bits.  Two blocks per ray (not three).
+struct RayDraws {
+  uint32_t a[4], c[4];
+  __device__ __forceinline__ RayDraws(uint32_t r, uint32_t g, uint32_t bin, uint32_t k0, uint32_t k1) {
+    a[0] = r; a[1] = g; a[2] = 0u; a[3] = bin;
+    c[0] = r; c[1] = g; c[2] = 1u; c[3] = bin;
+    philox4x32_10(a, k0, k1);
     philox4x32_10(c, k0, k1);
-    ++block;
-    d1 = u53(c[2], c[3]);
-    have = true;
-    return u53(c[0], c[1]);
   }
+  __device__ __forceinline__ double R1() const { return u52(a[0], a[1]); }
+  __device__ __forceinline__ double R2() const { return u52(a[2], a[3]); }
+  __device__ __forceinline__ double path() const { return u52(c[0], c[1]); }
+  __device__ __forceinline__ double sel() const { return u32(c[2]); }
+  __device__ __forceinline__ double th() const { return u32(c[3]); }
+  __device__ __forceinline__ double ph() const {
+    return u32(((a[1] & 0xFFFu) << 20) | ((a[3] & 0xFFFu) << 8) | ((c[1] & 0xFFFu) >> 4));
+  }
+  __device__ __forceinline__ double l1() const { return u32(a[2]); }
+  __device__ __forceinline__ double l2() const { return u32(a[3]); }
 };
 
 // ---------------------------------------------------------------------------
@@ -169,7 +199,8 @@ __device__ __forceinline__ bool point_in_polygon(double px, double py, const dou
 // candidates ordered by overlap area so the first test usually hits.  Every
 // polygon whose bbox meets a cell is listed in it, so the polygon that
 // contains a point is always a candidate of the point's cell; the bbox scan
-// in index order remains the fallback exactly as in the reference.
+// in index order remains the fallback exactly as in the reference.  Cells
+// wholly inside their first candidate are flagged and need no test at all.
 __device__ __forceinline__ int locate(const DevGrid& g, const int32_t* __restrict__ cell_start,
                                       const int32_t* __restrict__ items, const int32_t* __restrict__ nv,
                                       const double* __restrict__ xy, const double* __restrict__ bbox,
@@ -178,7 +209,10 @@ __device__ __forceinline__ int locate(const DevGrid& g, const int32_t* __restric
   double fj = floor(__dmul_rn(py - g.oy, g.inv_y));
   if (fi >= 0.0 && fi < (double)g.nx && fj >= 0.0 && fj < (double)g.ny) {
     int cell = g.cell_base + (int)fj * g.nx + (int)fi;
-    int k0 = cell_start[cell], k1 = cell_start[cell + 1];
+    uint32_t s0 = (uint32_t)cell_start[cell];
+    int k0 = (int)(s0 & 0x7FFFFFFFu), k1 = (int)((uint32_t)cell_start[cell + 1] & 0x7FFFFFFFu);
+    // bit 31: the first candidate contains the whole cell (convex, all corners inside)
+    if ((s0 >> 31) != 0u || (RTHX_ABLATE & 8) != 0) return k1 > k0 ? items[g.item_base + k0] : 0;
     for (int k = k0; k < k1; ++k) {
       int f = items[g.item_base + k];
       if (point_in_polygon(px, py, xy + 8 * (size_t)(first + f), nv[first + f])) return f;
@@ -193,11 +227,9 @@ __device__ __forceinline__ int locate(const DevGrid& g, const int32_t* __restric
   return -1;
 }
 
-__device__ __forceinline__ int locate_fine(const DevDomain& D, int c, double px, double py) {
-  int first = D.f_offset[c];
-  int count = D.f_offset[c + 1] - first;
-  return locate(D.f_grid[c], D.grid_cell_start, D.grid_items, D.f_nv, D.f_xy, D.f_bbox, first, count,
-                px, py);
+__device__ __forceinline__ int locate_fine(const DevDomain& D, const DevGrid& g, int first, int count, double px,
+                                           double py) {
+  return locate(g, D.grid_cell_start, D.grid_items, D.f_nv, D.f_xy, D.f_bbox, first, count, px, py);
 }
 
 __device__ __forceinline__ int locate_coarse(const DevDomain& D, double px, double py) {
@@ -207,95 +239,136 @@ __device__ __forceinline__ int locate_coarse(const DevDomain& D, double px, doub
 
 #define RTHX_TWO_PI 6.283185307179586
 
-// emitSurfaceRay2D.jl:1-26 + lambertSample2D.jl:1-10 (Float32-rounded
-// Lambert draws; un-normalised in-plane direction).
-template <bool faithful>
-__device__ __forceinline__ void emit_surface(const DevDomain& D, int f, int w, double eta,
-                                             RayRng& rng, double& px, double& py, double& dx,
-                                             double& dy) {
+// ---------------------------------------------------------------------------
+// Emitter: everything a ray of emitter g needs that does not depend on the
+// ray, gathered once per workgroup (g is workgroup-uniform).
+// ---------------------------------------------------------------------------
+struct Emitter {
+  double v[8];        // polygon vertices (volume) / v[0..3] = p1, p2 (surface)
+  double mx, my;      // fine midpoint (nudge target)
+  double tri_frac;    // area(ABC)/V (quad volume)
+  double tx, ty;      // unit tangent of the emitting wall (surface)
+  int nv;
+  int coarse;
+  bool surface;
+};
+
+__device__ __forceinline__ Emitter load_emitter(const DevDomain& D, int64_t g) {
+  Emitter e{};
+  int f, w = 0;
+  e.surface = g < D.n_surfaces;
+  if (e.surface) {
+    f = D.s_face[g];
+    w = D.s_wall[g];
+  } else {
+    f = (int)(g - D.n_surfaces);
+  }
+  e.nv = D.f_nv[f];
+  e.coarse = D.f_coarse[f];
+  e.mx = D.f_mid[2 * f];
+  e.my = D.f_mid[2 * f + 1];
+  e.tri_frac = D.f_trifrac[f];
   const double* xy = D.f_xy + 8 * (size_t)f;
-  int n = D.f_nv[f];
-  int w2 = (w + 1 == n) ? 0 : w + 1;
-  double p1x = xy[2 * w], p1y = xy[2 * w + 1];
-  double p2x = xy[2 * w2], p2y = xy[2 * w2 + 1];
-  double R = rng.next();
-  px = p1x + __dmul_rn(p2x - p1x, R);
-  py = p1y + __dmul_rn(p2y - p1y, R);
-  double mx = D.f_mid[2 * f], my = D.f_mid[2 * f + 1];
-  px = px + __dmul_rn(mx - px, eta);
-  py = py + __dmul_rn(my - py, eta);
-  float r1 = (float)rng.next();
-  float ct = (float)sqrt((double)r1);
-  float ct2 = __fmul_rn(ct, ct);
-  double st = sqrt(1.0 - (double)ct2);
-  float r2 = (float)rng.next();
-  double cpsi = faithful ? cos(RTHX_TWO_PI * (double)r2) : cospi(2.0 * (double)r2);
-  double xl = __dmul_rn(st, cpsi);
-  double zl = (double)ct;
-  double ex = p2x - p1x, ey = p2y - p1y;
-  double len = sqrt(__dmul_rn(ex, ex) + __dmul_rn(ey, ey));
-  double tx = ex / len, ty = ey / len;
-  dx = __dmul_rn(tx, xl) + __dmul_rn(-ty, zl);
-  dy = __dmul_rn(ty, xl) + __dmul_rn(tx, zl);
+  if (e.surface) {
+    int w2 = (w + 1 == e.nv) ? 0 : w + 1;
+    e.v[0] = xy[2 * w]; e.v[1] = xy[2 * w + 1];
+    e.v[2] = xy[2 * w2]; e.v[3] = xy[2 * w2 + 1];
+    // xVecLocal = normalize(p2 - p1) (emitSurfaceRay2D.jl:17)
+    double ex = e.v[2] - e.v[0], ey = e.v[3] - e.v[1];
+    double len = sqrt(__dmul_rn(ex, ex) + __dmul_rn(ey, ey));
+    e.tx = ex / len;
+    e.ty = ey / len;
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) e.v[i] = xy[i];
+  }
+  return e;
 }
 
-// emitVolumeRay2D.jl:1-33.
-template <bool faithful>
-__device__ __forceinline__ void emit_volume(const DevDomain& D, int f, double eta, RayRng& rng,
-                                            double& px, double& py, double& dx, double& dy) {
-  const double* v = D.f_xy + 8 * (size_t)f;
-  int n = D.f_nv[f];
-  double Ax = v[0], Ay = v[1], Bx = v[2], By = v[3], Cx = v[4], Cy = v[5];
-  double R1 = rng.next(), R2 = rng.next();
+// emitSurfaceRay2D.jl:1-26 + lambertSample2D.jl:1-10: uniform point on the
+// wall nudged relatively toward the midpoint; cosine-law direction with the
+// reference's Float32-rounded draws, rotated into (tangent, left normal) and
+// left un-normalised (in-plane projection of a 3D unit vector).
+template <bool FAITHFUL>
+__device__ __forceinline__ void emit_surface(const Emitter& e, double eta, const RayDraws& rd, double& px,
+                                             double& py, double& dx, double& dy) {
+  double R = rd.R1();
+  px = e.v[0] + __dmul_rn(e.v[2] - e.v[0], R);
+  py = e.v[1] + __dmul_rn(e.v[3] - e.v[1], R);
+  px = px + __dmul_rn(e.mx - px, eta);
+  py = py + __dmul_rn(e.my - py, eta);
+  float r1 = (float)rd.l1();
+  float ct = (float)sqrt((double)r1);  // correctly rounded Float32 sqrt
+  float ct2 = __fmul_rn(ct, ct);
+  double st = sqrt(1.0 - (double)ct2);
+  float r2 = (float)rd.l2();
+  double cpsi = FAITHFUL ? cos(RTHX_TWO_PI * (double)r2) : cospi(2.0 * (double)r2);
+  double xl = __dmul_rn(st, cpsi);
+  double zl = (double)ct;
+  dx = __dmul_rn(e.tx, xl) + __dmul_rn(-e.ty, zl);
+  dy = __dmul_rn(e.ty, xl) + __dmul_rn(e.tx, zl);
+}
+
+// emitVolumeRay2D.jl:1-33: uniform point (quad = triangles ABC / CDA chosen
+// by area), nudged toward the midpoint, isotropic 3D direction projected on
+// the plane (sin(theta) cos(phi), cos(theta)).
+template <bool FAITHFUL>
+__device__ __forceinline__ void emit_volume(const Emitter& e, double eta, const RayDraws& rd, double& px,
+                                            double& py, double& dx, double& dy) {
+  double R1 = rd.R1(), R2 = rd.R2();
   double s1 = sqrt(R1);
   double wa = 1.0 - s1, wb = __dmul_rn(s1, 1.0 - R2), wc = __dmul_rn(s1, R2);
-  if (n == 4) {
-    double Dx = v[6], Dy = v[7];
-    double sel = rng.next();
-    double a1 = __dmul_rn(0.5, __dmul_rn(Ax, By - Cy) + __dmul_rn(Bx, Cy - Ay) + __dmul_rn(Cx, Ay - By)) /
-                D.f_vol[f];
-    if (!(sel < a1)) {
-      // (C, D, A) triangle
-      Ax = Cx; Ay = Cy; Cx = v[0]; Cy = v[1]; Bx = Dx; By = Dy;
+  double Ax = e.v[0], Ay = e.v[1], Bx = e.v[2], By = e.v[3], Cx = e.v[4], Cy = e.v[5];
+  if (e.nv == 4) {
+    double sel = rd.sel();
+    if (!(sel < e.tri_frac)) {  // (C, D, A)
+      Ax = e.v[4]; Ay = e.v[5]; Bx = e.v[6]; By = e.v[7]; Cx = e.v[0]; Cy = e.v[1];
     }
   }
   px = __dmul_rn(wa, Ax) + __dmul_rn(wb, Bx) + __dmul_rn(wc, Cx);
   py = __dmul_rn(wa, Ay) + __dmul_rn(wb, By) + __dmul_rn(wc, Cy);
-  double mx = D.f_mid[2 * f], my = D.f_mid[2 * f + 1];
-  px = px + __dmul_rn(mx - px, eta);
-  py = py + __dmul_rn(my - py, eta);
-  double u4 = rng.next(), u5 = rng.next();
+  px = px + __dmul_rn(e.mx - px, eta);
+  py = py + __dmul_rn(e.my - py, eta);
+  double u4 = rd.th(), u5 = rd.ph();
   double st, ct;
-  if (faithful) {
+  if (FAITHFUL) {
     double theta = acos(1.0 - 2.0 * u4);
     st = sin(theta);
     ct = cos(theta);
   } else {
-    ct = 1.0 - 2.0 * u4;
-    st = 2.0 * sqrt(__dmul_rn(u4, 1.0 - u4));
+    ct = 1.0 - 2.0 * u4;                       // cos(acos(x)) = x
+    st = 2.0 * sqrt(__dmul_rn(u4, 1.0 - u4));  // sin(acos(x)) = sqrt((1-x)(1+x))
   }
-  double cphi = faithful ? cos(RTHX_TWO_PI * u5) : cospi(2.0 * u5);
+  double cphi = FAITHFUL ? cos(RTHX_TWO_PI * u5) : ((RTHX_ABLATE & 4) ? (1.0 - 2.0 * u5) : cospi(2.0 * u5));
   dx = __dmul_rn(st, cphi);
   dy = ct;
 }
 
+// ---------------------------------------------------------------------------
 // traceRayUniform (traceRay.jl:20-70) and traceRayVariable (:73-147).
 // The gas branch (:31-40 / :105-116) and the solid-wall branch (:42-52 /
 // :118-128) both move the point and locate its fine cell; they are merged so
 // that the wave runs one point location for both kinds of lanes.
-template <bool UNIFORM>
+// SINGLE: the domain has one coarse polygon, so the coarse data and its fine
+// grid are workgroup-uniform and a crossing can only leave the domain.
+// ---------------------------------------------------------------------------
+template <bool UNIFORM, bool SINGLE>
 __device__ __forceinline__ int64_t trace_ray(const DevDomain& D, const TraceParams& P, int c, double& px,
-                                             double& py, double dx, double dy, RayRng& rng) {
+                                             double& py, double dx, double dy, const RayDraws& rd) {
   const double eta = P.eta;
   double S = 0.0, target = 0.0, acc = 0.0;
   if (UNIFORM) {
-    double b = P.beta_uniform;
-    S = b > 0 ? -log(rng.next()) / b : __builtin_inf();
+    S = P.beta_uniform > 0 ? ((RTHX_ABLATE & 2) ? (1.0 - rd.path()) : -log(rd.path())) * P.inv_beta_uniform
+                           : __builtin_inf();
   } else {
-    target = -log(rng.next());
+    target = -log(rd.path());
   }
   const double* beta_bin = D.beta + (size_t)P.bin * D.n_fine;
+  if (SINGLE) c = 0;
   for (int it = 0; it < 10000; ++it) {
+    const DevGrid& fg_grid = D.f_grid[c];
+    const int first = D.f_offset[c];
+    const int count = D.f_offset[c + 1] - first;
     int k;
     double u = dist_to_polygon(px, py, dx, dy, D.c_xy + 8 * (size_t)c, D.c_nrm + 8 * (size_t)c, D.c_nv[c], k);
     bool gas;
@@ -303,9 +376,9 @@ __device__ __forceinline__ int64_t trace_ray(const DevDomain& D, const TracePara
     if (UNIFORM) {
       gas = S < u;
     } else {
-      int f0 = locate_fine(D, c, px, py);
+      int f0 = locate_fine(D, fg_grid, first, count, px, py);
       if (f0 < 0) return -1;
-      beta = beta_bin[D.f_offset[c] + f0];
+      beta = beta_bin[first + f0];
       tau_b = __dmul_rn(beta, u);
       gas = acc + tau_b >= target;
     }
@@ -314,14 +387,15 @@ __device__ __forceinline__ int64_t trace_ray(const DevDomain& D, const TracePara
       double t = gas ? (UNIFORM ? S : (target - acc) / beta) - eta : u - eta;
       px = px + __dmul_rn(t, dx);
       py = py + __dmul_rn(t, dy);
-      int f = locate_fine(D, c, px, py);
+      int f = locate_fine(D, fg_grid, first, count, px, py);
       if (f < 0) return -1;
-      int fg = D.f_offset[c] + f;
+      int fg = first + f;
       if (gas) return (int64_t)D.n_surfaces + fg;
       int w;
       dist_to_polygon(px, py, dx, dy, D.f_xy + 8 * (size_t)fg, D.f_nrm + 8 * (size_t)fg, D.f_nv[fg], w);
       return D.f_surf[4 * fg + w];  // -1 if the fine wall is not solid
     }
+    if (SINGLE) return -1;  // an open wall of the only polygon leads outside: locate_coarse finds nothing
     double t = u + eta;
     px = px + __dmul_rn(t, dx);
     py = py + __dmul_rn(t, dy);
@@ -332,25 +406,20 @@ __device__ __forceinline__ int64_t trace_ray(const DevDomain& D, const TracePara
   return -1;
 }
 
-// One ray (g, r): emit then trace (traceRay.jl:1-17 dispatch done by the
-// caller through UNIFORM).  Returns absorber (-1 = lost); (ox, oy) emission
-// point, (px, py) end point.
-template <bool UNIFORM, bool FAITHFUL>
-__device__ __forceinline__ int64_t trace_one(const DevDomain& D, const TraceParams& P, int64_t g, int64_t r,
-                                             double& ox, double& oy, double& px, double& py) {
-  RayRng rng((uint32_t)r, (uint32_t)g, (uint32_t)P.bin, P.key0, P.key1);
+// One ray (g, r) of emitter e: emit then trace.  Returns absorber (-1 =
+// lost); (ox, oy) emission point, (px, py) end point.
+template <bool UNIFORM, bool FAITHFUL, bool SINGLE>
+__device__ __forceinline__ int64_t trace_one(const DevDomain& D, const TraceParams& P, const Emitter& e, int64_t g,
+                                             int64_t r, double& ox, double& oy, double& px, double& py) {
+  const RayDraws rd((uint32_t)r, (uint32_t)g, (uint32_t)P.bin, P.key0, P.key1);
   double dx, dy;
-  int f;
-  if (g < D.n_surfaces) {
-    f = D.s_face[g];
-    emit_surface<FAITHFUL>(D, f, D.s_wall[g], P.eta, rng, px, py, dx, dy);
-  } else {
-    f = (int)(g - D.n_surfaces);
-    emit_volume<FAITHFUL>(D, f, P.eta, rng, px, py, dx, dy);
-  }
+  if (e.surface)
+    emit_surface<FAITHFUL>(e, P.eta, rd, px, py, dx, dy);
+  else
+    emit_volume<FAITHFUL>(e, P.eta, rd, px, py, dx, dy);
   ox = px;
   oy = py;
-  return trace_ray<UNIFORM>(D, P, D.f_coarse[f], px, py, dx, dy, rng);
+  return trace_ray<UNIFORM, SINGLE>(D, P, e.coarse, px, py, dx, dy, rd);
 }
 
 }  // namespace rthx

@@ -20,8 +20,8 @@ struct RecordParams {
   double* end;          // [n*R*2]
 };
 
-hipError_t launch_trace(const DevDomain& D, const TraceParams& P, bool uniform, bool pack16, bool faithful,
-                        int64_t n_emitters, int64_t n_rows, uint32_t* stage_cols, uint32_t* stage_cnt, int64_t row_cap,
+hipError_t launch_trace(const DevDomain* D, const TraceParams& P, bool uniform, bool pack16, bool faithful,
+                        bool single, int64_t n_emitters, int64_t n_rows, uint32_t* stage_cols, uint32_t* stage_cnt, int64_t row_cap,
                         uint32_t* row_nnz, uint32_t* row_tallied, const RecordParams& rec, size_t lds_bytes,
                         hipStream_t stream);
 

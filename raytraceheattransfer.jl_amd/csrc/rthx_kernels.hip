@@ -21,14 +21,15 @@ __device__ __forceinline__ uint32_t lane_id() {
   return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
 }
 
-template <bool UNIFORM, bool PACK16, bool FAITHFUL>
-__global__ __launch_bounds__(kTraceThreads) void trace_exchange_kernel(DevDomain D, TraceParams P, int64_t n_emitters,
+template <bool UNIFORM, bool PACK16, bool FAITHFUL, bool SINGLE, bool REC>
+__global__ __launch_bounds__(kTraceThreads) void trace_exchange_kernel(const DevDomain* __restrict__ Dp, TraceParams P, int64_t n_emitters,
                                                                      uint32_t* __restrict__ stage_cols,
                                                                      uint32_t* __restrict__ stage_cnt,
                                                                      int64_t row_cap, uint32_t* __restrict__ row_nnz,
                                                                      uint32_t* __restrict__ row_tallied,
                                                                      RecordParams rec) {
   extern __shared__ uint32_t hist[];
+  const DevDomain& D = *Dp;
   __shared__ uint32_t wave_sum[kTraceThreads / 64];
   __shared__ uint32_t s_running;
   __shared__ uint32_t s_tallied;
@@ -41,16 +42,19 @@ __global__ __launch_bounds__(kTraceThreads) void trace_exchange_kernel(DevDomain
   for (int64_t w = tid; w < n_words; w += kTraceThreads) hist[w] = 0u;
   if (tid == 0) { s_running = 0u; s_tallied = 0u; }
 
+  const Emitter e = load_emitter(D, g);
+
   // recorded emitter?  (RayRecorder ids, parallelRayTracing.jl:108)
   int rec_slot = -1;
-  for (int i = 0; i < rec.n; ++i)
-    if (rec.ids[i] == g) { rec_slot = i; break; }
+  if (REC)
+    for (int i = 0; i < rec.n; ++i)
+      if (rec.ids[i] == g) { rec_slot = i; break; }
   __syncthreads();
 
   uint32_t tallied = 0;
   for (int64_t r = tid; r < P.R; r += kTraceThreads) {
     double ox, oy, px, py;
-    int64_t a = trace_one<UNIFORM, FAITHFUL>(D, P, g, r, ox, oy, px, py);
+    int64_t a = trace_one<UNIFORM, FAITHFUL, SINGLE>(D, P, e, g, r, ox, oy, px, py);
     if (a >= 0) {
       if (PACK16)
         atomicAdd(&hist[a >> 1], 1u << ((uint32_t)(a & 1) << 4));
@@ -58,7 +62,7 @@ __global__ __launch_bounds__(kTraceThreads) void trace_exchange_kernel(DevDomain
         atomicAdd(&hist[a], 1u);
       ++tallied;
     }
-    if (rec_slot >= 0) {
+    if (REC && rec_slot >= 0) {
       size_t k = (size_t)rec_slot * (size_t)P.R + (size_t)r;
       rec.ok[k] = a >= 0 ? 1 : 0;
       rec.orig[2 * k] = ox; rec.orig[2 * k + 1] = oy;
@@ -173,12 +177,12 @@ __global__ __launch_bounds__(256) void csr_pack_kernel(const uint32_t* __restric
 // ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
-template <bool UNIFORM, bool PACK16, bool FAITHFUL>
-static hipError_t launch_trace_t(const DevDomain& D, const TraceParams& P, int64_t n_emitters, int64_t n_rows,
+template <bool UNIFORM, bool PACK16, bool FAITHFUL, bool SINGLE, bool REC>
+static hipError_t launch_trace_t(const DevDomain* D, const TraceParams& P, int64_t n_emitters, int64_t n_rows,
                                  uint32_t* stage_cols, uint32_t* stage_cnt, int64_t row_cap, uint32_t* row_nnz,
                                  uint32_t* row_tallied, const RecordParams& rec, size_t lds_bytes,
                                  hipStream_t stream) {
-  auto kern = trace_exchange_kernel<UNIFORM, PACK16, FAITHFUL>;
+  auto kern = trace_exchange_kernel<UNIFORM, PACK16, FAITHFUL, SINGLE, REC>;
   if (lds_bytes > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)lds_bytes);
@@ -189,13 +193,32 @@ static hipError_t launch_trace_t(const DevDomain& D, const TraceParams& P, int64
   return hipGetLastError();
 }
 
-hipError_t launch_trace(const DevDomain& D, const TraceParams& P, bool uniform, bool pack16, bool faithful,
-                        int64_t n_emitters, int64_t n_rows, uint32_t* stage_cols, uint32_t* stage_cnt,
+template <bool UNIFORM, bool PACK16, bool FAITHFUL>
+static hipError_t launch_trace_s(bool single, const DevDomain* D, const TraceParams& P, int64_t n_emitters,
+                                 int64_t n_rows, uint32_t* stage_cols, uint32_t* stage_cnt, int64_t row_cap,
+                                 uint32_t* row_nnz, uint32_t* row_tallied, const RecordParams& rec,
+                                 size_t lds_bytes, hipStream_t stream) {
+  // Recording is a plotting aid: one generic (non-SINGLE) instance carries it.
+  if (rec.n > 0)
+    return launch_trace_t<UNIFORM, PACK16, FAITHFUL, false, true>(D, P, n_emitters, n_rows, stage_cols, stage_cnt,
+                                                                  row_cap, row_nnz, row_tallied, rec, lds_bytes,
+                                                                  stream);
+  if (single)
+    return launch_trace_t<UNIFORM, PACK16, FAITHFUL, true, false>(D, P, n_emitters, n_rows, stage_cols, stage_cnt,
+                                                                  row_cap, row_nnz, row_tallied, rec, lds_bytes,
+                                                                  stream);
+  return launch_trace_t<UNIFORM, PACK16, FAITHFUL, false, false>(D, P, n_emitters, n_rows, stage_cols, stage_cnt,
+                                                                 row_cap, row_nnz, row_tallied, rec, lds_bytes,
+                                                                 stream);
+}
+
+hipError_t launch_trace(const DevDomain* D, const TraceParams& P, bool uniform, bool pack16, bool faithful,
+                        bool single, int64_t n_emitters, int64_t n_rows, uint32_t* stage_cols, uint32_t* stage_cnt,
                         int64_t row_cap, uint32_t* row_nnz, uint32_t* row_tallied, const RecordParams& rec,
                         size_t lds_bytes, hipStream_t stream) {
-#define RTHX_LAUNCH(U, P16, F)                                                                                  \
-  return launch_trace_t<U, P16, F>(D, P, n_emitters, n_rows, stage_cols, stage_cnt, row_cap, row_nnz, row_tallied, \
-                                   rec, lds_bytes, stream)
+#define RTHX_LAUNCH(U, P16, F)                                                                                 \
+  return launch_trace_s<U, P16, F>(single, D, P, n_emitters, n_rows, stage_cols, stage_cnt, row_cap, row_nnz, \
+                                   row_tallied, rec, lds_bytes, stream)
   if (faithful) {
     if (uniform) { if (pack16) RTHX_LAUNCH(true, true, true); else RTHX_LAUNCH(true, false, true); }
     if (pack16) RTHX_LAUNCH(false, true, true); else RTHX_LAUNCH(false, false, true);

@@ -1,0 +1,18 @@
+"""Per-ray view of the trace kernel's SQ counters (tools/gpu_sq.sh output)."""
+import json
+import sys
+
+d = json.load(open(sys.argv[1]))
+rays = float(sys.argv[2])
+k = next(x for x in d if "trace_exchange_kernel" in x)
+c = {n: v["mean"] for n, v in d[k].items()}
+wr = rays / 64.0  # wave-rays
+print("kernel", k)
+for n in sorted(c):
+    print(f"  {n:26s} {c[n]:16.4g}   per wave-ray {c[n] / wr:10.2f}")
+if "SQ_THREAD_CYCLES_VALU" in c and "SQ_ACTIVE_INST_VALU" in c:
+    print("  lane utilisation (THREAD_CYCLES_VALU / (64*ACTIVE_INST_VALU)):",
+          round(c["SQ_THREAD_CYCLES_VALU"] / (64 * c["SQ_ACTIVE_INST_VALU"]), 3))
+if "SQ_WAIT_ANY" in c and "SQ_WAVE_CYCLES" in c:
+    print("  wait fraction:", round(c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"], 3),
+          " issue-stall fraction:", round(c.get("SQ_WAIT_INST_ANY", 0) / c["SQ_WAVE_CYCLES"], 3))
