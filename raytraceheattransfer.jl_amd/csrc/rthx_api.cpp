@@ -19,6 +19,7 @@
 #include <vector>
 
 #include "../../include/rthx.h"
+#include "rthx_grid.h"
 #include "rthx_kernels.h"
 
 #define RTHX_EXPORT extern "C" __attribute__((visibility("default")))
@@ -149,180 +150,21 @@ int check_grid(const rthx_grid_desc& g, int32_t count, const char* what) {
   return RTHX_OK;
 }
 
-// ---------------------------------------------------------------------------
-// Device point-location grid (DESIGN.md "Point location").
-//
-// The reference locates a point with a uniform grid of cell size
-// 2*sqrt(mean area) whose cells list, in ascending order, every polygon whose
-// bbox meets the cell (spatialAccelerations.jl:2-59), then tests candidates in
-// order until the first point-in-polygon hit (findFace2D.jl:2-27).  With
-// ~9 candidates per cell that is the single largest cost of a ray on the GPU.
-// The device grid keeps the rule "every polygon whose bbox meets the cell is
-// a candidate" but uses cells of about half a polygon (per axis, from the mean
-// bbox extent), and orders each cell's candidates by the area of the polygon
-// inside the cell (largest first, ties by index), so that the first
-// point-in-polygon test nearly always hits.  Only a point that lies inside two
-// polygons at once -- within an ulp of a shared edge -- can resolve
-// differently from the reference's order.
-// ---------------------------------------------------------------------------
-constexpr double kGridCellsPerPolygon = 4.0;  // cells per mean polygon extent, per axis
-constexpr int64_t kGridMaxCellsPerPolygon = 64;
+// Device point-location grids: rthx_grid.cpp.  Cells per mean polygon extent
+// (per axis): at 2 a cell holds at most one vertex of a regular mesh.
+constexpr double kGridCellsPerPolygon = 2.0;
 
-// area of polygon (n <= 4 vertices) clipped to [x0,x1]x[y0,y1] (Sutherland-Hodgman)
-double clipped_area(const double* xy, int n, double x0, double x1, double y0, double y1) {
-  double a[16][2], b[16][2];
-  int na = n;
-  for (int i = 0; i < n; ++i) { a[i][0] = xy[2 * i]; a[i][1] = xy[2 * i + 1]; }
-  for (int edge = 0; edge < 4 && na > 0; ++edge) {
-    int nb = 0;
-    for (int i = 0; i < na; ++i) {
-      const double* P = a[i];
-      const double* Q = a[(i + 1) % na];
-      auto inside = [&](const double* v) {
-        switch (edge) {
-          case 0: return v[0] >= x0;
-          case 1: return v[0] <= x1;
-          case 2: return v[1] >= y0;
-          default: return v[1] <= y1;
-        }
-      };
-      auto cut = [&](double* out) {
-        double t;
-        switch (edge) {
-          case 0: t = (x0 - P[0]) / (Q[0] - P[0]); break;
-          case 1: t = (x1 - P[0]) / (Q[0] - P[0]); break;
-          case 2: t = (y0 - P[1]) / (Q[1] - P[1]); break;
-          default: t = (y1 - P[1]) / (Q[1] - P[1]); break;
-        }
-        out[0] = P[0] + t * (Q[0] - P[0]);
-        out[1] = P[1] + t * (Q[1] - P[1]);
-      };
-      bool pin = inside(P), qin = inside(Q);
-      if (pin && nb < 16) { b[nb][0] = P[0]; b[nb][1] = P[1]; ++nb; }
-      if (pin != qin && nb < 16) { cut(b[nb]); ++nb; }
-    }
-    for (int i = 0; i < nb; ++i) { a[i][0] = b[i][0]; a[i][1] = b[i][1]; }
-    na = nb;
-  }
-  double A = 0.0;
-  for (int i = 0; i < na; ++i) {
-    int j = (i + 1) % na;
-    A += a[i][0] * a[j][1] - a[j][0] * a[i][1];
-  }
-  return std::fabs(0.5 * A);
-}
-
-// Build one device grid over polygons [first, first+count) and append its
-// cells / items to the shared arrays.
-rthx::DevGrid build_device_grid(const int32_t* nv, const double* xy, int first, int count,
-                                std::vector<int32_t>& cell_start_all, std::vector<int32_t>& items_all) {
-  double minx = INFINITY, maxx = -INFINITY, miny = INFINITY, maxy = -INFINITY, sw = 0.0, sh = 0.0;
-  std::vector<double> bb(4 * (size_t)count);
-  for (int f = 0; f < count; ++f) {
-    const double* v = xy + 8 * (size_t)(first + f);
-    double a = INFINITY, b = -INFINITY, c = INFINITY, d = -INFINITY;
-    for (int i = 0; i < nv[first + f]; ++i) {
-      a = std::min(a, v[2 * i]); b = std::max(b, v[2 * i]);
-      c = std::min(c, v[2 * i + 1]); d = std::max(d, v[2 * i + 1]);
-    }
-    bb[4 * f] = a; bb[4 * f + 1] = b; bb[4 * f + 2] = c; bb[4 * f + 3] = d;
-    minx = std::min(minx, a); maxx = std::max(maxx, b); miny = std::min(miny, c); maxy = std::max(maxy, d);
-    sw += b - a;
-    sh += d - c;
-  }
-  double ext = std::max(maxx - minx, maxy - miny);
-  double sx = std::max(sw / count / kGridCellsPerPolygon, 1e-12 * ext);
-  double sy = std::max(sh / count / kGridCellsPerPolygon, 1e-12 * ext);
-  double padx = 0.01 * sx, pady = 0.01 * sy;
-  auto dims = [&](double& nxd, double& nyd) {
-    nxd = std::max(1.0, std::ceil((maxx - minx + 2 * padx) / sx));
-    nyd = std::max(1.0, std::ceil((maxy - miny + 2 * pady) / sy));
-  };
-  double nxd, nyd;
-  dims(nxd, nyd);
-  const double cap = (double)std::max<int64_t>(64, kGridMaxCellsPerPolygon * (int64_t)count);
-  if (nxd * nyd > cap) {
-    double k = std::sqrt(nxd * nyd / cap);
-    sx *= k; sy *= k; padx = 0.01 * sx; pady = 0.01 * sy;
-    dims(nxd, nyd);
-  }
+rthx::DevGrid add_grid(const int32_t* nv, const double* xy, int first, int count,
+                       std::vector<rthx::CellRec>& cells, std::vector<int32_t>& lists, std::vector<int32_t>& items) {
   rthx::DevGrid g{};
-  g.ox = minx - padx;
-  g.oy = miny - pady;
-  g.inv_x = 1.0 / sx;
-  g.inv_y = 1.0 / sy;
-  g.nx = (int32_t)nxd;
-  g.ny = (int32_t)nyd;
-  g.cell_base = (int32_t)cell_start_all.size();
-  g.item_base = (int32_t)items_all.size();
-  const int64_t ncell = (int64_t)g.nx * g.ny;
-  struct Cand { int64_t cell; int32_t f; double area; };
-  std::vector<Cand> cand;
-  cand.reserve((size_t)count * 9);
-  for (int f = 0; f < count; ++f) {
-    // same expression as the device lookup, so a point of f maps into [i0, i1]
-    int64_t i0 = (int64_t)std::floor((bb[4 * f] - g.ox) * g.inv_x);
-    int64_t i1 = (int64_t)std::floor((bb[4 * f + 1] - g.ox) * g.inv_x);
-    int64_t j0 = (int64_t)std::floor((bb[4 * f + 2] - g.oy) * g.inv_y);
-    int64_t j1 = (int64_t)std::floor((bb[4 * f + 3] - g.oy) * g.inv_y);
-    i0 = std::max<int64_t>(0, i0); j0 = std::max<int64_t>(0, j0);
-    i1 = std::min<int64_t>(g.nx - 1, i1); j1 = std::min<int64_t>(g.ny - 1, j1);
-    const double* v = xy + 8 * (size_t)(first + f);
-    for (int64_t j = j0; j <= j1; ++j)
-      for (int64_t i = i0; i <= i1; ++i) {
-        double cx0 = g.ox + i * sx, cy0 = g.oy + j * sy;
-        double area = clipped_area(v, nv[first + f], cx0, cx0 + sx, cy0, cy0 + sy);
-        cand.push_back({j * g.nx + i, f, area});
-      }
-  }
-  std::sort(cand.begin(), cand.end(), [](const Cand& a, const Cand& b) {
-    if (a.cell != b.cell) return a.cell < b.cell;
-    if (a.area != b.area) return a.area > b.area;
-    return a.f < b.f;
-  });
-  // A cell whose first candidate is convex and contains the whole cell (all
-  // four corners strictly inside every wall's half-plane) is flagged in bit 31
-  // of its cell_start entry: the device returns that polygon without a
-  // point-in-polygon test.
-  auto covers = [&](int f, int64_t cell) {
-    const double* v = xy + 8 * (size_t)(first + f);
-    int n = nv[first + f];
-    int pos = 0, neg = 0;
-    for (int i = 0; i < n; ++i) {
-      int j = (i + 1) % n, k2 = (i + 2) % n;
-      double cr = (v[2 * j] - v[2 * i]) * (v[2 * k2 + 1] - v[2 * j + 1]) -
-                  (v[2 * j + 1] - v[2 * i + 1]) * (v[2 * k2] - v[2 * j]);
-      pos += cr > 0;
-      neg += cr < 0;
-    }
-    if (pos != 0 && neg != 0) return false;  // not convex
-    double sgn = pos > 0 ? 1.0 : -1.0;       // CCW: interior on the left of each edge
-    int64_t i = cell % g.nx, j = cell / g.nx;
-    double cx[4] = {g.ox + i * sx, g.ox + (i + 1) * sx, g.ox + (i + 1) * sx, g.ox + i * sx};
-    double cy[4] = {g.oy + j * sy, g.oy + j * sy, g.oy + (j + 1) * sy, g.oy + (j + 1) * sy};
-    double margin = 1e-9 * std::max(sx, sy);
-    for (int e2 = 0; e2 < n; ++e2) {
-      int e3 = (e2 + 1) % n;
-      double ex = v[2 * e3] - v[2 * e2], ey = v[2 * e3 + 1] - v[2 * e2 + 1];
-      double len = std::sqrt(ex * ex + ey * ey);
-      for (int q = 0; q < 4; ++q) {
-        double side = sgn * (ex * (cy[q] - v[2 * e2 + 1]) - ey * (cx[q] - v[2 * e2])) / len;
-        if (!(side > margin)) return false;
-      }
-    }
-    return true;
-  };
-  size_t k = 0;
-  for (int64_t c = 0; c < ncell; ++c) {
-    uint32_t start = (uint32_t)k;
-    if (k < cand.size() && cand[k].cell == c && covers(cand[k].f, c)) start |= 0x80000000u;
-    cell_start_all.push_back((int32_t)start);
-    while (k < cand.size() && cand[k].cell == c) {
-      items_all.push_back(cand[k].f);
-      ++k;
-    }
-  }
-  cell_start_all.push_back((int32_t)k);
+  g.cell_base = (int32_t)cells.size();
+  rthx::GridBuild b = rthx::build_cell_grid(nv, xy, first, count, kGridCellsPerPolygon, cells, lists, items);
+  g.ox = b.ox;
+  g.oy = b.oy;
+  g.inv_x = b.inv_x;
+  g.inv_y = b.inv_y;
+  g.nx = b.nx;
+  g.ny = b.ny;
   return g;
 }
 
@@ -453,13 +295,15 @@ RTHX_EXPORT int rthx_domain_create(const rthx_domain_desc* desc, int32_t device,
     for (int f = s.fine_offset[c]; f < s.fine_offset[c + 1]; ++f) fcoarse[f] = c;
 
   // device point-location grids: coarse first, then one per coarse polygon
-  std::vector<int32_t> cell_start, items;
-  D.c_grid = build_device_grid(s.coarse_nv, s.coarse_xy, 0, s.n_coarse, cell_start, items);
+  std::vector<rthx::CellRec> gcells;
+  std::vector<int32_t> glists, gitems;
+  D.c_grid = add_grid(s.coarse_nv, s.coarse_xy, 0, s.n_coarse, gcells, glists, gitems);
   std::vector<rthx::DevGrid> fgrids(s.n_coarse);
   for (int c = 0; c < s.n_coarse; ++c)
-    fgrids[c] = build_device_grid(s.fine_nv, s.fine_xy, s.fine_offset[c], s.fine_offset[c + 1] - s.fine_offset[c],
-                                  cell_start, items);
-  if (cell_start.size() >= (1ull << 31) || items.size() >= (1ull << 31)) return bail(fail(RTHX_ERANGE, "grids too large"));
+    fgrids[c] = add_grid(s.fine_nv, s.fine_xy, s.fine_offset[c], s.fine_offset[c + 1] - s.fine_offset[c], gcells,
+                         glists, gitems);
+  if (gcells.size() >= (1ull << 30) || gitems.size() >= (1ull << 31)) return bail(fail(RTHX_ERANGE, "grids too large"));
+  if (gitems.empty()) gitems.push_back(0);
 
   const size_t nc = s.n_coarse, nf = s.n_fine;
 #define UP(src, n, dst)                                          \
@@ -482,17 +326,13 @@ RTHX_EXPORT int rthx_domain_create(const rthx_domain_desc* desc, int32_t device,
   UP(s.fine_surface, 4 * nf, D.f_surf);
   UP(fcoarse.data(), nf, D.f_coarse);
   UP(fgrids.data(), nc, D.f_grid);
-  UP(cell_start.data(), cell_start.size(), D.grid_cell_start);
-  UP(items.data(), items.size(), D.grid_items);
+  UP(reinterpret_cast<const rthx::DevCell*>(gcells.data()), gcells.size(), D.grid_cells);
+  UP(glists.data(), glists.size(), D.grid_lists);
+  UP(gitems.data(), gitems.size(), D.grid_items);
   UP(s.beta, (size_t)s.n_bins * nf, D.beta);
   UP(s_face.data(), s_face.size(), D.s_face);
   UP(s_wall.data(), s_wall.size(), D.s_wall);
 #undef UP
-  if (!D.grid_items) {  // an all-empty grid still needs a valid pointer
-    int32_t zero = 0;
-    int r2 = upload(d, &zero, 1, &D.grid_items, "grid_items");
-    if (r2) return bail(r2);
-  }
   {
     int r3 = upload(d, &d->D, 1, &d->d_dom, "domain record");
     if (r3) return bail(r3);

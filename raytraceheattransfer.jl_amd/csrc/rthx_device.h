@@ -33,8 +33,17 @@ struct DevGrid {
   double ox, oy;        // origin
   double inv_x, inv_y;  // 1/cell size in x and y
   int32_t nx, ny;
-  int32_t cell_base;    // offset of this grid's cell_start in grid_cell_start
-  int32_t item_base;    // offset of this grid's items in grid_items
+  int32_t cell_base;    // offset of this grid's cells in grid_cells (and grid_lists / 2)
+  int32_t reserved;
+};
+
+// Point-location cell record (built by rthx_grid.cpp, layout = CellRec):
+// code = (a0 x + b0 y + c0 < 0) | (a1 x + b1 y + c1 < 0) << 1 selects leaf[code]:
+// >= 0 polygon, -1 outside all polygons, -2 test the cell's candidate list.
+struct alignas(16) DevCell {
+  double a0, b0, c0;
+  double a1, b1, c1;
+  int32_t leaf[4];
 };
 
 struct DevDomain {
@@ -58,7 +67,8 @@ struct DevDomain {
   const int32_t RTHX_GLOBAL* f_coarse; // [n_fine]
   const DevGrid RTHX_GLOBAL* f_grid;   // [n_coarse]
   // grid storage (all grids concatenated)
-  const int32_t RTHX_GLOBAL* grid_cell_start;
+  const DevCell RTHX_GLOBAL* grid_cells;
+  const int32_t RTHX_GLOBAL* grid_lists;  // per cell: (start, count) into grid_items
   const int32_t RTHX_GLOBAL* grid_items;
   // extinction
   const double RTHX_GLOBAL* beta;      // [n_bins][n_fine]
@@ -194,28 +204,35 @@ __device__ __forceinline__ bool point_in_polygon(double px, double py, const dou
 
 // findFace2D, findFace2D.jl:48-68 (grid :2-27, bbox fallback :30-45).
 // Polygons [first, first+count) of (nv, xy, bbox); returns local index or -1.
-// The grid is the device acceleration grid built by rthx_domain_create
-// (DESIGN.md "Point location"): finer than the reference's, with each cell's
-// candidates ordered by overlap area so the first test usually hits.  Every
-// polygon whose bbox meets a cell is listed in it, so the polygon that
-// contains a point is always a candidate of the point's cell; the bbox scan
-// in index order remains the fallback exactly as in the reference.  Cells
-// wholly inside their first candidate are flagged and need no test at all.
-__device__ __forceinline__ int locate(const DevGrid& g, const int32_t* __restrict__ cell_start,
-                                      const int32_t* __restrict__ items, const int32_t* __restrict__ nv,
-                                      const double* __restrict__ xy, const double* __restrict__ bbox,
-                                      int first, int count, double px, double py) {
+// The grid is the device point-location grid built by rthx_domain_create
+// (rthx_grid.cpp, DESIGN.md "Point location"): each cell record splits the
+// cell by at most two polygon-edge lines into regions verified to lie in one
+// polygon each, so a lookup is two line tests for every lane; cells that do
+// not fit fall back to their candidate list and the point-in-polygon loop.
+// A point outside every polygon of the cell ends, as in the reference, in the
+// bbox-prefiltered scan in index order.
+__device__ __forceinline__ int locate(const DevGrid& g, const DevCell RTHX_GLOBAL* __restrict__ cells,
+                                      const int32_t RTHX_GLOBAL* __restrict__ lists,
+                                      const int32_t RTHX_GLOBAL* __restrict__ items, const int32_t* __restrict__ nv,
+                                      const double* __restrict__ xy, const double* __restrict__ bbox, int first,
+                                      int count, double px, double py) {
   double fi = floor(__dmul_rn(px - g.ox, g.inv_x));
   double fj = floor(__dmul_rn(py - g.oy, g.inv_y));
   if (fi >= 0.0 && fi < (double)g.nx && fj >= 0.0 && fj < (double)g.ny) {
-    int cell = g.cell_base + (int)fj * g.nx + (int)fi;
-    uint32_t s0 = (uint32_t)cell_start[cell];
-    int k0 = (int)(s0 & 0x7FFFFFFFu), k1 = (int)((uint32_t)cell_start[cell + 1] & 0x7FFFFFFFu);
-    // bit 31: the first candidate contains the whole cell (convex, all corners inside)
-    if ((s0 >> 31) != 0u || (RTHX_ABLATE & 8) != 0) return k1 > k0 ? items[g.item_base + k0] : 0;
-    for (int k = k0; k < k1; ++k) {
-      int f = items[g.item_base + k];
-      if (point_in_polygon(px, py, xy + 8 * (size_t)(first + f), nv[first + f])) return f;
+    const int cell = g.cell_base + (int)fj * g.nx + (int)fi;
+    const DevCell c = cells[cell];
+    double s0 = __dmul_rn(c.a0, px) + __dmul_rn(c.b0, py) + c.c0;
+    double s1 = __dmul_rn(c.a1, px) + __dmul_rn(c.b1, py) + c.c1;
+    int code = (s0 < 0.0 ? 1 : 0) | (s1 < 0.0 ? 2 : 0);
+    int leaf = code == 0 ? c.leaf[0] : code == 1 ? c.leaf[1] : code == 2 ? c.leaf[2] : c.leaf[3];
+    if (RTHX_ABLATE & 8) return leaf < 0 ? 0 : leaf;
+    if (leaf >= 0) return leaf;
+    if (leaf == -2) {
+      const int k0 = lists[2 * cell], k1 = k0 + lists[2 * cell + 1];
+      for (int k = k0; k < k1; ++k) {
+        int f = items[k];
+        if (point_in_polygon(px, py, xy + 8 * (size_t)(first + f), nv[first + f])) return f;
+      }
     }
   }
   for (int f = 0; f < count; ++f) {
@@ -229,11 +246,11 @@ __device__ __forceinline__ int locate(const DevGrid& g, const int32_t* __restric
 
 __device__ __forceinline__ int locate_fine(const DevDomain& D, const DevGrid& g, int first, int count, double px,
                                            double py) {
-  return locate(g, D.grid_cell_start, D.grid_items, D.f_nv, D.f_xy, D.f_bbox, first, count, px, py);
+  return locate(g, D.grid_cells, D.grid_lists, D.grid_items, D.f_nv, D.f_xy, D.f_bbox, first, count, px, py);
 }
 
 __device__ __forceinline__ int locate_coarse(const DevDomain& D, double px, double py) {
-  return locate(D.c_grid, D.grid_cell_start, D.grid_items, D.c_nv, D.c_xy, D.c_bbox, 0, D.n_coarse, px,
+  return locate(D.c_grid, D.grid_cells, D.grid_lists, D.grid_items, D.c_nv, D.c_xy, D.c_bbox, 0, D.n_coarse, px,
                 py);
 }
 

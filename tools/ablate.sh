@@ -11,5 +11,6 @@ for m in "$@"; do
   mkdir -p $d
   /opt/rocm/bin/hipcc $FLAGS -DRTHX_ABLATE=$m -c -o $d/k.o $CSRC/rthx_kernels.hip
   /opt/rocm/bin/hipcc $FLAGS -DRTHX_ABLATE=$m -x hip -c -o $d/a.o $CSRC/rthx_api.cpp
-  /opt/rocm/bin/hipcc $FLAGS -shared -o $d/librthx.so $d/k.o $d/a.o
+  g++ -O2 -std=c++17 -fPIC -ffp-contract=off -c -o $d/g.o $CSRC/rthx_grid.cpp
+  /opt/rocm/bin/hipcc $FLAGS -shared -o $d/librthx.so $d/k.o $d/a.o $d/g.o
 done
