@@ -144,6 +144,28 @@ struct RayDraws {
   __device__ __forceinline__ double l2() const { return u32(a[3]); }
 };
 
+// -ln(u) for u in [0, 1) (u = 0 -> +inf): fdlibm's __ieee754_log reduction
+// (x in [sqrt(2)/2, sqrt(2)), s = f/(2+f), degree-14 polynomial), <= 1 ulp
+// from the correctly rounded value; about half the instructions of ocml's
+// double-double log.  The free path S = -ln(u)/beta (traceRay.jl:25,79).
+__device__ __forceinline__ double neg_log_unit(double u) {
+  if (!(u > 0.0)) return __builtin_inf();
+  uint32_t hi = (uint32_t)__double2hiint(u);
+  uint32_t lo = (uint32_t)__double2loint(u);
+  int k = (int)((hi >> 20) & 0x7FFu) - 1023;
+  uint32_t hm = hi & 0x000FFFFFu;
+  uint32_t i = (hm + 0x95F64u) & 0x100000u;
+  double x = __hiloint2double((int)(hm | (i ^ 0x3FF00000u)), (int)lo);
+  k += (int)(i >> 20);
+  double f = x - 1.0;
+  double s = f / (2.0 + f), z = s * s, w = z * z;
+  double t1 = w * (3.999999999940941908e-01 + w * (2.222219843214978396e-01 + w * 1.531383769920937332e-01));
+  double t2 = z * (6.666666666666735130e-01 +
+                   w * (2.857142874366239149e-01 + w * (1.818357216161805012e-01 + w * 1.479819860511658591e-01)));
+  double R = t2 + t1, hfsq = 0.5 * f * f, dk = (double)k;
+  return -(dk * 6.93147180369123816490e-01 - ((hfsq - (s * (hfsq + R) + dk * 1.90821492927058770002e-10)) - f));
+}
+
 // ---------------------------------------------------------------------------
 // Geometry.
 // ---------------------------------------------------------------------------
@@ -369,16 +391,18 @@ __device__ __forceinline__ void emit_volume(const Emitter& e, double eta, const 
 // SINGLE: the domain has one coarse polygon, so the coarse data and its fine
 // grid are workgroup-uniform and a crossing can only leave the domain.
 // ---------------------------------------------------------------------------
-template <bool UNIFORM, bool SINGLE>
+template <bool UNIFORM, bool SINGLE, bool FAITHFUL>
 __device__ __forceinline__ int64_t trace_ray(const DevDomain& D, const TraceParams& P, int c, double& px,
                                              double& py, double dx, double dy, const RayDraws& rd) {
   const double eta = P.eta;
   double S = 0.0, target = 0.0, acc = 0.0;
   if (UNIFORM) {
-    S = P.beta_uniform > 0 ? ((RTHX_ABLATE & 2) ? (1.0 - rd.path()) : -log(rd.path())) * P.inv_beta_uniform
-                           : __builtin_inf();
+    const double u = rd.path();
+    S = P.beta_uniform > 0
+            ? ((RTHX_ABLATE & 2) ? (1.0 - u) : FAITHFUL ? -log(u) / P.beta_uniform : neg_log_unit(u) * P.inv_beta_uniform)
+            : __builtin_inf();
   } else {
-    target = -log(rd.path());
+    target = FAITHFUL ? -log(rd.path()) : neg_log_unit(rd.path());
   }
   const double* beta_bin = D.beta + (size_t)P.bin * D.n_fine;
   if (SINGLE) c = 0;
@@ -436,7 +460,7 @@ __device__ __forceinline__ int64_t trace_one(const DevDomain& D, const TracePara
     emit_volume<FAITHFUL>(e, P.eta, rd, px, py, dx, dy);
   ox = px;
   oy = py;
-  return trace_ray<UNIFORM, SINGLE>(D, P, e.coarse, px, py, dx, dy, rd);
+  return trace_ray<UNIFORM, SINGLE, FAITHFUL>(D, P, e.coarse, px, py, dx, dy, rd);
 }
 
 }  // namespace rthx
