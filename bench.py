@@ -86,8 +86,9 @@ def cpu_baseline(dom, R, nudge, seed, budget_s=12.0, threads=16):
 
 def read_pmc_traffic():
     """HBM bytes per trace launch from the committed rocprofv3 --pmc summary
-    (profiles/round1_pmc_trace.json, written by tools/pmc_summary.py), or None."""
-    p = os.path.join(ROOT, "profiles", "round1_pmc_trace.json")
+    (profiles/round1/pmc_traffic.json, written by tools/pmc_summary.py from
+    separate FETCH_SIZE / WRITE_SIZE passes of this bench), or None."""
+    p = os.path.join(ROOT, "profiles", "round1", "pmc_traffic.json")
     if not os.path.exists(p):
         return None
     try:

@@ -66,6 +66,27 @@ struct DevBuf {
   T* as() const { return static_cast<T*>(p); }
 };
 
+// Pinned host buffer with grow-only capacity (fast D2H of the CSR arrays).
+struct HostBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  hipError_t reserve(size_t bytes) {
+    if (bytes <= cap && p) return hipSuccess;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = bytes < 4096 ? 4096 : bytes;
+    hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+    if (e == hipSuccess) cap = want;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
 double now_ms() {
   using namespace std::chrono;
   return duration<double, std::milli>(steady_clock::now().time_since_epoch()).count();
@@ -99,9 +120,10 @@ struct rthx_result {
   DevBuf rec_ids, rec_ok, rec_orig, rec_end;
   bool valid = false;
   bool host_csr = false;
+  bool host_row_off = false;
   int64_t N = 0, R = 0, n_rows = 0, begin = 0, stride = 1;
   std::vector<int64_t> h_row_off;
-  std::vector<uint32_t> h_cols, h_cnt;
+  HostBuf h_cols, h_cnt;  // pinned
   std::vector<int64_t> rec_g;  // recorded emitters (ascending)
   std::vector<uint8_t> h_ok;
   std::vector<double> h_orig, h_end;
@@ -112,6 +134,8 @@ struct rthx_result {
     DevBuf* all[] = {&stage_cols, &stage_cnt, &row_nnz, &row_tallied, &row_off, &totals,
                      &cols,       &cnt,       &rec_ids, &rec_ok,      &rec_orig, &rec_end};
     for (DevBuf* b : all) b->release();
+    h_cols.release();
+    h_cnt.release();
   }
 };
 
@@ -467,9 +491,12 @@ RTHX_EXPORT int rthx_trace_exchange(rthx_domain* dom, const rthx_trace_args* a, 
 
   int64_t totals[3] = {0, 0, 0};
   HIP_TRY(hipMemcpyAsync(totals, res->totals.p, 24, hipMemcpyDeviceToHost, st), "hipMemcpy totals");
+  const bool device_only = (a->flags & RTHX_FLAG_DEVICE_ONLY) != 0;
   res->h_row_off.resize(n_rows + 1);
-  HIP_TRY(hipMemcpyAsync(res->h_row_off.data(), res->row_off.p, (n_rows + 1) * 8, hipMemcpyDeviceToHost, st),
-          "hipMemcpy row_off");
+  res->host_row_off = !device_only;
+  if (!device_only)
+    HIP_TRY(hipMemcpyAsync(res->h_row_off.data(), res->row_off.p, (n_rows + 1) * 8, hipMemcpyDeviceToHost, st),
+            "hipMemcpy row_off");
   HIP_TRY(hipStreamSynchronize(st), "trace kernels");
   float ms_trace = 0.f, ms_pack = 0.f;
   HIP_TRY(hipEventElapsedTime(&ms_trace, dom->ev[0], dom->ev[1]), "hipEventElapsedTime");
@@ -482,13 +509,13 @@ RTHX_EXPORT int rthx_trace_exchange(rthx_domain* dom, const rthx_trace_args* a, 
   res->info.pack_ms = ms_pack;
   res->valid = true;
 
-  if (!(a->flags & RTHX_FLAG_DEVICE_ONLY)) {
+  if (!device_only) {
     const size_t nnz = (size_t)totals[0];
-    res->h_cols.resize(nnz);
-    res->h_cnt.resize(nnz);
+    HIP_TRY(res->h_cols.reserve(nnz * 4), "hipHostMalloc cols");
+    HIP_TRY(res->h_cnt.reserve(nnz * 4), "hipHostMalloc counts");
     if (nnz) {
-      HIP_TRY(hipMemcpy(res->h_cols.data(), res->cols.p, nnz * 4, hipMemcpyDeviceToHost), "hipMemcpy cols");
-      HIP_TRY(hipMemcpy(res->h_cnt.data(), res->cnt.p, nnz * 4, hipMemcpyDeviceToHost), "hipMemcpy counts");
+      HIP_TRY(hipMemcpy(res->h_cols.p, res->cols.p, nnz * 4, hipMemcpyDeviceToHost), "hipMemcpy cols");
+      HIP_TRY(hipMemcpy(res->h_cnt.p, res->cnt.p, nnz * 4, hipMemcpyDeviceToHost), "hipMemcpy counts");
     }
     res->host_csr = true;
     if (n_rec > 0) {
@@ -528,13 +555,19 @@ RTHX_EXPORT int rthx_result_copy_csr(const rthx_result* cres, int64_t* row_ptr, 
   const size_t nnz = (size_t)res->info.nnz;
   if (!res->host_csr) {
     HIP_TRY(hipSetDevice(res->device), "hipSetDevice");
-    res->h_cols.resize(nnz);
-    res->h_cnt.resize(nnz);
+    HIP_TRY(res->h_cols.reserve(nnz * 4), "hipHostMalloc cols");
+    HIP_TRY(res->h_cnt.reserve(nnz * 4), "hipHostMalloc counts");
     if (nnz) {
-      HIP_TRY(hipMemcpy(res->h_cols.data(), res->cols.p, nnz * 4, hipMemcpyDeviceToHost), "hipMemcpy cols");
-      HIP_TRY(hipMemcpy(res->h_cnt.data(), res->cnt.p, nnz * 4, hipMemcpyDeviceToHost), "hipMemcpy counts");
+      HIP_TRY(hipMemcpy(res->h_cols.p, res->cols.p, nnz * 4, hipMemcpyDeviceToHost), "hipMemcpy cols");
+      HIP_TRY(hipMemcpy(res->h_cnt.p, res->cnt.p, nnz * 4, hipMemcpyDeviceToHost), "hipMemcpy counts");
     }
     res->host_csr = true;
+  }
+  if (row_ptr && !res->host_row_off) {
+    HIP_TRY(hipSetDevice(res->device), "hipSetDevice");
+    HIP_TRY(hipMemcpy(res->h_row_off.data(), res->row_off.p, (res->n_rows + 1) * 8, hipMemcpyDeviceToHost),
+            "hipMemcpy row_off");
+    res->host_row_off = true;
   }
   if (row_ptr) {
     // rows g = begin + k*stride hold slot k; all other rows are empty
@@ -549,8 +582,8 @@ RTHX_EXPORT int rthx_result_copy_csr(const rthx_result* cres, int64_t* row_ptr, 
       row_ptr[g + 1] = row_ptr[g] + n;
     }
   }
-  if (cols && nnz) std::memcpy(cols, res->h_cols.data(), nnz * 4);
-  if (counts && nnz) std::memcpy(counts, res->h_cnt.data(), nnz * 4);
+  if (cols && nnz) std::memcpy(cols, res->h_cols.p, nnz * 4);
+  if (counts && nnz) std::memcpy(counts, res->h_cnt.p, nnz * 4);
   return RTHX_OK;
 }
 

@@ -156,9 +156,9 @@ class DeviceResult:
         inf = self.info()
         n = inf["n_emitters"]
         nnz = inf["nnz"]
-        row_ptr = np.zeros(n + 1, dtype=np.int64)
-        cols = np.zeros(max(nnz, 1), dtype=np.int32)
-        counts = np.zeros(max(nnz, 1), dtype=np.uint32)
+        row_ptr = np.empty(n + 1, dtype=np.int64)
+        cols = np.empty(max(nnz, 1), dtype=np.int32)
+        counts = np.empty(max(nnz, 1), dtype=np.uint32)
         check(self._lib.rthx_result_copy_csr(self.handle, abi.ptr(row_ptr, C.c_int64),
                                              abi.ptr(cols, C.c_int32), abi.ptr(counts, C.c_uint32)))
         return row_ptr, cols[:nnz], counts[:nnz]
