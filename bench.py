@@ -107,15 +107,19 @@ def main():
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--emulate-world", type=int, default=0,
+                    help="diagnostic: run rank 0's shard of a W-GPU job on this one GPU (no value claim)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", str(args.gpus)))
+    if args.emulate_world > 1:
+        world = args.emulate_world
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and "WORLD_SIZE" in os.environ:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
     dist = None
-    if world > 1:
+    if world > 1 and args.emulate_world <= 1:
         import torch.distributed as dist  # noqa: F811
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -229,6 +233,10 @@ def main():
             "pack_ms": round(float(np.mean(pack_ms)), 4),
             "e2e_with_d2h_mrays_s": round(e2e, 3) if e2e else None,
         }
+        if args.emulate_world > 1:
+            out["emulated_rank0_of"] = world
+            out["value"] = None  # one rank's shard only: not a whole-job measurement
+            out["rank0_mrays_s"] = round(rays_rank * args.steps / elapsed / 1e6, 3)
         if world == 1 and not args.no_cpu:
             out["cpu_baseline"] = cpu_baseline(dom, R, nudge, args.seed, args.cpu_budget)
         else:

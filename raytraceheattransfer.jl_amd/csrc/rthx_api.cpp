@@ -116,12 +116,12 @@ struct rthx_domain {
 
 struct rthx_result {
   int device = -1;
-  DevBuf stage_cols, stage_cnt, row_nnz, row_tallied, row_off, totals, cols, cnt;
+  DevBuf stage_cols, stage_cnt, row_nnz, row_tallied, row_off, totals, cols, cnt, dense;
   DevBuf rec_ids, rec_ok, rec_orig, rec_end;
   bool valid = false;
   bool host_csr = false;
   bool host_row_off = false;
-  int64_t N = 0, R = 0, n_rows = 0, begin = 0, stride = 1;
+  int64_t N = 0, R = 0, n_rows = 0, begin = 0, stride = 1, split = 1;
   std::vector<int64_t> h_row_off;
   HostBuf h_cols, h_cnt;  // pinned
   std::vector<int64_t> rec_g;  // recorded emitters (ascending)
@@ -131,8 +131,8 @@ struct rthx_result {
   rthx_result_info info{};
   ~rthx_result() {
     if (device >= 0) (void)hipSetDevice(device);
-    DevBuf* all[] = {&stage_cols, &stage_cnt, &row_nnz, &row_tallied, &row_off, &totals,
-                     &cols,       &cnt,       &rec_ids, &rec_ok,      &rec_orig, &rec_end};
+    DevBuf* all[] = {&stage_cols, &stage_cnt, &row_nnz,  &row_tallied, &row_off,  &totals, &cols,
+                     &cnt,        &dense,     &rec_ids,  &rec_ok,      &rec_orig, &rec_end};
     for (DevBuf* b : all) b->release();
     h_cols.release();
     h_cnt.release();
@@ -173,6 +173,11 @@ int check_grid(const rthx_grid_desc& g, int32_t count, const char* what) {
       return fail(RTHX_EINVAL, std::string("grid item out of range: ") + what);
   return RTHX_OK;
 }
+
+// Row splitting: target number of workgroups per launch (>> 256 CUs x ~5
+// resident workgroups) and the fewest rays a split workgroup traces.
+constexpr int64_t kSplitTargetBlocks = 8192;
+constexpr int64_t kSplitMinRays = 2048;
 
 // Device point-location grids: rthx_grid.cpp.  Cells per mean polygon extent
 // (per axis): at 2 a cell holds at most one vertex of a regular mesh.
@@ -399,11 +404,22 @@ RTHX_EXPORT int rthx_trace_exchange(rthx_domain* dom, const rthx_trace_args* a, 
   const int64_t end = std::min<int64_t>(a->emitter_end, N);
   const int64_t n_rows = end > a->emitter_begin ? (end - a->emitter_begin + a->emitter_stride - 1) / a->emitter_stride : 0;
   if (n_rows >= (1ll << 31)) return fail(RTHX_ERANGE, "too many rows in one call");
-  const bool pack16 = R < 65536;
+  // Rows are split over several workgroups when there are too few rows to
+  // fill the chip (or a row's rays would overflow the packed 16-bit LDS
+  // counters of a large row); each workgroup then traces R/split rays.
+  const bool recording = a->n_record > 0 && a->record_bin == a->bin;
+  int64_t split = 1;
+  if (!recording && n_rows > 0 && n_rows < kSplitTargetBlocks && R >= 2 * kSplitMinRays)
+    split = std::min<int64_t>((kSplitTargetBlocks + n_rows - 1) / n_rows, R / kSplitMinRays);
+  if (!recording && R >= 65536 && ((N + 1) / 2) * 4 + 1024 <= (int64_t)rthx::kMaxLdsBytes &&
+      N * 4 + 1024 > (int64_t)rthx::kMaxLdsBytes)
+    split = std::max<int64_t>(split, (R + 65534) / 65535);
+  const int64_t rays_per_block = split > 1 ? (R + split - 1) / split : R;
+  const bool pack16 = rays_per_block < 65536;
   const int64_t words = pack16 ? (N + 1) / 2 : N;
   const size_t lds_bytes = (size_t)words * 4;
   if (lds_bytes + 1024 > rthx::kMaxLdsBytes)
-    return fail(RTHX_ERANGE, "N too large for the LDS row histogram of this build (N <= 81408 when R < 65536, N <= 40704 otherwise)");
+    return fail(RTHX_ERANGE, "N too large for the LDS row histogram of this build (N <= 81408)");
   const int64_t row_cap = std::max<int64_t>(1, std::min<int64_t>(N, R));
 
   res->valid = false;
@@ -419,6 +435,7 @@ RTHX_EXPORT int rthx_trace_exchange(rthx_domain* dom, const rthx_trace_args* a, 
   res->info.rows_traced = n_rows;
   res->info.rays_per_emitter = R;
   res->info.rays_traced = n_rows * R;
+  res->split = split;
 
   // recorded emitters traced by this call (ascending, unique)
   res->rec_g.clear();
@@ -440,6 +457,7 @@ RTHX_EXPORT int rthx_trace_exchange(rthx_domain* dom, const rthx_trace_args* a, 
   HIP_TRY(res->totals.reserve(4 * 8), "hipMalloc totals");
   HIP_TRY(res->cols.reserve((size_t)n_rows * row_cap * 4), "hipMalloc cols");
   HIP_TRY(res->cnt.reserve((size_t)n_rows * row_cap * 4), "hipMalloc cnt");
+  if (split > 1) HIP_TRY(res->dense.reserve((size_t)n_rows * N * 4), "hipMalloc dense rows");
   rthx::RecordParams rec{};
   if (n_rec > 0) {
     HIP_TRY(res->rec_ids.reserve(n_rec * 8), "hipMalloc rec_ids");
@@ -467,16 +485,40 @@ RTHX_EXPORT int rthx_trace_exchange(rthx_domain* dom, const rthx_trace_args* a, 
   P.inv_beta_uniform = P.beta_uniform > 0 ? 1.0 / P.beta_uniform : 0.0;
   const bool uniform = dom->uniform_beta[a->bin] > -0.1;  // traceRay.jl:4
 
+  rthx::TallyParams T{};
+  T.n_emitters = N;
+  T.n_rows = n_rows;
+  T.row_cap = row_cap;
+  T.split = (int32_t)split;
+  T.stage_cols = res->stage_cols.as<uint32_t>();
+  T.stage_cnt = res->stage_cnt.as<uint32_t>();
+  T.row_nnz = res->row_nnz.as<uint32_t>();
+  T.row_tallied = res->row_tallied.as<uint32_t>();
+  T.dense = split > 1 ? res->dense.as<uint32_t>() : nullptr;
+
   hipStream_t st = dom->stream;
+  if (split > 1 && n_rows > 0) {
+    HIP_TRY(hipMemsetAsync(T.dense, 0, (size_t)n_rows * N * 4, st), "hipMemset dense rows");
+    HIP_TRY(hipMemsetAsync(T.row_tallied, 0, (size_t)n_rows * 4, st), "hipMemset row_tallied");
+  }
   HIP_TRY(hipEventRecord(dom->ev[0], st), "hipEventRecord");
   if (n_rows > 0) {
-    HIP_TRY(rthx::launch_trace(dom->d_dom, P, uniform, pack16, (a->flags & RTHX_FLAG_FAITHFUL_SAMPLING) != 0, dom->single_convex, N, n_rows, res->stage_cols.as<uint32_t>(),
-                               res->stage_cnt.as<uint32_t>(), row_cap, res->row_nnz.as<uint32_t>(),
-                               res->row_tallied.as<uint32_t>(), rec, lds_bytes, st),
-            "trace_exchange_kernel launch");
+    rthx::LaunchCfg L{};
+    L.D = dom->d_dom;
+    L.P = P;
+    L.T = T;
+    L.rec = rec;
+    L.lds_bytes = lds_bytes;
+    L.stream = st;
+    L.uniform = uniform;
+    L.pack16 = pack16;
+    L.faithful = (a->flags & RTHX_FLAG_FAITHFUL_SAMPLING) != 0;
+    L.single = dom->single_convex;
+    HIP_TRY(rthx::launch_trace(L), "trace_exchange_kernel launch");
   }
   HIP_TRY(hipEventRecord(dom->ev[1], st), "hipEventRecord");
   if (n_rows > 0) {
+    if (split > 1) HIP_TRY(rthx::launch_compact(T, st), "row_compact_kernel launch");
     HIP_TRY(rthx::launch_scan(res->row_nnz.as<uint32_t>(), res->row_tallied.as<uint32_t>(), n_rows, R,
                               res->row_off.as<int64_t>(), res->totals.as<int64_t>(), st),
             "row_scan_kernel launch");

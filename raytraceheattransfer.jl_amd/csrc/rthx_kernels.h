@@ -9,7 +9,7 @@
 
 namespace rthx {
 
-constexpr int kTraceThreads = 256;               // 4 waves of 64 per emitter row
+constexpr int kTraceThreads = 256;               // 4 waves of 64 per emitter row (slice)
 constexpr size_t kMaxLdsBytes = 160 * 1024;      // gfx950 LDS per CU
 
 struct RecordParams {
@@ -20,14 +20,37 @@ struct RecordParams {
   double* end;          // [n*R*2]
 };
 
-hipError_t launch_trace(const DevDomain* D, const TraceParams& P, bool uniform, bool pack16, bool faithful,
-                        bool single, int64_t n_emitters, int64_t n_rows, uint32_t* stage_cols, uint32_t* stage_cnt, int64_t row_cap,
-                        uint32_t* row_nnz, uint32_t* row_tallied, const RecordParams& rec, size_t lds_bytes,
-                        hipStream_t stream);
+// Where the counts go.  Unsplit: each workgroup compacts its row into
+// stage_*[slot*row_cap ..] and writes row_nnz / row_tallied.  Split: the
+// `split` workgroups of a row add into dense[slot*N ..] and row_tallied
+// (both zeroed first); row_compact_kernel then fills stage_* / row_nnz.
+struct TallyParams {
+  int64_t n_emitters;   // N (histogram length)
+  int64_t n_rows;
+  int64_t row_cap;      // min(N, R)
+  int32_t split;        // workgroups per row (>= 1)
+  int32_t reserved;
+  uint32_t* stage_cols;
+  uint32_t* stage_cnt;
+  uint32_t* row_nnz;
+  uint32_t* row_tallied;
+  uint32_t* dense;      // split only: [n_rows][N]
+};
 
+struct LaunchCfg {
+  const DevDomain* D;
+  TraceParams P;
+  TallyParams T;
+  RecordParams rec;
+  size_t lds_bytes;
+  hipStream_t stream;
+  bool uniform, pack16, faithful, single;
+};
+
+hipError_t launch_trace(const LaunchCfg& L);
+hipError_t launch_compact(const TallyParams& T, hipStream_t stream);
 hipError_t launch_scan(const uint32_t* row_nnz, const uint32_t* row_tallied, int64_t n_rows, int64_t R,
                        int64_t* row_off, int64_t* totals, hipStream_t stream);
-
 hipError_t launch_pack(const uint32_t* stage_cols, const uint32_t* stage_cnt, int64_t row_cap, const int64_t* row_off,
                        int64_t n_rows, uint32_t* cols, uint32_t* cnt, hipStream_t stream);
 

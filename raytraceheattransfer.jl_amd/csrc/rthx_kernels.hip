@@ -1,12 +1,14 @@
 // rthx_kernels.hip — exchange-factor trace kernels for gfx950 (MI355X).
 //
-// trace_exchange_kernel: one workgroup per emitter row (computeExchangeFactorsBin's
-//   per-emitter loop, parallelRayTracing.jl:102-150).  The workgroup's 256 lanes
-//   trace the row's R rays, tally absorbers into an LDS histogram (uint16
-//   counters packed two per dword when R < 65536 — the Dict{Int,Int} row of
-//   the reference), then compact the histogram in ascending absorber order into
-//   a fixed-stride staging slot of min(N, R) entries (no global atomics, so the
-//   output is deterministic).
+// trace_exchange_kernel: the per-emitter loop of computeExchangeFactorsBin
+//   (parallelRayTracing.jl:102-150).  A workgroup of 256 lanes traces the
+//   rays of one emitter row (or, SPLIT, one slice of a row) and tallies
+//   absorbers into an LDS histogram -- the reference's Dict{Int,Int} row --
+//   with uint16 counters packed two per dword when a workgroup traces fewer
+//   than 65536 rays.  Unsplit rows are then compacted in ascending absorber
+//   order into a fixed-stride staging slot of min(N, R) entries (no global
+//   atomics, deterministic); split rows add their histogram into a dense
+//   per-row count buffer that row_compact_kernel compacts afterwards.
 // row_scan_kernel: exclusive scan of per-row nnz + lost-ray reductions.
 // csr_pack_kernel: copies every row's staging slot into the dense CSR arrays.
 #include <hip/hip_runtime.h>
@@ -21,33 +23,72 @@ __device__ __forceinline__ uint32_t lane_id() {
   return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
 }
 
-template <bool UNIFORM, bool PACK16, bool FAITHFUL, bool SINGLE, bool REC>
-__global__ __launch_bounds__(kTraceThreads) void trace_exchange_kernel(const DevDomain* __restrict__ Dp, TraceParams P, int64_t n_emitters,
-                                                                     uint32_t* __restrict__ stage_cols,
-                                                                     uint32_t* __restrict__ stage_cnt,
-                                                                     int64_t row_cap, uint32_t* __restrict__ row_nnz,
-                                                                     uint32_t* __restrict__ row_tallied,
+// Workgroup-wide compaction of one row's counts, ascending absorber order
+// (the reference's sparse() sorts columns, parallelRayTracing.jl:154).
+// count2(w) returns the counts of absorbers 2w and 2w+1 (PAIRS) or of w.
+// Returns the row's nnz (valid in every lane).
+template <bool PAIRS, class F>
+__device__ __forceinline__ uint32_t compact_row(int64_t n_words, F count2, uint32_t* __restrict__ out_c,
+                                                uint32_t* __restrict__ out_n, uint32_t* wave_sum,
+                                                uint32_t* s_running) {
+  const int tid = threadIdx.x;
+  const uint32_t lane = lane_id();
+  const int wave = tid >> 6;
+  const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  for (int64_t w0 = 0; w0 < n_words; w0 += kTraceThreads) {
+    int64_t w = w0 + tid;
+    uint32_t lo = 0u, hi = 0u;
+    if (w < n_words) count2(w, lo, hi);
+    uint64_t m_lo = __ballot(lo != 0u);
+    uint64_t m_hi = PAIRS ? __ballot(hi != 0u) : 0ull;
+    uint32_t pre = __popcll(m_lo & lt_mask) + __popcll(m_hi & lt_mask);
+    if (lane == 0) wave_sum[wave] = __popcll(m_lo) + __popcll(m_hi);
+    __syncthreads();
+    uint32_t base = *s_running;
+    for (int i = 0; i < wave; ++i) base += wave_sum[i];
+    uint32_t pos = base + pre;
+    if (lo) { out_c[pos] = PAIRS ? (uint32_t)(2 * w) : (uint32_t)w; out_n[pos] = lo; ++pos; }
+    if (PAIRS && hi) { out_c[pos] = (uint32_t)(2 * w + 1); out_n[pos] = hi; }
+    __syncthreads();
+    if (tid == 0) {
+      uint32_t tot = 0;
+      for (int i = 0; i < kTraceThreads / 64; ++i) tot += wave_sum[i];
+      *s_running += tot;
+    }
+    __syncthreads();
+  }
+  return *s_running;
+}
+
+template <bool UNIFORM, bool PACK16, bool FAITHFUL, bool SINGLE, bool REC, bool SPLIT>
+__global__ __launch_bounds__(kTraceThreads) void trace_exchange_kernel(const DevDomain* __restrict__ Dp,
+                                                                     TraceParams P, TallyParams T,
                                                                      RecordParams rec) {
   extern __shared__ uint32_t hist[];
   const DevDomain& D = *Dp;
   __shared__ uint32_t wave_sum[kTraceThreads / 64];
   __shared__ uint32_t s_running;
   __shared__ uint32_t s_tallied;
-
-  const int64_t slot = blockIdx.x;
-  const int64_t g = P.g_begin + slot * P.g_stride;
-  const int tid = threadIdx.x;
-  const int64_t n_words = PACK16 ? (n_emitters + 1) / 2 : n_emitters;
-
-  for (int64_t w = tid; w < n_words; w += kTraceThreads) hist[w] = 0u;
-  if (tid == 0) { s_running = 0u; s_tallied = 0u; }
-
   // Emitter data is workgroup-uniform: kept in LDS (broadcast ds_reads) rather
   // than in ~26 VGPRs; measured 2.12 ms vs 2.30 (asm memory clobber) and
   // 2.48 ms (volatile reload) per 1e8 rays.
   __shared__ Emitter s_emit;
-  if (tid == 0) s_emit = load_emitter(D, g);
 
+  const int tid = threadIdx.x;
+  const int64_t slot = SPLIT ? (int64_t)(blockIdx.x / T.split) : (int64_t)blockIdx.x;
+  const int64_t part = SPLIT ? (int64_t)(blockIdx.x % T.split) : 0;
+  const int64_t chunk = SPLIT ? (P.R + T.split - 1) / T.split : P.R;
+  const int64_t r_begin = part * chunk;
+  const int64_t r_end = SPLIT ? (r_begin + chunk < P.R ? r_begin + chunk : P.R) : P.R;
+  const int64_t g = P.g_begin + slot * P.g_stride;
+  const int64_t n_words = PACK16 ? (T.n_emitters + 1) / 2 : T.n_emitters;
+
+  for (int64_t w = tid; w < n_words; w += kTraceThreads) hist[w] = 0u;
+  if (tid == 0) {
+    s_running = 0u;
+    s_tallied = 0u;
+    s_emit = load_emitter(D, g);
+  }
   // recorded emitter?  (RayRecorder ids, parallelRayTracing.jl:108)
   int rec_slot = -1;
   if (REC)
@@ -56,7 +97,7 @@ __global__ __launch_bounds__(kTraceThreads) void trace_exchange_kernel(const Dev
   __syncthreads();
 
   uint32_t tallied = 0;
-  for (int64_t r = tid; r < P.R; r += kTraceThreads) {
+  for (int64_t r = r_begin + tid; r < r_end; r += kTraceThreads) {
     const Emitter& e = s_emit;
     double ox, oy, px, py;
     int64_t a = trace_one<UNIFORM, FAITHFUL, SINGLE>(D, P, e, g, r, ox, oy, px, py);
@@ -79,40 +120,48 @@ __global__ __launch_bounds__(kTraceThreads) void trace_exchange_kernel(const Dev
   if (lane_id() == 0) atomicAdd(&s_tallied, tallied);
   __syncthreads();
 
-  // Compaction: ascending absorber order (the reference's sparse() sorts
-  // columns, parallelRayTracing.jl:154).
-  const uint32_t lane = lane_id();
-  const int wave = tid >> 6;
-  const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  uint32_t* out_c = stage_cols + slot * row_cap;
-  uint32_t* out_n = stage_cnt + slot * row_cap;
-  for (int64_t w0 = 0; w0 < n_words; w0 += kTraceThreads) {
-    int64_t w = w0 + tid;
-    uint32_t v = (w < n_words) ? hist[w] : 0u;
-    uint32_t lo = PACK16 ? (v & 0xFFFFu) : v;
-    uint32_t hi = PACK16 ? (v >> 16) : 0u;
-    uint64_t m_lo = __ballot(lo != 0u);
-    uint64_t m_hi = PACK16 ? __ballot(hi != 0u) : 0ull;
-    uint32_t pre = __popcll(m_lo & lt_mask) + __popcll(m_hi & lt_mask);
-    if (lane == 0) wave_sum[wave] = __popcll(m_lo) + __popcll(m_hi);
-    __syncthreads();
-    uint32_t base = s_running;
-    for (int i = 0; i < wave; ++i) base += wave_sum[i];
-    uint32_t pos = base + pre;
-    if (lo) { out_c[pos] = PACK16 ? (uint32_t)(2 * w) : (uint32_t)w; out_n[pos] = lo; ++pos; }
-    if (PACK16 && hi) { out_c[pos] = (uint32_t)(2 * w + 1); out_n[pos] = hi; }
-    __syncthreads();
-    if (tid == 0) {
-      uint32_t tot = 0;
-      for (int i = 0; i < kTraceThreads / 64; ++i) tot += wave_sum[i];
-      s_running += tot;
+  if (SPLIT) {
+    // add this slice's nonzero counters into the row's dense buffer
+    uint32_t* dense = T.dense + slot * T.n_emitters;
+    for (int64_t w = tid; w < n_words; w += kTraceThreads) {
+      uint32_t v = hist[w];
+      if (v == 0u) continue;
+      if (PACK16) {
+        if (v & 0xFFFFu) atomicAdd(&dense[2 * w], v & 0xFFFFu);
+        if (v >> 16) atomicAdd(&dense[2 * w + 1], v >> 16);
+      } else {
+        atomicAdd(&dense[w], v);
+      }
     }
-    __syncthreads();
+    if (tid == 0) atomicAdd(&T.row_tallied[slot], s_tallied);
+    return;
   }
+  uint32_t nnz = compact_row<PACK16>(
+      n_words,
+      [&](int64_t w, uint32_t& lo, uint32_t& hi) {
+        uint32_t v = hist[w];
+        lo = PACK16 ? (v & 0xFFFFu) : v;
+        hi = PACK16 ? (v >> 16) : 0u;
+      },
+      T.stage_cols + slot * T.row_cap, T.stage_cnt + slot * T.row_cap, wave_sum, &s_running);
   if (tid == 0) {
-    row_nnz[slot] = s_running;
-    row_tallied[slot] = s_tallied;
+    T.row_nnz[slot] = nnz;
+    T.row_tallied[slot] = s_tallied;
   }
+}
+
+// Split rows: compact the dense per-row counts into the staging slots.
+__global__ __launch_bounds__(kTraceThreads) void row_compact_kernel(TallyParams T) {
+  __shared__ uint32_t wave_sum[kTraceThreads / 64];
+  __shared__ uint32_t s_running;
+  const int64_t slot = blockIdx.x;
+  if (threadIdx.x == 0) s_running = 0u;
+  __syncthreads();
+  const uint32_t* dense = T.dense + slot * T.n_emitters;
+  uint32_t nnz = compact_row<false>(
+      T.n_emitters, [&](int64_t w, uint32_t& lo, uint32_t& hi) { lo = dense[w]; hi = 0u; },
+      T.stage_cols + slot * T.row_cap, T.stage_cnt + slot * T.row_cap, wave_sum, &s_running);
+  if (threadIdx.x == 0) T.row_nnz[slot] = nnz;
 }
 
 // Exclusive scan of row_nnz -> row_off[n_rows+1]; totals of lost rays.
@@ -182,55 +231,44 @@ __global__ __launch_bounds__(256) void csr_pack_kernel(const uint32_t* __restric
 // ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
-template <bool UNIFORM, bool PACK16, bool FAITHFUL, bool SINGLE, bool REC>
-static hipError_t launch_trace_t(const DevDomain* D, const TraceParams& P, int64_t n_emitters, int64_t n_rows,
-                                 uint32_t* stage_cols, uint32_t* stage_cnt, int64_t row_cap, uint32_t* row_nnz,
-                                 uint32_t* row_tallied, const RecordParams& rec, size_t lds_bytes,
-                                 hipStream_t stream) {
-  auto kern = trace_exchange_kernel<UNIFORM, PACK16, FAITHFUL, SINGLE, REC>;
-  if (lds_bytes > 64 * 1024) {
+template <bool UNIFORM, bool PACK16, bool FAITHFUL, bool SINGLE, bool REC, bool SPLIT>
+static hipError_t launch_trace_t(const LaunchCfg& L) {
+  auto kern = trace_exchange_kernel<UNIFORM, PACK16, FAITHFUL, SINGLE, REC, SPLIT>;
+  if (L.lds_bytes > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)lds_bytes);
+                                       (int)L.lds_bytes);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(kern, dim3((unsigned)n_rows), dim3(kTraceThreads), lds_bytes, stream, D, P, n_emitters,
-                     stage_cols, stage_cnt, row_cap, row_nnz, row_tallied, rec);
+  const int64_t blocks = L.T.n_rows * (SPLIT ? L.T.split : 1);
+  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kTraceThreads), L.lds_bytes, L.stream, L.D, L.P, L.T,
+                     L.rec);
   return hipGetLastError();
 }
 
 template <bool UNIFORM, bool PACK16, bool FAITHFUL>
-static hipError_t launch_trace_s(bool single, const DevDomain* D, const TraceParams& P, int64_t n_emitters,
-                                 int64_t n_rows, uint32_t* stage_cols, uint32_t* stage_cnt, int64_t row_cap,
-                                 uint32_t* row_nnz, uint32_t* row_tallied, const RecordParams& rec,
-                                 size_t lds_bytes, hipStream_t stream) {
-  // Recording is a plotting aid: one generic (non-SINGLE) instance carries it.
-  if (rec.n > 0)
-    return launch_trace_t<UNIFORM, PACK16, FAITHFUL, false, true>(D, P, n_emitters, n_rows, stage_cols, stage_cnt,
-                                                                  row_cap, row_nnz, row_tallied, rec, lds_bytes,
-                                                                  stream);
-  if (single)
-    return launch_trace_t<UNIFORM, PACK16, FAITHFUL, true, false>(D, P, n_emitters, n_rows, stage_cols, stage_cnt,
-                                                                  row_cap, row_nnz, row_tallied, rec, lds_bytes,
-                                                                  stream);
-  return launch_trace_t<UNIFORM, PACK16, FAITHFUL, false, false>(D, P, n_emitters, n_rows, stage_cols, stage_cnt,
-                                                                 row_cap, row_nnz, row_tallied, rec, lds_bytes,
-                                                                 stream);
+static hipError_t launch_trace_u(const LaunchCfg& L) {
+  // Recording is a plotting aid: generic (non-SINGLE, unsplit) instances carry it.
+  if (L.rec.n > 0) return launch_trace_t<UNIFORM, PACK16, FAITHFUL, false, true, false>(L);
+  if (L.T.split > 1) {
+    if (L.single) return launch_trace_t<UNIFORM, PACK16, FAITHFUL, true, false, true>(L);
+    return launch_trace_t<UNIFORM, PACK16, FAITHFUL, false, false, true>(L);
+  }
+  if (L.single) return launch_trace_t<UNIFORM, PACK16, FAITHFUL, true, false, false>(L);
+  return launch_trace_t<UNIFORM, PACK16, FAITHFUL, false, false, false>(L);
 }
 
-hipError_t launch_trace(const DevDomain* D, const TraceParams& P, bool uniform, bool pack16, bool faithful,
-                        bool single, int64_t n_emitters, int64_t n_rows, uint32_t* stage_cols, uint32_t* stage_cnt,
-                        int64_t row_cap, uint32_t* row_nnz, uint32_t* row_tallied, const RecordParams& rec,
-                        size_t lds_bytes, hipStream_t stream) {
-#define RTHX_LAUNCH(U, P16, F)                                                                                 \
-  return launch_trace_s<U, P16, F>(single, D, P, n_emitters, n_rows, stage_cols, stage_cnt, row_cap, row_nnz, \
-                                   row_tallied, rec, lds_bytes, stream)
-  if (faithful) {
-    if (uniform) { if (pack16) RTHX_LAUNCH(true, true, true); else RTHX_LAUNCH(true, false, true); }
-    if (pack16) RTHX_LAUNCH(false, true, true); else RTHX_LAUNCH(false, false, true);
+hipError_t launch_trace(const LaunchCfg& L) {
+  if (L.faithful) {
+    if (L.uniform) return L.pack16 ? launch_trace_u<true, true, true>(L) : launch_trace_u<true, false, true>(L);
+    return L.pack16 ? launch_trace_u<false, true, true>(L) : launch_trace_u<false, false, true>(L);
   }
-  if (uniform) { if (pack16) RTHX_LAUNCH(true, true, false); else RTHX_LAUNCH(true, false, false); }
-  if (pack16) RTHX_LAUNCH(false, true, false); else RTHX_LAUNCH(false, false, false);
-#undef RTHX_LAUNCH
+  if (L.uniform) return L.pack16 ? launch_trace_u<true, true, false>(L) : launch_trace_u<true, false, false>(L);
+  return L.pack16 ? launch_trace_u<false, true, false>(L) : launch_trace_u<false, false, false>(L);
+}
+
+hipError_t launch_compact(const TallyParams& T, hipStream_t stream) {
+  hipLaunchKernelGGL(row_compact_kernel, dim3((unsigned)T.n_rows), dim3(kTraceThreads), 0, stream, T);
+  return hipGetLastError();
 }
 
 hipError_t launch_scan(const uint32_t* row_nnz, const uint32_t* row_tallied, int64_t n_rows, int64_t R,

@@ -149,6 +149,18 @@ def test_shards_union_equals_full(hip):
     assert np.array_equal(rp, full[0]) and np.array_equal(c, full[1]) and np.array_equal(v, full[2])
 
 
+def test_split_rows_exact(hip):
+    """Few rows, many rays: every row is split over several workgroups whose
+    histograms meet in a dense row buffer (rthx_api.cpp kSplitTargetBlocks)."""
+    dom = H.square_domain(11)
+    flat = dom.flat()
+    args, _k = _args(hip, flat, 20_000, seed=12)
+    assert_same(gpu_trace(hip, flat, args), oracle.trace_exchange(flat, args, 16))
+    # a strided shard (the multi-GPU row set) with R >= 65536
+    args, _k = _args(hip, flat, 80_000, seed=13, begin=3, stride=8)
+    assert_same(gpu_trace(hip, flat, args), oracle.trace_exchange(flat, args, 16))
+
+
 def test_edge_cases(hip):
     dom = H.square_domain(5)
     flat = dom.flat()
