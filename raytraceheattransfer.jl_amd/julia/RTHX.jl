@@ -1,0 +1,275 @@
+"""
+    RTHX
+
+Julia `ccall` shim that routes RayTraceHeatTransfer.jl's exchange-factor
+tracer (`mesh(N_rays; method=:exchange)`) to the MI355X kernels of
+`librthx.so` (C ABI: `include/rthx.h`).
+
+The seam is `computeExchangeFactorsBin`
+(src/RayTracing/RayTracing2D/ExchangeFactors2D/parallelRayTracing.jl:64-159);
+everything above it (bin grouping, surfaces-only truncation, `smooth_F`,
+`solveEquilibrium!`) is unchanged.  Usage:
+
+    using RayTraceHeatTransfer
+    include("raytraceheattransfer.jl_amd/julia/RTHX.jl")
+    RTHX.enable!(; lib = "raytraceheattransfer.jl_amd/csrc/_build/librthx.so", device = 0, seed = 1)
+    mesh(100_000_000; method = :exchange)      # traced on the GPU
+
+Not executable in the build container (no Julia toolchain); kept in step
+with `include/rthx.h` by `tests/test_abi.py::test_julia_shim_mirrors_header`.
+"""
+module RTHX
+
+using SparseArrays
+
+const RTHX_ABI_VERSION = Int32(1)
+const RTHX_FLAG_FAITHFUL_SAMPLING = UInt32(0x1)
+
+const LIB = Ref{String}("")
+const DEVICE = Ref{Int32}(0)
+const SEED = Ref{UInt64}(1)
+const FAITHFUL = Ref{Bool}(false)
+
+# --- C structs (field order and types exactly as include/rthx.h) ----------
+struct GridDesc
+    origin_x::Float64
+    origin_y::Float64
+    inv_cell_size::Float64
+    nx::Int32
+    ny::Int32
+    cell_start::Ptr{Int32}
+    cell_items::Ptr{Int32}
+end
+
+struct DomainDesc
+    abi_version::Int32
+    n_coarse::Int32
+    n_fine::Int32
+    n_surfaces::Int32
+    n_bins::Int32
+    reserved0::Int32
+    coarse_nv::Ptr{Int32}
+    coarse_xy::Ptr{Float64}
+    coarse_normal::Ptr{Float64}
+    coarse_solid::Ptr{UInt8}
+    coarse_bbox::Ptr{Float64}
+    coarse_grid::GridDesc
+    fine_offset::Ptr{Int32}
+    fine_nv::Ptr{Int32}
+    fine_xy::Ptr{Float64}
+    fine_normal::Ptr{Float64}
+    fine_mid::Ptr{Float64}
+    fine_volume::Ptr{Float64}
+    fine_bbox::Ptr{Float64}
+    fine_surface::Ptr{Int32}
+    fine_grid::Ptr{GridDesc}
+    beta::Ptr{Float64}
+    uniform_beta::Ptr{Float64}
+end
+
+struct TraceArgs
+    bin::Int32
+    flags::UInt32
+    rays_per_emitter::Int64
+    nudge::Float64
+    seed::UInt64
+    emitter_begin::Int64
+    emitter_end::Int64
+    emitter_stride::Int64
+    device::Int32
+    n_record::Int32
+    record_ids::Ptr{Int64}
+    record_bin::Int32
+    reserved0::Int32
+end
+
+struct ResultInfo
+    n_emitters::Int64
+    rows_traced::Int64
+    rays_per_emitter::Int64
+    rays_traced::Int64
+    nnz::Int64
+    lost_total::Int64
+    lost_max_row::Int64
+    n_recorded::Int64
+    trace_ms::Float64
+    pack_ms::Float64
+    total_ms::Float64
+end
+
+function check(rc::Integer)
+    if rc != 0
+        msg = unsafe_string(ccall((:rthx_last_error, LIB[]), Cstring, ()))
+        error("rthx error $rc: $msg")
+    end
+end
+
+# --- flattening RayTracingDomain2D (DomainStructs.jl:89-130) --------------
+"Host arrays of one flattened domain; kept alive while the descriptor is used."
+mutable struct Flat
+    arrays::Vector{Any}
+    grids::Vector{GridDesc}
+    desc::Base.RefValue{DomainDesc}
+end
+
+function grid_arrays(g)  # UniformGrid (DomainStructs.jl:79-86): cells[i, j] lists face indices
+    nx, ny = g.nx, g.ny
+    start = zeros(Int32, nx * ny + 1)
+    items = Int32[]
+    for j in 1:ny, i in 1:nx
+        for f in g.cells[i, j]
+            push!(items, Int32(f - 1))
+        end
+        start[(j - 1) * nx + i + 1] = length(items)
+    end
+    isempty(items) && push!(items, Int32(0))
+    return start, items
+end
+
+polyxy(p) = (v = zeros(Float64, 8); for (k, q) in enumerate(p.vertices); v[2k-1] = q[1]; v[2k] = q[2]; end;
+             length(p.vertices) == 3 && (v[7] = v[5]; v[8] = v[6]); v)
+polynrm(p) = (v = zeros(Float64, 8); for (k, q) in enumerate(p.inwardNormals); v[2k-1] = q[1]; v[2k] = q[2]; end; v)
+bbox(p) = (xs = [q[1] for q in p.vertices]; ys = [q[2] for q in p.vertices];
+           [minimum(xs), maximum(xs), minimum(ys), maximum(ys)])
+betaof(f, b) = f.kappa_g isa AbstractVector ? f.kappa_g[b] + f.sigma_s_g[b] : f.kappa_g + f.sigma_s_g
+
+function flatten(rtm)
+    coarse = rtm.coarse_mesh
+    fine = rtm.fine_mesh
+    nc = length(coarse)
+    offs = Int32[0; cumsum([Int32(length(s)) for s in fine])]
+    faces = [f for s in fine for f in s]
+    nf = length(faces)
+    ns = length(rtm.surface_mapping)
+    nb = rtm.n_spectral_bins
+    c_nv = Int32[length(c.vertices) for c in coarse]
+    c_xy = reduce(vcat, [polyxy(c) for c in coarse])
+    c_n = reduce(vcat, [polynrm(c) for c in coarse])
+    c_s = reduce(vcat, [UInt8[(k <= length(c.solidWalls) && c.solidWalls[k]) for k in 1:4] for c in coarse])
+    c_bb = reduce(vcat, [bbox(c) for c in coarse])
+    f_nv = Int32[length(f.vertices) for f in faces]
+    f_xy = reduce(vcat, [polyxy(f) for f in faces])
+    f_n = reduce(vcat, [polynrm(f) for f in faces])
+    f_mid = reduce(vcat, [[f.midPoint[1], f.midPoint[2]] for f in faces])
+    f_vol = Float64[f.volume for f in faces]
+    f_bb = reduce(vcat, [bbox(f) for f in faces])
+    f_surf = fill(Int32(-1), 4 * nf)
+    for ((c, f, w), s) in rtm.surface_mapping
+        f_surf[4 * (offs[c] + f - 1) + w] = Int32(s - 1)
+    end
+    beta = Float64[betaof(faces[k], b) for k in 1:nf, b in 1:nb][:]  # [bin][face] (column-major = bin-major)
+    ub = Float64.(rtm.uniform_across_bin)
+    cg_start, cg_items = grid_arrays(rtm.coarse_grid_opt)
+    keep = Any[c_nv, c_xy, c_n, c_s, c_bb, f_nv, f_xy, f_n, f_mid, f_vol, f_bb, f_surf, beta, ub, offs,
+               cg_start, cg_items]
+    mk(g, st, it) = GridDesc(g.origin[1], g.origin[2], g.inv_cell_size, Int32(g.nx), Int32(g.ny),
+                             pointer(st), pointer(it))
+    grids = GridDesc[]
+    for c in 1:nc
+        st, it = grid_arrays(rtm.fine_grids_opt[c])
+        push!(keep, st, it)
+        push!(grids, mk(rtm.fine_grids_opt[c], st, it))
+    end
+    push!(keep, grids)
+    desc = DomainDesc(RTHX_ABI_VERSION, Int32(nc), Int32(nf), Int32(ns), Int32(nb), Int32(0),
+                      pointer(c_nv), pointer(c_xy), pointer(c_n), pointer(c_s), pointer(c_bb),
+                      mk(rtm.coarse_grid_opt, cg_start, cg_items),
+                      pointer(offs), pointer(f_nv), pointer(f_xy), pointer(f_n), pointer(f_mid), pointer(f_vol),
+                      pointer(f_bb), pointer(f_surf), pointer(grids), pointer(beta), pointer(ub))
+    return Flat(keep, grids, Ref(desc))
+end
+
+# one uploaded domain per (rtm, device)
+const DOMAINS = IdDict{Any, Tuple{Flat, Ptr{Cvoid}}}()
+
+function device_domain(rtm)
+    haskey(DOMAINS, rtm) && return DOMAINS[rtm][2]
+    flat = flatten(rtm)
+    h = Ref{Ptr{Cvoid}}(C_NULL)
+    GC.@preserve flat begin
+        check(ccall((:rthx_domain_create, LIB[]), Cint, (Ptr{DomainDesc}, Int32, Ptr{Ptr{Cvoid}}),
+                    flat.desc, DEVICE[], h))
+    end
+    DOMAINS[rtm] = (flat, h[])
+    return h[]
+end
+
+"""
+    computeExchangeFactorsBin(rtm, rays_per_emitter, nudge, spectral_bin, surface_mapping,
+                              volume_mapping, num_surfaces, num_volumes, num_emitters, verbose, rec)
+
+Drop-in for parallelRayTracing.jl:64-159: one `rthx_trace_exchange` call,
+then `sparse` + `row_normalize!` exactly as the reference (:154-158).
+"""
+function computeExchangeFactorsBin(rtm, rays_per_emitter::Integer, nudge, spectral_bin::Integer,
+                                   surface_mapping, volume_mapping, num_surfaces, num_volumes, num_emitters,
+                                   verbose, rec)
+    dom = device_domain(rtm)
+    ids = rec === nothing ? Int64[] : Int64[i - 1 for i in rec.ids]
+    rbin = rec === nothing ? Int32(0) : Int32(rec.bin - 1)
+    args = Ref(TraceArgs(Int32(spectral_bin - 1), FAITHFUL[] ? RTHX_FLAG_FAITHFUL_SAMPLING : UInt32(0),
+                         Int64(rays_per_emitter), Float64(nudge), SEED[], 0, Int64(num_emitters), 1, DEVICE[],
+                         Int32(length(ids)), isempty(ids) ? Ptr{Int64}(C_NULL) : pointer(ids), rbin, Int32(0)))
+    res = Ref{Ptr{Cvoid}}(C_NULL)
+    check(ccall((:rthx_result_create, LIB[]), Cint, (Ptr{Ptr{Cvoid}},), res))
+    try
+        GC.@preserve ids begin
+            check(ccall((:rthx_trace_exchange, LIB[]), Cint, (Ptr{Cvoid}, Ptr{TraceArgs}, Ptr{Cvoid}),
+                        dom, args, res[]))
+        end
+        info = Ref{ResultInfo}()
+        check(ccall((:rthx_result_get_info, LIB[]), Cint, (Ptr{Cvoid}, Ptr{ResultInfo}), res[], info))
+        N, nnz = info[].n_emitters, info[].nnz
+        rowptr = Vector{Int64}(undef, N + 1)
+        cols = Vector{Int32}(undef, max(nnz, 1))
+        counts = Vector{UInt32}(undef, max(nnz, 1))
+        check(ccall((:rthx_result_copy_csr, LIB[]), Cint, (Ptr{Cvoid}, Ptr{Int64}, Ptr{Int32}, Ptr{UInt32}),
+                    res[], rowptr, cols, counts))
+        verbose && println("  rthx: $(info[].rays_traced) rays, nnz $nnz, trace $(round(info[].trace_ms; digits=3)) ms")
+        if rec !== nothing && info[].n_recorded > 0
+            n = info[].n_recorded
+            o = Vector{Float64}(undef, 2n); e = Vector{Float64}(undef, 2n); g = Vector{Int64}(undef, n)
+            nout = Ref{Int64}(0)
+            check(ccall((:rthx_result_copy_rays, LIB[]), Cint,
+                        (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}, Ptr{Int64}, Int64, Ptr{Int64}),
+                        res[], o, e, g, n, nout))
+            for k in 1:nout[]
+                push!(rec.origins[1], eltype(rec.origins[1])(o[2k-1], o[2k]))
+                push!(rec.endpoints[1], eltype(rec.endpoints[1])(e[2k-1], e[2k]))
+            end
+        end
+        # CSR of F (rows = emitters) is the CSC of F^T
+        inv_rays = 1.0 / rays_per_emitter
+        Ft = SparseMatrixCSC(N, N, rowptr .+ 1, Int64.(cols[1:nnz]) .+ 1, Float64.(counts[1:nnz]) .* inv_rays)
+        F = SparseMatrixCSC(transpose(Ft))
+        return parentmodule(@__MODULE__).RayTraceHeatTransfer.row_normalize!(F, rays_per_emitter)
+    finally
+        ccall((:rthx_result_destroy, LIB[]), Cvoid, (Ptr{Cvoid},), res[])
+    end
+end
+
+"""
+    enable!(; lib, device=0, seed=1, faithful=false)
+
+Redirect RayTraceHeatTransfer's `computeExchangeFactorsBin` to the GPU.
+"""
+function enable!(; lib::AbstractString, device::Integer = 0, seed::Integer = 1, faithful::Bool = false)
+    LIB[] = lib
+    DEVICE[] = Int32(device)
+    SEED[] = UInt64(seed)
+    FAITHFUL[] = faithful
+    v = ccall((:rthx_abi_version, LIB[]), Cint, ())
+    v == RTHX_ABI_VERSION || error("librthx ABI $v, shim expects $RTHX_ABI_VERSION")
+    RTHT = parentmodule(@__MODULE__).RayTraceHeatTransfer
+    @eval RTHT function computeExchangeFactorsBin(rtm::RayTracingDomain2D, rays_per_emitter::P, nudge::G,
+                                                  spectral_bin::P, surface_mapping, volume_mapping,
+                                                  num_surfaces, num_volumes, num_emitters, verbose,
+                                                  rec) where {P<:Integer, G}
+        return $(RTHX).computeExchangeFactorsBin(rtm, rays_per_emitter, nudge, spectral_bin, surface_mapping,
+                                                 volume_mapping, num_surfaces, num_volumes, num_emitters,
+                                                 verbose, rec)
+    end
+    return nothing
+end
+
+end # module
