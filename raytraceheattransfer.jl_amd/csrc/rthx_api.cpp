@@ -340,15 +340,36 @@ RTHX_EXPORT int rthx_domain_create(const rthx_domain_desc* desc, int32_t device,
     int _r = upload(d, (src), (n), &(dst), #dst);                \
     if (_r) return bail(_r);                                     \
   } while (0)
-  UP(s.coarse_nv, nc, D.c_nv);
-  UP(s.coarse_xy, 8 * nc, D.c_xy);
-  UP(s.coarse_normal, 8 * nc, D.c_nrm);
+  // polygon records padded to 4 slots (rthx_device.h DevPoly): a triangle
+  // repeats vertex 2 and has a zero normal in slot 3
+  auto polys = [](const int32_t* nv, const double* xy, const double* nrm, size_t n) {
+    std::vector<rthx::DevPoly> out(n);
+    for (size_t p = 0; p < n; ++p) {
+      rthx::DevPoly& q = out[p];
+      for (int i = 0; i < 4; ++i) {
+        const int v = i < nv[p] ? i : nv[p] - 1;
+        q.x[i] = xy[8 * p + 2 * v];
+        q.y[i] = xy[8 * p + 2 * v + 1];
+        q.nx[i] = i < nv[p] ? nrm[8 * p + 2 * i] : 0.0;
+        q.ny[i] = i < nv[p] ? nrm[8 * p + 2 * i + 1] : 0.0;
+      }
+    }
+    return out;
+  };
+  const std::vector<rthx::DevPoly> cpoly = polys(s.coarse_nv, s.coarse_xy, s.coarse_normal, nc);
+  const std::vector<rthx::DevPoly> fpoly = polys(s.fine_nv, s.fine_xy, s.fine_normal, nf);
+  // (cos, sin)(2 pi j / 256) for the emission azimuth (rthx_device.h cos_2pi_u32)
+  std::vector<double> cos_tab(2 * rthx::kCosTable);
+  for (int j = 0; j < rthx::kCosTable; ++j) {
+    cos_tab[2 * j] = std::cos(2.0 * M_PI * j / rthx::kCosTable);
+    cos_tab[2 * j + 1] = std::sin(2.0 * M_PI * j / rthx::kCosTable);
+  }
+  UP(cpoly.data(), nc, D.c_poly);
   UP(csolid.data(), nc, D.c_solid);
   UP(s.coarse_bbox, 4 * nc, D.c_bbox);
   UP(s.fine_offset, nc + 1, D.f_offset);
   UP(s.fine_nv, nf, D.f_nv);
-  UP(s.fine_xy, 8 * nf, D.f_xy);
-  UP(s.fine_normal, 8 * nf, D.f_nrm);
+  UP(fpoly.data(), nf, D.f_poly);
   UP(s.fine_mid, 2 * nf, D.f_mid);
   UP(trifrac.data(), nf, D.f_trifrac);
   UP(s.fine_bbox, 4 * nf, D.f_bbox);
@@ -361,6 +382,7 @@ RTHX_EXPORT int rthx_domain_create(const rthx_domain_desc* desc, int32_t device,
   UP(s.beta, (size_t)s.n_bins * nf, D.beta);
   UP(s_face.data(), s_face.size(), D.s_face);
   UP(s_wall.data(), s_wall.size(), D.s_wall);
+  UP(cos_tab.data(), cos_tab.size(), D.cos_tab);
 #undef UP
   {
     int r3 = upload(d, &d->D, 1, &d->d_dom, "domain record");
@@ -411,15 +433,15 @@ RTHX_EXPORT int rthx_trace_exchange(rthx_domain* dom, const rthx_trace_args* a, 
   int64_t split = 1;
   if (!recording && n_rows > 0 && n_rows < kSplitTargetBlocks && R >= 2 * kSplitMinRays)
     split = std::min<int64_t>((kSplitTargetBlocks + n_rows - 1) / n_rows, R / kSplitMinRays);
-  if (!recording && R >= 65536 && ((N + 1) / 2) * 4 + 1024 <= (int64_t)rthx::kMaxLdsBytes &&
-      N * 4 + 1024 > (int64_t)rthx::kMaxLdsBytes)
+  if (!recording && R >= 65536 && ((N + 1) / 2) * 4 + rthx::kStaticLdsBytes <= (int64_t)rthx::kMaxLdsBytes &&
+      N * 4 + rthx::kStaticLdsBytes > (int64_t)rthx::kMaxLdsBytes)
     split = std::max<int64_t>(split, (R + 65534) / 65535);
   const int64_t rays_per_block = split > 1 ? (R + split - 1) / split : R;
   const bool pack16 = rays_per_block < 65536;
   const int64_t words = pack16 ? (N + 1) / 2 : N;
   const size_t lds_bytes = (size_t)words * 4;
-  if (lds_bytes + 1024 > rthx::kMaxLdsBytes)
-    return fail(RTHX_ERANGE, "N too large for the LDS row histogram of this build (N <= 81408)");
+  if (lds_bytes + rthx::kStaticLdsBytes > rthx::kMaxLdsBytes)
+    return fail(RTHX_ERANGE, "N too large for the LDS row histogram of this build (N <= 78848)");
   const int64_t row_cap = std::max<int64_t>(1, std::min<int64_t>(N, R));
 
   res->valid = false;

@@ -37,6 +37,18 @@ struct DevGrid {
   int32_t reserved;
 };
 
+// Polygon record (128 B): vertices and unit inward normals
+// (calculateInwardNormal.jl:1-12), always 4 slots.  A triangle repeats its
+// last vertex in slot 3 and has a zero normal there, so every loop below runs
+// over 4 edges without a vertex-count test: the repeated vertex adds a
+// horizontal zero-length edge that never crosses (point in polygon), and the
+// zero normal gives |d.n| = 0 < 1e-10, which distToSurface2D treats as
+// parallel (no hit).
+struct alignas(16) DevPoly {
+  double x[4], y[4];
+  double nx[4], ny[4];
+};
+
 // Point-location cell record (built by rthx_grid.cpp, layout = CellRec):
 // code = (a0 x + b0 y + c0 < 0) | (a1 x + b1 y + c1 < 0) << 1 selects leaf[code]:
 // >= 0 polygon, -1 outside all polygons, -2 test the cell's candidate list.
@@ -46,20 +58,19 @@ struct alignas(16) DevCell {
   int32_t leaf[4];
 };
 
+constexpr int kCosTable = 256;  // cos/sin(2 pi j / 256), j < 256
+
 struct DevDomain {
   int32_t n_coarse, n_fine, n_surfaces, n_bins;
   // coarse polygons
-  const int32_t RTHX_GLOBAL* c_nv;
-  const double RTHX_GLOBAL* c_xy;      // [n_coarse][4][2]
-  const double RTHX_GLOBAL* c_nrm;     // [n_coarse][4][2] unit inward normals
+  const DevPoly RTHX_GLOBAL* c_poly;   // [n_coarse]
   const uint32_t RTHX_GLOBAL* c_solid; // [n_coarse] bit w = wall w solid
   const double RTHX_GLOBAL* c_bbox;    // [n_coarse][4]
   DevGrid c_grid;
   // fine polygons
   const int32_t RTHX_GLOBAL* f_offset; // [n_coarse+1]
   const int32_t RTHX_GLOBAL* f_nv;     // [n_fine]
-  const double RTHX_GLOBAL* f_xy;      // [n_fine][4][2]
-  const double RTHX_GLOBAL* f_nrm;     // [n_fine][4][2]
+  const DevPoly RTHX_GLOBAL* f_poly;   // [n_fine]
   const double RTHX_GLOBAL* f_mid;     // [n_fine][2]
   const double RTHX_GLOBAL* f_trifrac; // [n_fine] area(ABC)/V of quads (emitVolumeRay2D.jl:7)
   const double RTHX_GLOBAL* f_bbox;    // [n_fine][4]
@@ -75,6 +86,8 @@ struct DevDomain {
   // surface emitters
   const int32_t RTHX_GLOBAL* s_face;   // [Ns]
   const int32_t RTHX_GLOBAL* s_wall;   // [Ns]
+  // cos(2 pi j/256), sin(2 pi j/256) pairs, j < 256 (emission azimuth)
+  const double RTHX_GLOBAL* cos_tab;   // [256][2]
 };
 
 struct TraceParams {
@@ -92,14 +105,18 @@ struct TraceParams {
 // Philox-4x32-10 counter RNG (Salmon et al. SC'11).  Counter (r, g, block,
 // bin), key (seed lo, seed hi).
 // ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);  // gfx950 v_bitop3_b32: a ^ b ^ c
+}
+
 __device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
 #pragma unroll
   for (int i = 0; i < ((RTHX_ABLATE & 1) ? 1 : 10); ++i) {
     // one 32x32->64 multiply per product (v_mad_u64_u32) instead of mul_lo + mul_hi
     uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
     uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
-    uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0;
-    uint32_t n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1;
+    uint32_t n0 = xor3((uint32_t)(p1 >> 32), c[1], k0);
+    uint32_t n2 = xor3((uint32_t)(p0 >> 32), c[3], k1);
     c[0] = n0; c[1] = (uint32_t)p1; c[2] = n2; c[3] = (uint32_t)p0;
     k0 += 0x9E3779B9u;
     k1 += 0xBB67AE85u;
@@ -110,7 +127,7 @@ __device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32
 // 52 bits of (hi:lo) as the mantissa of a double in [1, 2), minus 1.
 __device__ __forceinline__ double u52(uint32_t hi, uint32_t lo) {
   uint32_t mhi = 0x3FF00000u | (hi >> 12);
-  uint32_t mlo = (hi << 20) | (lo >> 12);
+  uint32_t mlo = __builtin_amdgcn_alignbit(hi, lo, 12);  // (hi << 20) | (lo >> 12)
   return __hiloint2double((int)mhi, (int)mlo) - 1.0;
 }
 
@@ -137,9 +154,10 @@ struct RayDraws {
   __device__ __forceinline__ double path() const { return u52(c[0], c[1]); }
   __device__ __forceinline__ double sel() const { return u32(c[2]); }
   __device__ __forceinline__ double th() const { return u32(c[3]); }
-  __device__ __forceinline__ double ph() const {
-    return u32(((a[1] & 0xFFFu) << 20) | ((a[3] & 0xFFFu) << 8) | ((c[1] & 0xFFFu) >> 4));
+  __device__ __forceinline__ uint32_t ph_bits() const {
+    return ((a[1] & 0xFFFu) << 20) | ((a[3] & 0xFFFu) << 8) | ((c[1] & 0xFFFu) >> 4);
   }
+  __device__ __forceinline__ double ph() const { return u32(ph_bits()); }
   __device__ __forceinline__ double l1() const { return u32(a[2]); }
   __device__ __forceinline__ double l2() const { return u32(a[3]); }
 };
@@ -166,34 +184,53 @@ __device__ __forceinline__ double neg_log_unit(double u) {
   return -(dk * 6.93147180369123816490e-01 - ((hfsq - (s * (hfsq + R) + dk * 1.90821492927058770002e-10)) - f));
 }
 
+#define RTHX_TWO_PI 6.283185307179586
+
+// cos(2 pi w / 2^32) for a 32-bit draw w (emitVolumeRay2D.jl:28-31: phi = 2 pi u,
+// cos(phi)).  Table-and-polynomial: w = j 2^24 + m, with (cos, sin) of
+// 2 pi j/256 from `tab` and d = 2 pi m/2^32 < 2 pi/256, so cos(a + d) =
+// C cos d - S sin d with degree-6/7 Taylor polynomials in d (truncation
+// below 4e-18).  Within a few ulp of cos(2 pi u); about a quarter of ocml's
+// cospi.
+__device__ __forceinline__ double cos_2pi_u32(uint32_t w, const double* tab) {
+  const int j = (int)(w >> 24);
+  const double d = (double)(w & 0xFFFFFFu) * (RTHX_TWO_PI * 0x1.0p-32);
+  const double z = d * d;
+  const double cd = __builtin_fma(z, __builtin_fma(z, __builtin_fma(z, -1.0 / 720.0, 1.0 / 24.0), -0.5), 1.0);
+  const double ps = __builtin_fma(z, __builtin_fma(z, -1.0 / 5040.0, 1.0 / 120.0), -1.0 / 6.0);
+  const double sd = __builtin_fma(d * z, ps, d);
+  const double C = tab[2 * j], S = tab[2 * j + 1];
+  return __builtin_fma(C, cd, -(S * sd));
+}
+
 // ---------------------------------------------------------------------------
-// Geometry.
+// Geometry.  `Poly` is a DevPoly in global memory or LDS.
 // ---------------------------------------------------------------------------
 
 // distToSurface2D.jl:2-17: smallest positive parameter along d to the walls
 // of a polygon (inward unit normals), first index on ties, walls with
 // |d.n| < 1e-10 or parameter <= 0 are +Inf; all +Inf -> (Inf, 0).
 // The reference divides every wall's numerator by its denominator and takes
-// findmin; here the candidates (num/den > 0, i.e. num and den of one sign) are
-// compared by cross-multiplication |num_a| |den_b| < |num_b| |den_a| and only
-// the winner is divided: the same minimum and index except for walls whose
-// parameters tie to within an ulp (a ray through a corner).
-__device__ __forceinline__ double dist_to_polygon(double px, double py, double dx, double dy,
-                                                  const double* __restrict__ xy,
-                                                  const double* __restrict__ nrm, int n, int& widx) {
-  double bn = 1.0, bd = 0.0;  // best |num|, |den|; bd == 0 means "none yet"
+// findmin; here a wall is a candidate when num and den have one sign
+// (num/den > 0), candidates are compared by cross-multiplication
+// |num_a| |den_b| < |num_b| |den_a|, and only the winner is divided: the same
+// minimum and index except for walls whose parameters tie to within an ulp
+// (a ray through a corner).
+template <class Poly>
+__device__ __forceinline__ double dist_to_polygon(double px, double py, double dx, double dy, const Poly& q,
+                                                  int& widx) {
+  double bn = 1.0, bd = 0.0;  // best |num|, |den|; bd == 0 means "none yet" (an*0 < 1*ad for any candidate)
   int bi = 0;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    if (i < n) {
-      double nx = nrm[2 * i], ny = nrm[2 * i + 1];
-      double den = __dmul_rn(dx, nx) + __dmul_rn(dy, ny);
-      double num = __dmul_rn(xy[2 * i] - px, nx) + __dmul_rn(xy[2 * i + 1] - py, ny);
-      double an = fabs(num), ad = fabs(den);
-      bool ok = (ad >= 1e-10) && ((num > 0.0 && den > 0.0) || (num < 0.0 && den < 0.0));
-      bool better = ok && (bd == 0.0 || __dmul_rn(an, bd) < __dmul_rn(bn, ad));
-      if (better) { bn = an; bd = ad; bi = i; }
-    }
+    double nx = q.nx[i], ny = q.ny[i];
+    double den = __dmul_rn(dx, nx) + __dmul_rn(dy, ny);
+    double num = __dmul_rn(q.x[i] - px, nx) + __dmul_rn(q.y[i] - py, ny);
+    double an = fabs(num), ad = fabs(den);
+    bool better = (ad >= 1e-10) && (__dmul_rn(num, den) > 0.0) && (__dmul_rn(an, bd) < __dmul_rn(bn, ad));
+    bn = better ? an : bn;
+    bd = better ? ad : bd;
+    bi = better ? i : bi;
   }
   widx = bi;
   if (bd == 0.0) return __builtin_inf();
@@ -205,27 +242,26 @@ __device__ __forceinline__ double dist_to_polygon(double px, double py, double d
 // vertex).  The reference's  px < xi + (xj-xi)/(yj-yi) (py-yi)  is evaluated
 // without the division as  sign((xj-xi)(py-yi) - (px-xi)(yj-yi)) == sign(yj-yi),
 // which decides identically except for points within an ulp of the edge.
-__device__ __forceinline__ bool point_in_polygon(double px, double py, const double* __restrict__ xy, int n) {
+template <class Poly>
+__device__ __forceinline__ bool point_in_polygon(double px, double py, const Poly& q) {
   bool inside = false;
-  double xj = xy[2 * (n - 1)], yj = xy[2 * (n - 1) + 1];
+  double xj = q.x[3], yj = q.y[3];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    if (i < n) {
-      double xi = xy[2 * i], yi = xy[2 * i + 1];
-      double ey = yj - yi;
-      double cr = __dmul_rn(xj - xi, py - yi) - __dmul_rn(px - xi, ey);
-      bool crossing = (yi > py) != (yj > py);
-      bool left = ey > 0.0 ? (cr > 0.0) : (cr < 0.0);
-      inside ^= (crossing && left);
-      xj = xi;
-      yj = yi;
-    }
+    double xi = q.x[i], yi = q.y[i];
+    double ey = yj - yi;
+    double cr = __dmul_rn(xj - xi, py - yi) - __dmul_rn(px - xi, ey);
+    bool crossing = (yi > py) != (yj > py);
+    bool left = ey > 0.0 ? (cr > 0.0) : (cr < 0.0);
+    inside ^= (crossing && left);
+    xj = xi;
+    yj = yi;
   }
   return inside;
 }
 
 // findFace2D, findFace2D.jl:48-68 (grid :2-27, bbox fallback :30-45).
-// Polygons [first, first+count) of (nv, xy, bbox); returns local index or -1.
+// Polygons [first, first+count); returns local index or -1.
 // The grid is the device point-location grid built by rthx_domain_create
 // (rthx_grid.cpp, DESIGN.md "Point location"): each cell record splits the
 // cell by at most two polygon-edge lines into regions verified to lie in one
@@ -233,54 +269,50 @@ __device__ __forceinline__ bool point_in_polygon(double px, double py, const dou
 // not fit fall back to their candidate list and the point-in-polygon loop.
 // A point outside every polygon of the cell ends, as in the reference, in the
 // bbox-prefiltered scan in index order.
-__device__ __forceinline__ int locate(const DevGrid& g, const DevCell RTHX_GLOBAL* __restrict__ cells,
-                                      const int32_t RTHX_GLOBAL* __restrict__ lists,
-                                      const int32_t RTHX_GLOBAL* __restrict__ items, const int32_t* __restrict__ nv,
-                                      const double* __restrict__ xy, const double* __restrict__ bbox, int first,
-                                      int count, double px, double py) {
+template <class Grid>
+__device__ __forceinline__ int locate(const Grid& g, const DevDomain& D, const DevPoly RTHX_GLOBAL* __restrict__ polys,
+                                      const double RTHX_GLOBAL* __restrict__ bbox, int first, int count, double px,
+                                      double py) {
   double fi = floor(__dmul_rn(px - g.ox, g.inv_x));
   double fj = floor(__dmul_rn(py - g.oy, g.inv_y));
   if (fi >= 0.0 && fi < (double)g.nx && fj >= 0.0 && fj < (double)g.ny) {
     const int cell = g.cell_base + (int)fj * g.nx + (int)fi;
-    const DevCell c = cells[cell];
+    const DevCell c = D.grid_cells[cell];
     double s0 = __dmul_rn(c.a0, px) + __dmul_rn(c.b0, py) + c.c0;
     double s1 = __dmul_rn(c.a1, px) + __dmul_rn(c.b1, py) + c.c1;
-    int code = (s0 < 0.0 ? 1 : 0) | (s1 < 0.0 ? 2 : 0);
-    int leaf = code == 0 ? c.leaf[0] : code == 1 ? c.leaf[1] : code == 2 ? c.leaf[2] : c.leaf[3];
+    int leaf = s1 < 0.0 ? (s0 < 0.0 ? c.leaf[3] : c.leaf[2]) : (s0 < 0.0 ? c.leaf[1] : c.leaf[0]);
     if (RTHX_ABLATE & 8) return leaf < 0 ? 0 : leaf;
     if (leaf >= 0) return leaf;
     if (leaf == -2) {
-      const int k0 = lists[2 * cell], k1 = k0 + lists[2 * cell + 1];
+      const int k0 = D.grid_lists[2 * cell], k1 = k0 + D.grid_lists[2 * cell + 1];
       for (int k = k0; k < k1; ++k) {
-        int f = items[k];
-        if (point_in_polygon(px, py, xy + 8 * (size_t)(first + f), nv[first + f])) return f;
+        int f = D.grid_items[k];
+        if (point_in_polygon(px, py, polys[first + f])) return f;
       }
     }
   }
   for (int f = 0; f < count; ++f) {
-    const double* b = bbox + 4 * (size_t)(first + f);
+    const double RTHX_GLOBAL* b = bbox + 4 * (size_t)(first + f);
     if (b[0] <= px && px <= b[1] && b[2] <= py && py <= b[3]) {
-      if (point_in_polygon(px, py, xy + 8 * (size_t)(first + f), nv[first + f])) return f;
+      if (point_in_polygon(px, py, polys[first + f])) return f;
     }
   }
   return -1;
 }
 
-__device__ __forceinline__ int locate_fine(const DevDomain& D, const DevGrid& g, int first, int count, double px,
+template <class Grid>
+__device__ __forceinline__ int locate_fine(const DevDomain& D, const Grid& g, int first, int count, double px,
                                            double py) {
-  return locate(g, D.grid_cells, D.grid_lists, D.grid_items, D.f_nv, D.f_xy, D.f_bbox, first, count, px, py);
+  return locate(g, D, D.f_poly, D.f_bbox, first, count, px, py);
 }
 
 __device__ __forceinline__ int locate_coarse(const DevDomain& D, double px, double py) {
-  return locate(D.c_grid, D.grid_cells, D.grid_lists, D.grid_items, D.c_nv, D.c_xy, D.c_bbox, 0, D.n_coarse, px,
-                py);
+  return locate(D.c_grid, D, D.c_poly, D.c_bbox, 0, D.n_coarse, px, py);
 }
-
-#define RTHX_TWO_PI 6.283185307179586
 
 // ---------------------------------------------------------------------------
 // Emitter: everything a ray of emitter g needs that does not depend on the
-// ray, gathered once per workgroup (g is workgroup-uniform).
+// ray, gathered once per workgroup (g is workgroup-uniform) into LDS.
 // ---------------------------------------------------------------------------
 struct Emitter {
   double v[8];        // polygon vertices (volume) / v[0..3] = p1, p2 (surface)
@@ -307,11 +339,11 @@ __device__ __forceinline__ Emitter load_emitter(const DevDomain& D, int64_t g) {
   e.mx = D.f_mid[2 * f];
   e.my = D.f_mid[2 * f + 1];
   e.tri_frac = D.f_trifrac[f];
-  const double* xy = D.f_xy + 8 * (size_t)f;
+  const DevPoly RTHX_GLOBAL& q = D.f_poly[f];
   if (e.surface) {
     int w2 = (w + 1 == e.nv) ? 0 : w + 1;
-    e.v[0] = xy[2 * w]; e.v[1] = xy[2 * w + 1];
-    e.v[2] = xy[2 * w2]; e.v[3] = xy[2 * w2 + 1];
+    e.v[0] = q.x[w]; e.v[1] = q.y[w];
+    e.v[2] = q.x[w2]; e.v[3] = q.y[w2];
     // xVecLocal = normalize(p2 - p1) (emitSurfaceRay2D.jl:17)
     double ex = e.v[2] - e.v[0], ey = e.v[3] - e.v[1];
     double len = sqrt(__dmul_rn(ex, ex) + __dmul_rn(ey, ey));
@@ -319,7 +351,10 @@ __device__ __forceinline__ Emitter load_emitter(const DevDomain& D, int64_t g) {
     e.ty = ey / len;
   } else {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) e.v[i] = xy[i];
+    for (int i = 0; i < 4; ++i) {
+      e.v[2 * i] = q.x[i];
+      e.v[2 * i + 1] = q.y[i];
+    }
   }
   return e;
 }
@@ -350,10 +385,11 @@ __device__ __forceinline__ void emit_surface(const Emitter& e, double eta, const
 
 // emitVolumeRay2D.jl:1-33: uniform point (quad = triangles ABC / CDA chosen
 // by area), nudged toward the midpoint, isotropic 3D direction projected on
-// the plane (sin(theta) cos(phi), cos(theta)).
+// the plane (sin(theta) cos(phi), cos(theta)).  cos_tab: the kCosTable
+// (cos, sin) pairs in LDS (non-faithful sampling).
 template <bool FAITHFUL>
-__device__ __forceinline__ void emit_volume(const Emitter& e, double eta, const RayDraws& rd, double& px,
-                                            double& py, double& dx, double& dy) {
+__device__ __forceinline__ void emit_volume(const Emitter& e, double eta, const RayDraws& rd, const double* cos_tab,
+                                            double& px, double& py, double& dx, double& dy) {
   double R1 = rd.R1(), R2 = rd.R2();
   double s1 = sqrt(R1);
   double wa = 1.0 - s1, wb = __dmul_rn(s1, 1.0 - R2), wc = __dmul_rn(s1, R2);
@@ -368,32 +404,42 @@ __device__ __forceinline__ void emit_volume(const Emitter& e, double eta, const 
   py = __dmul_rn(wa, Ay) + __dmul_rn(wb, By) + __dmul_rn(wc, Cy);
   px = px + __dmul_rn(e.mx - px, eta);
   py = py + __dmul_rn(e.my - py, eta);
-  double u4 = rd.th(), u5 = rd.ph();
-  double st, ct;
+  double u4 = rd.th();
+  double st, ct, cphi;
   if (FAITHFUL) {
     double theta = acos(1.0 - 2.0 * u4);
     st = sin(theta);
     ct = cos(theta);
+    cphi = cos(RTHX_TWO_PI * rd.ph());
   } else {
     ct = 1.0 - 2.0 * u4;                       // cos(acos(x)) = x
     st = 2.0 * sqrt(__dmul_rn(u4, 1.0 - u4));  // sin(acos(x)) = sqrt((1-x)(1+x))
+    cphi = (RTHX_ABLATE & 4) ? (1.0 - 2.0 * rd.ph()) : cos_2pi_u32(rd.ph_bits(), cos_tab);
   }
-  double cphi = FAITHFUL ? cos(RTHX_TWO_PI * u5) : ((RTHX_ABLATE & 4) ? (1.0 - 2.0 * u5) : cospi(2.0 * u5));
   dx = __dmul_rn(st, cphi);
   dy = ct;
 }
+
+// The coarse polygon a SINGLE-domain workgroup traces in, staged in LDS:
+// its record, solid-wall mask and fine point-location grid.
+struct SingleCoarse {
+  DevPoly poly;
+  DevGrid grid;
+  uint32_t solid;
+  int32_t count;  // fine polygons (first = 0)
+};
 
 // ---------------------------------------------------------------------------
 // traceRayUniform (traceRay.jl:20-70) and traceRayVariable (:73-147).
 // The gas branch (:31-40 / :105-116) and the solid-wall branch (:42-52 /
 // :118-128) both move the point and locate its fine cell; they are merged so
 // that the wave runs one point location for both kinds of lanes.
-// SINGLE: the domain has one coarse polygon, so the coarse data and its fine
-// grid are workgroup-uniform and a crossing can only leave the domain.
+// SINGLE: the domain has one convex coarse polygon, held in LDS (`sc`), and a
+// crossing can only leave the domain.
 // ---------------------------------------------------------------------------
 template <bool UNIFORM, bool SINGLE, bool FAITHFUL>
-__device__ __forceinline__ int64_t trace_ray(const DevDomain& D, const TraceParams& P, int c, double& px,
-                                             double& py, double dx, double dy, const RayDraws& rd) {
+__device__ __forceinline__ int trace_ray(const DevDomain& D, const TraceParams& P, const SingleCoarse& sc, int c,
+                                         double& px, double& py, double dx, double dy, const RayDraws& rd) {
   const double eta = P.eta;
   double S = 0.0, target = 0.0, acc = 0.0;
   if (UNIFORM) {
@@ -404,36 +450,46 @@ __device__ __forceinline__ int64_t trace_ray(const DevDomain& D, const TracePara
   } else {
     target = FAITHFUL ? -log(rd.path()) : neg_log_unit(rd.path());
   }
-  const double* beta_bin = D.beta + (size_t)P.bin * D.n_fine;
-  if (SINGLE) c = 0;
-  for (int it = 0; it < 10000; ++it) {
-    const DevGrid& fg_grid = D.f_grid[c];
-    const int first = D.f_offset[c];
-    const int count = D.f_offset[c + 1] - first;
-    int k;
-    double u = dist_to_polygon(px, py, dx, dy, D.c_xy + 8 * (size_t)c, D.c_nrm + 8 * (size_t)c, D.c_nv[c], k);
+  const double RTHX_GLOBAL* beta_bin = D.beta + (size_t)P.bin * D.n_fine;
+  for (int it = 0; it < (SINGLE ? 1 : 10000); ++it) {
+    int k, first, count;
+    double u;
+    uint32_t solid;
+    if (SINGLE) {
+      first = 0;
+      count = sc.count;
+      u = dist_to_polygon(px, py, dx, dy, sc.poly, k);
+      solid = sc.solid;
+    } else {
+      first = D.f_offset[c];
+      count = D.f_offset[c + 1] - first;
+      u = dist_to_polygon(px, py, dx, dy, D.c_poly[c], k);
+      solid = D.c_solid[c];
+    }
     bool gas;
     double beta = 0.0, tau_b = 0.0;
     if (UNIFORM) {
       gas = S < u;
     } else {
-      int f0 = locate_fine(D, fg_grid, first, count, px, py);
+      int f0 = SINGLE ? locate_fine(D, sc.grid, first, count, px, py)
+                      : locate_fine(D, D.f_grid[c], first, count, px, py);
       if (f0 < 0) return -1;
       beta = beta_bin[first + f0];
       tau_b = __dmul_rn(beta, u);
       gas = acc + tau_b >= target;
     }
-    bool wall = !gas && ((D.c_solid[c] >> k) & 1u);
+    bool wall = !gas && ((solid >> k) & 1u);
     if (gas || wall) {
       double t = gas ? (UNIFORM ? S : (target - acc) / beta) - eta : u - eta;
       px = px + __dmul_rn(t, dx);
       py = py + __dmul_rn(t, dy);
-      int f = locate_fine(D, fg_grid, first, count, px, py);
+      int f = SINGLE ? locate_fine(D, sc.grid, first, count, px, py)
+                     : locate_fine(D, D.f_grid[c], first, count, px, py);
       if (f < 0) return -1;
       int fg = first + f;
-      if (gas) return (int64_t)D.n_surfaces + fg;
+      if (gas) return D.n_surfaces + fg;
       int w;
-      dist_to_polygon(px, py, dx, dy, D.f_xy + 8 * (size_t)fg, D.f_nrm + 8 * (size_t)fg, D.f_nv[fg], w);
+      dist_to_polygon(px, py, dx, dy, D.f_poly[fg], w);
       return D.f_surf[4 * fg + w];  // -1 if the fine wall is not solid
     }
     if (SINGLE) return -1;  // an open wall of the only polygon leads outside: locate_coarse finds nothing
@@ -450,17 +506,18 @@ __device__ __forceinline__ int64_t trace_ray(const DevDomain& D, const TracePara
 // One ray (g, r) of emitter e: emit then trace.  Returns absorber (-1 =
 // lost); (ox, oy) emission point, (px, py) end point.
 template <bool UNIFORM, bool FAITHFUL, bool SINGLE>
-__device__ __forceinline__ int64_t trace_one(const DevDomain& D, const TraceParams& P, const Emitter& e, int64_t g,
-                                             int64_t r, double& ox, double& oy, double& px, double& py) {
-  const RayDraws rd((uint32_t)r, (uint32_t)g, (uint32_t)P.bin, P.key0, P.key1);
+__device__ __forceinline__ int trace_one(const DevDomain& D, const TraceParams& P, const Emitter& e,
+                                         const SingleCoarse& sc, const double* cos_tab, uint32_t g, uint32_t r,
+                                         double& ox, double& oy, double& px, double& py) {
+  const RayDraws rd(r, g, (uint32_t)P.bin, P.key0, P.key1);
   double dx, dy;
   if (e.surface)
     emit_surface<FAITHFUL>(e, P.eta, rd, px, py, dx, dy);
   else
-    emit_volume<FAITHFUL>(e, P.eta, rd, px, py, dx, dy);
+    emit_volume<FAITHFUL>(e, P.eta, rd, cos_tab, px, py, dx, dy);
   ox = px;
   oy = py;
-  return trace_ray<UNIFORM, SINGLE, FAITHFUL>(D, P, e.coarse, px, py, dx, dy, rd);
+  return trace_ray<UNIFORM, SINGLE, FAITHFUL>(D, P, sc, e.coarse, px, py, dx, dy, rd);
 }
 
 }  // namespace rthx

@@ -19,6 +19,25 @@
 
 namespace rthx {
 
+#define RTHX_LDS __attribute__((address_space(3)))
+
+// Occupancy target of the trace kernel (waves per SIMD): the register
+// allocator keeps it within 512/N VGPRs instead of hoisting loop-invariant
+// LDS reads into registers.
+#ifndef RTHX_TRACE_WAVES_PER_EU
+#define RTHX_TRACE_WAVES_PER_EU 5
+#endif
+#define RTHX_TRACE_WAVES __attribute__((amdgpu_waves_per_eu(RTHX_TRACE_WAVES_PER_EU)))
+
+// The same LDS address, hidden from the optimiser (one v_mov): loads through
+// it are not hoisted out of the ray loop.
+template <class T>
+__device__ __forceinline__ const T RTHX_LDS* lds_opaque(const T* p) {
+  const T RTHX_LDS* q = (const T RTHX_LDS*)p;
+  __asm__ volatile("" : "+v"(q));
+  return q;
+}
+
 __device__ __forceinline__ uint32_t lane_id() {
   return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
 }
@@ -61,7 +80,7 @@ __device__ __forceinline__ uint32_t compact_row(int64_t n_words, F count2, uint3
 }
 
 template <bool UNIFORM, bool PACK16, bool FAITHFUL, bool SINGLE, bool REC, bool SPLIT>
-__global__ __launch_bounds__(kTraceThreads) void trace_exchange_kernel(const DevDomain* __restrict__ Dp,
+__global__ __launch_bounds__(kTraceThreads) RTHX_TRACE_WAVES void trace_exchange_kernel(const DevDomain* __restrict__ Dp,
                                                                      TraceParams P, TallyParams T,
                                                                      RecordParams rec) {
   extern __shared__ uint32_t hist[];
@@ -73,6 +92,10 @@ __global__ __launch_bounds__(kTraceThreads) void trace_exchange_kernel(const Dev
   // than in ~26 VGPRs; measured 2.12 ms vs 2.30 (asm memory clobber) and
   // 2.48 ms (volatile reload) per 1e8 rays.
   __shared__ Emitter s_emit;
+  // SINGLE: the one coarse polygon and its fine grid, also in LDS, so that
+  // its 16 doubles do not occupy SGPRs for the whole loop.
+  __shared__ SingleCoarse s_single;
+  __shared__ double s_cos[2 * kCosTable];
 
   const int tid = threadIdx.x;
   const int64_t slot = SPLIT ? (int64_t)(blockIdx.x / T.split) : (int64_t)blockIdx.x;
@@ -84,10 +107,18 @@ __global__ __launch_bounds__(kTraceThreads) void trace_exchange_kernel(const Dev
   const int64_t n_words = PACK16 ? (T.n_emitters + 1) / 2 : T.n_emitters;
 
   for (int64_t w = tid; w < n_words; w += kTraceThreads) hist[w] = 0u;
+  if (!FAITHFUL)
+    for (int i = tid; i < 2 * kCosTable; i += kTraceThreads) s_cos[i] = D.cos_tab[i];
   if (tid == 0) {
     s_running = 0u;
     s_tallied = 0u;
     s_emit = load_emitter(D, g);
+    if (SINGLE) {
+      s_single.poly = D.c_poly[0];
+      s_single.grid = D.f_grid[0];
+      s_single.solid = D.c_solid[0];
+      s_single.count = D.f_offset[1];
+    }
   }
   // recorded emitter?  (RayRecorder ids, parallelRayTracing.jl:108)
   int rec_slot = -1;
@@ -96,11 +127,18 @@ __global__ __launch_bounds__(kTraceThreads) void trace_exchange_kernel(const Dev
       if (rec.ids[i] == g) { rec_slot = i; break; }
   __syncthreads();
 
+  // R < 2^32 and N < 2^31 (checked by rthx_trace_exchange): 32-bit ray and
+  // absorber indices.
   uint32_t tallied = 0;
-  for (int64_t r = r_begin + tid; r < r_end; r += kTraceThreads) {
-    const Emitter& e = s_emit;
+  for (uint32_t r = (uint32_t)r_begin + tid; r < (uint32_t)r_end; r += kTraceThreads) {
     double ox, oy, px, py;
-    int64_t a = trace_one<UNIFORM, FAITHFUL, SINGLE>(D, P, e, g, r, ox, oy, px, py);
+    // Opaque LDS addresses: re-read the loop-invariant coarse record and cos
+    // table at their point of use instead of hoisting ~40 values into VGPRs.
+    const SingleCoarse RTHX_LDS* sc = lds_opaque(&s_single);
+    const double RTHX_LDS* tab = lds_opaque(&s_cos[0]);
+    const Emitter RTHX_LDS* em = lds_opaque(&s_emit);
+    int a = trace_one<UNIFORM, FAITHFUL, SINGLE>(D, P, *(const Emitter*)em, *(const SingleCoarse*)sc, (const double*)tab,
+                                                 (uint32_t)g, r, ox, oy, px, py);
     if (a >= 0) {
       if (PACK16)
         atomicAdd(&hist[a >> 1], 1u << ((uint32_t)(a & 1) << 4));
