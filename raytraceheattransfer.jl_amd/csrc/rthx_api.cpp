@@ -197,7 +197,41 @@ rthx::DevGrid add_grid(const int32_t* nv, const double* xy, int first, int count
   return g;
 }
 
+// Device lookup tables (rthx_device.h): cos/sin(2 pi j/256) for
+// cos_2pi_u32, and for neg_log_tab per entry i the centre c of its z interval
+// [0.6875 + ..), invc = fl(1/c) and ln(invc) split into hi + lo, evaluated in
+// long double.
+void fill_tables(double* t) {
+  for (int j = 0; j < rthx::kCosTable; ++j) {
+    const long double a = 2.0L * 3.141592653589793238462643383279502884L * j / rthx::kCosTable;
+    t[2 * j] = (double)cosl(a);
+    t[2 * j + 1] = (double)sinl(a);
+  }
+  double* L = t + rthx::kLogTableOffset;
+  for (int i = 0; i < rthx::kLogTable; ++i) {
+    const double z0 = rthx::bitsd(rthx::kLogOff + ((uint64_t)i << 45));
+    const double z1 = rthx::bitsd(rthx::kLogOff + ((uint64_t)(i + 1) << 45));
+    const double invc = (double)(2.0L / ((long double)z0 + (long double)z1));
+    const long double T = logl((long double)invc);
+    const double hi = (double)T;
+    L[4 * i] = invc;
+    L[4 * i + 1] = hi;
+    L[4 * i + 2] = (double)(T - (long double)hi);
+    L[4 * i + 3] = 0.0;
+  }
+}
+
 }  // namespace
+
+// Host evaluation of the device free-path log (tests/test_numerics.py); not
+// part of include/rthx.h.
+extern "C" __attribute__((visibility("default"))) int rthx_debug_neg_log(const double* u, int64_t n, double* out) {
+  if ((!u || !out) && n > 0) return -1;
+  std::vector<double> t(rthx::kTableDoubles);
+  fill_tables(t.data());
+  for (int64_t k = 0; k < n; ++k) out[k] = rthx::neg_log_tab(u[k], t.data() + rthx::kLogTableOffset);
+  return 0;
+}
 
 RTHX_EXPORT int rthx_abi_version(void) { return RTHX_ABI_VERSION; }
 
@@ -358,12 +392,10 @@ RTHX_EXPORT int rthx_domain_create(const rthx_domain_desc* desc, int32_t device,
   };
   const std::vector<rthx::DevPoly> cpoly = polys(s.coarse_nv, s.coarse_xy, s.coarse_normal, nc);
   const std::vector<rthx::DevPoly> fpoly = polys(s.fine_nv, s.fine_xy, s.fine_normal, nf);
-  // (cos, sin)(2 pi j / 256) for the emission azimuth (rthx_device.h cos_2pi_u32)
-  std::vector<double> cos_tab(2 * rthx::kCosTable);
-  for (int j = 0; j < rthx::kCosTable; ++j) {
-    cos_tab[2 * j] = std::cos(2.0 * M_PI * j / rthx::kCosTable);
-    cos_tab[2 * j + 1] = std::sin(2.0 * M_PI * j / rthx::kCosTable);
-  }
+  // (cos, sin)(2 pi j / 256) for the emission azimuth (cos_2pi_u32) and the
+  // free-path log table (neg_log_tab)
+  std::vector<double> tables(rthx::kTableDoubles);
+  fill_tables(tables.data());
   UP(cpoly.data(), nc, D.c_poly);
   UP(csolid.data(), nc, D.c_solid);
   UP(s.coarse_bbox, 4 * nc, D.c_bbox);
@@ -382,7 +414,7 @@ RTHX_EXPORT int rthx_domain_create(const rthx_domain_desc* desc, int32_t device,
   UP(s.beta, (size_t)s.n_bins * nf, D.beta);
   UP(s_face.data(), s_face.size(), D.s_face);
   UP(s_wall.data(), s_wall.size(), D.s_wall);
-  UP(cos_tab.data(), cos_tab.size(), D.cos_tab);
+  UP(tables.data(), tables.size(), D.tables);
 #undef UP
   {
     int r3 = upload(d, &d->D, 1, &d->d_dom, "domain record");
@@ -441,7 +473,7 @@ RTHX_EXPORT int rthx_trace_exchange(rthx_domain* dom, const rthx_trace_args* a, 
   const int64_t words = pack16 ? (N + 1) / 2 : N;
   const size_t lds_bytes = (size_t)words * 4;
   if (lds_bytes + rthx::kStaticLdsBytes > rthx::kMaxLdsBytes)
-    return fail(RTHX_ERANGE, "N too large for the LDS row histogram of this build (N <= 78848)");
+    return fail(RTHX_ERANGE, "N too large for the LDS row histogram of this build (N <= 76800)");
   const int64_t row_cap = std::max<int64_t>(1, std::min<int64_t>(N, R));
 
   res->valid = false;

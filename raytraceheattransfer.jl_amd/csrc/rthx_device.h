@@ -59,6 +59,9 @@ struct alignas(16) DevCell {
 };
 
 constexpr int kCosTable = 256;  // cos/sin(2 pi j / 256), j < 256
+constexpr int kLogTable = 128;  // neg_log_tab entries
+constexpr int kLogTableOffset = 2 * kCosTable;
+constexpr int kTableDoubles = kLogTableOffset + 4 * kLogTable;
 
 struct DevDomain {
   int32_t n_coarse, n_fine, n_surfaces, n_bins;
@@ -86,8 +89,9 @@ struct DevDomain {
   // surface emitters
   const int32_t RTHX_GLOBAL* s_face;   // [Ns]
   const int32_t RTHX_GLOBAL* s_wall;   // [Ns]
-  // cos(2 pi j/256), sin(2 pi j/256) pairs, j < 256 (emission azimuth)
-  const double RTHX_GLOBAL* cos_tab;   // [256][2]
+  // kTableDoubles doubles: cos(2 pi j/256), sin(2 pi j/256) pairs, j < 256
+  // (emission azimuth), then kLogTable (invc, ln(invc) hi, lo, 0) quads
+  const double RTHX_GLOBAL* tables;
 };
 
 struct TraceParams {
@@ -162,29 +166,58 @@ struct RayDraws {
   __device__ __forceinline__ double l2() const { return u32(a[3]); }
 };
 
-// -ln(u) for u in [0, 1) (u = 0 -> +inf): fdlibm's __ieee754_log reduction
-// (x in [sqrt(2)/2, sqrt(2)), s = f/(2+f), degree-14 polynomial), <= 1 ulp
-// from the correctly rounded value; about half the instructions of ocml's
-// double-double log.  The free path S = -ln(u)/beta (traceRay.jl:25,79).
-__device__ __forceinline__ double neg_log_unit(double u) {
-  if (!(u > 0.0)) return __builtin_inf();
-  uint32_t hi = (uint32_t)__double2hiint(u);
-  uint32_t lo = (uint32_t)__double2loint(u);
-  int k = (int)((hi >> 20) & 0x7FFu) - 1023;
-  uint32_t hm = hi & 0x000FFFFFu;
-  uint32_t i = (hm + 0x95F64u) & 0x100000u;
-  double x = __hiloint2double((int)(hm | (i ^ 0x3FF00000u)), (int)lo);
-  k += (int)(i >> 20);
-  double f = x - 1.0;
-  double s = f / (2.0 + f), z = s * s, w = z * z;
-  double t1 = w * (3.999999999940941908e-01 + w * (2.222219843214978396e-01 + w * 1.531383769920937332e-01));
-  double t2 = z * (6.666666666666735130e-01 +
-                   w * (2.857142874366239149e-01 + w * (1.818357216161805012e-01 + w * 1.479819860511658591e-01)));
-  double R = t2 + t1, hfsq = 0.5 * f * f, dk = (double)k;
-  return -(dk * 6.93147180369123816490e-01 - ((hfsq - (s * (hfsq + R) + dk * 1.90821492927058770002e-10)) - f));
+#define RTHX_TWO_PI 6.283185307179586
+
+__host__ __device__ __forceinline__ uint64_t dbits(double x) { return __builtin_bit_cast(uint64_t, x); }
+__host__ __device__ __forceinline__ double bitsd(uint64_t b) { return __builtin_bit_cast(double, b); }
+
+// -ln(u) for u in (0, 1] from a 128-entry table (the free path
+// S = -ln(u)/beta, traceRay.jl:25,79).  u = 2^k z with z in [0.6875, 1.375)
+// (so u near 1 keeps k = 0), table entry i = 7 bits of z below the exponent:
+// invc ~ 1/c (c = centre of the entry's z interval) and T = ln(invc) as
+// hi + lo (host, long double: fill_log_table).  Then r = z invc - 1 (one fma,
+// |r| <= 2^-8) and -ln(u) = -k ln2 + T - log1p(r), log1p by its degree-7
+// Taylor polynomial (truncation < 2e-18 relative).  Within ~1 ulp of the
+// correctly rounded value (tests/test_numerics.py); no division, about a
+// third of the instructions of fdlibm's log.  u = 0 -> +inf.
+constexpr uint64_t kLogOff = 0x3FE6000000000000ull;  // bits of 0.6875
+
+__host__ __device__ __forceinline__ double neg_log_tab(double u, const double* tab) {
+  const uint64_t ix = dbits(u);
+  const uint64_t tmp = ix - kLogOff;
+  const int i = (int)((tmp >> 45) & (kLogTable - 1));
+  const int64_t k = (int64_t)tmp >> 52;
+  const double z = bitsd(ix - (tmp & 0xFFF0000000000000ull));
+  const double invc = tab[4 * i], t_hi = tab[4 * i + 1], t_lo = tab[4 * i + 2];
+  const double r = __builtin_fma(z, invc, -1.0);
+  double q = __builtin_fma(r, 1.0 / 7.0, -1.0 / 6.0);
+  q = __builtin_fma(r, q, 1.0 / 5.0);
+  q = __builtin_fma(r, q, -1.0 / 4.0);
+  q = __builtin_fma(r, q, 1.0 / 3.0);
+  q = __builtin_fma(r, q, -0.5);
+  const double l1p = __builtin_fma(r * r, q, r);
+  const double kd = (double)k;
+  const double hi = __builtin_fma(-kd, 6.93147180369123816490e-01, t_hi);  // ln2_hi: k ln2_hi exact
+  const double lo = __builtin_fma(-kd, 1.90821492927058770002e-10, t_lo) - l1p;
+  const double v = hi + lo;
+  return u > 0.0 ? v : __builtin_inf();
 }
 
-#define RTHX_TWO_PI 6.283185307179586
+// sqrt(x) for x in {0} U [2^-60, 1]: the rsq + Newton sequence of the
+// correctly rounded IEEE sqrt without its subnormal/overflow rescaling
+// (the operands here are unit draws, far from either).
+__device__ __forceinline__ double sqrt_unit(double x) {
+  const double y = __builtin_amdgcn_rsq(x);
+  double g = x * y, h = 0.5 * y;
+  const double r = __builtin_fma(-h, g, 0.5);
+  g = __builtin_fma(g, r, g);
+  h = __builtin_fma(h, r, h);
+  double d = __builtin_fma(-g, g, x);
+  g = __builtin_fma(d, h, g);
+  d = __builtin_fma(-g, g, x);
+  g = __builtin_fma(d, h, g);
+  return x > 0.0 ? g : x;
+}
 
 // cos(2 pi w / 2^32) for a 32-bit draw w (emitVolumeRay2D.jl:28-31: phi = 2 pi u,
 // cos(phi)).  Table-and-polynomial: w = j 2^24 + m, with (cos, sin) of
@@ -391,7 +424,7 @@ template <bool FAITHFUL>
 __device__ __forceinline__ void emit_volume(const Emitter& e, double eta, const RayDraws& rd, const double* cos_tab,
                                             double& px, double& py, double& dx, double& dy) {
   double R1 = rd.R1(), R2 = rd.R2();
-  double s1 = sqrt(R1);
+  double s1 = FAITHFUL ? sqrt(R1) : sqrt_unit(R1);
   double wa = 1.0 - s1, wb = __dmul_rn(s1, 1.0 - R2), wc = __dmul_rn(s1, R2);
   double Ax = e.v[0], Ay = e.v[1], Bx = e.v[2], By = e.v[3], Cx = e.v[4], Cy = e.v[5];
   if (e.nv == 4) {
@@ -413,7 +446,7 @@ __device__ __forceinline__ void emit_volume(const Emitter& e, double eta, const 
     cphi = cos(RTHX_TWO_PI * rd.ph());
   } else {
     ct = 1.0 - 2.0 * u4;                       // cos(acos(x)) = x
-    st = 2.0 * sqrt(__dmul_rn(u4, 1.0 - u4));  // sin(acos(x)) = sqrt((1-x)(1+x))
+    st = 2.0 * sqrt_unit(__dmul_rn(u4, 1.0 - u4));  // sin(acos(x)) = sqrt((1-x)(1+x))
     cphi = (RTHX_ABLATE & 4) ? (1.0 - 2.0 * rd.ph()) : cos_2pi_u32(rd.ph_bits(), cos_tab);
   }
   dx = __dmul_rn(st, cphi);
@@ -438,17 +471,20 @@ struct SingleCoarse {
 // crossing can only leave the domain.
 // ---------------------------------------------------------------------------
 template <bool UNIFORM, bool SINGLE, bool FAITHFUL>
-__device__ __forceinline__ int trace_ray(const DevDomain& D, const TraceParams& P, const SingleCoarse& sc, int c,
-                                         double& px, double& py, double dx, double dy, const RayDraws& rd) {
+__device__ __forceinline__ int trace_ray(const DevDomain& D, const TraceParams& P, const SingleCoarse& sc,
+                                         const double* tabs, int c, double& px, double& py, double dx, double dy,
+                                         const RayDraws& rd) {
   const double eta = P.eta;
   double S = 0.0, target = 0.0, acc = 0.0;
   if (UNIFORM) {
     const double u = rd.path();
     S = P.beta_uniform > 0
-            ? ((RTHX_ABLATE & 2) ? (1.0 - u) : FAITHFUL ? -log(u) / P.beta_uniform : neg_log_unit(u) * P.inv_beta_uniform)
+            ? ((RTHX_ABLATE & 2) ? (1.0 - u)
+               : FAITHFUL        ? -log(u) / P.beta_uniform
+                                 : neg_log_tab(u, tabs + kLogTableOffset) * P.inv_beta_uniform)
             : __builtin_inf();
   } else {
-    target = FAITHFUL ? -log(rd.path()) : neg_log_unit(rd.path());
+    target = FAITHFUL ? -log(rd.path()) : neg_log_tab(rd.path(), tabs + kLogTableOffset);
   }
   const double RTHX_GLOBAL* beta_bin = D.beta + (size_t)P.bin * D.n_fine;
   for (int it = 0; it < (SINGLE ? 1 : 10000); ++it) {
@@ -507,17 +543,17 @@ __device__ __forceinline__ int trace_ray(const DevDomain& D, const TraceParams& 
 // lost); (ox, oy) emission point, (px, py) end point.
 template <bool UNIFORM, bool FAITHFUL, bool SINGLE>
 __device__ __forceinline__ int trace_one(const DevDomain& D, const TraceParams& P, const Emitter& e,
-                                         const SingleCoarse& sc, const double* cos_tab, uint32_t g, uint32_t r,
+                                         const SingleCoarse& sc, const double* tabs, uint32_t g, uint32_t r,
                                          double& ox, double& oy, double& px, double& py) {
   const RayDraws rd(r, g, (uint32_t)P.bin, P.key0, P.key1);
   double dx, dy;
   if (e.surface)
     emit_surface<FAITHFUL>(e, P.eta, rd, px, py, dx, dy);
   else
-    emit_volume<FAITHFUL>(e, P.eta, rd, cos_tab, px, py, dx, dy);
+    emit_volume<FAITHFUL>(e, P.eta, rd, tabs, px, py, dx, dy);
   ox = px;
   oy = py;
-  return trace_ray<UNIFORM, SINGLE, FAITHFUL>(D, P, sc, e.coarse, px, py, dx, dy, rd);
+  return trace_ray<UNIFORM, SINGLE, FAITHFUL>(D, P, sc, tabs, e.coarse, px, py, dx, dy, rd);
 }
 
 }  // namespace rthx

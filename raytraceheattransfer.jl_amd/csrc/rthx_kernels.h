@@ -11,7 +11,7 @@ namespace rthx {
 
 constexpr int kTraceThreads = 256;               // 4 waves of 64 per emitter row (slice)
 constexpr size_t kMaxLdsBytes = 160 * 1024;      // gfx950 LDS per CU
-constexpr int64_t kStaticLdsBytes = 6144;       // the trace kernel's static LDS (emitter, coarse, cos table, ...)
+constexpr int64_t kStaticLdsBytes = 10240;      // the trace kernel's static LDS (emitter, coarse, tables, ...)
 
 struct RecordParams {
   int32_t n;            // recorded emitters in this call

@@ -95,7 +95,7 @@ __global__ __launch_bounds__(kTraceThreads) RTHX_TRACE_WAVES void trace_exchange
   // SINGLE: the one coarse polygon and its fine grid, also in LDS, so that
   // its 16 doubles do not occupy SGPRs for the whole loop.
   __shared__ SingleCoarse s_single;
-  __shared__ double s_cos[2 * kCosTable];
+  __shared__ double s_tab[kTableDoubles];  // cos and log tables (rthx_device.h)
 
   const int tid = threadIdx.x;
   const int64_t slot = SPLIT ? (int64_t)(blockIdx.x / T.split) : (int64_t)blockIdx.x;
@@ -108,7 +108,7 @@ __global__ __launch_bounds__(kTraceThreads) RTHX_TRACE_WAVES void trace_exchange
 
   for (int64_t w = tid; w < n_words; w += kTraceThreads) hist[w] = 0u;
   if (!FAITHFUL)
-    for (int i = tid; i < 2 * kCosTable; i += kTraceThreads) s_cos[i] = D.cos_tab[i];
+    for (int i = tid; i < kTableDoubles; i += kTraceThreads) s_tab[i] = D.tables[i];
   if (tid == 0) {
     s_running = 0u;
     s_tallied = 0u;
@@ -135,7 +135,7 @@ __global__ __launch_bounds__(kTraceThreads) RTHX_TRACE_WAVES void trace_exchange
     // Opaque LDS addresses: re-read the loop-invariant coarse record and cos
     // table at their point of use instead of hoisting ~40 values into VGPRs.
     const SingleCoarse RTHX_LDS* sc = lds_opaque(&s_single);
-    const double RTHX_LDS* tab = lds_opaque(&s_cos[0]);
+    const double RTHX_LDS* tab = lds_opaque(&s_tab[0]);
     const Emitter RTHX_LDS* em = lds_opaque(&s_emit);
     int a = trace_one<UNIFORM, FAITHFUL, SINGLE>(D, P, *(const Emitter*)em, *(const SingleCoarse*)sc, (const double*)tab,
                                                  (uint32_t)g, r, ox, oy, px, py);

@@ -203,7 +203,7 @@ def test_lds_limit_reports_erange(hip):
 
     from rthx import abi
 
-    dom = H.square_domain(286)  # N = 1144 + 81796 > 81408
+    dom = H.square_domain(286)  # N = 1144 + 81796 > 76800
     flat = dom.flat()
     dd = hip.DeviceDomain(flat, 0)
     res = hip.DeviceResult()

@@ -1,0 +1,56 @@
+"""Host evaluation of the device free-path logarithm (rthx_device.h
+neg_log_tab, through the debug export rthx_debug_neg_log): -ln(u) within
+about one ulp of glibc's log over the whole unit interval, including the
+table-interval boundaries, powers of two and u -> 1, where the absolute error
+must stay at the 1e-18 level (it becomes the ray's free path)."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from rthx import _lib
+
+
+@pytest.fixture(scope="module")
+def neg_log():
+    lib = _lib.load()
+    f = lib.rthx_debug_neg_log
+    f.argtypes = [C.POINTER(C.c_double), C.c_int64, C.POINTER(C.c_double)]
+
+    def run(u):
+        u = np.ascontiguousarray(u, dtype=np.float64)
+        out = np.empty_like(u)
+        assert f(u.ctypes.data_as(C.POINTER(C.c_double)), u.size, out.ctypes.data_as(C.POINTER(C.c_double))) == 0
+        return out
+    return run
+
+
+def ulps(a, b):
+    return np.abs(a - b) / np.spacing(np.abs(b))
+
+
+def test_neg_log_random_draws(neg_log):
+    rng = np.random.default_rng(7)
+    # u52 draws: k / 2^52
+    u = (rng.integers(1, 2**52, size=2_000_000, dtype=np.int64)).astype(np.float64) * 2.0**-52
+    got, ref = neg_log(u), -np.log(u)
+    small = ref < 1e-3  # u -> 1: cancellation against the table's ln(invc); absolute error counts
+    e = ulps(got[~small], ref[~small])
+    assert e.max() <= 1.5 and e.mean() < 0.3
+    assert np.abs(got[small] - ref[small]).max() <= 1e-18
+
+
+def test_neg_log_edges(neg_log):
+    k = np.arange(1, 53)
+    pow2 = 2.0 ** -k.astype(np.float64)
+    bounds = np.array([np.frombuffer(np.uint64(0x3FE6000000000000 + (i << 45)).tobytes(), np.float64)[0]
+                       for i in range(128)])
+    bounds = bounds[bounds < 1.0]
+    u = np.concatenate([pow2, pow2 * (1 - 2.0**-52), bounds, np.nextafter(bounds, 0), 1 - np.arange(1, 2000) * 2.0**-52,
+                        [2.0**-52, 0.6875, 0.5, 1.0]])
+    got, ref = neg_log(u), -np.log(u)
+    small = ref < 1e-3
+    assert ulps(got[~small], ref[~small]).max() <= 1.5
+    assert np.abs(got[small] - ref[small]).max() <= 1e-18
+    assert neg_log(np.array([0.0]))[0] == np.inf
+    assert neg_log(np.array([1.0]))[0] == 0.0
