@@ -44,39 +44,51 @@ __device__ __forceinline__ uint32_t lane_id() {
 
 // Workgroup-wide compaction of one row's counts, ascending absorber order
 // (the reference's sparse() sorts columns, parallelRayTracing.jl:154).
-// count2(w) returns the counts of absorbers 2w and 2w+1 (PAIRS) or of w.
-// Returns the row's nnz (valid in every lane).
+// count2(w, lo, hi) gives the counts of absorbers 2w and 2w+1 (PAIRS) or of w
+// (hi = 0).  Wave v owns a contiguous quarter of the words and walks it 64
+// words per step: a counting pass (ballot + popcount, no barrier), one
+// barrier to combine the four wave totals, then a writing pass whose lanes
+// store consecutive entries (coalesced).  Returns the row's nnz (valid in
+// every lane).
 template <bool PAIRS, class F>
 __device__ __forceinline__ uint32_t compact_row(int64_t n_words, F count2, uint32_t* __restrict__ out_c,
-                                                uint32_t* __restrict__ out_n, uint32_t* wave_sum,
-                                                uint32_t* s_running) {
-  const int tid = threadIdx.x;
+                                                uint32_t* __restrict__ out_n, uint32_t* wave_sum) {
+  constexpr int kWaves = kTraceThreads / 64;
   const uint32_t lane = lane_id();
-  const int wave = tid >> 6;
+  const int wave = threadIdx.x >> 6;
   const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  for (int64_t w0 = 0; w0 < n_words; w0 += kTraceThreads) {
-    int64_t w = w0 + tid;
+  const int64_t per = ((n_words + kWaves * 64 - 1) / (kWaves * 64)) * 64;
+  const int64_t wb = wave * per;
+  const int64_t we = wb + per < n_words ? wb + per : n_words;
+  uint32_t cnt = 0;
+  for (int64_t w0 = wb; w0 < we; w0 += 64) {
+    const int64_t w = w0 + lane;
     uint32_t lo = 0u, hi = 0u;
-    if (w < n_words) count2(w, lo, hi);
-    uint64_t m_lo = __ballot(lo != 0u);
-    uint64_t m_hi = PAIRS ? __ballot(hi != 0u) : 0ull;
-    uint32_t pre = __popcll(m_lo & lt_mask) + __popcll(m_hi & lt_mask);
-    if (lane == 0) wave_sum[wave] = __popcll(m_lo) + __popcll(m_hi);
-    __syncthreads();
-    uint32_t base = *s_running;
-    for (int i = 0; i < wave; ++i) base += wave_sum[i];
-    uint32_t pos = base + pre;
+    if (w < we) count2(w, lo, hi);
+    cnt += __popcll(__ballot(lo != 0u)) + (PAIRS ? __popcll(__ballot(hi != 0u)) : 0);
+  }
+  if (lane == 0) wave_sum[wave] = cnt;
+  __syncthreads();
+  uint32_t base = 0, total = 0;
+#pragma unroll
+  for (int i = 0; i < kWaves; ++i) {
+    const uint32_t ws = wave_sum[i];
+    base += i < wave ? ws : 0u;
+    total += ws;
+  }
+  for (int64_t w0 = wb; w0 < we; w0 += 64) {
+    const int64_t w = w0 + lane;
+    uint32_t lo = 0u, hi = 0u;
+    if (w < we) count2(w, lo, hi);
+    const uint64_t m_lo = __ballot(lo != 0u);
+    const uint64_t m_hi = PAIRS ? __ballot(hi != 0u) : 0ull;
+    uint32_t pos = base + __popcll(m_lo & lt_mask) + __popcll(m_hi & lt_mask);
     if (lo) { out_c[pos] = PAIRS ? (uint32_t)(2 * w) : (uint32_t)w; out_n[pos] = lo; ++pos; }
     if (PAIRS && hi) { out_c[pos] = (uint32_t)(2 * w + 1); out_n[pos] = hi; }
-    __syncthreads();
-    if (tid == 0) {
-      uint32_t tot = 0;
-      for (int i = 0; i < kTraceThreads / 64; ++i) tot += wave_sum[i];
-      *s_running += tot;
-    }
-    __syncthreads();
+    base += __popcll(m_lo) + __popcll(m_hi);
   }
-  return *s_running;
+  __syncthreads();  // wave_sum may be reused by the caller
+  return total;
 }
 
 template <bool UNIFORM, bool PACK16, bool FAITHFUL, bool SINGLE, bool REC, bool SPLIT>
@@ -86,7 +98,6 @@ __global__ __launch_bounds__(kTraceThreads) RTHX_TRACE_WAVES void trace_exchange
   extern __shared__ uint32_t hist[];
   const DevDomain& D = *Dp;
   __shared__ uint32_t wave_sum[kTraceThreads / 64];
-  __shared__ uint32_t s_running;
   __shared__ uint32_t s_tallied;
   // Emitter data is workgroup-uniform: kept in LDS (broadcast ds_reads) rather
   // than in ~26 VGPRs; measured 2.12 ms vs 2.30 (asm memory clobber) and
@@ -110,7 +121,6 @@ __global__ __launch_bounds__(kTraceThreads) RTHX_TRACE_WAVES void trace_exchange
   if (!FAITHFUL)
     for (int i = tid; i < kTableDoubles; i += kTraceThreads) s_tab[i] = D.tables[i];
   if (tid == 0) {
-    s_running = 0u;
     s_tallied = 0u;
     s_emit = load_emitter(D, g);
     if (SINGLE) {
@@ -181,11 +191,37 @@ __global__ __launch_bounds__(kTraceThreads) RTHX_TRACE_WAVES void trace_exchange
         lo = PACK16 ? (v & 0xFFFFu) : v;
         hi = PACK16 ? (v >> 16) : 0u;
       },
-      T.stage_cols + slot * T.row_cap, T.stage_cnt + slot * T.row_cap, wave_sum, &s_running);
+      T.stage_cols + slot * T.row_cap, T.stage_cnt + slot * T.row_cap, wave_sum);
   if (tid == 0) {
     T.row_nnz[slot] = nnz;
     T.row_tallied[slot] = s_tallied;
   }
+}
+
+// Compaction of a row held in global memory (split rows): coalesced reads,
+// 256 words per step, ballot + popcount offsets within the step.
+__device__ __forceinline__ uint32_t compact_row_global(int64_t n, const uint32_t* __restrict__ dense,
+                                                       uint32_t* __restrict__ out_c, uint32_t* __restrict__ out_n,
+                                                       uint32_t* wave_sum, uint32_t* s_running) {
+  const int tid = threadIdx.x;
+  const uint32_t lane = lane_id();
+  const int wave = tid >> 6;
+  const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  for (int64_t w0 = 0; w0 < n; w0 += kTraceThreads) {
+    const int64_t w = w0 + tid;
+    const uint32_t v = w < n ? dense[w] : 0u;
+    const uint64_t m = __ballot(v != 0u);
+    if (lane == 0) wave_sum[wave] = __popcll(m);
+    __syncthreads();
+    uint32_t pos = *s_running + __popcll(m & lt_mask);
+    for (int i = 0; i < wave; ++i) pos += wave_sum[i];
+    if (v) { out_c[pos] = (uint32_t)w; out_n[pos] = v; }
+    __syncthreads();
+    if (tid == 0)
+      for (int i = 0; i < kTraceThreads / 64; ++i) *s_running += wave_sum[i];
+    __syncthreads();
+  }
+  return *s_running;
 }
 
 // Split rows: compact the dense per-row counts into the staging slots.
@@ -196,9 +232,8 @@ __global__ __launch_bounds__(kTraceThreads) void row_compact_kernel(TallyParams 
   if (threadIdx.x == 0) s_running = 0u;
   __syncthreads();
   const uint32_t* dense = T.dense + slot * T.n_emitters;
-  uint32_t nnz = compact_row<false>(
-      T.n_emitters, [&](int64_t w, uint32_t& lo, uint32_t& hi) { lo = dense[w]; hi = 0u; },
-      T.stage_cols + slot * T.row_cap, T.stage_cnt + slot * T.row_cap, wave_sum, &s_running);
+  uint32_t nnz = compact_row_global(T.n_emitters, dense, T.stage_cols + slot * T.row_cap,
+                                    T.stage_cnt + slot * T.row_cap, wave_sum, &s_running);
   if (threadIdx.x == 0) T.row_nnz[slot] = nnz;
 }
 

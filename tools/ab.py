@@ -1,0 +1,75 @@
+"""A/B timing of several librthx.so builds in ONE process (diagnostic).
+
+Each library is loaded with RTLD_LOCAL, gets its own domain and result on
+device 0, and the libraries are timed in interleaved rounds so that clock and
+thermal drift hit them alike.  Prints the median trace-kernel time (HIP
+events) per library.
+
+  python tools/ab.py --rays 100000000 --rounds 8 libA.so libB.so ...
+"""
+import argparse
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "raytraceheattransfer.jl_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: F401,E402  (one HIP runtime for all libraries)
+
+from rthx import abi, _lib  # noqa: E402
+
+
+def open_lib(path):
+    lib = C.CDLL(path, mode=os.RTLD_LOCAL)
+    lib.rthx_last_error.restype = C.c_char_p
+    lib.rthx_domain_create.argtypes = [C.POINTER(abi.DomainDesc), C.c_int32, C.POINTER(C.c_void_p)]
+    lib.rthx_result_create.argtypes = [C.POINTER(C.c_void_p)]
+    lib.rthx_trace_exchange.argtypes = [C.c_void_p, C.POINTER(abi.TraceArgs), C.c_void_p]
+    lib.rthx_result_get_info.argtypes = [C.c_void_p, C.POINTER(abi.ResultInfo)]
+    return lib
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("libs", nargs="+")
+    ap.add_argument("--rays", type=int, default=100_000_000)
+    ap.add_argument("--rounds", type=int, default=8)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--ndim", type=int, default=101)
+    args = ap.parse_args()
+    import bench
+
+    dom = bench.build_domain(args.ndim)
+    flat = dom.flat()
+    N = flat.n_emitters
+    R = args.rays // N
+    nudge = 10_000 * np.finfo(np.float64).eps
+    targs, _k = _lib.make_args(0, R, nudge, 1, 0, N, 1, flags=abi.RTHX_FLAG_DEVICE_ONLY)
+    runs = []
+    for p in args.libs:
+        lib = open_lib(p)
+        h, r = C.c_void_p(), C.c_void_p()
+        assert lib.rthx_domain_create(C.byref(flat.desc), 0, C.byref(h)) == 0, lib.rthx_last_error()
+        assert lib.rthx_result_create(C.byref(r)) == 0
+        for _ in range(2):
+            assert lib.rthx_trace_exchange(h, C.byref(targs), r) == 0, lib.rthx_last_error()
+        runs.append((p, lib, h, r, []))
+    for _ in range(args.rounds):
+        for p, lib, h, r, ts in runs:
+            for _ in range(args.steps):
+                assert lib.rthx_trace_exchange(h, C.byref(targs), r) == 0
+                inf = abi.ResultInfo()
+                lib.rthx_result_get_info(r, C.byref(inf))
+                ts.append(inf.trace_ms)
+    for p, lib, h, r, ts in runs:
+        t = np.array(ts)
+        print(f"{os.path.basename(os.path.dirname(p)) or p:12s} median {np.median(t):.4f} ms  min {t.min():.4f}  "
+              f"p90 {np.percentile(t, 90):.4f}  {N * R / np.median(t) / 1e6:.1f} Mrays/s (R={R})", flush=True)
+
+
+if __name__ == "__main__":
+    main()
