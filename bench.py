@@ -98,11 +98,36 @@ def read_pmc_traffic():
         return None
 
 
+def read_fp64_flops_per_ray():
+    """fp64 FLOP per traced ray of the trace kernel from the committed SQ
+    counter summary (profiles/round1/pmc_sq.json, tools/gpu_sq.sh):
+    (ADD + MUL + 2 FMA + TRANS) fp64 instructions per wave-ray -- one
+    instruction per wave covers the 64 rays of its lanes."""
+    p = os.path.join(ROOT, "profiles", "round1", "pmc_sq.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        with open(p) as fh:
+            d = json.load(fh)
+        k = next(x for x in d if TRACE_KERNEL in x)
+        c = {n: v["mean"] for n, v in d[k].items()}
+        rays = float(d.get("_rays_per_launch", 99994545))
+        wave_rays = rays / 64.0
+        f = (c["SQ_INSTS_VALU_ADD_F64"] + c["SQ_INSTS_VALU_MUL_F64"] + 2 * c["SQ_INSTS_VALU_FMA_F64"]
+             + c["SQ_INSTS_VALU_TRANS_F64"])
+        return f / wave_rays
+    except Exception:
+        return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--prewarm-s", type=float, default=0.25,
+                    help="untimed steps run for this long before the W warmup steps, so that the timed steps see "
+                         "the steady-state GPU clock (the first ~15 steps of a fresh process run up to 20%% slower)")
     ap.add_argument("--rays-per-gpu", type=int, default=RAYS_PER_GPU)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
@@ -144,6 +169,11 @@ def main():
         if dist is not None:
             dist.barrier()
 
+    t_pre = time.perf_counter()
+    prewarm_steps = 0
+    while time.perf_counter() - t_pre < args.prewarm_s:
+        res.trace(dd, targs)
+        prewarm_steps += 1
     for _ in range(args.warmup):
         res.trace(dd, targs)
     _lib.synchronize(device)
@@ -195,6 +225,14 @@ def main():
         b_alg = 8.0 * rays_rank + 12.0 * nnz_rank
         achieved = b_alg / (avg_trace_ms * 1e-3) / 1e9
         traffic = read_pmc_traffic()
+        fpr = read_fp64_flops_per_ray()
+        fp64_roof = None
+        if fpr is not None:
+            tf = rays_rank * fpr / (avg_trace_ms * 1e-3) / 1e12
+            fp64_roof = {"bound": "fp64-valu", "achieved": round(tf, 3), "peak": FP64_VECTOR_PEAK_TFLOPS,
+                         "unit": "TFLOP/s", "frac": round(tf / FP64_VECTOR_PEAK_TFLOPS, 4),
+                         "flop_per_ray": round(fpr, 1),
+                         "note": "fp64 VALU instructions per ray from profiles/round1/pmc_sq.json (SQ counters)"}
         out = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -202,6 +240,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "prewarm_steps": prewarm_steps,
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
             "scaling": "weak",
@@ -231,6 +270,7 @@ def main():
                 "note": "latency/fp64-VALU bound path; HBM fraction reported as mandated (DESIGN.md)",
             },
             "pack_ms": round(float(np.mean(pack_ms)), 4),
+            "roofline_fp64": fp64_roof,
             "e2e_with_d2h_mrays_s": round(e2e, 3) if e2e else None,
         }
         if args.emulate_world > 1:
