@@ -14,6 +14,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -106,6 +107,7 @@ struct rthx_domain {
   std::vector<double> uniform_beta;  // per bin
   std::vector<double> beta_first;    // beta of fine face 0 per bin (traceRay.jl:6-11)
   bool single_convex = false;        // one convex coarse polygon (SINGLE kernels)
+  bool axis_rect = false;            // every polygon an axis-aligned rectangle in canonical order (AXIS kernels)
   ~rthx_domain() {
     for (void* p : allocs) (void)hipFree(p);
     for (auto& e : ev)
@@ -392,6 +394,17 @@ RTHX_EXPORT int rthx_domain_create(const rthx_domain_desc* desc, int32_t device,
   };
   const std::vector<rthx::DevPoly> cpoly = polys(s.coarse_nv, s.coarse_xy, s.coarse_normal, nc);
   const std::vector<rthx::DevPoly> fpoly = polys(s.fine_nv, s.fine_xy, s.fine_normal, nf);
+  // AXIS kernels (rthx_device.h dist_to_rect): v0 the min corner, CCW, wall
+  // normals exactly (0,-1), (1,0), (0,1), (-1,0) (calculateInwardNormal's
+  // orientation)
+  auto canonical_rect = [](const int32_t nv, const rthx::DevPoly& q) {
+    return nv == 4 && q.x[0] < q.x[1] && q.y[0] < q.y[2] && q.x[1] == q.x[2] && q.x[3] == q.x[0] &&
+           q.y[1] == q.y[0] && q.y[3] == q.y[2] && q.nx[0] == 0.0 && q.ny[0] == -1.0 && q.nx[1] == 1.0 &&
+           q.ny[1] == 0.0 && q.nx[2] == 0.0 && q.ny[2] == 1.0 && q.nx[3] == -1.0 && q.ny[3] == 0.0;
+  };
+  d->axis_rect = true;
+  for (size_t c = 0; c < nc && d->axis_rect; ++c) d->axis_rect = canonical_rect(s.coarse_nv[c], cpoly[c]);
+  for (size_t f = 0; f < nf && d->axis_rect; ++f) d->axis_rect = canonical_rect(s.fine_nv[f], fpoly[f]);
   // (cos, sin)(2 pi j / 256) for the emission azimuth (cos_2pi_u32) and the
   // free-path log table (neg_log_tab)
   std::vector<double> tables(rthx::kTableDoubles);
@@ -568,6 +581,7 @@ RTHX_EXPORT int rthx_trace_exchange(rthx_domain* dom, const rthx_trace_args* a, 
     L.pack16 = pack16;
     L.faithful = (a->flags & RTHX_FLAG_FAITHFUL_SAMPLING) != 0;
     L.single = dom->single_convex;
+    L.axis = dom->axis_rect && !(getenv("RTHX_NO_AXIS") && getenv("RTHX_NO_AXIS")[0] == '1');
     HIP_TRY(rthx::launch_trace(L), "trace_exchange_kernel launch");
   }
   HIP_TRY(hipEventRecord(dom->ev[1], st), "hipEventRecord");

@@ -271,6 +271,43 @@ __device__ __forceinline__ double dist_to_polygon(double px, double py, double d
   return u > 0.0 ? u : __builtin_inf();
 }
 
+// distToSurface2D on an axis-aligned rectangle stored in canonical order:
+// v0 = (x0,y0) the min corner, counter-clockwise, and wall normals exactly
+// (0,-1), (1,0), (0,1), (-1,0) -- calculateInwardNormal.jl:1-12 flips its
+// normal away from the polygon midpoint, so the stored "inward" normals
+// point out of the cell (the parameter num/den is the same either way);
+// rthx_domain_create checks the pattern.  The general expressions reduce
+// exactly: num_i = (v_i - p).n_i is py-y0, x1-px, y1-py, px-x0 and
+// den_i = d.n_i is -dy, dx, dy, -dx (products with +-1 and +-0 are exact), so
+// the same candidates, comparisons and first-index ties as dist_to_polygon,
+// with 4 of its 16 geometry reads and no multiplies for num/den.
+template <class Poly>
+__device__ __forceinline__ double dist_to_rect(double px, double py, double dx, double dy, const Poly& q,
+                                               int& widx) {
+  const double x0 = q.x[0], x1 = q.x[1], y0 = q.y[0], y1 = q.y[2];
+  const double num[4] = {py - y0, x1 - px, y1 - py, px - x0};
+  const double den[4] = {-dy, dx, dy, -dx};
+  double bn = 1.0, bd = 0.0;
+  int bi = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    double an = fabs(num[i]), ad = fabs(den[i]);
+    bool better = (ad >= 1e-10) && (__dmul_rn(num[i], den[i]) > 0.0) && (__dmul_rn(an, bd) < __dmul_rn(bn, ad));
+    bn = better ? an : bn;
+    bd = better ? ad : bd;
+    bi = better ? i : bi;
+  }
+  widx = bi;
+  if (bd == 0.0) return __builtin_inf();
+  double u = bn / bd;
+  return u > 0.0 ? u : __builtin_inf();
+}
+
+template <bool AXIS, class Poly>
+__device__ __forceinline__ double dist_to_cell(double px, double py, double dx, double dy, const Poly& q, int& widx) {
+  return AXIS ? dist_to_rect(px, py, dx, dy, q, widx) : dist_to_polygon(px, py, dx, dy, q, widx);
+}
+
 // pointInPolygonFast2D, findFace2D.jl:77-101 (crossing test, j = previous
 // vertex).  The reference's  px < xi + (xj-xi)/(yj-yi) (py-yi)  is evaluated
 // without the division as  sign((xj-xi)(py-yi) - (px-xi)(yj-yi)) == sign(yj-yi),
@@ -470,7 +507,7 @@ struct SingleCoarse {
 // SINGLE: the domain has one convex coarse polygon, held in LDS (`sc`), and a
 // crossing can only leave the domain.
 // ---------------------------------------------------------------------------
-template <bool UNIFORM, bool SINGLE, bool FAITHFUL>
+template <bool UNIFORM, bool SINGLE, bool FAITHFUL, bool AXIS>
 __device__ __forceinline__ int trace_ray(const DevDomain& D, const TraceParams& P, const SingleCoarse& sc,
                                          const double* tabs, int c, double& px, double& py, double dx, double dy,
                                          const RayDraws& rd) {
@@ -494,12 +531,12 @@ __device__ __forceinline__ int trace_ray(const DevDomain& D, const TraceParams& 
     if (SINGLE) {
       first = 0;
       count = sc.count;
-      u = dist_to_polygon(px, py, dx, dy, sc.poly, k);
+      u = dist_to_cell<AXIS>(px, py, dx, dy, sc.poly, k);
       solid = sc.solid;
     } else {
       first = D.f_offset[c];
       count = D.f_offset[c + 1] - first;
-      u = dist_to_polygon(px, py, dx, dy, D.c_poly[c], k);
+      u = dist_to_cell<AXIS>(px, py, dx, dy, D.c_poly[c], k);
       solid = D.c_solid[c];
     }
     bool gas;
@@ -525,7 +562,7 @@ __device__ __forceinline__ int trace_ray(const DevDomain& D, const TraceParams& 
       int fg = first + f;
       if (gas) return D.n_surfaces + fg;
       int w;
-      dist_to_polygon(px, py, dx, dy, D.f_poly[fg], w);
+      dist_to_cell<AXIS>(px, py, dx, dy, D.f_poly[fg], w);
       return D.f_surf[4 * fg + w];  // -1 if the fine wall is not solid
     }
     if (SINGLE) return -1;  // an open wall of the only polygon leads outside: locate_coarse finds nothing
@@ -541,7 +578,7 @@ __device__ __forceinline__ int trace_ray(const DevDomain& D, const TraceParams& 
 
 // One ray (g, r) of emitter e: emit then trace.  Returns absorber (-1 =
 // lost); (ox, oy) emission point, (px, py) end point.
-template <bool UNIFORM, bool FAITHFUL, bool SINGLE>
+template <bool UNIFORM, bool FAITHFUL, bool SINGLE, bool AXIS>
 __device__ __forceinline__ int trace_one(const DevDomain& D, const TraceParams& P, const Emitter& e,
                                          const SingleCoarse& sc, const double* tabs, uint32_t g, uint32_t r,
                                          double& ox, double& oy, double& px, double& py) {
@@ -553,7 +590,7 @@ __device__ __forceinline__ int trace_one(const DevDomain& D, const TraceParams& 
     emit_volume<FAITHFUL>(e, P.eta, rd, tabs, px, py, dx, dy);
   ox = px;
   oy = py;
-  return trace_ray<UNIFORM, SINGLE, FAITHFUL>(D, P, sc, tabs, e.coarse, px, py, dx, dy, rd);
+  return trace_ray<UNIFORM, SINGLE, FAITHFUL, AXIS>(D, P, sc, tabs, e.coarse, px, py, dx, dy, rd);
 }
 
 }  // namespace rthx

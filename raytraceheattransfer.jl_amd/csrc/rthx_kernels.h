@@ -45,7 +45,7 @@ struct LaunchCfg {
   RecordParams rec;
   size_t lds_bytes;
   hipStream_t stream;
-  bool uniform, pack16, faithful, single;
+  bool uniform, pack16, faithful, single, axis;
 };
 
 hipError_t launch_trace(const LaunchCfg& L);

@@ -91,7 +91,7 @@ __device__ __forceinline__ uint32_t compact_row(int64_t n_words, F count2, uint3
   return total;
 }
 
-template <bool UNIFORM, bool PACK16, bool FAITHFUL, bool SINGLE, bool REC, bool SPLIT>
+template <bool UNIFORM, bool PACK16, bool FAITHFUL, bool SINGLE, bool REC, bool SPLIT, bool AXIS>
 __global__ __launch_bounds__(kTraceThreads) RTHX_TRACE_WAVES void trace_exchange_kernel(const DevDomain* __restrict__ Dp,
                                                                      TraceParams P, TallyParams T,
                                                                      RecordParams rec) {
@@ -147,7 +147,7 @@ __global__ __launch_bounds__(kTraceThreads) RTHX_TRACE_WAVES void trace_exchange
     const SingleCoarse RTHX_LDS* sc = lds_opaque(&s_single);
     const double RTHX_LDS* tab = lds_opaque(&s_tab[0]);
     const Emitter RTHX_LDS* em = lds_opaque(&s_emit);
-    int a = trace_one<UNIFORM, FAITHFUL, SINGLE>(D, P, *(const Emitter*)em, *(const SingleCoarse*)sc, (const double*)tab,
+    int a = trace_one<UNIFORM, FAITHFUL, SINGLE, AXIS>(D, P, *(const Emitter*)em, *(const SingleCoarse*)sc, (const double*)tab,
                                                  (uint32_t)g, r, ox, oy, px, py);
     if (a >= 0) {
       if (PACK16)
@@ -304,9 +304,9 @@ __global__ __launch_bounds__(256) void csr_pack_kernel(const uint32_t* __restric
 // ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
-template <bool UNIFORM, bool PACK16, bool FAITHFUL, bool SINGLE, bool REC, bool SPLIT>
+template <bool UNIFORM, bool PACK16, bool FAITHFUL, bool SINGLE, bool REC, bool SPLIT, bool AXIS>
 static hipError_t launch_trace_t(const LaunchCfg& L) {
-  auto kern = trace_exchange_kernel<UNIFORM, PACK16, FAITHFUL, SINGLE, REC, SPLIT>;
+  auto kern = trace_exchange_kernel<UNIFORM, PACK16, FAITHFUL, SINGLE, REC, SPLIT, AXIS>;
   if (L.lds_bytes > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)L.lds_bytes);
@@ -318,16 +318,22 @@ static hipError_t launch_trace_t(const LaunchCfg& L) {
   return hipGetLastError();
 }
 
+template <bool UNIFORM, bool PACK16, bool FAITHFUL, bool AXIS>
+static hipError_t launch_trace_a(const LaunchCfg& L) {
+  if (L.T.split > 1) {
+    if (L.single) return launch_trace_t<UNIFORM, PACK16, FAITHFUL, true, false, true, AXIS>(L);
+    return launch_trace_t<UNIFORM, PACK16, FAITHFUL, false, false, true, AXIS>(L);
+  }
+  if (L.single) return launch_trace_t<UNIFORM, PACK16, FAITHFUL, true, false, false, AXIS>(L);
+  return launch_trace_t<UNIFORM, PACK16, FAITHFUL, false, false, false, AXIS>(L);
+}
+
 template <bool UNIFORM, bool PACK16, bool FAITHFUL>
 static hipError_t launch_trace_u(const LaunchCfg& L) {
-  // Recording is a plotting aid: generic (non-SINGLE, unsplit) instances carry it.
-  if (L.rec.n > 0) return launch_trace_t<UNIFORM, PACK16, FAITHFUL, false, true, false>(L);
-  if (L.T.split > 1) {
-    if (L.single) return launch_trace_t<UNIFORM, PACK16, FAITHFUL, true, false, true>(L);
-    return launch_trace_t<UNIFORM, PACK16, FAITHFUL, false, false, true>(L);
-  }
-  if (L.single) return launch_trace_t<UNIFORM, PACK16, FAITHFUL, true, false, false>(L);
-  return launch_trace_t<UNIFORM, PACK16, FAITHFUL, false, false, false>(L);
+  // Recording is a plotting aid: generic (non-SINGLE, unsplit, general
+  // polygon) instances carry it.
+  if (L.rec.n > 0) return launch_trace_t<UNIFORM, PACK16, FAITHFUL, false, true, false, false>(L);
+  return L.axis ? launch_trace_a<UNIFORM, PACK16, FAITHFUL, true>(L) : launch_trace_a<UNIFORM, PACK16, FAITHFUL, false>(L);
 }
 
 hipError_t launch_trace(const LaunchCfg& L) {

@@ -67,6 +67,21 @@ def test_c1_exact(hip, flags):
     assert_same(gpu_trace(hip, flat, args), oracle.trace_exchange(flat, args, 16))
 
 
+@pytest.mark.parametrize("ndim", [11, 51])
+def test_axis_rect_kernels_match_general_polygon_kernels(hip, ndim, monkeypatch):
+    """Square meshes take the axis-aligned-rectangle kernels (dist_to_rect);
+    RTHX_NO_AXIS=1 forces the general-polygon kernels on the same domain.
+    Both must give identical counts, and both must equal the oracle."""
+    dom = H.square_domain(ndim)
+    flat = dom.flat()
+    args, _k = _args(hip, flat, 200_000 // flat.n_emitters + 1)
+    a = gpu_trace(hip, flat, args)
+    monkeypatch.setenv("RTHX_NO_AXIS", "1")
+    b = gpu_trace(hip, flat, args)
+    assert_same(a, b)
+    assert_same(a, oracle.trace_exchange(flat, args, 16))
+
+
 def test_c1_matches_committed_golden(hip):
     g = np.load(H.os.path.join(H.GOLDEN, "oracle_c1_seed1.npz"))
     dom = H.square_domain(11)
