@@ -9,7 +9,8 @@
 
 namespace rthx {
 
-constexpr int kTraceThreads = 256;               // 4 waves of 64 per emitter row (slice)
+constexpr int kTraceThreads = 256;               // default workgroup: 4 waves of 64 per emitter row (slice)
+constexpr int kMaxTraceThreads = 1024;           // large-N rows (LDS-bound occupancy) use up to 16 waves
 constexpr size_t kMaxLdsBytes = 160 * 1024;      // gfx950 LDS per CU
 constexpr int64_t kStaticLdsBytes = 10240;      // the trace kernel's static LDS (emitter, coarse, tables, ...)
 

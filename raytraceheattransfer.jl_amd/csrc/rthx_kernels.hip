@@ -27,7 +27,7 @@ namespace rthx {
 #ifndef RTHX_TRACE_WAVES_PER_EU
 #define RTHX_TRACE_WAVES_PER_EU 5
 #endif
-#define RTHX_TRACE_WAVES __attribute__((amdgpu_waves_per_eu(RTHX_TRACE_WAVES_PER_EU)))
+#define RTHX_TRACE_WAVES __attribute__((amdgpu_waves_per_eu(SINGLE ? RTHX_TRACE_WAVES_PER_EU : RTHX_TRACE_WAVES_PER_EU - 1)))
 
 // The same LDS address, hidden from the optimiser (one v_mov): loads through
 // it are not hoisted out of the ray loop.
@@ -53,7 +53,7 @@ __device__ __forceinline__ uint32_t lane_id() {
 template <bool PAIRS, class F>
 __device__ __forceinline__ uint32_t compact_row(int64_t n_words, F count2, uint32_t* __restrict__ out_c,
                                                 uint32_t* __restrict__ out_n, uint32_t* wave_sum) {
-  constexpr int kWaves = kTraceThreads / 64;
+  const int kWaves = (int)(blockDim.x >> 6);
   const uint32_t lane = lane_id();
   const int wave = threadIdx.x >> 6;
   const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
@@ -70,7 +70,6 @@ __device__ __forceinline__ uint32_t compact_row(int64_t n_words, F count2, uint3
   if (lane == 0) wave_sum[wave] = cnt;
   __syncthreads();
   uint32_t base = 0, total = 0;
-#pragma unroll
   for (int i = 0; i < kWaves; ++i) {
     const uint32_t ws = wave_sum[i];
     base += i < wave ? ws : 0u;
@@ -92,12 +91,12 @@ __device__ __forceinline__ uint32_t compact_row(int64_t n_words, F count2, uint3
 }
 
 template <bool UNIFORM, bool PACK16, bool FAITHFUL, bool SINGLE, bool REC, bool SPLIT, bool AXIS>
-__global__ __launch_bounds__(kTraceThreads) RTHX_TRACE_WAVES void trace_exchange_kernel(const DevDomain* __restrict__ Dp,
+__global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_exchange_kernel(const DevDomain* __restrict__ Dp,
                                                                      TraceParams P, TallyParams T,
                                                                      RecordParams rec) {
   extern __shared__ uint32_t hist[];
   const DevDomain& D = *Dp;
-  __shared__ uint32_t wave_sum[kTraceThreads / 64];
+  __shared__ uint32_t wave_sum[kMaxTraceThreads / 64];
   __shared__ uint32_t s_tallied;
   // Emitter data is workgroup-uniform: kept in LDS (broadcast ds_reads) rather
   // than in ~26 VGPRs; measured 2.12 ms vs 2.30 (asm memory clobber) and
@@ -117,9 +116,10 @@ __global__ __launch_bounds__(kTraceThreads) RTHX_TRACE_WAVES void trace_exchange
   const int64_t g = P.g_begin + slot * P.g_stride;
   const int64_t n_words = PACK16 ? (T.n_emitters + 1) / 2 : T.n_emitters;
 
-  for (int64_t w = tid; w < n_words; w += kTraceThreads) hist[w] = 0u;
+  const int nthr = (int)blockDim.x;  // 256, 512 or 1024 (launch_trace_t)
+  for (int64_t w = tid; w < n_words; w += nthr) hist[w] = 0u;
   if (!FAITHFUL)
-    for (int i = tid; i < kTableDoubles; i += kTraceThreads) s_tab[i] = D.tables[i];
+    for (int i = tid; i < kTableDoubles; i += nthr) s_tab[i] = D.tables[i];
   if (tid == 0) {
     s_tallied = 0u;
     s_emit = load_emitter(D, g);
@@ -140,7 +140,7 @@ __global__ __launch_bounds__(kTraceThreads) RTHX_TRACE_WAVES void trace_exchange
   // R < 2^32 and N < 2^31 (checked by rthx_trace_exchange): 32-bit ray and
   // absorber indices.
   uint32_t tallied = 0;
-  for (uint32_t r = (uint32_t)r_begin + tid; r < (uint32_t)r_end; r += kTraceThreads) {
+  for (uint32_t r = (uint32_t)r_begin + tid; r < (uint32_t)r_end; r += (uint32_t)nthr) {
     double ox, oy, px, py;
     // Opaque LDS addresses: re-read the loop-invariant coarse record and cos
     // table at their point of use instead of hoisting ~40 values into VGPRs.
@@ -171,7 +171,7 @@ __global__ __launch_bounds__(kTraceThreads) RTHX_TRACE_WAVES void trace_exchange
   if (SPLIT) {
     // add this slice's nonzero counters into the row's dense buffer
     uint32_t* dense = T.dense + slot * T.n_emitters;
-    for (int64_t w = tid; w < n_words; w += kTraceThreads) {
+    for (int64_t w = tid; w < n_words; w += nthr) {
       uint32_t v = hist[w];
       if (v == 0u) continue;
       if (PACK16) {
@@ -313,8 +313,20 @@ static hipError_t launch_trace_t(const LaunchCfg& L) {
     if (e != hipSuccess) return e;
   }
   const int64_t blocks = L.T.n_rows * (SPLIT ? L.T.split : 1);
-  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kTraceThreads), L.lds_bytes, L.stream, L.D, L.P, L.T,
-                     L.rec);
+  // Workgroup size: the one that keeps most waves resident per CU.  With a
+  // large LDS row histogram (large N) only one or two workgroups fit a CU,
+  // and 1024-lane workgroups keep 16 waves busy instead of 4.
+  int threads = kTraceThreads, best_waves = 0;
+  for (int t = kTraceThreads; t <= kMaxTraceThreads; t *= 2) {
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, t, L.lds_bytes) != hipSuccess)
+      break;
+    if (per_cu * (t / 64) > best_waves) {
+      best_waves = per_cu * (t / 64);
+      threads = t;
+    }
+  }
+  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(threads), L.lds_bytes, L.stream, L.D, L.P, L.T, L.rec);
   return hipGetLastError();
 }
 
