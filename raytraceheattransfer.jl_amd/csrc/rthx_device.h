@@ -507,90 +507,104 @@ struct SingleCoarse {
 // SINGLE: the domain has one convex coarse polygon, held in LDS (`sc`), and a
 // crossing can only leave the domain.
 // ---------------------------------------------------------------------------
-template <bool UNIFORM, bool SINGLE, bool FAITHFUL, bool AXIS>
-__device__ __forceinline__ int trace_ray(const DevDomain& D, const TraceParams& P, const SingleCoarse& sc,
-                                         const double* tabs, int c, double& px, double& py, double dx, double dy,
-                                         const RayDraws& rd) {
+constexpr int kRayContinue = -3;  // segment(): the ray crossed into another coarse polygon
+
+// One coarse-polygon segment of traceRayUniform / traceRayVariable (the loop
+// body of traceRay.jl:27-68 / :85-145).  Returns the absorber (>= 0), -1 for a
+// lost ray, or kRayContinue after a crossing (p, c, S / acc updated).
+// UNIFORM: S is the free path left; otherwise S is tau* and acc the optical
+// depth accumulated so far.
+template <bool UNIFORM, bool SINGLE, bool AXIS>
+__device__ __forceinline__ int segment(const DevDomain& D, const TraceParams& P, const SingleCoarse& sc, int& c,
+                                       double& px, double& py, double dx, double dy, double& S, double& acc) {
   const double eta = P.eta;
-  double S = 0.0, target = 0.0, acc = 0.0;
-  if (UNIFORM) {
-    const double u = rd.path();
-    S = P.beta_uniform > 0
-            ? ((RTHX_ABLATE & 2) ? (1.0 - u)
-               : FAITHFUL        ? -log(u) / P.beta_uniform
-                                 : neg_log_tab(u, tabs + kLogTableOffset) * P.inv_beta_uniform)
-            : __builtin_inf();
+  int k, first, count;
+  double u;
+  uint32_t solid;
+  if (SINGLE) {
+    first = 0;
+    count = sc.count;
+    u = dist_to_cell<AXIS>(px, py, dx, dy, sc.poly, k);
+    solid = sc.solid;
   } else {
-    target = FAITHFUL ? -log(rd.path()) : neg_log_tab(rd.path(), tabs + kLogTableOffset);
+    first = D.f_offset[c];
+    count = D.f_offset[c + 1] - first;
+    u = dist_to_cell<AXIS>(px, py, dx, dy, D.c_poly[c], k);
+    solid = D.c_solid[c];
   }
-  const double RTHX_GLOBAL* beta_bin = D.beta + (size_t)P.bin * D.n_fine;
-  for (int it = 0; it < (SINGLE ? 1 : 10000); ++it) {
-    int k, first, count;
-    double u;
-    uint32_t solid;
-    if (SINGLE) {
-      first = 0;
-      count = sc.count;
-      u = dist_to_cell<AXIS>(px, py, dx, dy, sc.poly, k);
-      solid = sc.solid;
-    } else {
-      first = D.f_offset[c];
-      count = D.f_offset[c + 1] - first;
-      u = dist_to_cell<AXIS>(px, py, dx, dy, D.c_poly[c], k);
-      solid = D.c_solid[c];
-    }
-    bool gas;
-    double beta = 0.0, tau_b = 0.0;
-    if (UNIFORM) {
-      gas = S < u;
-    } else {
-      int f0 = SINGLE ? locate_fine(D, sc.grid, first, count, px, py)
-                      : locate_fine(D, D.f_grid[c], first, count, px, py);
-      if (f0 < 0) return -1;
-      beta = beta_bin[first + f0];
-      tau_b = __dmul_rn(beta, u);
-      gas = acc + tau_b >= target;
-    }
-    bool wall = !gas && ((solid >> k) & 1u);
-    if (gas || wall) {
-      double t = gas ? (UNIFORM ? S : (target - acc) / beta) - eta : u - eta;
-      px = px + __dmul_rn(t, dx);
-      py = py + __dmul_rn(t, dy);
-      int f = SINGLE ? locate_fine(D, sc.grid, first, count, px, py)
-                     : locate_fine(D, D.f_grid[c], first, count, px, py);
-      if (f < 0) return -1;
-      int fg = first + f;
-      if (gas) return D.n_surfaces + fg;
-      int w;
-      dist_to_cell<AXIS>(px, py, dx, dy, D.f_poly[fg], w);
-      return D.f_surf[4 * fg + w];  // -1 if the fine wall is not solid
-    }
-    if (SINGLE) return -1;  // an open wall of the only polygon leads outside: locate_coarse finds nothing
-    double t = u + eta;
+  bool gas;
+  double beta = 0.0, tau_b = 0.0;
+  if (UNIFORM) {
+    gas = S < u;
+  } else {
+    int f0 = SINGLE ? locate_fine(D, sc.grid, first, count, px, py) : locate_fine(D, D.f_grid[c], first, count, px, py);
+    if (f0 < 0) return -1;
+    beta = D.beta[(size_t)P.bin * D.n_fine + first + f0];
+    tau_b = __dmul_rn(beta, u);
+    gas = acc + tau_b >= S;
+  }
+  bool wall = !gas && ((solid >> k) & 1u);
+  if (gas || wall) {
+    double t = gas ? (UNIFORM ? S : (S - acc) / beta) - eta : u - eta;
     px = px + __dmul_rn(t, dx);
     py = py + __dmul_rn(t, dy);
-    if (UNIFORM) S -= u; else acc += tau_b;
-    c = locate_coarse(D, px, py);
-    if (c < 0) return -1;
+    int f = SINGLE ? locate_fine(D, sc.grid, first, count, px, py) : locate_fine(D, D.f_grid[c], first, count, px, py);
+    if (f < 0) return -1;
+    int fg = first + f;
+    if (gas) return D.n_surfaces + fg;
+    int w;
+    dist_to_cell<AXIS>(px, py, dx, dy, D.f_poly[fg], w);
+    return D.f_surf[4 * fg + w];  // -1 if the fine wall is not solid
   }
-  return -1;
+  if (SINGLE) return -1;  // an open wall of the only polygon leads outside: locate_coarse finds nothing
+  double t = u + eta;
+  px = px + __dmul_rn(t, dx);
+  py = py + __dmul_rn(t, dy);
+  if (UNIFORM) S -= u; else acc += tau_b;
+  c = locate_coarse(D, px, py);
+  return c < 0 ? -1 : kRayContinue;
 }
 
-// One ray (g, r) of emitter e: emit then trace.  Returns absorber (-1 =
-// lost); (ox, oy) emission point, (px, py) end point.
-template <bool UNIFORM, bool FAITHFUL, bool SINGLE, bool AXIS>
-__device__ __forceinline__ int trace_one(const DevDomain& D, const TraceParams& P, const Emitter& e,
-                                         const SingleCoarse& sc, const double* tabs, uint32_t g, uint32_t r,
-                                         double& ox, double& oy, double& px, double& py) {
+// S = -ln(u)/beta (uniform, traceRay.jl:25) or tau* = -ln(u) (variable, :79).
+template <bool UNIFORM, bool FAITHFUL>
+__device__ __forceinline__ double free_path(const TraceParams& P, const double* tabs, double u) {
+  if (UNIFORM)
+    return P.beta_uniform > 0 ? ((RTHX_ABLATE & 2) ? (1.0 - u)
+                                 : FAITHFUL        ? -log(u) / P.beta_uniform
+                                                   : neg_log_tab(u, tabs + kLogTableOffset) * P.inv_beta_uniform)
+                              : __builtin_inf();
+  return FAITHFUL ? -log(u) : neg_log_tab(u, tabs + kLogTableOffset);
+}
+
+// Emission of ray (g, r): point, direction and free path / tau*.
+template <bool UNIFORM, bool FAITHFUL>
+__device__ __forceinline__ void start_ray(const TraceParams& P, const Emitter& e, const double* tabs, uint32_t g,
+                                          uint32_t r, double& px, double& py, double& dx, double& dy, double& S) {
   const RayDraws rd(r, g, (uint32_t)P.bin, P.key0, P.key1);
-  double dx, dy;
   if (e.surface)
     emit_surface<FAITHFUL>(e, P.eta, rd, px, py, dx, dy);
   else
     emit_volume<FAITHFUL>(e, P.eta, rd, tabs, px, py, dx, dy);
+  S = free_path<UNIFORM, FAITHFUL>(P, tabs, rd.path());
+}
+
+// One ray (g, r) of emitter e traced to the end (SINGLE domains: one
+// segment).  Returns absorber (-1 = lost); (ox, oy) emission point, (px, py)
+// end point.
+template <bool UNIFORM, bool FAITHFUL, bool SINGLE, bool AXIS>
+__device__ __forceinline__ int trace_one(const DevDomain& D, const TraceParams& P, const Emitter& e,
+                                         const SingleCoarse& sc, const double* tabs, uint32_t g, uint32_t r,
+                                         double& ox, double& oy, double& px, double& py) {
+  double dx, dy, S, acc = 0.0;
+  start_ray<UNIFORM, FAITHFUL>(P, e, tabs, g, r, px, py, dx, dy, S);
   ox = px;
   oy = py;
-  return trace_ray<UNIFORM, SINGLE, FAITHFUL, AXIS>(D, P, sc, tabs, e.coarse, px, py, dx, dy, rd);
+  int c = e.coarse;
+  for (int it = 0; it < (SINGLE ? 1 : 10000); ++it) {  // traceRay.jl:27 (10,000 steps, then lost)
+    const int a = segment<UNIFORM, SINGLE, AXIS>(D, P, sc, c, px, py, dx, dy, S, acc);
+    if (a != kRayContinue) return a;
+  }
+  return -1;
 }
 
 }  // namespace rthx

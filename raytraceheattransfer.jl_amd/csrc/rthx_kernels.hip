@@ -98,6 +98,7 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
   const DevDomain& D = *Dp;
   __shared__ uint32_t wave_sum[kMaxTraceThreads / 64];
   __shared__ uint32_t s_tallied;
+  __shared__ uint32_t s_next;  // next ray index of the row (ray regeneration, multi-polygon domains)
   // Emitter data is workgroup-uniform: kept in LDS (broadcast ds_reads) rather
   // than in ~26 VGPRs; measured 2.12 ms vs 2.30 (asm memory clobber) and
   // 2.48 ms (volatile reload) per 1e8 rays.
@@ -122,6 +123,7 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
     for (int i = tid; i < kTableDoubles; i += nthr) s_tab[i] = D.tables[i];
   if (tid == 0) {
     s_tallied = 0u;
+    s_next = (uint32_t)r_begin;
     s_emit = load_emitter(D, g);
     if (SINGLE) {
       s_single.poly = D.c_poly[0];
@@ -140,15 +142,7 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
   // R < 2^32 and N < 2^31 (checked by rthx_trace_exchange): 32-bit ray and
   // absorber indices.
   uint32_t tallied = 0;
-  for (uint32_t r = (uint32_t)r_begin + tid; r < (uint32_t)r_end; r += (uint32_t)nthr) {
-    double ox, oy, px, py;
-    // Opaque LDS addresses: re-read the loop-invariant coarse record and cos
-    // table at their point of use instead of hoisting ~40 values into VGPRs.
-    const SingleCoarse RTHX_LDS* sc = lds_opaque(&s_single);
-    const double RTHX_LDS* tab = lds_opaque(&s_tab[0]);
-    const Emitter RTHX_LDS* em = lds_opaque(&s_emit);
-    int a = trace_one<UNIFORM, FAITHFUL, SINGLE, AXIS>(D, P, *(const Emitter*)em, *(const SingleCoarse*)sc, (const double*)tab,
-                                                 (uint32_t)g, r, ox, oy, px, py);
+  auto tally = [&](int a) {
     if (a >= 0) {
       if (PACK16)
         atomicAdd(&hist[a >> 1], 1u << ((uint32_t)(a & 1) << 4));
@@ -156,11 +150,73 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
         atomicAdd(&hist[a], 1u);
       ++tallied;
     }
+  };
+  auto record = [&](uint32_t r, int a, double ox, double oy, double px, double py) {
     if (REC && rec_slot >= 0) {
       size_t k = (size_t)rec_slot * (size_t)P.R + (size_t)r;
       rec.ok[k] = a >= 0 ? 1 : 0;
       rec.orig[2 * k] = ox; rec.orig[2 * k + 1] = oy;
       rec.end[2 * k] = px; rec.end[2 * k + 1] = py;
+    }
+  };
+  if (SINGLE) {
+    // One segment per ray: every lane traces rays r = tid, tid + nthr, ...
+    for (uint32_t r = (uint32_t)r_begin + tid; r < (uint32_t)r_end; r += (uint32_t)nthr) {
+      double ox, oy, px, py;
+      // Opaque LDS addresses: re-read the loop-invariant coarse record and cos
+      // table at their point of use instead of hoisting ~40 values into VGPRs.
+      const SingleCoarse RTHX_LDS* sc = lds_opaque(&s_single);
+      const double RTHX_LDS* tab = lds_opaque(&s_tab[0]);
+      const Emitter RTHX_LDS* em = lds_opaque(&s_emit);
+      int a = trace_one<UNIFORM, FAITHFUL, SINGLE, AXIS>(D, P, *(const Emitter*)em, *(const SingleCoarse*)sc,
+                                                         (const double*)tab, (uint32_t)g, r, ox, oy, px, py);
+      tally(a);
+      record(r, a, ox, oy, px, py);
+    }
+  } else {
+    // Several domains' rays cross many coarse polygons (the greenhouse's 67
+    // layers), and their segment counts differ widely.  Ray regeneration: a
+    // lane whose ray ended takes the next ray index of the row from an LDS
+    // counter, so waves do not idle until their longest ray ends.  Refills
+    // are batched (a wave emits once at least kRefill of its lanes are idle)
+    // so the emission code runs for many lanes at a time.
+    constexpr int kRefill = 16;
+    double px = 0.0, py = 0.0, dx = 0.0, dy = 0.0, S = 0.0, acc = 0.0, ox = 0.0, oy = 0.0;
+    int c = 0, it = 0;
+    uint32_t r = 0;
+    bool live = false, more = true;
+    while (true) {
+      if (more) {
+        const uint64_t idle = __ballot(!live);
+        if (__popcll(idle) >= kRefill || __ballot(live) == 0ull) {
+          if (!live) {
+            r = atomicAdd(&s_next, 1u);
+            if (r < (uint32_t)r_end) {
+              const double RTHX_LDS* tab = lds_opaque(&s_tab[0]);
+              const Emitter RTHX_LDS* em = lds_opaque(&s_emit);
+              const Emitter& e = *(const Emitter*)em;
+              start_ray<UNIFORM, FAITHFUL>(P, e, (const double*)tab, (uint32_t)g, r, px, py, dx, dy, S);
+              ox = px;
+              oy = py;
+              acc = 0.0;
+              c = e.coarse;
+              it = 0;
+              live = true;
+            }
+          }
+          more = __ballot(!live) == 0ull;  // a lane found the row exhausted: no more refills
+        }
+      }
+      if (__ballot(live) == 0ull) break;
+      if (live) {
+        int a = it < 10000 ? segment<UNIFORM, false, AXIS>(D, P, s_single, c, px, py, dx, dy, S, acc) : -1;
+        ++it;
+        if (a != kRayContinue) {
+          tally(a);
+          record(r, a, ox, oy, px, py);
+          live = false;
+        }
+      }
     }
   }
   // wave reduce the tallied count, one LDS atomic per wave
