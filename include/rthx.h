@@ -186,6 +186,59 @@ int rthx_result_copy_rays(const rthx_result* res, double* origins_xy,
                           double* endpoints_xy, int64_t* emitter, int64_t cap,
                           int64_t* n_out);
 
+/* ------------------------------------------------------------------------
+ * Exchange-factor smoothing: smooth_F of
+ * src/HeatTransfer/exchangeFactorSmoothing/smoothExchangeFactors.jl:412-459,
+ * with DkAP (:299-318: OP + Dykstra rounds, PCG on the dual system :1-33)
+ * and AP (:550-611: alternating projection with the reference's defect
+ * schedule and floor acceptance) on the device.  Dense when F_raw is denser
+ * than 1/4 (:425-427), sparse otherwise; the result has the same kind.
+ * ------------------------------------------------------------------------ */
+typedef struct rthx_smooth_args {
+  int32_t device;
+  int32_t max_iters;             /* AP iteration cap (reference default 1000) */
+  int32_t k_dykstra;             /* Dykstra rounds; -1 = smooth_F's automatic choice (:430-440) */
+  int32_t smooth_surfaces_only;  /* smooth_surfaces_only keyword */
+  int32_t renorm;                /* w ./ minimum(w) (reference default true) */
+  int32_t verbose;               /* print the reference's progress lines */
+  int32_t input_dense;           /* F_raw was a dense Matrix in the caller: the
+                                    reference smooths it densely whatever its
+                                    density (it branches on the type, :425-446) */
+  int32_t reserved0;
+} rthx_smooth_args;
+
+typedef struct rthx_smooth_info {
+  int64_t n;                /* F_smooth is n x n */
+  int64_t nnz;              /* stored entries (n*n when dense) */
+  int32_t dense;            /* 1: dense result (copy_dense), 0: CSR (copy_csr) */
+  int32_t k_dykstra;        /* Dykstra rounds run */
+  int32_t pcg_iters;        /* PCG iterations of the last OP */
+  int32_t ap_iters;         /* AP iterations k */
+  int32_t converged;        /* delta <= 8 eps, or the floor was accepted */
+  int32_t floor_accepted;
+  double chi;               /* cross coupling of F_raw (0 with smooth_surfaces_only) */
+  double delta_init;        /* defect after the first reciprocity projection */
+  double delta_final;       /* defect of the returned iterate */
+  double ms_op;             /* host wall time of the Dykstra / OP rounds */
+  double ms_ap;             /* host wall time of AP */
+  double ms_total;
+} rthx_smooth_info;
+
+typedef struct rthx_smooth_result rthx_smooth_result;
+
+/* F_raw as CSR (row_ptr[n+1], cols, vals; rows need not be sorted), weights
+ * w[n_w] (get_w: wall lengths, then max(1e-6, 4 beta V), smoothExchangeFactors.jl
+ * :320-341) and the number of surface elements. */
+int rthx_smooth_F(const int64_t* row_ptr, const int32_t* cols, const double* vals, int64_t n,
+                  const double* w, int64_t n_w, int32_t num_surfaces,
+                  const rthx_smooth_args* args, rthx_smooth_result** out);
+int rthx_smooth_get_info(const rthx_smooth_result* res, rthx_smooth_info* info);
+/* Dense result: out[n*n], row-major. */
+int rthx_smooth_copy_dense(const rthx_smooth_result* res, double* out);
+/* Sparse result: row_ptr[n+1], cols[nnz], vals[nnz], columns ascending. */
+int rthx_smooth_copy_csr(const rthx_smooth_result* res, int64_t* row_ptr, int32_t* cols, double* vals);
+void rthx_smooth_destroy(rthx_smooth_result* res);
+
 #ifdef __cplusplus
 }
 #endif

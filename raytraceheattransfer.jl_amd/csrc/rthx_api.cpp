@@ -23,77 +23,21 @@
 #include "rthx_grid.h"
 #include "rthx_kernels.h"
 
-#define RTHX_EXPORT extern "C" __attribute__((visibility("default")))
+#include "rthx_common.h"
 
-namespace {
+using rthx::DevBuf;
+using rthx::HostBuf;
+using rthx::fail;
+using rthx::hip_fail;
+using rthx::now_ms;
 
+namespace rthx {
 thread_local std::string g_last_error;
-
 int fail(int code, const std::string& msg) {
   g_last_error = msg;
   return code;
 }
-
-int hip_fail(hipError_t e, const char* what) {
-  return fail(RTHX_EDEVICE, std::string(what) + ": " + hipGetErrorString(e));
-}
-
-#define HIP_TRY(expr, what)                 \
-  do {                                      \
-    hipError_t _e = (expr);                 \
-    if (_e != hipSuccess) return hip_fail(_e, what); \
-  } while (0)
-
-// Device buffer with grow-only capacity.
-struct DevBuf {
-  void* p = nullptr;
-  size_t cap = 0;
-  hipError_t reserve(size_t bytes) {
-    if (bytes <= cap && p) return hipSuccess;
-    if (p) (void)hipFree(p);
-    p = nullptr;
-    cap = 0;
-    size_t want = bytes < 256 ? 256 : bytes;
-    hipError_t e = hipMalloc(&p, want);
-    if (e == hipSuccess) cap = want;
-    return e;
-  }
-  void release() {
-    if (p) (void)hipFree(p);
-    p = nullptr;
-    cap = 0;
-  }
-  template <class T>
-  T* as() const { return static_cast<T*>(p); }
-};
-
-// Pinned host buffer with grow-only capacity (fast D2H of the CSR arrays).
-struct HostBuf {
-  void* p = nullptr;
-  size_t cap = 0;
-  hipError_t reserve(size_t bytes) {
-    if (bytes <= cap && p) return hipSuccess;
-    if (p) (void)hipHostFree(p);
-    p = nullptr;
-    cap = 0;
-    size_t want = bytes < 4096 ? 4096 : bytes;
-    hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
-    if (e == hipSuccess) cap = want;
-    return e;
-  }
-  void release() {
-    if (p) (void)hipHostFree(p);
-    p = nullptr;
-    cap = 0;
-  }
-};
-
-double now_ms() {
-  using namespace std::chrono;
-  return duration<double, std::milli>(steady_clock::now().time_since_epoch()).count();
-}
-
-}  // namespace
+}  // namespace rthx
 
 struct rthx_domain {
   int device = 0;
@@ -237,7 +181,7 @@ extern "C" __attribute__((visibility("default"))) int rthx_debug_neg_log(const d
 
 RTHX_EXPORT int rthx_abi_version(void) { return RTHX_ABI_VERSION; }
 
-RTHX_EXPORT const char* rthx_last_error(void) { return g_last_error.c_str(); }
+RTHX_EXPORT const char* rthx_last_error(void) { return rthx::g_last_error.c_str(); }
 
 RTHX_EXPORT int rthx_device_count(int32_t* count) {
   if (!count) return fail(RTHX_EINVAL, "null count");

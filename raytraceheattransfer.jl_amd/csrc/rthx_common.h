@@ -1,0 +1,87 @@
+// rthx_common.h -- host-side helpers shared by the C-ABI translation units
+// (rthx_api.cpp, rthx_smooth.cpp): exported-symbol macro, thread-local error
+// message, HIP error mapping, grow-only device / pinned host buffers.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <string>
+
+#include "../../include/rthx.h"
+
+#define RTHX_EXPORT extern "C" __attribute__((visibility("default")))
+
+namespace rthx {
+
+extern thread_local std::string g_last_error;
+int fail(int code, const std::string& msg);
+
+inline int hip_fail(hipError_t e, const char* what) {
+  return fail(RTHX_EDEVICE, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define HIP_TRY(expr, what)                              \
+  do {                                                   \
+    hipError_t _e = (expr);                              \
+    if (_e != hipSuccess) return rthx::hip_fail(_e, what); \
+  } while (0)
+
+// Device buffer with grow-only capacity.
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() { release(); }
+  hipError_t reserve(size_t bytes) {
+    if (bytes <= cap && p) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = bytes < 256 ? 256 : bytes;
+    hipError_t e = hipMalloc(&p, want);
+    if (e == hipSuccess) cap = want;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  template <class T>
+  T* as() const { return static_cast<T*>(p); }
+};
+
+// Pinned host buffer with grow-only capacity (fast D2H copies).
+struct HostBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  HostBuf() = default;
+  HostBuf(const HostBuf&) = delete;
+  HostBuf& operator=(const HostBuf&) = delete;
+  ~HostBuf() { release(); }
+  hipError_t reserve(size_t bytes) {
+    if (bytes <= cap && p) return hipSuccess;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = bytes < 4096 ? 4096 : bytes;
+    hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+    if (e == hipSuccess) cap = want;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+inline double now_ms() {
+  using namespace std::chrono;
+  return duration<double, std::milli>(steady_clock::now().time_since_epoch()).count();
+}
+
+}  // namespace rthx

@@ -1,0 +1,37 @@
+// rthx_smooth.h -- launchers of the smoothing kernels (rthx_smooth_kernels.hip),
+// driven by the C ABI in rthx_smooth.cpp.  Dense matrices are n x n
+// row-major; sparse ones CSR with int64 row pointers and int32 columns.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rthx {
+namespace sm {
+
+hipError_t rowsum(const double* A, int64_t n, double* out, hipStream_t s);
+hipError_t dual_setup(const double* w2, int64_t n, double* rowsum, double* dinv, hipStream_t s);
+hipError_t rmul(const double* w2, const double* rowsum, const double* p, int64_t n, double* out, hipStream_t s);
+hipError_t ap_step(double* X, const double* u, const double* w, int64_t n, double* r, double* u_next, hipStream_t s);
+hipError_t hunger(const double* X, const double* w, int64_t n, double* r, double* u, hipStream_t s);
+hipError_t delta_rows(const double* X, const double* u, const double* w2, int64_t n, double* part, hipStream_t s);
+hipError_t recover(double* X, const double* r, int64_t n, hipStream_t s);
+hipError_t renorm(double* F, int64_t n, hipStream_t s);
+hipError_t op_dykstra(const double* Xbar, const double* lam, const double* w2, const double* inv_w, int64_t n,
+                      double* P, bool keep_p, double* Fs, hipStream_t s);
+hipError_t build_x(const double* F, const double* w, int64_t n, double* X, hipStream_t s);
+hipError_t xbar(const double* F, const double* inv_w, const double* w2, int64_t n, double* Xbar, hipStream_t s);
+hipError_t dot(const double* a, const double* b, int64_t n, double* out, hipStream_t s);
+hipError_t pcg_xr(double* x, double* r, const double* p, const double* Ap, double alpha, int64_t n, hipStream_t s);
+hipError_t vmul(const double* a, const double* b, int64_t n, double* out, hipStream_t s);
+hipError_t pcg_p(double* p, const double* z, double beta, int64_t n, hipStream_t s);
+hipError_t make_b(const double* rs, const double* w, bool dyk, int64_t n, double* b, hipStream_t s);
+hipError_t sp_step(const int64_t* rp, const int32_t* ci, double* v, const double* u, const double* w, int64_t n,
+                   bool scale, double* r, double* u_next, hipStream_t s);
+hipError_t sp_delta_rows(const int64_t* rp, const int32_t* ci, const double* v, const double* u, const double* w2,
+                         int64_t n, double* part, hipStream_t s);
+hipError_t scatter(const int64_t* rp, const int32_t* ci, const double* v, int64_t n, double* A, hipStream_t s);
+hipError_t sp_recover(const int64_t* rp, double* v, const double* r, int64_t n, hipStream_t s);
+
+}  // namespace sm
+}  // namespace rthx

@@ -1,0 +1,411 @@
+// rthx_smooth_kernels.hip -- device kernels of the exchange-factor smoothing
+// (smooth_F, src/HeatTransfer/exchangeFactorSmoothing/smoothExchangeFactors.jl).
+//
+// All work is streaming over the N x N (dense) or nnz (sparse) entries of F
+// and X: HBM-bound except the Y-matrix products, whose entries
+// Y_ij = w_i^2 w_j^2 / (w_i^2 + w_j^2) (Y_mat, :253-270) are recomputed on the
+// fly instead of being stored (N^2 doubles saved, one division per entry).
+// Row kernels use one 256-lane workgroup per row and a fixed reduction order,
+// so every result is deterministic run to run.  Dense matrices are row-major
+// with leading dimension n.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rthx_smooth.h"
+
+namespace rthx {
+namespace sm {
+
+constexpr int kRow = 256;   // lanes per row workgroup
+constexpr int kTile = 32;   // transposed tiles: 32 x 32, workgroup 32 x 8
+
+// Sum over the workgroup (kRow lanes), identical in every lane.  Fixed order:
+// wave butterflies, then the 4 wave totals in wave order.
+__device__ __forceinline__ double block_sum(double v, double* sh) {
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  const int wave = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) sh[wave] = v;
+  __syncthreads();
+  double t = 0.0;
+  for (int i = 0; i < kRow / 64; ++i) t += sh[i];
+  __syncthreads();
+  return t;
+}
+
+__device__ __forceinline__ double Y(double a2, double b2) { return (a2 * b2) / (a2 + b2); }  // :262
+
+// ---------------------------------------------------------------------------
+// dense row kernels
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kRow) void k_rowsum(const double* __restrict__ A, int64_t n, double* __restrict__ out) {
+  __shared__ double sh[kRow / 64];
+  const int64_t i = blockIdx.x;
+  const double* a = A + i * n;
+  double s = 0.0;
+  for (int64_t j = threadIdx.x; j < n; j += kRow) s += a[j];
+  s = block_sum(s, sh);
+  if (threadIdx.x == 0) out[i] = s;
+}
+
+// DualSolver (:8-12): rowsum_i = sum_j Y_ij, dinv_i = 1 / (Y_ii + rowsum_i).
+__global__ __launch_bounds__(kRow) void k_dual_setup(const double* __restrict__ w2, int64_t n,
+                                                     double* __restrict__ rowsum, double* __restrict__ dinv) {
+  __shared__ double sh[kRow / 64];
+  const int64_t i = blockIdx.x;
+  const double a2 = w2[i];
+  double s = 0.0;
+  for (int64_t j = threadIdx.x; j < n; j += kRow) s += Y(a2, w2[j]);
+  s = block_sum(s, sh);
+  if (threadIdx.x == 0) {
+    rowsum[i] = s;
+    dinv[i] = 1.0 / (Y(a2, a2) + s);
+  }
+}
+
+// Rmul! (:14): out = Y p + rowsum .* p.
+__global__ __launch_bounds__(kRow) void k_rmul(const double* __restrict__ w2, const double* __restrict__ rowsum,
+                                               const double* __restrict__ p, int64_t n, double* __restrict__ out) {
+  __shared__ double sh[kRow / 64];
+  const int64_t i = blockIdx.x;
+  const double a2 = w2[i];
+  double s = 0.0;
+  for (int64_t j = threadIdx.x; j < n; j += kRow) s += Y(a2, w2[j]) * p[j];
+  s = block_sum(s, sh);
+  if (threadIdx.x == 0) out[i] = s + rowsum[i] * p[i];
+}
+
+// One AP step (:512-520 scale! then :492-496 hunger!): X_ij *= (u_i + u_j)/2
+// with the current u, then r_i = sum_j X_ij and u_next_i = w_i / r_i.
+__global__ __launch_bounds__(kRow) void k_ap_step(double* __restrict__ X, const double* __restrict__ u,
+                                                  const double* __restrict__ w, int64_t n, double* __restrict__ r,
+                                                  double* __restrict__ u_next) {
+  __shared__ double sh[kRow / 64];
+  const int64_t i = blockIdx.x;
+  double* x = X + i * n;
+  const double ui = u[i];
+  double s = 0.0;
+  for (int64_t j = threadIdx.x; j < n; j += kRow) {
+    const double v = x[j] * (0.5 * (ui + u[j]));
+    x[j] = v;
+    s += v;
+  }
+  s = block_sum(s, sh);
+  if (threadIdx.x == 0) {
+    r[i] = s;
+    u_next[i] = w[i] / s;
+  }
+}
+
+// hunger! alone (the first (X_0, u_0)).
+__global__ __launch_bounds__(kRow) void k_hunger(const double* __restrict__ X, const double* __restrict__ w, int64_t n,
+                                                 double* __restrict__ r, double* __restrict__ u) {
+  __shared__ double sh[kRow / 64];
+  const int64_t i = blockIdx.x;
+  const double* x = X + i * n;
+  double s = 0.0;
+  for (int64_t j = threadIdx.x; j < n; j += kRow) s += x[j];
+  s = block_sum(s, sh);
+  if (threadIdx.x == 0) {
+    r[i] = s;
+    u[i] = w[i] / s;
+  }
+}
+
+// delta_R_X_dense (:98-115) per row: sum_{j>i} (X_ij (u_i - u_j))^2 / (w_i^2 + w_j^2).
+__global__ __launch_bounds__(kRow) void k_delta_rows(const double* __restrict__ X, const double* __restrict__ u,
+                                                     const double* __restrict__ w2, int64_t n,
+                                                     double* __restrict__ part) {
+  __shared__ double sh[kRow / 64];
+  const int64_t i = blockIdx.x;
+  const double* x = X + i * n;
+  const double ui = u[i], a2 = w2[i];
+  double s = 0.0;
+  for (int64_t j = i + 1 + threadIdx.x; j < n; j += kRow) {
+    const double d = x[j] * (ui - u[j]);
+    s += d * d / (a2 + w2[j]);
+  }
+  s = block_sum(s, sh);
+  if (threadIdx.x == 0) part[i] = s;
+}
+
+// recover_F (:548): F_ij = X_ij / r_i, in place.
+__global__ __launch_bounds__(kRow) void k_recover(double* __restrict__ X, const double* __restrict__ r, int64_t n) {
+  const int64_t i = blockIdx.x;
+  double* x = X + i * n;
+  const double ri = r[i];
+  for (int64_t j = threadIdx.x; j < n; j += kRow) x[j] = x[j] / ri;
+}
+
+// F ./= sum(F, dims = 2) (:316), in place.
+__global__ __launch_bounds__(kRow) void k_renorm(double* __restrict__ F, int64_t n) {
+  __shared__ double sh[kRow / 64];
+  const int64_t i = blockIdx.x;
+  double* f = F + i * n;
+  double s = 0.0;
+  for (int64_t j = threadIdx.x; j < n; j += kRow) s += f[j];
+  s = block_sum(s, sh);
+  for (int64_t j = threadIdx.x; j < n; j += kRow) f[j] = f[j] / s;
+}
+
+// OP (:292-297) + the Dykstra update (:308-316) in one pass:
+//   G = Diagonal(1 ./ w) (Xbar - Y .* (lambda .+ lambda'))
+//   Fs = max.(G + P, 0);  P = G + P - Fs  (when another round follows)
+// With P == nullptr the round is the first (P = 0).  G may alias Xbar, Fs
+// may alias Xbar.
+__global__ __launch_bounds__(kRow) void k_op_dykstra(const double* Xbar, const double* __restrict__ lam,
+                                                     const double* __restrict__ w2,
+                                                     const double* __restrict__ inv_w, int64_t n, double* P,
+                                                     int keep_p, double* Fs) {
+  const int64_t i = blockIdx.x;
+  const double li = lam[i], a2 = w2[i], iw = inv_w[i];
+  for (int64_t j = threadIdx.x; j < n; j += kRow) {
+    const int64_t k = i * n + j;
+    const double g = iw * (Xbar[k] - Y(a2, w2[j]) * (li + lam[j]));
+    const double gp = P ? g + P[k] : g;
+    const double f = gp > 0.0 ? gp : 0.0;
+    Fs[k] = f;
+    if (keep_p) P[k] = gp - f;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// dense transposed-pair kernels (32 x 32 tiles staged in LDS)
+// ---------------------------------------------------------------------------
+// build_X (:479-489): X_ij = 0.5 (w_i F_ij + w_j F_ji).
+// Xbar_b (:272-290):   Xbar_ij = Y_ij (inv_w_i F_ij + F_ji inv_w_j).
+template <bool XBAR>
+__global__ __launch_bounds__(kTile * 8) void k_pair(const double* __restrict__ F, const double* __restrict__ w,
+                                                    const double* __restrict__ inv_w, const double* __restrict__ w2,
+                                                    int64_t n, double* __restrict__ out) {
+  __shared__ double t[kTile][kTile + 1];  // F_ji block, transposed on read
+  const int64_t bi = (int64_t)blockIdx.y * kTile, bj = (int64_t)blockIdx.x * kTile;
+  const int tx = threadIdx.x, ty = threadIdx.y;
+  for (int y = ty; y < kTile; y += 8) {
+    const int64_t r = bj + y, c = bi + tx;  // F[bj + y][bi + tx]
+    t[y][tx] = (r < n && c < n) ? F[r * n + c] : 0.0;
+  }
+  __syncthreads();
+  for (int y = ty; y < kTile; y += 8) {
+    const int64_t i = bi + y, j = bj + tx;
+    if (i < n && j < n) {
+      const double fij = F[i * n + j], fji = t[tx][y];
+      double v;
+      if (XBAR)
+        v = Y(w2[i], w2[j]) * (inv_w[i] * fij + fji * inv_w[j]);
+      else
+        v = 0.5 * (w[i] * fij + w[j] * fji);
+      out[i * n + j] = v;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// vectors
+// ---------------------------------------------------------------------------
+// out[0] = sum_i a_i b_i (b == nullptr: sum_i a_i), one workgroup, fixed order.
+__global__ __launch_bounds__(1024) void k_dot(const double* __restrict__ a, const double* __restrict__ b, int64_t n,
+                                              double* __restrict__ out) {
+  __shared__ double sh[16];
+  double s = 0.0;
+  for (int64_t i = threadIdx.x; i < n; i += 1024) s += b ? a[i] * b[i] : a[i];
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int i = 0; i < 16; ++i) t += sh[i];
+    out[0] = t;
+  }
+}
+
+// PCG pieces of solve_R (:16-33).
+__global__ void k_pcg_xr(double* __restrict__ x, double* __restrict__ r, const double* __restrict__ p,
+                         const double* __restrict__ Ap, double alpha, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    x[i] += alpha * p[i];
+    r[i] -= alpha * Ap[i];
+  }
+}
+__global__ void k_mul(const double* __restrict__ a, const double* __restrict__ b, int64_t n, double* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = a[i] * b[i];
+}
+__global__ void k_pcg_p(double* __restrict__ p, const double* __restrict__ z, double beta, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = z[i] + beta * p[i];
+}
+// b_i = (rowsum_i - 1) w_i  (delta_perp :DYK, :136) or rowsum_i - w_i (Xbar_b, :288).
+__global__ void k_b(const double* __restrict__ rs, const double* __restrict__ w, int dyk, int64_t n,
+                    double* __restrict__ b) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) b[i] = dyk ? w[i] * (rs[i] - 1.0) : rs[i] - w[i];
+}
+
+// ---------------------------------------------------------------------------
+// sparse (CSR, full symmetric pattern, columns ascending): one wave per row
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double wave_sum(double v) {
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  return v;
+}
+
+__global__ __launch_bounds__(kRow) void k_sp_step(const int64_t* __restrict__ rp, const int32_t* __restrict__ ci,
+                                                  double* __restrict__ v, const double* __restrict__ u,
+                                                  const double* __restrict__ w, int64_t n, int scale,
+                                                  double* __restrict__ r, double* __restrict__ u_next) {
+  const int64_t i = (int64_t)blockIdx.x * (kRow / 64) + (threadIdx.x >> 6);
+  if (i >= n) return;
+  const int lane = threadIdx.x & 63;
+  const double ui = scale ? u[i] : 0.0;
+  double s = 0.0;
+  for (int64_t k = rp[i] + lane; k < rp[i + 1]; k += 64) {
+    double x = v[k];
+    if (scale) {
+      x = x * (0.5 * (ui + u[ci[k]]));
+      v[k] = x;
+    }
+    s += x;
+  }
+  s = wave_sum(s);
+  if (lane == 0) {
+    r[i] = s;
+    u_next[i] = w[i] / s;
+  }
+}
+
+__global__ __launch_bounds__(kRow) void k_sp_delta_rows(const int64_t* __restrict__ rp, const int32_t* __restrict__ ci,
+                                                        const double* __restrict__ v, const double* __restrict__ u,
+                                                        const double* __restrict__ w2, int64_t n,
+                                                        double* __restrict__ part) {
+  const int64_t i = (int64_t)blockIdx.x * (kRow / 64) + (threadIdx.x >> 6);
+  if (i >= n) return;
+  const int lane = threadIdx.x & 63;
+  const double ui = u[i], a2 = w2[i];
+  double s = 0.0;
+  for (int64_t k = rp[i] + lane; k < rp[i + 1]; k += 64) {
+    const int64_t j = ci[k];
+    if (j > i) {
+      const double d = v[k] * (ui - u[j]);
+      s += d * d / (a2 + w2[j]);
+    }
+  }
+  s = wave_sum(s);
+  if (lane == 0) part[i] = s;
+}
+
+__global__ __launch_bounds__(kRow) void k_sp_recover(const int64_t* __restrict__ rp, double* __restrict__ v,
+                                                     const double* __restrict__ r, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * (kRow / 64) + (threadIdx.x >> 6);
+  if (i >= n) return;
+  const int lane = threadIdx.x & 63;
+  const double ri = r[i];
+  for (int64_t k = rp[i] + lane; k < rp[i + 1]; k += 64) v[k] = v[k] / ri;
+}
+
+// Dense matrix from CSR (the matrix must be zeroed first): one wave per row.
+__global__ __launch_bounds__(kRow) void k_scatter(const int64_t* __restrict__ rp, const int32_t* __restrict__ ci,
+                                                  const double* __restrict__ v, int64_t n, double* __restrict__ A) {
+  const int64_t i = (int64_t)blockIdx.x * (kRow / 64) + (threadIdx.x >> 6);
+  if (i >= n) return;
+  for (int64_t k = rp[i] + (threadIdx.x & 63); k < rp[i + 1]; k += 64) {
+    const int32_t c = ci[k];
+    if (c < n) A[i * n + c] = v[k];  // columns beyond a truncated block are dropped
+  }
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------
+static unsigned grid1(int64_t n, int t) { return (unsigned)((n + t - 1) / t); }
+
+hipError_t rowsum(const double* A, int64_t n, double* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_rowsum, dim3((unsigned)n), dim3(kRow), 0, s, A, n, out);
+  return hipGetLastError();
+}
+hipError_t dual_setup(const double* w2, int64_t n, double* rowsum, double* dinv, hipStream_t s) {
+  hipLaunchKernelGGL(k_dual_setup, dim3((unsigned)n), dim3(kRow), 0, s, w2, n, rowsum, dinv);
+  return hipGetLastError();
+}
+hipError_t rmul(const double* w2, const double* rowsum, const double* p, int64_t n, double* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_rmul, dim3((unsigned)n), dim3(kRow), 0, s, w2, rowsum, p, n, out);
+  return hipGetLastError();
+}
+hipError_t ap_step(double* X, const double* u, const double* w, int64_t n, double* r, double* u_next, hipStream_t s) {
+  hipLaunchKernelGGL(k_ap_step, dim3((unsigned)n), dim3(kRow), 0, s, X, u, w, n, r, u_next);
+  return hipGetLastError();
+}
+hipError_t hunger(const double* X, const double* w, int64_t n, double* r, double* u, hipStream_t s) {
+  hipLaunchKernelGGL(k_hunger, dim3((unsigned)n), dim3(kRow), 0, s, X, w, n, r, u);
+  return hipGetLastError();
+}
+hipError_t delta_rows(const double* X, const double* u, const double* w2, int64_t n, double* part, hipStream_t s) {
+  hipLaunchKernelGGL(k_delta_rows, dim3((unsigned)n), dim3(kRow), 0, s, X, u, w2, n, part);
+  return hipGetLastError();
+}
+hipError_t recover(double* X, const double* r, int64_t n, hipStream_t s) {
+  hipLaunchKernelGGL(k_recover, dim3((unsigned)n), dim3(kRow), 0, s, X, r, n);
+  return hipGetLastError();
+}
+hipError_t renorm(double* F, int64_t n, hipStream_t s) {
+  hipLaunchKernelGGL(k_renorm, dim3((unsigned)n), dim3(kRow), 0, s, F, n);
+  return hipGetLastError();
+}
+hipError_t op_dykstra(const double* Xbar, const double* lam, const double* w2, const double* inv_w, int64_t n,
+                      double* P, bool keep_p, double* Fs, hipStream_t s) {
+  hipLaunchKernelGGL(k_op_dykstra, dim3((unsigned)n), dim3(kRow), 0, s, Xbar, lam, w2, inv_w, n, P, keep_p ? 1 : 0,
+                     Fs);
+  return hipGetLastError();
+}
+hipError_t build_x(const double* F, const double* w, int64_t n, double* X, hipStream_t s) {
+  dim3 g(grid1(n, kTile), grid1(n, kTile));
+  hipLaunchKernelGGL(k_pair<false>, g, dim3(kTile, 8), 0, s, F, w, nullptr, nullptr, n, X);
+  return hipGetLastError();
+}
+hipError_t xbar(const double* F, const double* inv_w, const double* w2, int64_t n, double* Xbar, hipStream_t s) {
+  dim3 g(grid1(n, kTile), grid1(n, kTile));
+  hipLaunchKernelGGL(k_pair<true>, g, dim3(kTile, 8), 0, s, F, nullptr, inv_w, w2, n, Xbar);
+  return hipGetLastError();
+}
+hipError_t dot(const double* a, const double* b, int64_t n, double* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_dot, dim3(1), dim3(1024), 0, s, a, b, n, out);
+  return hipGetLastError();
+}
+hipError_t pcg_xr(double* x, double* r, const double* p, const double* Ap, double alpha, int64_t n, hipStream_t s) {
+  hipLaunchKernelGGL(k_pcg_xr, dim3(grid1(n, 256)), dim3(256), 0, s, x, r, p, Ap, alpha, n);
+  return hipGetLastError();
+}
+hipError_t vmul(const double* a, const double* b, int64_t n, double* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_mul, dim3(grid1(n, 256)), dim3(256), 0, s, a, b, n, out);
+  return hipGetLastError();
+}
+hipError_t pcg_p(double* p, const double* z, double beta, int64_t n, hipStream_t s) {
+  hipLaunchKernelGGL(k_pcg_p, dim3(grid1(n, 256)), dim3(256), 0, s, p, z, beta, n);
+  return hipGetLastError();
+}
+hipError_t make_b(const double* rs, const double* w, bool dyk, int64_t n, double* b, hipStream_t s) {
+  hipLaunchKernelGGL(k_b, dim3(grid1(n, 256)), dim3(256), 0, s, rs, w, dyk ? 1 : 0, n, b);
+  return hipGetLastError();
+}
+hipError_t sp_step(const int64_t* rp, const int32_t* ci, double* v, const double* u, const double* w, int64_t n,
+                   bool scale, double* r, double* u_next, hipStream_t s) {
+  hipLaunchKernelGGL(k_sp_step, dim3(grid1(n, kRow / 64)), dim3(kRow), 0, s, rp, ci, v, u, w, n, scale ? 1 : 0, r,
+                     u_next);
+  return hipGetLastError();
+}
+hipError_t sp_delta_rows(const int64_t* rp, const int32_t* ci, const double* v, const double* u, const double* w2,
+                         int64_t n, double* part, hipStream_t s) {
+  hipLaunchKernelGGL(k_sp_delta_rows, dim3(grid1(n, kRow / 64)), dim3(kRow), 0, s, rp, ci, v, u, w2, n, part);
+  return hipGetLastError();
+}
+hipError_t scatter(const int64_t* rp, const int32_t* ci, const double* v, int64_t n, double* A, hipStream_t s) {
+  hipLaunchKernelGGL(k_scatter, dim3(grid1(n, kRow / 64)), dim3(kRow), 0, s, rp, ci, v, n, A);
+  return hipGetLastError();
+}
+hipError_t sp_recover(const int64_t* rp, double* v, const double* r, int64_t n, hipStream_t s) {
+  hipLaunchKernelGGL(k_sp_recover, dim3(grid1(n, kRow / 64)), dim3(kRow), 0, s, rp, v, r, n);
+  return hipGetLastError();
+}
+
+}  // namespace sm
+}  // namespace rthx

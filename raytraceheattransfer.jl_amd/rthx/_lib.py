@@ -61,6 +61,15 @@ def load(path: Optional[str] = None) -> C.CDLL:
                                          C.POINTER(C.c_uint32)]
     lib.rthx_result_copy_rays.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double),
                                           C.POINTER(C.c_int64), C.c_int64, C.POINTER(C.c_int64)]
+    lib.rthx_smooth_F.argtypes = [C.POINTER(C.c_int64), C.POINTER(C.c_int32), C.POINTER(C.c_double), C.c_int64,
+                                  C.POINTER(C.c_double), C.c_int64, C.c_int32, C.POINTER(abi.SmoothArgs),
+                                  C.POINTER(C.c_void_p)]
+    lib.rthx_smooth_get_info.argtypes = [C.c_void_p, C.POINTER(abi.SmoothInfo)]
+    lib.rthx_smooth_copy_dense.argtypes = [C.c_void_p, C.POINTER(C.c_double)]
+    lib.rthx_smooth_copy_csr.argtypes = [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int32),
+                                         C.POINTER(C.c_double)]
+    lib.rthx_smooth_destroy.argtypes = [C.c_void_p]
+    lib.rthx_smooth_destroy.restype = None
     if lib.rthx_abi_version() != abi.RTHX_ABI_VERSION:
         raise RthxError("librthx ABI version mismatch")
     _lib = lib

@@ -101,6 +101,43 @@ class ResultInfo(C.Structure):
         return {name: getattr(self, name) for name, _ in self._fields_}
 
 
+class SmoothArgs(C.Structure):
+    """rthx_smooth_args (include/rthx.h)."""
+    _fields_ = [
+        ("device", C.c_int32),
+        ("max_iters", C.c_int32),
+        ("k_dykstra", C.c_int32),
+        ("smooth_surfaces_only", C.c_int32),
+        ("renorm", C.c_int32),
+        ("verbose", C.c_int32),
+        ("input_dense", C.c_int32),
+        ("reserved0", C.c_int32),
+    ]
+
+
+class SmoothInfo(C.Structure):
+    """rthx_smooth_info (include/rthx.h)."""
+    _fields_ = [
+        ("n", C.c_int64),
+        ("nnz", C.c_int64),
+        ("dense", C.c_int32),
+        ("k_dykstra", C.c_int32),
+        ("pcg_iters", C.c_int32),
+        ("ap_iters", C.c_int32),
+        ("converged", C.c_int32),
+        ("floor_accepted", C.c_int32),
+        ("chi", C.c_double),
+        ("delta_init", C.c_double),
+        ("delta_final", C.c_double),
+        ("ms_op", C.c_double),
+        ("ms_ap", C.c_double),
+        ("ms_total", C.c_double),
+    ]
+
+    def as_dict(self) -> dict:
+        return {name: getattr(self, name) for name, _ in self._fields_}
+
+
 # Every symbol include/rthx.h declares (checked by tests/test_abi_symbols.py).
 EXPORTED_SYMBOLS = (
     "rthx_abi_version",
@@ -115,6 +152,11 @@ EXPORTED_SYMBOLS = (
     "rthx_result_get_info",
     "rthx_result_copy_csr",
     "rthx_result_copy_rays",
+    "rthx_smooth_F",
+    "rthx_smooth_get_info",
+    "rthx_smooth_copy_dense",
+    "rthx_smooth_copy_csr",
+    "rthx_smooth_destroy",
 )
 
 

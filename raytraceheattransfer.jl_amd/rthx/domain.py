@@ -361,20 +361,24 @@ class RayTracingDomain2D:
 
     def __call__(self, rays_tot: int, method: str = "exchange", nudge: Optional[float] = None,
                  k_dykstra=None, max_iters: int = 1000, verbose: Optional[bool] = None,
-                 rec=None, seed: int = 1, device: int = 0, faithful: bool = False):
-        """multiDispatchRayTrace2D.jl:1-18 (``method=:exchange`` only).
-
-        ``k_dykstra`` / ``max_iters`` belong to the host smoothing stage
-        (smooth_F), which this package does not provide; F_smooth stays None.
+                 rec=None, seed: int = 1, device: int = 0, faithful: bool = False, smooth: bool = True):
+        """multiDispatchRayTrace2D.jl:1-18 (``method=:exchange`` only): trace
+        (F_raw) then smooth (F_smooth, exchangeRayTracing.jl:13-74) on the
+        device.  ``smooth=False`` stops after tracing (F_smooth stays None).
         """
         from .exchange import exchange_ray_tracing
+        from .smoothing import smooth_exchange_factors
 
         if verbose is None:
             verbose = self.verbose
         trace_nudge = 10_000 * np.finfo(np.float64).eps if nudge is None else float(nudge)
         if method == "exchange":
-            return exchange_ray_tracing(self, int(rays_tot), trace_nudge, verbose, rec,
-                                        seed=seed, device=device, faithful=faithful)
+            F_raw = exchange_ray_tracing(self, int(rays_tot), trace_nudge, verbose, rec,
+                                         seed=seed, device=device, faithful=faithful)
+            if smooth:
+                self.F_smooth = smooth_exchange_factors(self, F_raw, max_iters=max_iters, k_dykstra=k_dykstra,
+                                                        verbose=verbose, device=device)
+            return F_raw
         if method == "direct":
             raise NotImplementedError("method=:direct is out of scope (SURVEY.md §8(f) f3)")
         raise ValueError(f"Unknown ray tracing method: {method}, must be :exchange or :direct")

@@ -1,0 +1,103 @@
+"""Exchange-factor smoothing on the MI355X.
+
+Host mirror of src/HeatTransfer/exchangeFactorSmoothing/smoothExchangeFactors.jl
+(smooth_F :412-459, get_w :320-341) and of the smoothing half of
+exchangeRayTracing! (ExchangeFactors2D/exchangeRayTracing.jl:13-71).  Every
+matrix pass runs in librthx (rthx_smooth_F, csrc/rthx_smooth*.{cpp,hip}); as
+with tracing there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional
+
+import numpy as np
+import scipy.sparse as sp
+
+from . import abi
+from ._lib import check, load
+
+
+def get_w(dom, spectral_bin: int = 1) -> np.ndarray:
+    """get_w, smoothExchangeFactors.jl:320-341: wall lengths for surfaces, then
+    max(1e-6, 4 beta V) for volumes (1-based ``spectral_bin``)."""
+    ns = len(dom.surface_mapping)
+    w = np.zeros(ns + len(dom.volume_mapping))
+    for (c, f, wall), s in dom.surface_mapping.items():
+        w[s - 1] = dom.fine_mesh[c - 1][f - 1].area[wall - 1]
+    for (c, f), v in dom.volume_mapping.items():
+        face = dom.fine_mesh[c - 1][f - 1]
+        w[ns + v - 1] = max(1e-6, 4.0 * face.beta(spectral_bin - 1) * face.volume)
+    return w
+
+
+def smooth_F(F_raw, w, num_surfaces: int, max_iters: int = 1000, smooth_surfaces_only: bool = False,
+             k_dykstra: Optional[int] = None, verbose: bool = True, renorm: bool = True, device: int = 0,
+             info: Optional[dict] = None):
+    """smooth_F (smoothExchangeFactors.jl:412-459) on the device.
+
+    Returns a dense ``ndarray`` when the reference would smooth densely
+    (F_raw denser than 1/4, or Dykstra rounds) and a CSR matrix otherwise.
+    ``info`` (optional dict) receives the run's rthx_smooth_info."""
+    lib = load()
+    F = sp.csr_matrix(F_raw) if not sp.issparse(F_raw) else F_raw.tocsr()
+    F.sum_duplicates()
+    n = F.shape[0]
+    rp = np.ascontiguousarray(F.indptr, dtype=np.int64)
+    ci = np.ascontiguousarray(F.indices, dtype=np.int32)
+    vv = np.ascontiguousarray(F.data, dtype=np.float64)
+    ww = np.ascontiguousarray(w, dtype=np.float64)
+    a = abi.SmoothArgs()
+    a.device = device
+    a.max_iters = max_iters
+    a.k_dykstra = -1 if k_dykstra is None else int(k_dykstra)
+    a.smooth_surfaces_only = 1 if smooth_surfaces_only else 0
+    a.renorm = 1 if renorm else 0
+    a.verbose = 1 if verbose else 0
+    a.input_dense = 0 if sp.issparse(F_raw) else 1
+    h = C.c_void_p()
+    check(lib.rthx_smooth_F(abi.ptr(rp, C.c_int64), abi.ptr(ci, C.c_int32), abi.ptr(vv, C.c_double), n,
+                            abi.ptr(ww, C.c_double), len(ww), int(num_surfaces), C.byref(a), C.byref(h)))
+    try:
+        inf = abi.SmoothInfo()
+        check(lib.rthx_smooth_get_info(h, C.byref(inf)))
+        m = inf.n
+        if inf.dense:
+            out = np.empty((m, m))
+            check(lib.rthx_smooth_copy_dense(h, abi.ptr(out, C.c_double)))
+        else:
+            orp = np.empty(m + 1, dtype=np.int64)
+            oci = np.empty(max(inf.nnz, 1), dtype=np.int32)
+            ov = np.empty(max(inf.nnz, 1))
+            check(lib.rthx_smooth_copy_csr(h, abi.ptr(orp, C.c_int64), abi.ptr(oci, C.c_int32),
+                                           abi.ptr(ov, C.c_double)))
+            out = sp.csr_matrix((ov[:inf.nnz], oci[:inf.nnz], orp), shape=(m, m))
+        if info is not None:
+            info.update(inf.as_dict())
+    finally:
+        lib.rthx_smooth_destroy(h)
+    return out
+
+
+def smooth_exchange_factors(dom, F_raw, max_iters: int = 1000, k_dykstra: Optional[int] = None,
+                            verbose: bool = True, device: int = 0):
+    """The smoothing half of exchangeRayTracing! (exchangeRayTracing.jl:13-71):
+    per-bin smoothing with per-bin weights in spectral_variable mode (grouped
+    uniform bins share one smoothed matrix), one smoothing otherwise."""
+    from .exchange import group_uniform_bins
+
+    ns = len(dom.surface_mapping)
+    kw = dict(max_iters=max_iters, k_dykstra=k_dykstra, verbose=verbose,
+              smooth_surfaces_only=dom.surfaces_only, device=device)
+    if dom.spectral_mode == "spectral_variable":
+        out = [None] * dom.n_spectral_bins
+        groups, _reps, nonuniform = group_uniform_bins(dom.uniform_across_bin)
+        for b in nonuniform:
+            out[b - 1] = smooth_F(F_raw[b - 1], get_w(dom, b), ns, **kw)
+        for idx_group in groups:
+            rep = idx_group[0]
+            Fs = smooth_F(F_raw[rep - 1], get_w(dom, rep), ns, **kw)
+            for j in idx_group:
+                out[j - 1] = Fs
+        return out
+    return smooth_F(F_raw, get_w(dom), ns, **kw)

@@ -16,7 +16,7 @@ HEADER = os.path.join(H.ROOT, "include", "rthx.h")
 
 def declared_functions():
     txt = open(HEADER).read()
-    return sorted(set(re.findall(r"\b(rthx_[a-z_]+)\s*\(", txt)))
+    return sorted(set(re.findall(r"\b(rthx_[A-Za-z_]+)\s*\(", txt)))
 
 
 @pytest.fixture(scope="module")
@@ -34,7 +34,7 @@ def test_header_and_python_mirror_agree():
 
 def test_every_declared_symbol_is_exported(lib):
     out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True, check=True).stdout
-    exported = set(re.findall(r"\b(rthx_[a-z_]+)\b", out))
+    exported = set(re.findall(r"\b(rthx_[A-Za-z_]+)\b", out))
     missing = [s for s in declared_functions() if s not in exported]
     assert not missing, missing
     for s in declared_functions():
@@ -46,6 +46,8 @@ def test_struct_sizes_match_header():
     assert C.sizeof(abi.GridDesc) == 48
     assert C.sizeof(abi.TraceArgs) == 80
     assert C.sizeof(abi.ResultInfo) == 88
+    assert C.sizeof(abi.SmoothArgs) == 32
+    assert C.sizeof(abi.SmoothInfo) == 88
 
 
 def test_validation_without_gpu(lib):
