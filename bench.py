@@ -159,7 +159,10 @@ def main():
     N = flat.n_emitters
     total_rays = args.rays_per_gpu * world
     R = total_rays // N
-    device = local_rank
+    # one process per GPU: rank r drives device LOCAL_RANK (more ranks than
+    # devices, e.g. a 2-rank rehearsal on a 1-GPU box, share devices round robin)
+    ndev = _lib.device_count()
+    device = local_rank % max(ndev, 1)
     dd = _lib.DeviceDomain(flat, device)
     targs, _keep = _lib.make_args(0, R, nudge, args.seed, rank, N, world, device=device,
                                   flags=abi.RTHX_FLAG_DEVICE_ONLY)
@@ -224,7 +227,9 @@ def main():
         # B_alg = 8 B/ray + 12 B x nnz/(N R)
         b_alg = 8.0 * rays_rank + 12.0 * nnz_rank
         achieved = b_alg / (avg_trace_ms * 1e-3) / 1e9
-        traffic = read_pmc_traffic()
+        # the committed PMC traffic was measured on the 1-GPU launch; other
+        # shard shapes (row-split launches) are not covered by it
+        traffic = read_pmc_traffic() if world == 1 else None
         fpr = read_fp64_flops_per_ray()
         fp64_roof = None
         if fpr is not None:
