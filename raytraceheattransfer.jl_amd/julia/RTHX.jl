@@ -97,6 +97,34 @@ struct ResultInfo
     total_ms::Float64
 end
 
+struct SmoothArgs
+    device::Int32
+    max_iters::Int32
+    k_dykstra::Int32
+    smooth_surfaces_only::Int32
+    renorm::Int32
+    verbose::Int32
+    input_dense::Int32
+    reserved0::Int32
+end
+
+struct SmoothInfo
+    n::Int64
+    nnz::Int64
+    dense::Int32
+    k_dykstra::Int32
+    pcg_iters::Int32
+    ap_iters::Int32
+    converged::Int32
+    floor_accepted::Int32
+    chi::Float64
+    delta_init::Float64
+    delta_final::Float64
+    ms_op::Float64
+    ms_ap::Float64
+    ms_total::Float64
+end
+
 function check(rc::Integer)
     if rc != 0
         msg = unsafe_string(ccall((:rthx_last_error, LIB[]), Cstring, ()))
@@ -249,11 +277,58 @@ function computeExchangeFactorsBin(rtm, rays_per_emitter::Integer, nudge, spectr
 end
 
 """
+    smooth_F(F_raw, w, num_surfaces; max_iters=1000, smooth_surfaces_only=false,
+             k_dykstra=nothing, verbose=true, renorm=true)
+
+Device smoothing with the signature and result kind of the reference's
+smooth_F (smoothExchangeFactors.jl:412-459): a dense Matrix when it smooths
+densely, a SparseMatrixCSC otherwise.
+"""
+function smooth_F(F_raw::AbstractMatrix, w::AbstractVector, num_surfaces::Integer; max_iters::Integer = 1000,
+                  smooth_surfaces_only::Bool = false, k_dykstra = nothing, verbose::Bool = true,
+                  renorm::Bool = true)
+    input_dense = !(F_raw isa SparseMatrixCSC)
+    Fr = SparseMatrixCSC(transpose(sparse(F_raw)))      # CSC of F' = CSR of F
+    n = size(F_raw, 1)
+    rowptr = Int64.(Fr.colptr) .- 1
+    cols = Int32.(Fr.rowval) .- Int32(1)
+    vals = Vector{Float64}(Fr.nzval)
+    ww = Vector{Float64}(w)
+    args = Ref(SmoothArgs(DEVICE[], Int32(max_iters), Int32(k_dykstra === nothing ? -1 : k_dykstra),
+                          Int32(smooth_surfaces_only), Int32(renorm), Int32(verbose), Int32(input_dense), Int32(0)))
+    h = Ref{Ptr{Cvoid}}(C_NULL)
+    check(ccall((:rthx_smooth_F, LIB[]), Cint,
+                (Ptr{Int64}, Ptr{Int32}, Ptr{Float64}, Int64, Ptr{Float64}, Int64, Int32, Ptr{SmoothArgs},
+                 Ptr{Ptr{Cvoid}}),
+                rowptr, cols, vals, n, ww, length(ww), Int32(num_surfaces), args, h))
+    try
+        info = Ref{SmoothInfo}()
+        check(ccall((:rthx_smooth_get_info, LIB[]), Cint, (Ptr{Cvoid}, Ptr{SmoothInfo}), h[], info))
+        m = info[].n
+        if info[].dense == 1
+            out = Matrix{Float64}(undef, m, m)   # row-major from the library = transpose in Julia
+            check(ccall((:rthx_smooth_copy_dense, LIB[]), Cint, (Ptr{Cvoid}, Ptr{Float64}), h[], out))
+            return permutedims(out)
+        else
+            nnz = info[].nnz
+            rp = Vector{Int64}(undef, m + 1); ci = Vector{Int32}(undef, max(nnz, 1)); v = Vector{Float64}(undef, max(nnz, 1))
+            check(ccall((:rthx_smooth_copy_csr, LIB[]), Cint, (Ptr{Cvoid}, Ptr{Int64}, Ptr{Int32}, Ptr{Float64}),
+                        h[], rp, ci, v))
+            Ft = SparseMatrixCSC(m, m, rp .+ 1, Int64.(ci[1:nnz]) .+ 1, v[1:nnz])
+            return SparseMatrixCSC(transpose(Ft))
+        end
+    finally
+        ccall((:rthx_smooth_destroy, LIB[]), Cvoid, (Ptr{Cvoid},), h[])
+    end
+end
+
+"""
     enable!(; lib, device=0, seed=1, faithful=false)
 
 Redirect RayTraceHeatTransfer's `computeExchangeFactorsBin` to the GPU.
 """
-function enable!(; lib::AbstractString, device::Integer = 0, seed::Integer = 1, faithful::Bool = false)
+function enable!(; lib::AbstractString, device::Integer = 0, seed::Integer = 1, faithful::Bool = false,
+                 smoothing::Bool = false)
     LIB[] = lib
     DEVICE[] = Int32(device)
     SEED[] = UInt64(seed)
@@ -268,6 +343,11 @@ function enable!(; lib::AbstractString, device::Integer = 0, seed::Integer = 1, 
         return $(RTHX).computeExchangeFactorsBin(rtm, rays_per_emitter, nudge, spectral_bin, surface_mapping,
                                                  volume_mapping, num_surfaces, num_volumes, num_emitters,
                                                  verbose, rec)
+    end
+    if smoothing  # optional: smooth_F on the device as well
+        @eval RTHT function smooth_F(F_raw::AbstractMatrix, w::AbstractVector, num_surfaces::Int; kw...)
+            return $(RTHX).smooth_F(F_raw, w, num_surfaces; kw...)
+        end
     end
     return nothing
 end
