@@ -72,15 +72,30 @@ def cpu_baseline(dom, R, nudge, seed, budget_s=12.0, threads=16):
     _rp, _c, _n, info, _ = oracle.trace_exchange(flat, args, threads)
     dt = time.perf_counter() - t
     rays = info["rays_traced"]
+    # single thread (T = nproc and T = 1), ~budget/3 s
+    stride1 = 256
+    args1, _k1 = _lib.make_args(0, R, nudge, seed, 0, N, stride1)
+    t = time.perf_counter()
+    oracle.trace_exchange(flat, args1, 1)
+    dt1 = time.perf_counter() - t
+    rows1 = len(range(0, N, stride1))
+    stride1 = max(1, N // max(rows1, int(rows1 / max(dt1, 1e-6) * budget_s / 3)))
+    args1, _k1 = _lib.make_args(0, R, nudge, seed, 0, N, stride1)
+    t = time.perf_counter()
+    _rp, _c, _n, info1, _ = oracle.trace_exchange(flat, args1, 1)
+    dt1 = time.perf_counter() - t
     return {
         "value": rays / dt / 1e6,
         "unit": "Mrays/s",
         "cores": threads,
         "kind": "port",
+        "value_1_thread": info1["rays_traced"] / dt1 / 1e6,
+        "host_logical_cpus": os.cpu_count(),
         "sample": (f"CPU restatement of the reference algorithm (oracle/rthx_oracle.c: pthreads, static emitter "
                    f"partition, per-thread hash tallies, COO->CSR) on every {stride}-th emitter row of the same "
                    f"101x101 workload: {info['rows_traced']} rows x R={R} = {rays} rays in {dt:.2f} s, "
-                   f"{threads} threads"),
+                   f"{threads} threads (the GPU box's CPU share; os.cpu_count() reports the whole host's logical "
+                   f"CPUs); single thread: every {stride1}-th row, {info1['rays_traced']} rays in {dt1:.2f} s"),
     }
 
 
