@@ -239,6 +239,46 @@ int rthx_smooth_copy_dense(const rthx_smooth_result* res, double* out);
 int rthx_smooth_copy_csr(const rthx_smooth_result* res, int64_t* row_ptr, int32_t* cols, double* vals);
 void rthx_smooth_destroy(rthx_smooth_result* res);
 
+/* ------------------------------------------------------------------------
+ * Grey GERT solve: the linear system of equilibriumGrey2D!
+ * (src/HeatTransfer/equilibrium/equilibriumGrey2D.jl:136-166),
+ *     (I - Diagonal(coeff) F') j = h,   then  g = F' j   (:176-201),
+ * solved on the device by restarted GMRES (the reference's sparse branch:
+ * GMRES(memory = 50), rtol = 1e-12, Krylov.jl's atol = sqrt(eps), :158-160;
+ * its dense branch uses an LU solve, which GMRES matches within the stated
+ * tolerance).  F may be given as host CSR, as a dense host matrix, or as a
+ * device-resident dense smoothing result.
+ * ------------------------------------------------------------------------ */
+typedef struct rthx_solve_args {
+  int32_t device;
+  int32_t memory;     /* Krylov subspace per cycle (reference: 50) */
+  int32_t itmax;      /* iteration cap; 0 = 2n (Krylov.jl default) */
+  int32_t reserved0;
+  double rtol;        /* reference: 1e-12 */
+  double atol;        /* Krylov.jl default sqrt(eps(Float64)) */
+} rthx_solve_args;
+
+typedef struct rthx_solve_info {
+  int64_t n;
+  int32_t iterations;  /* Arnoldi steps */
+  int32_t cycles;      /* restart cycles */
+  int32_t converged;
+  int32_t reserved0;
+  double residual;     /* true residual ||h - M j|| at exit */
+  double tolerance;    /* atol + rtol ||h|| */
+  double ms_total;
+} rthx_solve_info;
+
+/* F as host CSR (row_ptr[n+1], cols, vals) when `dense` is NULL, else a dense
+ * row-major host matrix dense[n*n].  coeff[n], h[n]; j_out[n], g_out[n]. */
+int rthx_solve_grey(const int64_t* row_ptr, const int32_t* cols, const double* vals, const double* dense,
+                    int64_t n, const double* coeff, const double* h, const rthx_solve_args* args,
+                    double* j_out, double* g_out, rthx_solve_info* info);
+/* F = a dense rthx_smooth_F result, already on the device. */
+int rthx_solve_grey_smoothed(const rthx_smooth_result* F, const double* coeff, const double* h,
+                             const rthx_solve_args* args, double* j_out, double* g_out,
+                             rthx_solve_info* info);
+
 #ifdef __cplusplus
 }
 #endif

@@ -22,24 +22,6 @@ using rthx::DevBuf;
 using rthx::fail;
 using rthx::now_ms;
 
-struct rthx_smooth_result {
-  int device = -1;
-  hipStream_t stream = nullptr;
-  bool dense = true;
-  int64_t n = 0;
-  DevBuf F;           // dense result (n*n) or sparse values
-  DevBuf rp, ci;      // sparse pattern
-  int64_t nnz = 0;
-  rthx_smooth_info info{};
-  ~rthx_smooth_result() {
-    if (device >= 0) (void)hipSetDevice(device);
-    F.release();
-    rp.release();
-    ci.release();
-    if (stream) (void)hipStreamDestroy(stream);
-  }
-};
-
 namespace {
 
 constexpr double kEps = std::numeric_limits<double>::epsilon();

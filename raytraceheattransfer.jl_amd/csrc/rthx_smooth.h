@@ -6,6 +6,28 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "rthx_common.h"
+
+// The smoothing result handle (opaque in include/rthx.h).  The solver
+// (rthx_solve.cpp) reads a dense result in place.
+struct rthx_smooth_result {
+  int device = -1;
+  hipStream_t stream = nullptr;
+  bool dense = true;
+  int64_t n = 0;
+  rthx::DevBuf F;           // dense result (n*n, row-major) or sparse values
+  rthx::DevBuf rp, ci;      // sparse pattern
+  int64_t nnz = 0;
+  rthx_smooth_info info{};
+  ~rthx_smooth_result() {
+    if (device >= 0) (void)hipSetDevice(device);
+    F.release();
+    rp.release();
+    ci.release();
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+};
+
 namespace rthx {
 namespace sm {
 

@@ -70,6 +70,11 @@ def load(path: Optional[str] = None) -> C.CDLL:
                                          C.POINTER(C.c_double)]
     lib.rthx_smooth_destroy.argtypes = [C.c_void_p]
     lib.rthx_smooth_destroy.restype = None
+    dp = C.POINTER(C.c_double)
+    lib.rthx_solve_grey.argtypes = [C.POINTER(C.c_int64), C.POINTER(C.c_int32), dp, dp, C.c_int64, dp, dp,
+                                    C.POINTER(abi.SolveArgs), dp, dp, C.POINTER(abi.SolveInfo)]
+    lib.rthx_solve_grey_smoothed.argtypes = [C.c_void_p, dp, dp, C.POINTER(abi.SolveArgs), dp, dp,
+                                             C.POINTER(abi.SolveInfo)]
     if lib.rthx_abi_version() != abi.RTHX_ABI_VERSION:
         raise RthxError("librthx ABI version mismatch")
     _lib = lib

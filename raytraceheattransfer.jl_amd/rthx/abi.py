@@ -138,6 +138,35 @@ class SmoothInfo(C.Structure):
         return {name: getattr(self, name) for name, _ in self._fields_}
 
 
+class SolveArgs(C.Structure):
+    """rthx_solve_args (include/rthx.h)."""
+    _fields_ = [
+        ("device", C.c_int32),
+        ("memory", C.c_int32),
+        ("itmax", C.c_int32),
+        ("reserved0", C.c_int32),
+        ("rtol", C.c_double),
+        ("atol", C.c_double),
+    ]
+
+
+class SolveInfo(C.Structure):
+    """rthx_solve_info (include/rthx.h)."""
+    _fields_ = [
+        ("n", C.c_int64),
+        ("iterations", C.c_int32),
+        ("cycles", C.c_int32),
+        ("converged", C.c_int32),
+        ("reserved0", C.c_int32),
+        ("residual", C.c_double),
+        ("tolerance", C.c_double),
+        ("ms_total", C.c_double),
+    ]
+
+    def as_dict(self) -> dict:
+        return {name: getattr(self, name) for name, _ in self._fields_}
+
+
 # Every symbol include/rthx.h declares (checked by tests/test_abi_symbols.py).
 EXPORTED_SYMBOLS = (
     "rthx_abi_version",
@@ -157,6 +186,8 @@ EXPORTED_SYMBOLS = (
     "rthx_smooth_copy_dense",
     "rthx_smooth_copy_csr",
     "rthx_smooth_destroy",
+    "rthx_solve_grey",
+    "rthx_solve_grey_smoothed",
 )
 
 

@@ -31,14 +31,34 @@ def get_w(dom, spectral_bin: int = 1) -> np.ndarray:
     return w
 
 
+class SmoothHandle:
+    """A device-resident rthx_smooth_result (kept for rthx_solve_grey_smoothed)."""
+
+    def __init__(self, lib, h, device: int, dense: bool):
+        self._lib, self.handle, self.device, self.dense = lib, h, device, dense
+
+    def close(self) -> None:
+        if getattr(self, "handle", None):
+            self._lib.rthx_smooth_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def smooth_F(F_raw, w, num_surfaces: int, max_iters: int = 1000, smooth_surfaces_only: bool = False,
              k_dykstra: Optional[int] = None, verbose: bool = True, renorm: bool = True, device: int = 0,
-             info: Optional[dict] = None):
+             info: Optional[dict] = None, keep_device: bool = False):
     """smooth_F (smoothExchangeFactors.jl:412-459) on the device.
 
     Returns a dense ``ndarray`` when the reference would smooth densely
     (F_raw denser than 1/4, or Dykstra rounds) and a CSR matrix otherwise.
-    ``info`` (optional dict) receives the run's rthx_smooth_info."""
+    ``info`` (optional dict) receives the run's rthx_smooth_info.  With
+    ``keep_device`` the result stays on the device too: returns
+    (F_smooth, SmoothHandle)."""
     lib = load()
     F = sp.csr_matrix(F_raw) if not sp.issparse(F_raw) else F_raw.tocsr()
     F.sum_duplicates()
@@ -74,8 +94,12 @@ def smooth_F(F_raw, w, num_surfaces: int, max_iters: int = 1000, smooth_surfaces
             out = sp.csr_matrix((ov[:inf.nnz], oci[:inf.nnz], orp), shape=(m, m))
         if info is not None:
             info.update(inf.as_dict())
-    finally:
+    except Exception:
         lib.rthx_smooth_destroy(h)
+        raise
+    if keep_device:
+        return out, SmoothHandle(lib, h, device, bool(inf.dense))
+    lib.rthx_smooth_destroy(h)
     return out
 
 
@@ -100,4 +124,9 @@ def smooth_exchange_factors(dom, F_raw, max_iters: int = 1000, k_dykstra: Option
             for j in idx_group:
                 out[j - 1] = Fs
         return out
-    return smooth_F(F_raw, get_w(dom), ns, **kw)
+    F_s, handle = smooth_F(F_raw, get_w(dom), ns, keep_device=True, **kw)
+    old = getattr(dom, "_F_smooth_device", None)
+    if old is not None:
+        old[1].close()
+    dom._F_smooth_device = (F_s, handle)  # rthx.equilibrium solves on it in place
+    return F_s

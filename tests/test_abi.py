@@ -48,6 +48,8 @@ def test_struct_sizes_match_header():
     assert C.sizeof(abi.ResultInfo) == 88
     assert C.sizeof(abi.SmoothArgs) == 32
     assert C.sizeof(abi.SmoothInfo) == 88
+    assert C.sizeof(abi.SolveArgs) == 32
+    assert C.sizeof(abi.SolveInfo) == 48
 
 
 def test_validation_without_gpu(lib):

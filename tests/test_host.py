@@ -124,3 +124,17 @@ def test_shard_rows_and_merge_csr():
     assert np.array_equal(rp, full.indptr) and np.array_equal(c, full.indices) and np.array_equal(v, full.data)
     with pytest.raises(ValueError):
         merge_csr([pieces[0], pieces[0]], n)
+
+
+def test_populate_workspace_matches_reference_order():
+    """rthx.equilibrium.populate_workspace (WorkspaceStructs.jl:68-118) gives the
+    per-element arrays in global order, as the test restatement does."""
+    from rthx.equilibrium import populate_workspace
+
+    dom = H.square_domain(5, kappa=0.5, sigma_s=0.25, epsilon=0.7)
+    ws = populate_workspace(dom)
+    a = H.element_arrays(dom)
+    assert np.allclose(ws["Area"], a["area"]) and np.allclose(ws["epsw"], a["eps"])
+    assert np.allclose(ws["Tw"], a["Tw"]) and np.allclose(ws["Volume"], a["vol"])
+    assert np.allclose(ws["kappa_g"], a["kappa"]) and np.allclose(ws["omega_g"], a["omega"])
+    assert np.array_equal(ws["Qg_known"], (a["Tg"] < 0).astype(int))

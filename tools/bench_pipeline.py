@@ -1,0 +1,43 @@
+"""The whole device pipeline on a BASELINE config (diagnostic): mesh(N;
+method=:exchange) = trace + F_raw to the host + smooth_F, then
+solveEquilibrium! (grey GERT solve) on the device-resident F_smooth.
+
+  python tools/bench_pipeline.py [--ndim 101] [--rays 1e8]
+"""
+import argparse
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "raytraceheattransfer.jl_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+import helpers as H  # noqa: E402
+from rthx.equilibrium import solve_equilibrium  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ndim", type=int, default=101)
+    ap.add_argument("--rays", type=float, default=1e8)
+    ap.add_argument("--repeat", type=int, default=2)
+    a = ap.parse_args()
+    for r in range(a.repeat):
+        dom = H.square_domain(a.ndim)
+        t0 = time.perf_counter()
+        dom(int(a.rays), seed=1 + r, verbose=False)
+        t1 = time.perf_counter()
+        info = {}
+        from rthx.equilibrium import equilibrium_grey
+        T, j, Abs, rr = equilibrium_grey(dom, dom.F_smooth, info=info)
+        t2 = time.perf_counter()
+        tr = dom.last_trace_info[0]
+        print(f"ndim {a.ndim} rays {a.rays:.0e}: mesh() {1e3 * (t1 - t0):.0f} ms (trace kernel "
+              f"{tr['trace_ms']:.2f} ms), solve {1e3 * (t2 - t1):.0f} ms (GMRES {info['iterations']} iterations, "
+              f"library {info['ms_total']:.1f} ms, residual {info['residual']:.2e}), energy error "
+              f"{dom.energy_error:.2e}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
