@@ -279,6 +279,66 @@ int rthx_solve_grey_smoothed(const rthx_smooth_result* F, const double* coeff, c
                              const rthx_solve_args* args, double* j_out, double* g_out,
                              rthx_solve_info* info);
 
+/* ------------------------------------------------------------------------
+ * method=:direct: energy-partition Monte Carlo of one
+ * spectral bin, replacing the ray loop of directRayTracingSingleBin!
+ * (src/RayTracing/RayTracing2D/DirectTracing2D/directRayTracing.jl:19-152)
+ * with traceSingleRay (traceSingleRay.jl:1-83).  Element index e runs over
+ * the global element order of the exchange path (surfaces 0..Ns-1, then
+ * volumes Ns..Ns+Nfine-1).  Each ray draws its emitter with probability
+ * weights[e] / sum(weights) (prepareEmitters.jl:1-88 energies; StatsBase
+ * `sample` with Weights), then bounces until absorbed, lost, rouletted or
+ * capped, exactly as traceSingleRay.  Per element the call returns
+ *   counts[0*n + e]  emitted     wall_emitted_count / gas_emitted_count
+ *   counts[1*n + e]  absorbed    wall_absorbed_count / absorbed_count
+ *   counts[2*n + e]  redirected  reflected_count / scattered_count
+ * with the reference's bookkeeping: emission is counted when the ray starts
+ * from an element with prescribed temperature (reemit[e] == 0,
+ * directRayTracing.jl:73-90); path events (reflection, scattering,
+ * re-emission, :107-124) count only for rays that end absorbed — a lost ray
+ * (escape, Russian roulette, max_iters) contributes its emission only.
+ * Counts ACCUMULATE into `counts` (zero it first), so shards of one bin may
+ * share a buffer.  Deviation: wall reflection (epsilon < 1) is a diffuse
+ * Lambert reflection off the hit wall; the reference's branch calls an
+ * undefined helper (traceSingleRay.jl:44, sampleReflectionDirection2D.jl:1-16)
+ * and raises.
+ * ------------------------------------------------------------------------ */
+typedef struct rthx_direct_args {
+  int64_t rays;            /* rays_tot of this bin (ray ids 0..rays-1) */
+  int64_t ray_begin;       /* this call traces ray ids [ray_begin, ray_end) */
+  int64_t ray_end;         /* clamped to rays */
+  double nudge;            /* eta (multiDispatchRayTrace2D.jl:10) */
+  uint64_t seed;           /* Philox key */
+  int32_t bin;             /* 0-based spectral bin */
+  int32_t device;
+  int32_t max_iters;       /* traceSingleRay cap: 100000 (directRayTracing.jl:90) */
+  int32_t roulette_after;  /* Russian roulette from this iteration on: 1000 (traceSingleRay.jl:12) */
+  double roulette_kill;    /* a ray dies when rand() > roulette_kill: 0.8 (:12) */
+  uint32_t flags;          /* RTHX_FLAG_FAITHFUL_SAMPLING */
+  int32_t reserved0;
+} rthx_direct_args;
+
+typedef struct rthx_direct_info {
+  int64_t rays_traced;     /* ray_end - ray_begin */
+  int64_t absorbed;        /* rays that ended absorbed */
+  int64_t escaped;         /* traceRay returned nothing (left the domain / lost) */
+  int64_t rouletted;       /* killed by Russian roulette */
+  int64_t capped;          /* reached max_iters */
+  int64_t events;          /* path events (reflections, scatterings, re-emissions) of absorbed rays */
+  int64_t replayed;        /* lost rays whose path events were rolled back */
+  double trace_ms;         /* device time of the trace launches */
+  double total_ms;         /* wall time of the call */
+} rthx_direct_info;
+
+/* weights[n_elem] >= 0 and finite (emitter energies; need not be normalised,
+ * their sum > 0); eps[Ns] wall emissivity and omega[Nfine] scattering albedo
+ * sigma_s / (kappa + sigma_s) of this bin; reemit[n_elem] = 1 where the
+ * element is in radiative equilibrium (T_in < 0: re-emits what it absorbs).
+ * counts[3 * n_elem] accumulates (see above). */
+int rthx_trace_direct(rthx_domain* dom, const double* weights, const double* eps, const double* omega,
+                      const uint8_t* reemit, const rthx_direct_args* args, uint64_t* counts,
+                      rthx_direct_info* info);
+
 #ifdef __cplusplus
 }
 #endif

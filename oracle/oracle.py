@@ -53,6 +53,11 @@ def load() -> C.CDLL:
     lib.oracle_result_free.restype = None
     lib.oracle_trace_ray.argtypes = [C.POINTER(abi.DomainDesc), C.POINTER(abi.TraceArgs), C.c_int64, C.c_int64,
                                      C.POINTER(C.c_int64), C.POINTER(C.c_double), C.POINTER(C.c_double)]
+    dp = C.POINTER(C.c_double)
+    lib.oracle_build_alias.argtypes = [dp, C.c_int64, C.POINTER(C.c_uint64)]
+    lib.oracle_trace_direct.argtypes = [C.POINTER(abi.DomainDesc), dp, dp, dp, C.POINTER(C.c_uint8),
+                                        C.POINTER(abi.DirectArgs), C.c_int, C.POINTER(C.c_uint64),
+                                        C.POINTER(abi.DirectInfo)]
     lib.oracle_last_error.restype = C.c_char_p
     _lib = lib
     return lib
@@ -120,6 +125,33 @@ def trace_exchange(flat, args, nthreads: int = 0):
         lib.oracle_result_free(h)
 
 
+def build_alias(weights) -> np.ndarray:
+    """The alias table of rthx_oracle.c (entries (alias << 32) | threshold)."""
+    w = np.ascontiguousarray(weights, dtype=np.float64)
+    out = np.zeros(len(w), dtype=np.uint64)
+    rc = load().oracle_build_alias(abi.ptr(w, C.c_double), len(w), abi.ptr(out, C.c_uint64))
+    assert rc == 0
+    return out
+
+
+def trace_direct(flat, weights, eps, omega, reemit, args, nthreads: int = 0):
+    """method=:direct restated on the CPU: (counts[3, n] uint64, info dict)."""
+    lib = load()
+    n = flat.n_emitters
+    w = np.ascontiguousarray(weights, dtype=np.float64)
+    e = np.ascontiguousarray(eps, dtype=np.float64) if len(eps) else np.zeros(1)
+    o = np.ascontiguousarray(omega, dtype=np.float64)
+    r = np.ascontiguousarray(reemit, dtype=np.uint8)
+    counts = np.zeros(3 * n, dtype=np.uint64)
+    inf = abi.DirectInfo()
+    rc = lib.oracle_trace_direct(C.byref(flat.desc), abi.ptr(w, C.c_double), abi.ptr(e, C.c_double),
+                                 abi.ptr(o, C.c_double), abi.ptr(r, C.c_uint8), C.byref(args), nthreads,
+                                 abi.ptr(counts, C.c_uint64), C.byref(inf))
+    if rc != 0:
+        raise RuntimeError(f"oracle error {rc}: {lib.oracle_last_error().decode()}")
+    return counts.reshape(3, n), inf.as_dict()
+
+
 class OracleBackend:
     """Backend object for rthx.exchange's host logic, for CPU tests only."""
 
@@ -138,3 +170,10 @@ class OracleBackend:
         out = trace_exchange(flat, args, self.nthreads)
         del keep
         return out
+
+    def trace_direct(self, dom, weights, eps, omega, reemit, bin0, rays, ray_begin, ray_end, nudge, seed, device,
+                     faithful):
+        from rthx.direct import make_direct_args
+
+        args = make_direct_args(bin0, rays, nudge, seed, ray_begin, ray_end, device, faithful)
+        return trace_direct(dom.flat(), weights, eps, omega, reemit, args, self.nthreads)

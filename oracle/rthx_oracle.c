@@ -94,9 +94,10 @@ typedef struct {
   double R1, R2, path, sel, th, ph, l1, l2;
 } draws_t;
 
-static void ray_draws(uint64_t seed, uint32_t bin, uint32_t g, uint32_t r, draws_t* d) {
+/* Draws from the counter pair (w0, w1, blk, w3), (w0, w1, blk + 1, w3). */
+static void draws_at(uint64_t seed, uint32_t w0, uint32_t w1, uint32_t blk, uint32_t w3, draws_t* d) {
   uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
-  uint32_t ca[4] = {r, g, 0u, bin}, cc[4] = {r, g, 1u, bin};
+  uint32_t ca[4] = {w0, w1, blk, w3}, cc[4] = {w0, w1, blk + 1u, w3};
   uint32_t a[4], c[4];
   oracle_philox4x32_10(ca, key, a);
   oracle_philox4x32_10(cc, key, c);
@@ -108,6 +109,10 @@ static void ray_draws(uint64_t seed, uint32_t bin, uint32_t g, uint32_t r, draws
   d->ph = u32(((a[1] & 0xFFFu) << 20) | ((a[3] & 0xFFFu) << 8) | ((c[1] & 0xFFFu) >> 4));
   d->l1 = u32(a[2]);
   d->l2 = u32(a[3]);
+}
+
+static void ray_draws(uint64_t seed, uint32_t bin, uint32_t g, uint32_t r, draws_t* d) {
+  draws_at(seed, r, g, 0u, bin, d);
 }
 
 ORACLE_API void oracle_ray_draws(uint64_t seed, uint32_t bin, uint32_t g, uint32_t r, double out[8]) {
@@ -214,6 +219,32 @@ static inline int locate_coarse(const dom_t* D, double px, double py) {
 
 #define TWO_PI 6.283185307179586 /* Float64(2pi), Julia's 2*pi / 2π */
 
+/* lambertSample2D.jl:1-10 rotated by emitSurfaceRay2D.jl:17-24: cosine-law
+ * direction in the frame (t, left normal (-t_y, t_x)) of a wall with unit
+ * tangent t.  lambertSample2D: R_angle1 = Float32(rand()); cosTheta =
+ * sqrt(R_angle1) (Float32); sinTheta = sqrt(1.0 - cosTheta^2) (cosTheta^2 in
+ * Float32); psi = 2*pi*Float32(rand()) (Float64).  Un-normalised. */
+static void lambert_dir(double tx, double ty, double l1, double l2, int faithful, double* dir) {
+  float r1 = (float)l1;
+  float ct = (float)sqrt((double)r1); /* correctly rounded Float32 sqrt */
+  float ct2 = ct * ct;
+  double st = sqrt(1.0 - (double)ct2);
+  float r2 = (float)l2;
+  double cpsi;
+  if (faithful) {
+    double psi = TWO_PI * (double)r2;
+    cpsi = cos(psi);
+  } else {
+    cpsi = cos(TWO_PI * (double)r2);
+  }
+  double xl = st * cpsi;
+  double zl = (double)ct;
+  double nx = -ty, ny = tx;
+  /* RotationMatrix * i1_loc (emitSurfaceRay2D.jl:21-23) */
+  dir[0] = tx * xl + nx * zl;
+  dir[1] = ty * xl + ny * zl;
+}
+
 /* emitSurfaceRay2D.jl:1-26 with lambertSample2D.jl:1-10.  Emission point
  * uniform on wall w, nudged relatively toward the fine midpoint; cosine-law
  * direction in the (tangent, left normal) frame, with the Float32-rounded
@@ -233,32 +264,10 @@ static void emit_surface(const rthx_domain_desc* d, int f, int w, double eta, in
   px = px + (m[0] - px) * eta;
   py = py + (m[1] - py) * eta;
 
-  /* lambertSample2D: R_angle1 = Float32(rand()); cosTheta = sqrt(R_angle1)
-   * (Float32); sinTheta = sqrt(1.0 - cosTheta^2) (cosTheta^2 in Float32);
-   * psi = 2*pi*Float32(rand()) (Float64). */
-  float r1 = (float)rd->l1;
-  float ct = (float)sqrt((double)r1); /* correctly rounded Float32 sqrt */
-  float ct2 = ct * ct;
-  double st = sqrt(1.0 - (double)ct2);
-  float r2 = (float)rd->l2;
-  double cpsi;
-  if (faithful) {
-    double psi = TWO_PI * (double)r2;
-    cpsi = cos(psi);
-  } else {
-    cpsi = cos(TWO_PI * (double)r2);
-  }
-  double xl = st * cpsi;
-  double zl = (double)ct;
-
-  /* xVecLocal = normalize(p2 - p1); yVecLocal = (-x[2], x[1]) */
+  /* xVecLocal = normalize(p2 - p1) */
   double ex = p2x - p1x, ey = p2y - p1y;
   double len = sqrt(ex * ex + ey * ey);
-  double tx = ex / len, ty = ey / len;
-  double nx = -ty, ny = tx;
-  /* RotationMatrix * i1_loc (emitSurfaceRay2D.jl:21-23) */
-  dir[0] = tx * xl + nx * zl;
-  dir[1] = ty * xl + ny * zl;
+  lambert_dir(ex / len, ey / len, rd->l1, rd->l2, faithful, dir);
   p[0] = px;
   p[1] = py;
 }
@@ -320,14 +329,15 @@ static void emit_volume(const rthx_domain_desc* d, int f, double eta, int faithf
 typedef struct {
   int64_t absorber;
   double end[2];
+  int coarse; /* coarse polygon of the end point (the next traceRay's start, traceSingleRay.jl:78) */
 } hit_t;
 
 /* traceRayUniform, traceRay.jl:20-70 (free path S = -ln u / beta). */
 static hit_t trace_uniform(const dom_t* D, double px, double py, double dx, double dy,
-                           double beta, double eta, int c, const draws_t* rd) {
+                           double beta, double eta, int c, double u_path) {
   const rthx_domain_desc* d = D->d;
-  hit_t h = {-1, {px, py}};
-  double S = beta > 0 ? -log(rd->path) / beta : INFINITY;
+  hit_t h = {-1, {px, py}, c};
+  double S = beta > 0 ? -log(u_path) / beta : INFINITY;
   for (int it = 0; it < 10000; ++it) {
     int k;
     double u = dist_to_polygon(px, py, dx, dy, d->coarse_xy + 8 * (size_t)c,
@@ -339,7 +349,7 @@ static hit_t trace_uniform(const dom_t* D, double px, double py, double dx, doub
       int f = locate_fine(D, c, px, py);
       if (f < 0) return h;
       h.absorber = d->n_surfaces + d->fine_offset[c] + f;
-      h.end[0] = px; h.end[1] = py;
+      h.end[0] = px; h.end[1] = py; h.coarse = c;
       return h;
     } else if (d->coarse_solid[4 * (size_t)c + k]) {
       double t = u - eta;
@@ -352,7 +362,7 @@ static hit_t trace_uniform(const dom_t* D, double px, double py, double dx, doub
       dist_to_polygon(px, py, dx, dy, d->fine_xy + 8 * (size_t)fg, d->fine_normal + 8 * (size_t)fg,
                       d->fine_nv[fg], &w);
       h.absorber = d->fine_surface[4 * (size_t)fg + w]; /* -1 if not solid */
-      h.end[0] = px; h.end[1] = py;
+      h.end[0] = px; h.end[1] = py; h.coarse = c;
       return h;
     } else {
       double t = u + eta;
@@ -369,11 +379,11 @@ static hit_t trace_uniform(const dom_t* D, double px, double py, double dx, doub
 /* traceRayVariable, traceRay.jl:73-147 (optical-depth sampling; beta taken
  * from the fine cell containing each segment's start point). */
 static hit_t trace_variable(const dom_t* D, double px, double py, double dx, double dy, int bin,
-                            double eta, int c, const draws_t* rd) {
+                            double eta, int c, double u_path) {
   const rthx_domain_desc* d = D->d;
-  hit_t h = {-1, {px, py}};
+  hit_t h = {-1, {px, py}, c};
   const double* beta_bin = d->beta + (size_t)bin * d->n_fine;
-  double target = -log(rd->path);
+  double target = -log(u_path);
   double acc = 0.0;
   for (int it = 0; it < 10000; ++it) {
     int k;
@@ -391,7 +401,7 @@ static hit_t trace_variable(const dom_t* D, double px, double py, double dx, dou
       int f = locate_fine(D, c, px, py);
       if (f < 0) return h;
       h.absorber = d->n_surfaces + d->fine_offset[c] + f;
-      h.end[0] = px; h.end[1] = py;
+      h.end[0] = px; h.end[1] = py; h.coarse = c;
       return h;
     } else if (d->coarse_solid[4 * (size_t)c + k]) {
       double t = u - eta;
@@ -404,7 +414,7 @@ static hit_t trace_variable(const dom_t* D, double px, double py, double dx, dou
       dist_to_polygon(px, py, dx, dy, d->fine_xy + 8 * (size_t)fg, d->fine_normal + 8 * (size_t)fg,
                       d->fine_nv[fg], &w);
       h.absorber = d->fine_surface[4 * (size_t)fg + w];
-      h.end[0] = px; h.end[1] = py;
+      h.end[0] = px; h.end[1] = py; h.coarse = c;
       return h;
     } else {
       double t = u + eta;
@@ -441,9 +451,9 @@ static hit_t trace_one(const dom_t* D, const rthx_trace_args* a, int64_t g, int6
   int c = D->coarse_of[f];
   if (d->uniform_beta[a->bin] > -0.1) {
     double beta = d->beta[(size_t)a->bin * d->n_fine + 0];
-    return trace_uniform(D, p[0], p[1], dir[0], dir[1], beta, a->nudge, c, &rd);
+    return trace_uniform(D, p[0], p[1], dir[0], dir[1], beta, a->nudge, c, rd.path);
   }
-  return trace_variable(D, p[0], p[1], dir[0], dir[1], a->bin, a->nudge, c, &rd);
+  return trace_variable(D, p[0], p[1], dir[0], dir[1], a->bin, a->nudge, c, rd.path);
 }
 
 /* ------------------------------------------------------------------------ */
@@ -809,5 +819,288 @@ ORACLE_API int oracle_trace_ray(const rthx_domain_desc* d, const rthx_trace_args
   end[0] = h.end[0];
   end[1] = h.end[1];
   free(D.surf_face); free(D.surf_wall); free(D.coarse_of);
+  return RTHX_OK;
+}
+
+/* ======================================================================== */
+/* method=:direct: directRayTracingSingleBin!            */
+/* (DirectTracing2D/directRayTracing.jl:19-152) and traceSingleRay          */
+/* (traceSingleRay.jl:1-83), restated per ray with the Philox blocks the    */
+/* HIP kernel draws (csrc/rthx_direct_kernels.hip header):                  */
+/*   blk 0: emitter (alias table); blk 1, 2: emission draws (draws_at);     */
+/*   blk 2i+2: interaction of iteration i (choice, direction);              */
+/*   blk 2i+1 (i >= 2): roulette + free path of iteration i;                */
+/*   blk 3: roulette of iteration 1 when roulette_after == 0.               */
+/* Path events are buffered per ray and committed only when the ray ends    */
+/* absorbed, as the reference does (traceSingleRay returns `nothing` for a  */
+/* lost ray and directRayTracing.jl:101 then skips its path).               */
+/* ======================================================================== */
+#define DIRECT_TAG 0x80000000u
+
+static void dom_init(dom_t* D, const rthx_domain_desc* d) {
+  D->d = d;
+  D->n_emitters = (int64_t)d->n_surfaces + d->n_fine;
+  D->surf_face = (int32_t*)malloc(sizeof(int32_t) * (d->n_surfaces + 1));
+  D->surf_wall = (int8_t*)malloc(d->n_surfaces + 1);
+  D->coarse_of = (int32_t*)malloc(sizeof(int32_t) * (d->n_fine + 1));
+  for (int c = 0; c < d->n_coarse; ++c)
+    for (int f = d->fine_offset[c]; f < d->fine_offset[c + 1]; ++f) D->coarse_of[f] = c;
+  for (int f = 0; f < d->n_fine; ++f)
+    for (int w = 0; w < 4; ++w) {
+      int s = d->fine_surface[4 * (size_t)f + w];
+      if (s >= 0) { D->surf_face[s] = f; D->surf_wall[s] = (int8_t)w; }
+    }
+}
+
+static void dom_free(dom_t* D) {
+  free(D->surf_face); free(D->surf_wall); free(D->coarse_of);
+}
+
+/* Alias table of the emitter energies in exact integer arithmetic (the
+ * library's rthx::build_alias, csrc/rthx_direct.cpp, states the scheme):
+ * masses floor(w_i / W * n * 2^32) with the remainder on the largest, Vose
+ * pairing with index stacks.  entry = (alias << 32) | threshold.  Sampling
+ * from it is distributionally StatsBase's sample(emitters, Weights(energy))
+ * (directRayTracing.jl:70) up to the 2^-32 quantisation of the masses. */
+ORACLE_API int oracle_build_alias(const double* w, int64_t n, uint64_t* out) {
+  if (!w || !out || n < 1) return RTHX_EINVAL;
+  const uint64_t one = (uint64_t)1 << 32;
+  double W = 0.0;
+  for (int64_t i = 0; i < n; ++i) W += w[i];
+  uint64_t* q = (uint64_t*)malloc(sizeof(uint64_t) * (size_t)n);
+  int64_t* small = (int64_t*)malloc(sizeof(int64_t) * (size_t)n);
+  int64_t* large = (int64_t*)malloc(sizeof(int64_t) * (size_t)n);
+  uint64_t sum = 0;
+  int64_t big = 0, ns = 0, nl = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    double m = w[i] / W * (double)n * 4294967296.0;
+    q[i] = m > 0.0 ? (uint64_t)m : 0u;
+    sum += q[i];
+    if (q[i] > q[big]) big = i;
+  }
+  uint64_t total = (uint64_t)n * one;
+  if (sum <= total) q[big] += total - sum; else q[big] -= sum - total;
+  for (int64_t i = 0; i < n; ++i) {
+    if (q[i] < one) small[ns++] = i; else large[nl++] = i;
+  }
+  while (ns > 0 && nl > 0) {
+    int64_t s = small[--ns];
+    int64_t l = large[nl - 1];
+    out[s] = ((uint64_t)l << 32) | q[s];
+    q[l] -= one - q[s];
+    if (q[l] < one) { --nl; small[ns++] = l; }
+  }
+  for (int64_t k = 0; k < nl; ++k) out[large[k]] = ((uint64_t)large[k] << 32) | 0xFFFFFFFFull;
+  for (int64_t k = 0; k < ns; ++k) out[small[k]] = ((uint64_t)small[k] << 32) | 0xFFFFFFFFull;
+  free(q); free(small); free(large);
+  return RTHX_OK;
+}
+
+/* isotropicScatter2D.jl:1-4: theta = acos(2u - 1), phi = 2 pi v,
+ * (sin(theta) cos(phi), cos(theta)). */
+static void iso_dir(double u, double v, int faithful, double* dir) {
+  double st, ct;
+  if (faithful) {
+    double theta = acos(2.0 * u - 1.0);
+    st = sin(theta);
+    ct = cos(theta);
+  } else {
+    ct = 2.0 * u - 1.0;
+    st = 2.0 * sqrt(u * (1.0 - u));
+  }
+  dir[0] = st * cos(TWO_PI * v);
+  dir[1] = ct;
+}
+
+typedef struct {
+  const dom_t* D;
+  const rthx_direct_args* a;
+  const uint64_t* alias;
+  const double* eps;
+  const double* omega;
+  const uint8_t* reemit;
+  int64_t r_begin, r_end;
+  uint64_t* counts; /* [3n], thread-local */
+  int64_t absorbed, escaped, rouletted, capped, events, replayed;
+  int32_t* path;    /* buffered (kind, element) pairs of the current ray */
+  size_t path_cap;
+  int err;
+} dworker_t;
+
+static void block_at(uint64_t seed, uint32_t r0, uint32_t r1, uint32_t blk, uint32_t tag, uint32_t out[4]) {
+  uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+  uint32_t ctr[4] = {r0, r1, blk, tag};
+  oracle_philox4x32_10(ctr, key, out);
+}
+
+static hit_t trace_leg(const dom_t* D, const rthx_direct_args* a, const double* p, const double* dir, int c,
+                       double u_path) {
+  const rthx_domain_desc* d = D->d;
+  if (d->uniform_beta[a->bin] > -0.1)
+    return trace_uniform(D, p[0], p[1], dir[0], dir[1], d->beta[(size_t)a->bin * d->n_fine], a->nudge, c, u_path);
+  return trace_variable(D, p[0], p[1], dir[0], dir[1], a->bin, a->nudge, c, u_path);
+}
+
+/* One ray: the body of the loop directRayTracing.jl:69-128. */
+static void direct_ray(dworker_t* W, uint64_t ray) {
+  const dom_t* D = W->D;
+  const rthx_domain_desc* d = D->d;
+  const rthx_direct_args* a = W->a;
+  const int64_t n = D->n_emitters;
+  const int32_t ns = d->n_surfaces;
+  const int faithful = (a->flags & RTHX_FLAG_FAITHFUL_SAMPLING) != 0;
+  const uint32_t r0 = (uint32_t)ray, r1 = (uint32_t)(ray >> 32), tag = (uint32_t)a->bin | DIRECT_TAG;
+  uint32_t w[4];
+  /* emitter = sample(local_rng, emitters, Weights(energy)) (:70) */
+  block_at(a->seed, r0, r1, 0u, tag, w);
+  uint32_t col = (uint32_t)(((uint64_t)w[0] * (uint64_t)n) >> 32);
+  uint64_t at = W->alias[col];
+  int64_t g = (w[1] < (uint32_t)at) ? (int64_t)col : (int64_t)(at >> 32);
+  draws_t rd;
+  draws_at(a->seed, r0, r1, 1u, tag, &rd);
+  double p[2], dir[2];
+  int f;
+  if (g < ns) { /* :72-78 */
+    f = D->surf_face[g];
+    emit_surface(d, f, D->surf_wall[g], a->nudge, faithful, &rd, p, dir);
+  } else {       /* :79-87 */
+    f = (int)(g - ns);
+    emit_volume(d, f, a->nudge, faithful, &rd, p, dir);
+  }
+  if (!W->reemit[g]) W->counts[g]++; /* temp_value >= 0.0 -> emitted count */
+  int c = D->coarse_of[f];
+  double u_path = rd.path;
+  size_t np = 0;  /* buffered (kind, element) entries */
+  int64_t nev = 0; /* path events (a re-emission buffers two entries) */
+  int it = 1;
+  if (a->roulette_after < 1) {
+    block_at(a->seed, r0, r1, 3u, tag, w);
+    if (u52(w[0], w[1]) > a->roulette_kill) { W->rouletted++; return; }
+  }
+  for (;;) {
+    hit_t h = trace_leg(D, a, p, dir, c, u_path); /* traceSingleRay.jl:17 */
+    if (h.absorber < 0) { W->escaped++; break; }  /* :19-21 */
+    int64_t e = h.absorber;
+    c = h.coarse;
+    block_at(a->seed, r0, r1, 2u * (uint32_t)it + 2u, tag, w);
+    int wall = e < ns;
+    int lt = u52(w[0], w[1]) < (wall ? W->eps[e] : W->omega[e - ns]);
+    int redirect = wall ? !lt : lt;
+    if (!redirect && !W->reemit[e]) {
+      /* true absorption (:42-43 / :72-74): commit the path (:103-125) */
+      W->counts[n + e]++;
+      for (size_t k = 0; k < np; ++k) W->counts[(size_t)W->path[2 * k] * (size_t)n + (size_t)W->path[2 * k + 1]]++;
+      W->absorbed++;
+      W->events += nev;
+      return;
+    }
+    if (np + 2 >= W->path_cap) {
+      size_t cap = W->path_cap ? 2 * W->path_cap : 256;
+      int32_t* q = (int32_t*)realloc(W->path, sizeof(int32_t) * 2 * cap);
+      if (!q) { W->err = 1; return; }
+      W->path = q;
+      W->path_cap = cap;
+    }
+    nev++;
+    if (redirect) { /* :reflection (:45-49) / :scattering (:58-62) */
+      W->path[2 * np] = 2; W->path[2 * np + 1] = (int32_t)e; np++;
+    } else {        /* :reemission: absorbed and emitted again (:116-124) */
+      W->path[2 * np] = 1; W->path[2 * np + 1] = (int32_t)e; np++;
+      W->path[2 * np] = 0; W->path[2 * np + 1] = (int32_t)e; np++;
+    }
+    if (wall) {
+      /* re-emission: emitSurfaceRay2D's direction from a point nudged toward
+       * the fine midpoint (:36-40); reflection: the same diffuse (Lambert)
+       * direction from the hit point (the reference's :44 helper is undefined) */
+      int fe = D->surf_face[e], we = D->surf_wall[e];
+      const double* xy = d->fine_xy + 8 * (size_t)fe;
+      int nv = d->fine_nv[fe];
+      int w2 = (we + 1) % nv;
+      double ex = xy[2 * w2] - xy[2 * we], ey = xy[2 * w2 + 1] - xy[2 * we + 1];
+      double len = sqrt(ex * ex + ey * ey);
+      p[0] = h.end[0];
+      p[1] = h.end[1];
+      if (!redirect) {
+        const double* m = d->fine_mid + 2 * (size_t)fe;
+        p[0] = p[0] + (m[0] - p[0]) * a->nudge;
+        p[1] = p[1] + (m[1] - p[1]) * a->nudge;
+      }
+      lambert_dir(ex / len, ey / len, u32(w[2]), u32(w[3]), faithful, dir);
+    } else {
+      /* isotropicScatter2D from the interaction point (:60-61, :68-69) */
+      p[0] = h.end[0];
+      p[1] = h.end[1];
+      iso_dir(u32(w[2]), u32(w[3]), faithful, dir);
+    }
+    if (it >= a->max_iters) { W->capped++; break; } /* while iteration_count < max_iters (:7) */
+    ++it;
+    block_at(a->seed, r0, r1, 2u * (uint32_t)it + 1u, tag, w);
+    if (it > a->roulette_after && u52(w[0], w[1]) > a->roulette_kill) { W->rouletted++; break; } /* :12-14 */
+    u_path = u52(w[2], w[3]);
+  }
+  if (np > 0) W->replayed++; /* lost with path events: the library rolls them back */
+}
+
+static void* direct_worker(void* arg) {
+  dworker_t* W = (dworker_t*)arg;
+  for (int64_t r = W->r_begin; r < W->r_end && !W->err; ++r) direct_ray(W, (uint64_t)r);
+  return NULL;
+}
+
+/* Counts ACCUMULATE into counts[3n] like rthx_trace_direct; info as there
+ * (replayed = lost rays that had path events). */
+ORACLE_API int oracle_trace_direct(const rthx_domain_desc* d, const double* weights, const double* eps,
+                                   const double* omega, const uint8_t* reemit, const rthx_direct_args* a,
+                                   int nthreads, uint64_t* counts, rthx_direct_info* info) {
+  double t0 = now_ms();
+  if (!d || !a || !weights || !omega || !reemit || !counts || (d->n_surfaces > 0 && !eps) || a->bin < 0 ||
+      a->bin >= d->n_bins || a->max_iters < 1 || a->roulette_after < 0 || a->ray_begin < 0) {
+    snprintf(g_err, sizeof g_err, "invalid arguments");
+    return RTHX_EINVAL;
+  }
+  dom_t D;
+  dom_init(&D, d);
+  const int64_t n = D.n_emitters;
+  int64_t end = a->ray_end < a->rays ? a->ray_end : a->rays;
+  int64_t rays = end > a->ray_begin ? end - a->ray_begin : 0;
+  rthx_direct_info inf;
+  memset(&inf, 0, sizeof inf);
+  inf.rays_traced = rays;
+  if (rays == 0) {
+    dom_free(&D);
+    if (info) *info = inf;
+    return RTHX_OK;
+  }
+  uint64_t* alias = (uint64_t*)malloc(sizeof(uint64_t) * (size_t)n);
+  oracle_build_alias(weights, n, alias);
+  if (nthreads <= 0) nthreads = (int)sysconf(_SC_NPROCESSORS_ONLN);
+  if (nthreads < 1) nthreads = 1;
+  dworker_t* W = (dworker_t*)calloc((size_t)nthreads, sizeof(dworker_t));
+  pthread_t* th = (pthread_t*)calloc((size_t)nthreads, sizeof(pthread_t));
+  /* contiguous ray ranges per thread (directRayTracing.jl:37-49) */
+  int64_t per = rays / nthreads, rem = rays % nthreads, start = a->ray_begin;
+  for (int t = 0; t < nthreads; ++t) {
+    int64_t sz = per + (t < rem ? 1 : 0);
+    W[t].D = &D; W[t].a = a; W[t].alias = alias; W[t].eps = eps; W[t].omega = omega; W[t].reemit = reemit;
+    W[t].r_begin = start; W[t].r_end = start + sz;
+    W[t].counts = (uint64_t*)calloc(3 * (size_t)n, sizeof(uint64_t));
+    start += sz;
+  }
+  for (int t = 1; t < nthreads; ++t) pthread_create(&th[t], NULL, direct_worker, &W[t]);
+  direct_worker(&W[0]);
+  for (int t = 1; t < nthreads; ++t) pthread_join(th[t], NULL);
+  int err = 0;
+  for (int t = 0; t < nthreads; ++t) { /* merge (:130-145) */
+    for (int64_t k = 0; k < 3 * n; ++k) counts[k] += W[t].counts[k];
+    inf.absorbed += W[t].absorbed; inf.escaped += W[t].escaped; inf.rouletted += W[t].rouletted;
+    inf.capped += W[t].capped; inf.events += W[t].events; inf.replayed += W[t].replayed;
+    err |= W[t].err;
+    free(W[t].counts); free(W[t].path);
+  }
+  free(W); free(th); free(alias);
+  dom_free(&D);
+  inf.trace_ms = inf.total_ms = now_ms() - t0;
+  if (info) *info = inf;
+  if (err) { snprintf(g_err, sizeof g_err, "out of host memory"); return RTHX_ENOMEM; }
   return RTHX_OK;
 }

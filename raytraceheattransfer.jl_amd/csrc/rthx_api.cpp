@@ -24,6 +24,7 @@
 #include "rthx_kernels.h"
 
 #include "rthx_common.h"
+#include "rthx_domain.h"
 
 using rthx::DevBuf;
 using rthx::HostBuf;
@@ -38,27 +39,6 @@ int fail(int code, const std::string& msg) {
   return code;
 }
 }  // namespace rthx
-
-struct rthx_domain {
-  int device = 0;
-  hipStream_t stream = nullptr;
-  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-  rthx::DevDomain D{};
-  const rthx::DevDomain* d_dom = nullptr;  // copy of D in device memory (kernel argument)
-  std::vector<void*> allocs;
-  int64_t n_emitters = 0;
-  int32_t n_bins = 1;
-  std::vector<double> uniform_beta;  // per bin
-  std::vector<double> beta_first;    // beta of fine face 0 per bin (traceRay.jl:6-11)
-  bool single_convex = false;        // one convex coarse polygon (SINGLE kernels)
-  bool axis_rect = false;            // every polygon an axis-aligned rectangle in canonical order (AXIS kernels)
-  ~rthx_domain() {
-    for (void* p : allocs) (void)hipFree(p);
-    for (auto& e : ev)
-      if (e) (void)hipEventDestroy(e);
-    if (stream) (void)hipStreamDestroy(stream);
-  }
-};
 
 struct rthx_result {
   int device = -1;

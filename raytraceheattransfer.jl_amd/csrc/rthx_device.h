@@ -147,9 +147,13 @@ __device__ __forceinline__ double u32(uint32_t w) { return (double)w * 0x1.0p-32
 // triangle selection use 32 bits.  Two blocks per ray (not three).
 struct RayDraws {
   uint32_t a[4], c[4];
-  __device__ __forceinline__ RayDraws(uint32_t r, uint32_t g, uint32_t bin, uint32_t k0, uint32_t k1) {
-    a[0] = r; a[1] = g; a[2] = 0u; a[3] = bin;
-    c[0] = r; c[1] = g; c[2] = 1u; c[3] = bin;
+  __device__ __forceinline__ RayDraws(uint32_t r, uint32_t g, uint32_t bin, uint32_t k0, uint32_t k1)
+      : RayDraws(r, g, 0u, bin, k0, k1) {}
+  // Generic counters (w0, w1, blk, w3) -> a and (w0, w1, blk + 1, w3) -> c
+  // (the direct method's emission, rthx_direct_kernels.hip).
+  __device__ __forceinline__ RayDraws(uint32_t w0, uint32_t w1, uint32_t blk, uint32_t w3, uint32_t k0, uint32_t k1) {
+    a[0] = w0; a[1] = w1; a[2] = blk; a[3] = w3;
+    c[0] = w0; c[1] = w1; c[2] = blk + 1u; c[3] = w3;
     philox4x32_10(a, k0, k1);
     philox4x32_10(c, k0, k1);
   }
@@ -395,37 +399,48 @@ struct Emitter {
 };
 
 __device__ __forceinline__ Emitter load_emitter(const DevDomain& D, int64_t g) {
-  Emitter e{};
+  // every field is assigned from a local exactly once (conditional stores
+  // into the struct made the compiler keep it in scratch)
+  Emitter e;
+  const bool surface = g < D.n_surfaces;
   int f, w = 0;
-  e.surface = g < D.n_surfaces;
-  if (e.surface) {
+  if (surface) {
     f = D.s_face[g];
     w = D.s_wall[g];
   } else {
     f = (int)(g - D.n_surfaces);
   }
-  e.nv = D.f_nv[f];
+  const DevPoly RTHX_GLOBAL& q = D.f_poly[f];
+  const int nv = D.f_nv[f];
+  double v[8];
+  double tx = 0.0, ty = 0.0;
+  if (surface) {
+    const int w2 = (w + 1 == nv) ? 0 : w + 1;
+    v[0] = q.x[w]; v[1] = q.y[w];
+    v[2] = q.x[w2]; v[3] = q.y[w2];
+    v[4] = v[5] = v[6] = v[7] = 0.0;
+    // xVecLocal = normalize(p2 - p1) (emitSurfaceRay2D.jl:17)
+    const double ex = v[2] - v[0], ey = v[3] - v[1];
+    const double len = sqrt(__dmul_rn(ex, ex) + __dmul_rn(ey, ey));
+    tx = ex / len;
+    ty = ey / len;
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[2 * i] = q.x[i];
+      v[2 * i + 1] = q.y[i];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) e.v[i] = v[i];
+  e.nv = nv;
   e.coarse = D.f_coarse[f];
   e.mx = D.f_mid[2 * f];
   e.my = D.f_mid[2 * f + 1];
   e.tri_frac = D.f_trifrac[f];
-  const DevPoly RTHX_GLOBAL& q = D.f_poly[f];
-  if (e.surface) {
-    int w2 = (w + 1 == e.nv) ? 0 : w + 1;
-    e.v[0] = q.x[w]; e.v[1] = q.y[w];
-    e.v[2] = q.x[w2]; e.v[3] = q.y[w2];
-    // xVecLocal = normalize(p2 - p1) (emitSurfaceRay2D.jl:17)
-    double ex = e.v[2] - e.v[0], ey = e.v[3] - e.v[1];
-    double len = sqrt(__dmul_rn(ex, ex) + __dmul_rn(ey, ey));
-    e.tx = ex / len;
-    e.ty = ey / len;
-  } else {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      e.v[2 * i] = q.x[i];
-      e.v[2 * i + 1] = q.y[i];
-    }
-  }
+  e.tx = tx;
+  e.ty = ty;
+  e.surface = surface;
   return e;
 }
 
@@ -433,6 +448,23 @@ __device__ __forceinline__ Emitter load_emitter(const DevDomain& D, int64_t g) {
 // wall nudged relatively toward the midpoint; cosine-law direction with the
 // reference's Float32-rounded draws, rotated into (tangent, left normal) and
 // left un-normalised (in-plane projection of a 3D unit vector).
+// lambertSample2D.jl:1-10 rotated by emitSurfaceRay2D.jl:17-24: cosine-law
+// direction from the Float32-rounded draws l1, l2, in the frame (tangent t,
+// left normal (-t_y, t_x)) of the wall, un-normalised.
+template <bool FAITHFUL>
+__device__ __forceinline__ void lambert_dir(double tx, double ty, double l1, double l2, double& dx, double& dy) {
+  float r1 = (float)l1;
+  float ct = (float)sqrt((double)r1);  // correctly rounded Float32 sqrt
+  float ct2 = __fmul_rn(ct, ct);
+  double st = sqrt(1.0 - (double)ct2);
+  float r2 = (float)l2;
+  double cpsi = FAITHFUL ? cos(RTHX_TWO_PI * (double)r2) : cospi(2.0 * (double)r2);
+  double xl = __dmul_rn(st, cpsi);
+  double zl = (double)ct;
+  dx = __dmul_rn(tx, xl) + __dmul_rn(-ty, zl);
+  dy = __dmul_rn(ty, xl) + __dmul_rn(tx, zl);
+}
+
 template <bool FAITHFUL>
 __device__ __forceinline__ void emit_surface(const Emitter& e, double eta, const RayDraws& rd, double& px,
                                              double& py, double& dx, double& dy) {
@@ -441,16 +473,29 @@ __device__ __forceinline__ void emit_surface(const Emitter& e, double eta, const
   py = e.v[1] + __dmul_rn(e.v[3] - e.v[1], R);
   px = px + __dmul_rn(e.mx - px, eta);
   py = py + __dmul_rn(e.my - py, eta);
-  float r1 = (float)rd.l1();
-  float ct = (float)sqrt((double)r1);  // correctly rounded Float32 sqrt
-  float ct2 = __fmul_rn(ct, ct);
-  double st = sqrt(1.0 - (double)ct2);
-  float r2 = (float)rd.l2();
-  double cpsi = FAITHFUL ? cos(RTHX_TWO_PI * (double)r2) : cospi(2.0 * (double)r2);
-  double xl = __dmul_rn(st, cpsi);
-  double zl = (double)ct;
-  dx = __dmul_rn(e.tx, xl) + __dmul_rn(-e.ty, zl);
-  dy = __dmul_rn(e.ty, xl) + __dmul_rn(e.tx, zl);
+  lambert_dir<FAITHFUL>(e.tx, e.ty, rd.l1(), rd.l2(), dx, dy);
+}
+
+// isotropicScatter2D.jl:1-4: theta = acos(2u - 1), phi = 2 pi v, direction
+// (sin(theta) cos(phi), cos(theta)) -- the isotropic 3D direction projected
+// on the plane, as for volume emission (emitVolumeRay2D.jl:26-31).
+// u = u32(w_th), v = u32(w_ph).
+template <bool FAITHFUL>
+__device__ __forceinline__ void iso_dir(uint32_t w_th, uint32_t w_ph, const double* cos_tab, double& dx, double& dy) {
+  const double u = u32(w_th);
+  double st, ct, cphi;
+  if (FAITHFUL) {
+    const double theta = acos(2.0 * u - 1.0);
+    st = sin(theta);
+    ct = cos(theta);
+    cphi = cos(RTHX_TWO_PI * u32(w_ph));
+  } else {
+    ct = 2.0 * u - 1.0;                           // cos(acos(x)) = x
+    st = 2.0 * sqrt_unit(__dmul_rn(u, 1.0 - u));  // sin(acos(x)) = sqrt((1-x)(1+x))
+    cphi = cos_2pi_u32(w_ph, cos_tab);
+  }
+  dx = __dmul_rn(st, cphi);
+  dy = ct;
 }
 
 // emitVolumeRay2D.jl:1-33: uniform point (quad = triangles ABC / CDA chosen

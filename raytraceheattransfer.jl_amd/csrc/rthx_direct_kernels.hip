@@ -1,0 +1,354 @@
+// rthx_direct_kernels.hip -- method=:direct on gfx950.
+//
+// trace_direct_kernel: the ray loop of directRayTracingSingleBin!
+//   (DirectTracing2D/directRayTracing.jl:69-128) with traceSingleRay
+//   (traceSingleRay.jl:1-83).  A persistent grid; every lane owns one ray at a
+//   time and advances it one coarse-polygon segment per loop trip (the
+//   exchange kernel's segment(), rthx_device.h), so a wave keeps all 64 lanes
+//   busy although paths range from one leg to thousands of bounces.  Idle
+//   lanes take new ray ids from a wave-private pool refilled by one global
+//   atomic per 256 rays.
+//
+// Random numbers: ray r (64-bit) owns the Philox blocks with counter
+// (r lo, r hi, blk, bin | kDirectTag):
+//   blk 0            emitter draw: column = mulhi(w0, n), accept w1 < threshold (alias table)
+//   blk 1, 2         emission (the exchange tracer's RayDraws layout: point, direction, first free path)
+//   blk 2i+2, i >= 1 interaction of iteration i: choice u52(w0,w1), direction draws w2, w3
+//   blk 2i+1, i >= 2 start of iteration i: roulette u52(w0,w1), free path u52(w2,w3)
+//   blk 3            roulette of iteration 1 (only when roulette_after == 0)
+// oracle/rthx_oracle.c (oracle_trace_direct) draws the same blocks.
+//
+// Bookkeeping (directRayTracing.jl:72-128): the emission count is added when
+// the ray starts; path events (reflection, scattering, re-emission) are added
+// as they happen, and a ray that is then lost (escape, roulette, max_iters)
+// must not keep them (the reference drops the whole path, :101).  Such rays
+// are listed, and a replay launch of the same kernel re-traces exactly those
+// rays (same code, same draws, bit-identical paths) subtracting every path
+// event -- lost rays are rare, so the common path never buffers events.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rthx_device.h"
+#include "rthx_direct.h"
+#include "rthx_wave.h"
+
+namespace rthx {
+
+constexpr int kDirectThreads = 256;      // default workgroup
+constexpr int kDirectMaxThreads = 1024;  // large LDS counter arrays: one workgroup of 16 waves per CU
+constexpr uint32_t kPoolClaim = 256;  // rays per global claim (one atomic per 256 rays)
+constexpr int kDirectRefill = 16;     // refill once this many lanes of a wave are idle
+
+__device__ __forceinline__ void philox_block(uint32_t w[4], uint32_t r0, uint32_t r1, uint32_t blk, uint32_t tag,
+                                             uint32_t k0, uint32_t k1) {
+  w[0] = r0; w[1] = r1; w[2] = blk; w[3] = tag;
+  philox4x32_10(w, k0, k1);
+}
+
+template <bool UNIFORM, bool FAITHFUL, bool SINGLE, bool AXIS>
+__global__ __launch_bounds__(FAITHFUL ? kDirectThreads : kDirectMaxThreads) void trace_direct_kernel(const DevDomain* __restrict__ Dp,
+                                                                      DirectParams Q) {
+  extern __shared__ uint32_t hist[];  // Q.hist: [3][n_elem] per-workgroup counters
+  __shared__ double s_tab[kTableDoubles];
+  __shared__ SingleCoarse s_single;
+  const DevDomain& D = *Dp;
+  const int tid = threadIdx.x;
+  const int nthr = (int)blockDim.x;
+  const int n = Q.n_elem;
+  const bool use_hist = Q.hist != 0;
+  const bool replay = Q.replay != nullptr;
+  if (use_hist)
+    for (int i = tid; i < 3 * n; i += nthr) hist[i] = 0u;
+  if (!FAITHFUL)
+    for (int i = tid; i < kTableDoubles; i += nthr) s_tab[i] = D.tables[i];
+  if (SINGLE && tid == 0) {
+    s_single.poly = D.c_poly[0];
+    s_single.grid = D.f_grid[0];
+    s_single.solid = D.c_solid[0];
+    s_single.count = D.f_offset[1];
+  }
+  __syncthreads();
+
+  const uint32_t k0 = Q.P.key0, k1 = Q.P.key1;
+  const uint32_t tag = (uint32_t)Q.P.bin | kDirectTag;
+  const int Ns = D.n_surfaces;
+  const double eta = Q.P.eta;
+  const int64_t n_items = replay ? (int64_t)*Q.n_replay : Q.n_items;
+  // first pass adds +1 per path event, the replay pass -1 (u32 / u64 wrap)
+  const uint32_t sign = replay ? 0xFFFFFFFFu : 1u;
+  auto add = [&](int kind, int e, uint32_t v) {
+    if (use_hist)
+      atomicAdd(&hist[kind * n + e], v);
+    else
+      atomicAdd(&Q.counts[(size_t)kind * n + e], (unsigned long long)(int64_t)(int32_t)v);
+  };
+
+  const uint32_t lane = lane_id();
+  const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  uint64_t pool = 0, pool_end = 0;  // wave-uniform: unclaimed items of this wave
+  bool more = true, live = false, dirty = false;
+  uint32_t item = 0, r0 = 0, r1 = 0;
+  double px = 0.0, py = 0.0, dx = 0.0, dy = 0.0, S = 0.0, acc = 0.0;
+  int c = 0, seg = 0, it = 0;
+  uint32_t ev = 0;
+  uint32_t n_absorbed = 0, n_escaped = 0, n_roulette = 0, n_capped = 0, n_events = 0;
+
+  while (true) {
+    if (more) {
+      const uint64_t idle = __ballot(!live);
+      if (__popcll(idle) >= kDirectRefill || __ballot(live) == 0ull) {
+        const uint32_t need = (uint32_t)__popcll(idle);
+        const uint64_t avail = pool_end - pool;
+        uint64_t fresh = 0;
+        if (need > avail) {
+          unsigned long long b = 0;
+          if (lane == 0) b = atomicAdd(Q.next, (unsigned long long)kPoolClaim);
+          fresh = ((uint64_t)__shfl((int)(b >> 32), 0) << 32) | (uint32_t)__shfl((int)(uint32_t)b, 0);
+        }
+        const uint64_t rank = (uint64_t)__popcll(idle & lt_mask);
+        const uint64_t mine = rank < avail ? pool + rank : fresh + (rank - avail);
+        if (need > avail) {
+          pool = fresh + (need - avail);
+          pool_end = fresh + kPoolClaim;
+        } else {
+          pool += need;
+        }
+        bool got = false;
+        if (!live && (int64_t)mine < n_items) {
+          got = true;
+          item = (uint32_t)mine;
+          const uint64_t ray = (uint64_t)Q.ray_begin + (replay ? (uint64_t)Q.replay[item] : (uint64_t)item);
+          r0 = (uint32_t)ray;
+          r1 = (uint32_t)(ray >> 32);
+          // emitter: sample(emitters, Weights(energy)) (directRayTracing.jl:70) by the alias method
+          uint32_t w[4];
+          philox_block(w, r0, r1, 0u, tag, k0, k1);
+          const uint32_t col = (uint32_t)(((uint64_t)w[0] * (uint64_t)(uint32_t)n) >> 32);
+          const uint64_t at = Q.alias[col];
+          const int g = (w[1] < (uint32_t)at) ? (int)col : (int)(at >> 32);
+          const double* tab = (const double*)lds_opaque(&s_tab[0]);
+          const Emitter e = load_emitter(D, g);
+          const RayDraws rd(r0, r1, 1u, tag, k0, k1);
+          if (e.surface)
+            emit_surface<FAITHFUL>(e, eta, rd, px, py, dx, dy);
+          else
+            emit_volume<FAITHFUL>(e, eta, rd, tab, px, py, dx, dy);
+          S = free_path<UNIFORM, FAITHFUL>(Q.P, tab, rd.path());
+          acc = 0.0;
+          c = e.coarse;
+          seg = 0;
+          it = 1;
+          ev = 0;
+          dirty = false;
+          live = true;
+          if (!replay && !Q.el[g].reemit) add(0, g, 1u);  // directRayTracing.jl:75-77 / :85-87
+          if (Q.roulette_after < 1) {                       // iteration 1 is already past the roulette threshold
+            philox_block(w, r0, r1, 3u, tag, k0, k1);
+            if (u52(w[0], w[1]) > Q.roulette_kill) {
+              live = false;
+              if (!replay) ++n_roulette;
+            }
+          }
+        }
+        // a lane that found the items exhausted: every later claim is too
+        more = __ballot(!live && !got) == 0ull;
+      }
+    }
+    if (__ballot(live) == 0ull) break;
+    if (live) {
+      // traceRay (traceRay.jl:20-147) one coarse segment at a time, 10,000 per call
+      int a;
+      if (SINGLE) {
+        const SingleCoarse RTHX_LDS* sc = lds_opaque(&s_single);
+        a = seg < 10000 ? segment<UNIFORM, SINGLE, AXIS>(D, Q.P, *(const SingleCoarse*)sc, c, px, py, dx, dy, S, acc)
+                        : -1;
+      } else {
+        a = seg < 10000 ? segment<UNIFORM, SINGLE, AXIS>(D, Q.P, s_single, c, px, py, dx, dy, S, acc) : -1;
+      }
+      ++seg;
+      if (a != kRayContinue) {
+        int fate = -1;  // -1: next iteration; else a DirectStat
+        if (a < 0) {
+          fate = kStatEscaped;  // traceRay returned nothing (traceSingleRay.jl:20-22)
+        } else {
+          uint32_t w[4];
+          philox_block(w, r0, r1, 2u * (uint32_t)it + 2u, tag, k0, k1);
+          const DirectElem E = Q.el[a];
+          const bool wall = a < Ns;
+          const bool lt = u52(w[0], w[1]) < E.p;
+          // wall: rand() < epsilon absorbs (:35), else reflects (:45-49);
+          // gas: rand() < omega scatters (:58-62), else absorbs (:63-75)
+          const bool redirect = wall ? !lt : lt;
+          if (!redirect && !E.reemit) {
+            if (!replay) add(1, a, 1u);  // true absorption: wall_absorbed / absorbed (directRayTracing.jl:104-108)
+            fate = kStatAbsorbed;
+          } else {
+            if (redirect) {
+              add(2, a, sign);  // reflected / scattered (:112-115)
+            } else {
+              add(1, a, sign);  // re-emission: absorbed and emitted again (:116-124)
+              add(0, a, sign);
+            }
+            dirty = true;
+            ++ev;
+            const double* tab = (const double*)lds_opaque(&s_tab[0]);
+            if (wall) {
+              const SurfGeo sg = Q.sgeo[a];
+              if (!redirect) {  // re-emission point nudged toward the fine midpoint (traceSingleRay.jl:40)
+                px = px + __dmul_rn(sg.mx - px, eta);
+                py = py + __dmul_rn(sg.my - py, eta);
+              }
+              lambert_dir<FAITHFUL>(sg.tx, sg.ty, u32(w[2]), u32(w[3]), dx, dy);
+            } else {
+              iso_dir<FAITHFUL>(w[2], w[3], tab, dx, dy);
+            }
+            if (it >= Q.max_iters) {
+              fate = kStatCapped;  // while iteration_count < max_iters (traceSingleRay.jl:7)
+            } else {
+              ++it;
+              philox_block(w, r0, r1, 2u * (uint32_t)it + 1u, tag, k0, k1);
+              if (it > Q.roulette_after && u52(w[0], w[1]) > Q.roulette_kill) {
+                fate = kStatRoulette;  // traceSingleRay.jl:12-14
+              } else {
+                S = free_path<UNIFORM, FAITHFUL>(Q.P, tab, u52(w[2], w[3]));
+                acc = 0.0;
+                seg = 0;
+              }
+            }
+          }
+        }
+        if (fate >= 0) {
+          live = false;
+          if (!replay) {
+            n_absorbed += fate == kStatAbsorbed ? 1u : 0u;
+            n_escaped += fate == kStatEscaped ? 1u : 0u;
+            n_roulette += fate == kStatRoulette ? 1u : 0u;
+            n_capped += fate == kStatCapped ? 1u : 0u;
+            n_events += fate == kStatAbsorbed ? ev : 0u;
+            if (fate != kStatAbsorbed && dirty) Q.lost[atomicAdd(Q.n_lost, 1u)] = item;
+          }
+        }
+      }
+    }
+  }
+
+  if (!replay) {
+    const uint32_t st[kDirectStats] = {n_absorbed, n_escaped, n_roulette, n_capped, n_events};
+#pragma unroll
+    for (int k = 0; k < kDirectStats; ++k) {
+      uint32_t v = st[k];
+      for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+      if (lane == 0 && v) atomicAdd(&Q.stats[k], (unsigned long long)v);
+    }
+  }
+  if (use_hist) {
+    // this workgroup's counters to its slice of the partial buffer (coalesced);
+    // counter_reduce_kernel sums the slices
+    __syncthreads();
+    uint32_t* out = Q.partial + (size_t)blockIdx.x * 3 * n;
+    for (int i = tid; i < 3 * n; i += nthr) out[i] = hist[i];
+  }
+}
+
+// counts[i] += sum over workgroups of partial[b][i]; the replay pass's
+// counters are negative (two's complement u32).
+__global__ __launch_bounds__(256) void counter_reduce_kernel(const uint32_t* __restrict__ partial, int32_t n_blocks,
+                                                             int64_t len, int32_t is_signed,
+                                                             unsigned long long* __restrict__ counts) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= len) return;
+  int64_t s = 0;
+  for (int b = 0; b < n_blocks; ++b) {
+    const uint32_t v = partial[(size_t)b * len + i];
+    s += is_signed ? (int64_t)(int32_t)v : (int64_t)v;
+  }
+  counts[i] += (unsigned long long)s;
+}
+
+// Wall frames of every surface (SurfGeo), from the same load_emitter the
+// emission uses, so re-emitted and first-emitted rays share one tangent.
+__global__ __launch_bounds__(256) void surface_frames_kernel(const DevDomain* __restrict__ Dp, int32_t ns,
+                                                             SurfGeo* __restrict__ out) {
+  const int s = blockIdx.x * 256 + threadIdx.x;
+  if (s >= ns) return;
+  const Emitter e = load_emitter(*Dp, s);
+  out[s] = SurfGeo{e.tx, e.ty, e.mx, e.my};
+}
+
+template <bool UNIFORM, bool FAITHFUL, bool SINGLE, bool AXIS>
+static hipError_t direct_shape_t(const DirectLaunch& L, int* threads, int* blocks) {
+  auto kern = trace_direct_kernel<UNIFORM, FAITHFUL, SINGLE, AXIS>;
+  const size_t lds = L.Q.hist ? (size_t)3 * L.Q.n_elem * 4 : 0;
+  if (lds > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  int dev = 0, cus = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (e != hipSuccess) return e;
+  // the workgroup size that keeps most waves resident (large LDS counter
+  // arrays fit one workgroup per CU: 1024 lanes keep 16 waves busy)
+  int best_t = kDirectThreads, best_b = 0, best_w = 0;
+  // (the FAITHFUL kernels, libm-heavy, are built for 256 lanes only)
+  for (int t = kDirectThreads; t <= (FAITHFUL ? kDirectThreads : kDirectMaxThreads); t *= 2) {
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, t, lds) != hipSuccess) break;
+    if (per_cu * (t / 64) > best_w) {
+      best_w = per_cu * (t / 64);
+      best_t = t;
+      best_b = per_cu;
+    }
+  }
+  if (best_w == 0) return hipErrorInvalidConfiguration;
+  *threads = best_t;
+  *blocks = (cus > 0 ? cus : 1) * best_b;  // persistent grid: every resident slot once
+  return hipSuccess;
+}
+
+template <bool UNIFORM, bool FAITHFUL, bool SINGLE, bool AXIS>
+static hipError_t launch_direct_t(const DirectLaunch& L) {
+  auto kern = trace_direct_kernel<UNIFORM, FAITHFUL, SINGLE, AXIS>;
+  const size_t lds = L.Q.hist ? (size_t)3 * L.Q.n_elem * 4 : 0;
+  hipLaunchKernelGGL(kern, dim3((unsigned)L.blocks), dim3(L.threads), lds, L.stream, L.D, L.Q);
+  return hipGetLastError();
+}
+
+template <bool SHAPE, bool UNIFORM, bool FAITHFUL>
+static hipError_t dispatch_u(const DirectLaunch& L, int* threads, int* blocks) {
+  if (L.single) {
+    if (L.axis)
+      return SHAPE ? direct_shape_t<UNIFORM, FAITHFUL, true, true>(L, threads, blocks)
+                   : launch_direct_t<UNIFORM, FAITHFUL, true, true>(L);
+    return SHAPE ? direct_shape_t<UNIFORM, FAITHFUL, true, false>(L, threads, blocks)
+                 : launch_direct_t<UNIFORM, FAITHFUL, true, false>(L);
+  }
+  return SHAPE ? direct_shape_t<UNIFORM, FAITHFUL, false, false>(L, threads, blocks)
+               : launch_direct_t<UNIFORM, FAITHFUL, false, false>(L);
+}
+
+template <bool SHAPE>
+static hipError_t dispatch(const DirectLaunch& L, int* threads, int* blocks) {
+  if (L.faithful) return L.uniform ? dispatch_u<SHAPE, true, true>(L, threads, blocks) : dispatch_u<SHAPE, false, true>(L, threads, blocks);
+  return L.uniform ? dispatch_u<SHAPE, true, false>(L, threads, blocks) : dispatch_u<SHAPE, false, false>(L, threads, blocks);
+}
+
+hipError_t direct_shape(const DirectLaunch& L, int* threads, int* blocks) { return dispatch<true>(L, threads, blocks); }
+
+hipError_t launch_direct(const DirectLaunch& L) { return dispatch<false>(L, nullptr, nullptr); }
+
+hipError_t launch_counter_reduce(const uint32_t* partial, int32_t n_blocks, int64_t len, bool is_signed,
+                                 unsigned long long* counts, hipStream_t stream) {
+  hipLaunchKernelGGL(counter_reduce_kernel, dim3((unsigned)((len + 255) / 256)), dim3(256), 0, stream, partial,
+                     n_blocks, len, is_signed ? 1 : 0, counts);
+  return hipGetLastError();
+}
+
+hipError_t launch_surface_frames(const DevDomain* D, int32_t n_surfaces, SurfGeo* out, hipStream_t stream) {
+  if (n_surfaces <= 0) return hipSuccess;
+  hipLaunchKernelGGL(surface_frames_kernel, dim3((unsigned)((n_surfaces + 255) / 256)), dim3(256), 0, stream, D,
+                     n_surfaces, out);
+  return hipGetLastError();
+}
+
+}  // namespace rthx

@@ -16,10 +16,9 @@
 
 #include "rthx_device.h"
 #include "rthx_kernels.h"
+#include "rthx_wave.h"
 
 namespace rthx {
-
-#define RTHX_LDS __attribute__((address_space(3)))
 
 // Occupancy target of the trace kernel (waves per SIMD): the register
 // allocator keeps it within 512/N VGPRs instead of hoisting loop-invariant
@@ -28,19 +27,6 @@ namespace rthx {
 #define RTHX_TRACE_WAVES_PER_EU 5
 #endif
 #define RTHX_TRACE_WAVES __attribute__((amdgpu_waves_per_eu(SINGLE ? RTHX_TRACE_WAVES_PER_EU : RTHX_TRACE_WAVES_PER_EU - 1)))
-
-// The same LDS address, hidden from the optimiser (one v_mov): loads through
-// it are not hoisted out of the ray loop.
-template <class T>
-__device__ __forceinline__ const T RTHX_LDS* lds_opaque(const T* p) {
-  const T RTHX_LDS* q = (const T RTHX_LDS*)p;
-  __asm__ volatile("" : "+v"(q));
-  return q;
-}
-
-__device__ __forceinline__ uint32_t lane_id() {
-  return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-}
 
 // Workgroup-wide compaction of one row's counts, ascending absorber order
 // (the reference's sparse() sorts columns, parallelRayTracing.jl:154).

@@ -75,6 +75,9 @@ def load(path: Optional[str] = None) -> C.CDLL:
                                     C.POINTER(abi.SolveArgs), dp, dp, C.POINTER(abi.SolveInfo)]
     lib.rthx_solve_grey_smoothed.argtypes = [C.c_void_p, dp, dp, C.POINTER(abi.SolveArgs), dp, dp,
                                              C.POINTER(abi.SolveInfo)]
+    lib.rthx_trace_direct.argtypes = [C.c_void_p, dp, dp, dp, C.POINTER(C.c_uint8), C.POINTER(abi.DirectArgs),
+                                      C.POINTER(C.c_uint64), C.POINTER(abi.DirectInfo)]
+    lib.rthx_debug_alias.argtypes = [dp, C.c_int64, C.POINTER(C.c_uint64)]
     if lib.rthx_abi_version() != abi.RTHX_ABI_VERSION:
         raise RthxError("librthx ABI version mismatch")
     _lib = lib
@@ -123,6 +126,15 @@ def make_args(bin0: int, rays_per_emitter: int, nudge: float, seed: int, emitter
         a.record_ids = C.cast(None, C.POINTER(C.c_int64))
         a.record_bin = 0
     return a, keep
+
+
+def device_domain(dom, device: int = 0) -> "DeviceDomain":
+    """The domain's cached upload on `device` (created on first use)."""
+    dd = dom._device_domains.get(device)
+    if dd is None:
+        dd = DeviceDomain(dom.flat(), device)
+        dom._device_domains[device] = dd
+    return dd
 
 
 class DeviceDomain:
@@ -210,10 +222,7 @@ class HipBackend:
               faithful: bool, record_ids=None, record_bin0: int = 0, emitter_begin: int = 0,
               emitter_end: Optional[int] = None, emitter_stride: int = 1):
         flat = dom.flat()
-        dd = dom._device_domains.get(device)
-        if dd is None:
-            dd = DeviceDomain(flat, device)
-            dom._device_domains[device] = dd
+        dd = device_domain(dom, device)
         end = flat.n_emitters if emitter_end is None else emitter_end
         flags = abi.RTHX_FLAG_FAITHFUL_SAMPLING if faithful else 0
         args, keep = make_args(bin0, rays_per_emitter, nudge, seed, emitter_begin, end, emitter_stride,

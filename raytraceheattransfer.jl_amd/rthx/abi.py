@@ -167,6 +167,42 @@ class SolveInfo(C.Structure):
         return {name: getattr(self, name) for name, _ in self._fields_}
 
 
+class DirectArgs(C.Structure):
+    """rthx_direct_args (include/rthx.h)."""
+    _fields_ = [
+        ("rays", C.c_int64),
+        ("ray_begin", C.c_int64),
+        ("ray_end", C.c_int64),
+        ("nudge", C.c_double),
+        ("seed", C.c_uint64),
+        ("bin", C.c_int32),
+        ("device", C.c_int32),
+        ("max_iters", C.c_int32),
+        ("roulette_after", C.c_int32),
+        ("roulette_kill", C.c_double),
+        ("flags", C.c_uint32),
+        ("reserved0", C.c_int32),
+    ]
+
+
+class DirectInfo(C.Structure):
+    """rthx_direct_info (include/rthx.h)."""
+    _fields_ = [
+        ("rays_traced", C.c_int64),
+        ("absorbed", C.c_int64),
+        ("escaped", C.c_int64),
+        ("rouletted", C.c_int64),
+        ("capped", C.c_int64),
+        ("events", C.c_int64),
+        ("replayed", C.c_int64),
+        ("trace_ms", C.c_double),
+        ("total_ms", C.c_double),
+    ]
+
+    def as_dict(self) -> dict:
+        return {name: getattr(self, name) for name, _ in self._fields_}
+
+
 # Every symbol include/rthx.h declares (checked by tests/test_abi_symbols.py).
 EXPORTED_SYMBOLS = (
     "rthx_abi_version",
@@ -188,6 +224,7 @@ EXPORTED_SYMBOLS = (
     "rthx_smooth_destroy",
     "rthx_solve_grey",
     "rthx_solve_grey_smoothed",
+    "rthx_trace_direct",
 )
 
 

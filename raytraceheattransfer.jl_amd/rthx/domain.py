@@ -326,6 +326,7 @@ class RayTracingDomain2D:
         self.fine_bboxes = [_bboxes(sub) for sub in self.fine_mesh]
         self.fine_grids_opt = [build_uniform_grid(sub, bb) for sub, bb in zip(self.fine_mesh, self.fine_bboxes)]
 
+        self.wavelength_band_limits = None  # DomainStructs.jl:105 (set by the user for spectral runs)
         self.F_raw = None
         self.F_smooth = None
         self.rays_per_emitter = None
@@ -362,9 +363,11 @@ class RayTracingDomain2D:
     def __call__(self, rays_tot: int, method: str = "exchange", nudge: Optional[float] = None,
                  k_dykstra=None, max_iters: int = 1000, verbose: Optional[bool] = None,
                  rec=None, seed: int = 1, device: int = 0, faithful: bool = False, smooth: bool = True):
-        """multiDispatchRayTrace2D.jl:1-18 (``method=:exchange`` only): trace
-        (F_raw) then smooth (F_smooth, exchangeRayTracing.jl:13-74) on the
-        device.  ``smooth=False`` stops after tracing (F_smooth stays None).
+        """multiDispatchRayTrace2D.jl:1-18.  ``method="exchange"``: trace (F_raw)
+        then smooth (F_smooth, exchangeRayTracing.jl:13-74) on the device;
+        ``smooth=False`` stops after tracing (F_smooth stays None).
+        ``method="direct"``: directRayTracing! (directRayTracing.jl:1-17) on
+        the device; writes powers and temperatures into the fine faces.
         """
         from .exchange import exchange_ray_tracing
         from .smoothing import smooth_exchange_factors
@@ -380,5 +383,9 @@ class RayTracingDomain2D:
                                                         verbose=verbose, device=device)
             return F_raw
         if method == "direct":
-            raise NotImplementedError("method=:direct is out of scope (SURVEY.md §8(f) f3)")
+            from .direct import direct_ray_tracing
+
+            direct_ray_tracing(self, int(rays_tot), trace_nudge, verbose, seed=seed, device=device,
+                               faithful=faithful)
+            return None
         raise ValueError(f"Unknown ray tracing method: {method}, must be :exchange or :direct")

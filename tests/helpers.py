@@ -54,7 +54,7 @@ def square_domain(ndim=11, **kw) -> RayTracingDomain2D:
     return RayTracingDomain2D([square_face(**kw)], [(ndim, ndim)])
 
 
-def wedge_domain(n_wedges=16, ndim=2, kappa=1.0, T_half=(1000.0, 0.0)):
+def wedge_domain(n_wedges=16, ndim=2, kappa=1.0, T_half=(1000.0, 0.0), sigma_s=0.0, epsilon=1.0):
     """Circle of triangle wedges around the origin (test/test_triangle_mesh.jl:1-46).
 
     Outer walls solid, spokes open; the first half of the wedges' outer walls
@@ -65,10 +65,10 @@ def wedge_domain(n_wedges=16, ndim=2, kappa=1.0, T_half=(1000.0, 0.0)):
         a0 = 2 * math.pi * k / n_wedges
         a1 = 2 * math.pi * (k + 1) / n_wedges
         verts = [(0.0, 0.0), (math.cos(a0), math.sin(a0)), (math.cos(a1), math.sin(a1))]
-        f = PolyVolume2D(verts, [False, True, False], 1, kappa, 0.0)
+        f = PolyVolume2D(verts, [False, True, False], 1, kappa, sigma_s)
         T = T_half[0] if k < n_wedges // 2 else T_half[1]
         f.T_in_w = [0.0, T, 0.0]
-        f.epsilon = [1.0, 1.0, 1.0]
+        f.epsilon = [epsilon] * 3
         f.T_in_g = -1.0
         f.q_in_g = 0.0
         faces.append(f)

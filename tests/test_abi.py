@@ -50,6 +50,38 @@ def test_struct_sizes_match_header():
     assert C.sizeof(abi.SmoothInfo) == 88
     assert C.sizeof(abi.SolveArgs) == 32
     assert C.sizeof(abi.SolveInfo) == 48
+    assert C.sizeof(abi.DirectArgs) == 72
+    assert C.sizeof(abi.DirectInfo) == 72
+
+
+_MIRRORS = [("rthx_grid_desc", abi.GridDesc), ("rthx_domain_desc", abi.DomainDesc),
+            ("rthx_trace_args", abi.TraceArgs), ("rthx_result_info", abi.ResultInfo),
+            ("rthx_smooth_args", abi.SmoothArgs), ("rthx_smooth_info", abi.SmoothInfo),
+            ("rthx_solve_args", abi.SolveArgs), ("rthx_solve_info", abi.SolveInfo),
+            ("rthx_direct_args", abi.DirectArgs), ("rthx_direct_info", abi.DirectInfo)]
+
+
+def test_struct_layouts_match_c_compiler(tmp_path):
+    """Every field offset and struct size of the ctypes mirror equals what gcc
+    computes from include/rthx.h."""
+    lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HEADER}"', "int main(void) {"]
+    for c_name, py in _MIRRORS:
+        lines.append(f'  printf("{c_name} size %zu\\n", sizeof({c_name}));')
+        for f, _ in py._fields_:
+            lines.append(f'  printf("{c_name} {f} %zu\\n", offsetof({c_name}, {f}));')
+    lines += ["  return 0;", "}"]
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c11", "-o", str(exe), str(src)], check=True)
+    got = dict()
+    for line in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.splitlines():
+        k1, k2, v = line.split()
+        got[(k1, k2)] = int(v)
+    for c_name, py in _MIRRORS:
+        assert got[(c_name, "size")] == C.sizeof(py), c_name
+        for f, _ in py._fields_:
+            assert got[(c_name, f)] == getattr(py, f).offset, (c_name, f)
 
 
 def test_validation_without_gpu(lib):
