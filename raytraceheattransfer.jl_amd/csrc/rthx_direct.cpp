@@ -201,7 +201,9 @@ RTHX_EXPORT int rthx_trace_direct(rthx_domain* dom, const double* weights, const
   Q.roulette_kill = a->roulette_kill;
   Q.hist = 3 * n * 4 <= rthx::kHistBytes ? 1 : 0;
 
-  HIP_TRY(rthx::direct_shape(L, &L.threads, &L.blocks), "direct kernel occupancy");
+  int copies = 0;
+  HIP_TRY(rthx::direct_shape(L, &L.threads, &L.blocks, &copies), "direct kernel occupancy");
+  if (Q.hist) Q.hist = copies;
   if (Q.hist) {
     HIP_TRY(Wk.partial.reserve((size_t)L.blocks * 3 * n * 4), "hipMalloc partial counters");
     Q.partial = Wk.partial.as<uint32_t>();

@@ -49,7 +49,8 @@ struct DirectParams {
   int32_t n_elem;
   int32_t max_iters;
   int32_t roulette_after;
-  int32_t hist;                   // 1: per-workgroup LDS counters (3 n_elem u32) dumped to `partial` at the end
+  int32_t hist;                   // > 0: per-workgroup LDS counters (hist copies of 3 n_elem u32), summed
+                                  // and dumped to `partial` at the end; 0: global u64 atomics
   double roulette_kill;
   uint32_t* partial;              // hist: [blocks][3 n_elem] per-workgroup counters
 };
@@ -62,8 +63,9 @@ struct DirectLaunch {
   int threads, blocks;            // from direct_shape
 };
 
-// Workgroup size and persistent grid for L (occupancy with its LDS counters).
-hipError_t direct_shape(const DirectLaunch& L, int* threads, int* blocks);
+// Workgroup size, persistent grid and LDS counter copies for L (L.Q.hist > 0:
+// LDS counters wanted), by occupancy.
+hipError_t direct_shape(const DirectLaunch& L, int* threads, int* blocks, int* copies);
 hipError_t launch_direct(const DirectLaunch& L);
 hipError_t launch_counter_reduce(const uint32_t* partial, int32_t n_blocks, int64_t len, bool is_signed,
                                  unsigned long long* counts, hipStream_t stream);

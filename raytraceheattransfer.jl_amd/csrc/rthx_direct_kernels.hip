@@ -37,7 +37,10 @@ namespace rthx {
 constexpr int kDirectThreads = 256;      // default workgroup
 constexpr int kDirectMaxThreads = 1024;  // large LDS counter arrays: one workgroup of 16 waves per CU
 constexpr uint32_t kPoolClaim = 256;  // rays per global claim (one atomic per 256 rays)
-constexpr int kDirectRefill = 16;     // refill once this many lanes of a wave are idle
+#ifndef RTHX_DIRECT_REFILL
+#define RTHX_DIRECT_REFILL 16
+#endif
+constexpr int kDirectRefill = RTHX_DIRECT_REFILL;  // refill once this many lanes of a wave are idle
 
 __device__ __forceinline__ void philox_block(uint32_t w[4], uint32_t r0, uint32_t r1, uint32_t blk, uint32_t tag,
                                              uint32_t k0, uint32_t k1) {
@@ -48,7 +51,9 @@ __device__ __forceinline__ void philox_block(uint32_t w[4], uint32_t r0, uint32_
 template <bool UNIFORM, bool FAITHFUL, bool SINGLE, bool AXIS>
 __global__ __launch_bounds__(FAITHFUL ? kDirectThreads : kDirectMaxThreads) void trace_direct_kernel(const DevDomain* __restrict__ Dp,
                                                                       DirectParams Q) {
-  extern __shared__ uint32_t hist[];  // Q.hist: [3][n_elem] per-workgroup counters
+  // Q.hist: Q.hist copies of the [3][n_elem] counters; wave v adds into copy
+  // v % Q.hist (fewer lanes contend for one LDS address on small domains)
+  extern __shared__ uint32_t hist[];
   __shared__ double s_tab[kTableDoubles];
   __shared__ SingleCoarse s_single;
   const DevDomain& D = *Dp;
@@ -56,9 +61,11 @@ __global__ __launch_bounds__(FAITHFUL ? kDirectThreads : kDirectMaxThreads) void
   const int nthr = (int)blockDim.x;
   const int n = Q.n_elem;
   const bool use_hist = Q.hist != 0;
+  const int copies = use_hist ? Q.hist : 1;
+  uint32_t* my_hist = hist + (size_t)((tid >> 6) % copies) * 3 * n;
   const bool replay = Q.replay != nullptr;
   if (use_hist)
-    for (int i = tid; i < 3 * n; i += nthr) hist[i] = 0u;
+    for (int i = tid; i < copies * 3 * n; i += nthr) hist[i] = 0u;
   if (!FAITHFUL)
     for (int i = tid; i < kTableDoubles; i += nthr) s_tab[i] = D.tables[i];
   if (SINGLE && tid == 0) {
@@ -78,7 +85,7 @@ __global__ __launch_bounds__(FAITHFUL ? kDirectThreads : kDirectMaxThreads) void
   const uint32_t sign = replay ? 0xFFFFFFFFu : 1u;
   auto add = [&](int kind, int e, uint32_t v) {
     if (use_hist)
-      atomicAdd(&hist[kind * n + e], v);
+      atomicAdd(&my_hist[kind * n + e], v);
     else
       atomicAdd(&Q.counts[(size_t)kind * n + e], (unsigned long long)(int64_t)(int32_t)v);
   };
@@ -246,23 +253,30 @@ __global__ __launch_bounds__(FAITHFUL ? kDirectThreads : kDirectMaxThreads) void
     // counter_reduce_kernel sums the slices
     __syncthreads();
     uint32_t* out = Q.partial + (size_t)blockIdx.x * 3 * n;
-    for (int i = tid; i < 3 * n; i += nthr) out[i] = hist[i];
+    for (int i = tid; i < 3 * n; i += nthr) {
+      uint32_t v = 0u;
+      for (int k = 0; k < copies; ++k) v += hist[(size_t)k * 3 * n + i];
+      out[i] = v;
+    }
   }
 }
 
 // counts[i] += sum over workgroups of partial[b][i]; the replay pass's
-// counters are negative (two's complement u32).
+// counters are negative (two's complement u32).  Grid (len/256, kReduceSlices):
+// slice y sums workgroups y, y + kReduceSlices, ... and adds its sum with one
+// u64 atomic, so short counter arrays still spread over many CUs.
+constexpr int kReduceSlices = 64;
 __global__ __launch_bounds__(256) void counter_reduce_kernel(const uint32_t* __restrict__ partial, int32_t n_blocks,
                                                              int64_t len, int32_t is_signed,
                                                              unsigned long long* __restrict__ counts) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= len) return;
   int64_t s = 0;
-  for (int b = 0; b < n_blocks; ++b) {
+  for (int b = blockIdx.y; b < n_blocks; b += gridDim.y) {
     const uint32_t v = partial[(size_t)b * len + i];
     s += is_signed ? (int64_t)(int32_t)v : (int64_t)v;
   }
-  counts[i] += (unsigned long long)s;
+  if (s != 0) atomicAdd(&counts[i], (unsigned long long)s);
 }
 
 // Wall frames of every surface (SurfGeo), from the same load_emitter the
@@ -275,71 +289,91 @@ __global__ __launch_bounds__(256) void surface_frames_kernel(const DevDomain* __
   out[s] = SurfGeo{e.tx, e.ty, e.mx, e.my};
 }
 
+// LDS counter copies for a workgroup of t lanes: one per wave while all
+// copies fit kCopyBytes, else a single copy.
+constexpr int64_t kCopyBytes = 32 * 1024;
+static int counter_copies(int t, int32_t n_elem) {
+  const int64_t one = (int64_t)3 * n_elem * 4;
+  const int64_t fit = kCopyBytes / (one > 0 ? one : 1);
+  const int64_t waves = t / 64;
+  return (int)(fit < 1 ? 1 : (fit < waves ? fit : waves));
+}
+
 template <bool UNIFORM, bool FAITHFUL, bool SINGLE, bool AXIS>
-static hipError_t direct_shape_t(const DirectLaunch& L, int* threads, int* blocks) {
+static hipError_t direct_shape_t(const DirectLaunch& L, int* threads, int* blocks, int* copies) {
   auto kern = trace_direct_kernel<UNIFORM, FAITHFUL, SINGLE, AXIS>;
-  const size_t lds = L.Q.hist ? (size_t)3 * L.Q.n_elem * 4 : 0;
-  if (lds > 64 * 1024) {
-    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
-  }
   int dev = 0, cus = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   if (e != hipSuccess) return e;
   // the workgroup size that keeps most waves resident (large LDS counter
   // arrays fit one workgroup per CU: 1024 lanes keep 16 waves busy)
-  int best_t = kDirectThreads, best_b = 0, best_w = 0;
   // (the FAITHFUL kernels, libm-heavy, are built for 256 lanes only)
+  int best_t = kDirectThreads, best_b = 0, best_w = 0, best_c = 1;
   for (int t = kDirectThreads; t <= (FAITHFUL ? kDirectThreads : kDirectMaxThreads); t *= 2) {
+    const int c = L.Q.hist ? counter_copies(t, L.Q.n_elem) : 0;
+    const size_t lds = (size_t)c * 3 * L.Q.n_elem * 4;
+    if (lds > 64 * 1024) {
+      e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      if (e != hipSuccess) return e;
+    }
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, t, lds) != hipSuccess) break;
     if (per_cu * (t / 64) > best_w) {
       best_w = per_cu * (t / 64);
       best_t = t;
       best_b = per_cu;
+      best_c = c;
     }
   }
   if (best_w == 0) return hipErrorInvalidConfiguration;
   *threads = best_t;
   *blocks = (cus > 0 ? cus : 1) * best_b;  // persistent grid: every resident slot once
+  *copies = best_c;
   return hipSuccess;
 }
 
 template <bool UNIFORM, bool FAITHFUL, bool SINGLE, bool AXIS>
 static hipError_t launch_direct_t(const DirectLaunch& L) {
   auto kern = trace_direct_kernel<UNIFORM, FAITHFUL, SINGLE, AXIS>;
-  const size_t lds = L.Q.hist ? (size_t)3 * L.Q.n_elem * 4 : 0;
+  const size_t lds = (size_t)L.Q.hist * 3 * L.Q.n_elem * 4;
+  if (lds > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
   hipLaunchKernelGGL(kern, dim3((unsigned)L.blocks), dim3(L.threads), lds, L.stream, L.D, L.Q);
   return hipGetLastError();
 }
 
 template <bool SHAPE, bool UNIFORM, bool FAITHFUL>
-static hipError_t dispatch_u(const DirectLaunch& L, int* threads, int* blocks) {
+static hipError_t dispatch_u(const DirectLaunch& L, int* t, int* b, int* c) {
   if (L.single) {
     if (L.axis)
-      return SHAPE ? direct_shape_t<UNIFORM, FAITHFUL, true, true>(L, threads, blocks)
+      return SHAPE ? direct_shape_t<UNIFORM, FAITHFUL, true, true>(L, t, b, c)
                    : launch_direct_t<UNIFORM, FAITHFUL, true, true>(L);
-    return SHAPE ? direct_shape_t<UNIFORM, FAITHFUL, true, false>(L, threads, blocks)
+    return SHAPE ? direct_shape_t<UNIFORM, FAITHFUL, true, false>(L, t, b, c)
                  : launch_direct_t<UNIFORM, FAITHFUL, true, false>(L);
   }
-  return SHAPE ? direct_shape_t<UNIFORM, FAITHFUL, false, false>(L, threads, blocks)
+  return SHAPE ? direct_shape_t<UNIFORM, FAITHFUL, false, false>(L, t, b, c)
                : launch_direct_t<UNIFORM, FAITHFUL, false, false>(L);
 }
 
 template <bool SHAPE>
-static hipError_t dispatch(const DirectLaunch& L, int* threads, int* blocks) {
-  if (L.faithful) return L.uniform ? dispatch_u<SHAPE, true, true>(L, threads, blocks) : dispatch_u<SHAPE, false, true>(L, threads, blocks);
-  return L.uniform ? dispatch_u<SHAPE, true, false>(L, threads, blocks) : dispatch_u<SHAPE, false, false>(L, threads, blocks);
+static hipError_t dispatch(const DirectLaunch& L, int* t, int* b, int* c) {
+  if (L.faithful) return L.uniform ? dispatch_u<SHAPE, true, true>(L, t, b, c) : dispatch_u<SHAPE, false, true>(L, t, b, c);
+  return L.uniform ? dispatch_u<SHAPE, true, false>(L, t, b, c) : dispatch_u<SHAPE, false, false>(L, t, b, c);
 }
 
-hipError_t direct_shape(const DirectLaunch& L, int* threads, int* blocks) { return dispatch<true>(L, threads, blocks); }
+hipError_t direct_shape(const DirectLaunch& L, int* threads, int* blocks, int* copies) {
+  return dispatch<true>(L, threads, blocks, copies);
+}
 
-hipError_t launch_direct(const DirectLaunch& L) { return dispatch<false>(L, nullptr, nullptr); }
+hipError_t launch_direct(const DirectLaunch& L) { return dispatch<false>(L, nullptr, nullptr, nullptr); }
 
 hipError_t launch_counter_reduce(const uint32_t* partial, int32_t n_blocks, int64_t len, bool is_signed,
                                  unsigned long long* counts, hipStream_t stream) {
-  hipLaunchKernelGGL(counter_reduce_kernel, dim3((unsigned)((len + 255) / 256)), dim3(256), 0, stream, partial,
+  const unsigned slices = (unsigned)(n_blocks < kReduceSlices ? n_blocks : kReduceSlices);
+  hipLaunchKernelGGL(counter_reduce_kernel, dim3((unsigned)((len + 255) / 256), slices), dim3(256), 0, stream, partial,
                      n_blocks, len, is_signed ? 1 : 0, counts);
   return hipGetLastError();
 }

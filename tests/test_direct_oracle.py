@@ -176,3 +176,33 @@ def test_exchange_vs_direct_temperatures(kw):
     Tg = np.array([f.T_g for f in dd.fine_mesh[0]])
     rel = np.abs(Tg0 - Tg) / np.maximum(Tg0, 1.0)
     assert np.all(rel < 0.05), rel.max()
+
+
+def _spectral_square(n_bins=10, nd=5, kappa=1.0):
+    """createSpectralUniformMesh (test/test_2d_spectral.jl:31-82)."""
+    face = H.square_face(kappa=np.full(n_bins, kappa), sigma_s=np.zeros(n_bins), n_bins=n_bins,
+                         epsilon=np.ones(n_bins))
+    face.T_in_w = [1000.0, 0.0, 0.0, 0.0]
+    dom = H.RayTracingDomain2D([face], [(nd, nd)])
+    dom.wavelength_band_limits = 10 ** np.linspace(np.log10(1e-8), np.log10(0.1), n_bins + 1)
+    return dom
+
+
+def test_spectral_uniform_direct_matches_grey():
+    """Grey vs spectral-uniform (test/test_2d_spectral.jl:143-190, 5 %) for the
+    direct method: band fractions weight the emitters per bin, every bin is
+    traced, and the temperatures come from the summed band powers."""
+    dom = _spectral_square()
+    assert dom.spectral_mode == "spectral_uniform"
+    infos = DR.direct_ray_tracing(dom, 300_000, H.NUDGE, seed=6, backend=BACKEND)
+    # bins without emission at 1000 K (the shortest bands) are skipped, as the
+    # reference does (directRayTracing.jl:24-27)
+    traced = {i["bin"] for i in infos}
+    assert traced == {b for b in range(1, 11) if DR.prepare_emitters(dom, b)[1] > 0} and 5 in traced
+    grey = H.square_domain(5)
+    DR.direct_ray_tracing(grey, 1_000_000, H.NUDGE, seed=7, backend=BACKEND)
+    Ts = np.array([f.T_g for f in dom.fine_mesh[0]])
+    Tg = np.array([f.T_g for f in grey.fine_mesh[0]])
+    assert np.all(np.abs(Ts - Tg) / np.maximum(Tg, 1.0) < 0.05)
+    f = dom.fine_mesh[0][0]
+    assert len(f.e_g) == 10 and np.sum(f.e_g) > 0

@@ -59,3 +59,35 @@ def test_two_rank_gather_equals_single_process(tmp_path):
     assert np.array_equal(m["row_ptr"], rp)
     assert np.array_equal(m["cols"], cols)
     assert np.array_equal(m["counts"], cnt)
+
+
+def _direct_worker(rank, world, port, out_path):
+    """method=:direct sharded by ray range; the per-element counts are summed
+    with an all-reduce (rthx.direct, distributed=True)."""
+    sys.path[:0] = [H.PKG, H.ROOT, os.path.join(H.ROOT, "tests")]
+    import torch.distributed as dist
+
+    from oracle import oracle
+    from rthx import direct as DR
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    dom = H.square_domain(5, kappa=0.5, sigma_s=0.5, epsilon=0.7)
+    counts, total, info = DR.direct_ray_tracing_single_bin(dom, 30_001, H.NUDGE, 1, seed=5,
+                                                           backend=oracle.OracleBackend(2), distributed=True)
+    assert info["rays_traced"] == DR.ray_shard(rank, world, 30_001)[1] - DR.ray_shard(rank, world, 30_001)[0]
+    if rank == 0:
+        np.save(out_path, counts)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_direct_allreduce_equals_single_process(tmp_path):
+    out = str(tmp_path / "direct.npy")
+    mp.spawn(_direct_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    from oracle import oracle
+    from rthx import direct as DR
+
+    dom = H.square_domain(5, kappa=0.5, sigma_s=0.5, epsilon=0.7)
+    counts, _total, _info = DR.direct_ray_tracing_single_bin(dom, 30_001, H.NUDGE, 1, seed=5,
+                                                             backend=oracle.OracleBackend(4))
+    assert np.array_equal(np.load(out), counts)

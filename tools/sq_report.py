@@ -1,10 +1,14 @@
-"""Per-ray view of the trace kernel's SQ counters (tools/gpu_sq.sh output)."""
+"""Per-ray view of a trace kernel's SQ counters (tools/gpu_sq.sh output).
+
+  python tools/sq_report.py sq.json RAYS [KERNEL_SUBSTRING]
+"""
 import json
 import sys
 
 d = json.load(open(sys.argv[1]))
 rays = float(sys.argv[2])
-k = next(x for x in d if "trace_exchange_kernel" in x)
+name = sys.argv[3] if len(sys.argv) > 3 else "trace_exchange_kernel"
+k = next(x for x in d if name in x)
 c = {n: v["mean"] for n, v in d[k].items()}
 wr = rays / 64.0  # wave-rays
 print("kernel", k)
