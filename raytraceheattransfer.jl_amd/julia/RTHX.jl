@@ -125,6 +125,33 @@ struct SmoothInfo
     ms_total::Float64
 end
 
+struct DirectArgs
+    rays::Int64
+    ray_begin::Int64
+    ray_end::Int64
+    nudge::Float64
+    seed::UInt64
+    bin::Int32
+    device::Int32
+    max_iters::Int32
+    roulette_after::Int32
+    roulette_kill::Float64
+    flags::UInt32
+    reserved0::Int32
+end
+
+struct DirectInfo
+    rays_traced::Int64
+    absorbed::Int64
+    escaped::Int64
+    rouletted::Int64
+    capped::Int64
+    events::Int64
+    replayed::Int64
+    trace_ms::Float64
+    total_ms::Float64
+end
+
 function check(rc::Integer)
     if rc != 0
         msg = unsafe_string(ccall((:rthx_last_error, LIB[]), Cstring, ()))
@@ -323,12 +350,77 @@ function smooth_F(F_raw::AbstractMatrix, w::AbstractVector, num_surfaces::Intege
 end
 
 """
+    directRayTracingSingleBin!(rtm, rays_tot, nudge, spectral_bin)
+
+Drop-in for directRayTracing.jl:19-152: the reference's prepareEmitters gives
+the energies; the ray loop (:69-128, traceSingleRay) is one
+`rthx_trace_direct` call; the counts go back into the reference's nested
+counter arrays and through its own updateSpectralResults! (:148-151).
+"""
+function directRayTracingSingleBin!(rtm, rays_tot::Integer, nudge, spectral_bin::Integer)
+    RTHT = parentmodule(@__MODULE__).RayTraceHeatTransfer
+    emitters, total_energy = RTHT.prepareEmitters(rtm, nudge, spectral_bin)
+    if total_energy == 0.0
+        @warn "No emitters found for spectral bin $spectral_bin, skipping ray tracing"
+        return
+    end
+    Ns = length(rtm.surface_mapping)
+    n = Ns + length(rtm.volume_mapping)
+    w = zeros(Float64, n); eps = zeros(Float64, max(Ns, 1)); omega = zeros(Float64, n - Ns); reemit = zeros(UInt8, n)
+    for e in emitters  # energies in global element order (getGlobalIndex2D.jl:1-15)
+        g = e.type == :surface ? rtm.surface_mapping[(e.coarse_index, e.fine_index, e.wall_index)] :
+                                 Ns + rtm.volume_mapping[(e.coarse_index, e.fine_index)]
+        w[g] = e.energy
+    end
+    pick(v, b) = v isa AbstractVector ? v[b] : v
+    for ((c, f, k), s) in rtm.surface_mapping
+        face = rtm.fine_mesh[c][f]
+        eps[s] = pick(face.epsilon[k], spectral_bin)
+        reemit[s] = face.T_in_w[k] < 0.0
+    end
+    for ((c, f), v) in rtm.volume_mapping
+        face = rtm.fine_mesh[c][f]
+        kap = pick(face.kappa_g, spectral_bin); sig = pick(face.sigma_s_g, spectral_bin)
+        omega[v] = kap + sig != 0 ? sig / (kap + sig) : 0.0
+        reemit[Ns + v] = face.T_in_g < 0.0
+    end
+    args = Ref(DirectArgs(Int64(rays_tot), 0, Int64(rays_tot), Float64(nudge), SEED[], Int32(spectral_bin - 1),
+                          DEVICE[], Int32(100_000), Int32(1000), 0.8,
+                          FAITHFUL[] ? RTHX_FLAG_FAITHFUL_SAMPLING : UInt32(0), Int32(0)))
+    counts = zeros(UInt64, 3n)
+    info = Ref{DirectInfo}()
+    check(ccall((:rthx_trace_direct, LIB[]), Cint,
+                (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{UInt8}, Ptr{DirectArgs}, Ptr{UInt64},
+                 Ptr{DirectInfo}),
+                device_domain(rtm), w, eps, omega, reemit, args, counts, info))
+    # back into the reference's counters (directRayTracing.jl:29-34)
+    cm = rtm.coarse_mesh
+    absorbed = [zeros(Int, length(cf.subVolumes)) for cf in cm]
+    gas_emitted = [zeros(Int, length(cf.subVolumes)) for cf in cm]
+    scattered = [zeros(Int, length(cf.subVolumes)) for cf in cm]
+    wall_emitted = [[zeros(Int, length(f.solidWalls)) for f in cf.subVolumes] for cf in cm]
+    reflected = [[zeros(Int, length(f.solidWalls)) for f in cf.subVolumes] for cf in cm]
+    wall_absorbed = [[zeros(Int, length(f.solidWalls)) for f in cf.subVolumes] for cf in cm]
+    for ((c, f, k), s) in rtm.surface_mapping
+        wall_emitted[c][f][k] = counts[s]; wall_absorbed[c][f][k] = counts[n + s]; reflected[c][f][k] = counts[2n + s]
+    end
+    for ((c, f), v) in rtm.volume_mapping
+        g = Ns + v
+        gas_emitted[c][f] = counts[g]; absorbed[c][f] = counts[n + g]; scattered[c][f] = counts[2n + g]
+    end
+    RTHT.updateSpectralResults!(rtm, absorbed, gas_emitted, wall_emitted, reflected, scattered, wall_absorbed,
+                                total_energy, rays_tot, spectral_bin)
+    return nothing
+end
+
+"""
     enable!(; lib, device=0, seed=1, faithful=false)
 
-Redirect RayTraceHeatTransfer's `computeExchangeFactorsBin` to the GPU.
+Redirect RayTraceHeatTransfer's `computeExchangeFactorsBin` (and, with
+`direct = true`, `directRayTracingSingleBin!`) to the GPU.
 """
 function enable!(; lib::AbstractString, device::Integer = 0, seed::Integer = 1, faithful::Bool = false,
-                 smoothing::Bool = false)
+                 smoothing::Bool = false, direct::Bool = true)
     LIB[] = lib
     DEVICE[] = Int32(device)
     SEED[] = UInt64(seed)
@@ -343,6 +435,12 @@ function enable!(; lib::AbstractString, device::Integer = 0, seed::Integer = 1, 
         return $(RTHX).computeExchangeFactorsBin(rtm, rays_per_emitter, nudge, spectral_bin, surface_mapping,
                                                  volume_mapping, num_surfaces, num_volumes, num_emitters,
                                                  verbose, rec)
+    end
+    if direct  # method=:direct on the device as well
+        @eval RTHT function directRayTracingSingleBin!(rtm::RayTracingDomain2D, rays_tot::P, nudge::G,
+                                                      spectral_bin::P) where {G, P<:Integer}
+            return $(RTHX).directRayTracingSingleBin!(rtm, rays_tot, nudge, spectral_bin)
+        end
     end
     if smoothing  # optional: smooth_F on the device as well
         @eval RTHT function smooth_F(F_raw::AbstractMatrix, w::AbstractVector, num_surfaces::Int; kw...)
