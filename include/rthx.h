@@ -339,6 +339,32 @@ int rthx_trace_direct(rthx_domain* dom, const double* weights, const double* eps
                       const uint8_t* reemit, const rthx_direct_args* args, uint64_t* counts,
                       rthx_direct_info* info);
 
+/* ------------------------------------------------------------------------
+ * 3D analytic view factors: the matrix of
+ * enclosureViewFactors3D (src/RayTracing/ViewFactor3D/enclosureViewFactors3D.jl:1-94)
+ * for a surface enclosure of planar polygons, each pair by the closed form of
+ * viewFactor3D (viewFactor3D.jl:33-196, Narayanaswamy, IJHMT 91 (2015)
+ * 841-847).  xyz[n][4][3] holds the vertices (a triangle ignores slot 3),
+ * nv[n] = 3 or 4.  F_out[n*n] (row-major, F[a][b] = view factor from a to b,
+ * F[a][a] = 0, NaN -> 0 as :42) may be NULL to compute only area_out[n]
+ * (the reference's area formulas, :47-76).  Polygons must be coplanar within
+ * the reference's 10 eps (:60-63).
+ * ------------------------------------------------------------------------ */
+typedef struct rthx_vf3d_args {
+  int32_t device;
+  int32_t reserved0;
+} rthx_vf3d_args;
+
+typedef struct rthx_vf3d_info {
+  int64_t n;
+  int64_t pairs;       /* ordered pairs evaluated: n (n - 1) */
+  double kernel_ms;    /* device time of the view-factor launches */
+  double total_ms;
+} rthx_vf3d_info;
+
+int rthx_view_factors_3d(const double* xyz, const int32_t* nv, int64_t n, const rthx_vf3d_args* args,
+                         double* F_out, double* area_out, rthx_vf3d_info* info);
+
 #ifdef __cplusplus
 }
 #endif

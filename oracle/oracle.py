@@ -58,6 +58,7 @@ def load() -> C.CDLL:
     lib.oracle_trace_direct.argtypes = [C.POINTER(abi.DomainDesc), dp, dp, dp, C.POINTER(C.c_uint8),
                                         C.POINTER(abi.DirectArgs), C.c_int, C.POINTER(C.c_uint64),
                                         C.POINTER(abi.DirectInfo)]
+    lib.oracle_view_factors_3d.argtypes = [dp, C.POINTER(C.c_int32), C.c_int64, C.c_int, dp, dp]
     lib.oracle_last_error.restype = C.c_char_p
     _lib = lib
     return lib
@@ -150,6 +151,19 @@ def trace_direct(flat, weights, eps, omega, reemit, args, nthreads: int = 0):
     if rc != 0:
         raise RuntimeError(f"oracle error {rc}: {lib.oracle_last_error().decode()}")
     return counts.reshape(3, n), inf.as_dict()
+
+
+def view_factors_3d(xyz, nv, nthreads: int = 0, with_F: bool = True):
+    """viewFactor3D for all ordered pairs (CPU restatement): (F[n, n], area[n])."""
+    x = np.ascontiguousarray(xyz, dtype=np.float64).reshape(-1, 12)
+    k = np.ascontiguousarray(nv, dtype=np.int32)
+    n = len(k)
+    F = np.zeros((n, n)) if with_F else None
+    area = np.zeros(n)
+    rc = load().oracle_view_factors_3d(abi.ptr(x, C.c_double), abi.ptr(k, C.c_int32), n, nthreads,
+                                       abi.ptr(F, C.c_double) if with_F else None, abi.ptr(area, C.c_double))
+    assert rc == 0
+    return F, area
 
 
 class OracleBackend:

@@ -1104,3 +1104,200 @@ ORACLE_API int oracle_trace_direct(const rthx_domain_desc* d, const double* weig
   if (err) { snprintf(g_err, sizeof g_err, "out of host memory"); return RTHX_ENOMEM; }
   return RTHX_OK;
 }
+
+/* ======================================================================== */
+/* 3D analytic view factors: viewFactor3D               */
+/* (src/RayTracing/ViewFactor3D/viewFactor3D.jl:33-196, Narayanaswamy 2015) */
+/* for every ordered pair of polygons, as enclosureViewFactors3D           */
+/* (enclosureViewFactors3D.jl:12-50) does.  Restated from the paper's      */
+/* equations as the reference evaluates them; pinned by the reference's    */
+/* Narayanaswamy examples and EES cube table (test/test_3d_viewfactors.jl, */
+/* tests/test_vf3d_oracle.py).                                              */
+/* ======================================================================== */
+#define VF_PI 3.141592653589793
+#define VF_TWO_PI 6.283185307179586
+#define VF_ALMOST_ZERO 2.220446049250313e-15 /* 10 eps(Float64), viewFactor3D.jl:37 */
+#define VF_HALF_TOL 2.220446049250313e-14    /* 10 almostZero, :38 */
+
+typedef struct {
+  double x, y, z;
+} vf_v3;
+
+static vf_v3 v3_add(vf_v3 a, vf_v3 b) { vf_v3 r = {a.x + b.x, a.y + b.y, a.z + b.z}; return r; }
+static vf_v3 v3_sub(vf_v3 a, vf_v3 b) { vf_v3 r = {a.x - b.x, a.y - b.y, a.z - b.z}; return r; }
+static vf_v3 v3_mul(vf_v3 a, double s) { vf_v3 r = {a.x * s, a.y * s, a.z * s}; return r; }
+static vf_v3 v3_div(vf_v3 a, double s) { vf_v3 r = {a.x / s, a.y / s, a.z / s}; return r; }
+static double v3_dot(vf_v3 a, vf_v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+static double v3_norm(vf_v3 a) { return sqrt(v3_dot(a, a)); }
+static vf_v3 v3_cross(vf_v3 a, vf_v3 b) {
+  vf_v3 r = {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+  return r;
+}
+
+/* Cl3D.jl:7-26, Eq. (26): Chebyshev fit of the Clausen integral. */
+static double vf_clausen(double theta) {
+  double r = fmod(theta, VF_TWO_PI); /* Julia mod: result takes the sign of 2 pi */
+  if (r == 0.0) r = 0.0;
+  else if (r < 0.0) r += VF_TWO_PI;
+  theta = r;
+  double x = theta / VF_PI - 1.0;
+  double x2 = x * x, x3 = x2 * x, x5 = x3 * x2, x7 = x5 * x2, x9 = x7 * x2, x11 = x9 * x2, x13 = x11 * x2;
+  double T[7] = {x,
+                 4 * x3 - 3 * x,
+                 16 * x5 - 20 * x3 + 5 * x,
+                 64 * x7 - 112 * x5 + 56 * x3 - 7 * x,
+                 256 * x9 - 576 * x7 + 432 * x5 - 120 * x3 + 9 * x,
+                 1024 * x11 - 2816 * x9 + 2816 * x7 - 1232 * x5 + 220 * x3 - 11 * x,
+                 4096 * x13 - 13312 * x11 + 16640 * x9 - 9984 * x7 + 2912 * x5 - 364 * x3 + 13 * x};
+  static const double b[7] = {1.865555351433979e-1, 6.269948963579612e-2, 3.139559104552675e-4,
+                              3.916780537368088e-6, 6.499672439854756e-8, 1.238143696612060e-9,
+                              5.586505893753557e-13};
+  double cheb = 0.0;
+  for (int k = 0; k < 7; ++k) cheb += b[k] * T[k];
+  return (theta - VF_PI) * (2.0 + log(VF_PI * VF_PI / 2.0)) +
+         (VF_TWO_PI - theta) * log((VF_TWO_PI - theta) * (1.0 - VF_ALMOST_ZERO) + VF_ALMOST_ZERO) -
+         theta * log(theta * (1.0 - VF_ALMOST_ZERO) + VF_ALMOST_ZERO) + cheb;
+}
+
+/* imagLi2_3D.jl:7-17, Eq. (24). */
+static double vf_imag_li2(double mag, double angle) {
+  if (mag > VF_ALMOST_ZERO) {
+    double omega = atan2(mag * sin(angle), 1.0 - mag * cos(angle));
+    return 0.5 * vf_clausen(2.0 * angle) + 0.5 * vf_clausen(2.0 * omega) -
+           0.5 * vf_clausen(2.0 * omega + 2.0 * angle) + log(mag) * omega;
+  }
+  return mag * sin(angle);
+}
+
+/* f3D.jl:9-34, Eq. (22b). */
+static double vf_f(double s, double l, double alpha, double ca, double sa, double d) {
+  double s2 = s * s, l2 = l * l, d2 = d * d, sa2 = sa * sa;
+  double wsqrt = sqrt(s2 + d2 / sa2), psqrt = sqrt(l2 + d2 / sa2);
+  double wdim = fabs(s + wsqrt) > 0 ? s + wsqrt : VF_ALMOST_ZERO;
+  double pdim = fabs(l + psqrt) > 0 ? l + psqrt : VF_ALMOST_ZERO;
+  return (0.5 * ca * (s2 + l2) - s * l) * log(s2 + l2 - 2 * s * l * ca + d2) +
+         s * sa * wsqrt * atan2(sqrt(s2 * sa2 + d2), l - s * ca) +
+         l * sa * psqrt * atan2(sqrt(l2 * sa2 + d2), s - l * ca) + s * l +
+         0.5 * (d2 / sa) *
+             (vf_imag_li2(wdim / pdim, alpha) + vf_imag_li2(pdim / wdim, alpha) -
+              2 * vf_imag_li2((wdim - 2 * s) / pdim, VF_PI - alpha));
+}
+
+/* fparallel3D.jl:8-24, Eq. (23). */
+static double vf_f_parallel(double s, double l, double d) {
+  if (d == 0) d = VF_ALMOST_ZERO;
+  double sl = s - l, sl2 = sl * sl, s2 = s * s, l2 = l * l, d2 = d * d;
+  double term = sl / sqrt(s2 + l2 - 2 * s * l + d2 + VF_ALMOST_ZERO);
+  term = term >= 0.999999 ? 0.999999 : term <= -0.999999 ? -0.999999 : term;
+  return 0.5 * (sl2 - d2) * log(sl2 + d2) - 2 * sl * d * acos(term) + s * l;
+}
+
+/* One edge pair: edgePairParameters3D.jl:8-70 and viewFactor3D.jl:139-185. */
+static double vf_edge_pair(vf_v3 ri, vf_v3 rj, vf_v3 rp, vf_v3 rq) {
+  vf_v3 nudge = {VF_ALMOST_ZERO, VF_ALMOST_ZERO, VF_ALMOST_ZERO};
+  if (v3_norm(v3_sub(ri, rp)) < VF_HALF_TOL || v3_norm(v3_sub(rj, rp)) < VF_HALF_TOL) rp = v3_add(rp, nudge);
+  else if (v3_norm(v3_sub(ri, rq)) < VF_HALF_TOL || v3_norm(v3_sub(rj, rq)) < VF_HALF_TOL) rq = v3_add(rq, nudge);
+  vf_v3 u = v3_sub(rj, ri), v = v3_sub(rq, rp), w = v3_sub(ri, rp);
+  u = v3_div(u, v3_norm(u));
+  v = v3_div(v, v3_norm(v));
+  double b = v3_dot(u, v), d = v3_dot(u, w), e = v3_dot(v, w);
+  double den = 1.0 - b * b;
+  int skew = den > VF_ALMOST_ZERO;
+  double s, l, D;
+  if (skew) {
+    s = (b * e - d) / den;
+    l = (e - b * d) / den;
+    D = v3_norm(v3_sub(v3_add(w, v3_mul(u, s)), v3_mul(v, l)));
+  } else {
+    s = 0.0;
+    l = e;
+    D = v3_norm(v3_sub(w, v3_mul(v, e)));
+  }
+  vf_v3 sO = v3_add(ri, v3_mul(u, s)), lO = v3_add(rp, v3_mul(v, l));
+  double s_end = v3_norm(v3_sub(rj, sO)), l_end = v3_norm(v3_sub(rq, lO));
+  vf_v3 sHat = fabs(s) < s_end ? v3_div(v3_sub(rj, sO), v3_norm(v3_sub(rj, sO)))
+                               : v3_div(v3_sub(ri, sO), v3_norm(v3_sub(ri, sO)));
+  vf_v3 lHat = fabs(l) < l_end ? v3_div(v3_sub(rq, lO), v3_norm(v3_sub(rq, lO)))
+                               : v3_div(v3_sub(rp, lO), v3_norm(v3_sub(rp, lO)));
+  if (!skew) lHat = sHat;
+  double si = v3_dot(v3_sub(ri, sO), sHat), sj = v3_dot(v3_sub(rj, sO), sHat);
+  double lp = v3_dot(v3_sub(rp, lO), lHat), lq = v3_dot(v3_sub(rq, lO), lHat);
+  if (skew) {
+    double c = v3_dot(sHat, lHat);
+    double ca = c > 0.999 ? 0.999 : c < -0.999 ? -0.999 : c;
+    double alpha = acos(ca), sa = sin(alpha);
+    return ca * (vf_f(sj, lq, alpha, ca, sa, D) - vf_f(si, lq, alpha, ca, sa, D) -
+                 vf_f(sj, lp, alpha, ca, sa, D) + vf_f(si, lp, alpha, ca, sa, D));
+  }
+  return v3_dot(sHat, lHat) * (vf_f_parallel(sj, lq, D) - vf_f_parallel(si, lq, D) -
+                               vf_f_parallel(sj, lp, D) + vf_f_parallel(si, lp, D));
+}
+
+static vf_v3 vf_vertex(const double* p, int k) { vf_v3 r = {p[3 * k], p[3 * k + 1], p[3 * k + 2]}; return r; }
+
+/* viewFactor3D.jl:47-76: polygon area (triangle: |n|/2; quad: |(P3-P1) x (P4-P2)|/2). */
+static double vf_area(const double* p, int n) {
+  vf_v3 P1 = vf_vertex(p, 0), P2 = vf_vertex(p, 1), P3 = vf_vertex(p, 2);
+  if (n == 3) return v3_norm(v3_cross(v3_sub(P2, P1), v3_sub(P3, P1))) / 2;
+  vf_v3 P4 = vf_vertex(p, 3);
+  return v3_norm(v3_cross(v3_sub(P3, P1), v3_sub(P4, P2))) / 2;
+}
+
+/* A_a F_ab: |sum of edge-pair terms| / 4 pi (viewFactor3D.jl:187-190). */
+static double vf_conductance(const double* A, int na, const double* B, int nb) {
+  double sum = 0.0;
+  for (int p = 0; p < nb; ++p)
+    for (int i = 0; i < na; ++i)
+      sum += vf_edge_pair(vf_vertex(A, i), vf_vertex(A, (i + 1) % na), vf_vertex(B, p), vf_vertex(B, (p + 1) % nb));
+  return fabs(sum) / (4.0 * VF_PI);
+}
+
+typedef struct {
+  const double* xyz;
+  const int32_t* nv;
+  const double* area;
+  int64_t n, r0, r1;
+  double* F;
+} vf_worker_t;
+
+static void* vf_worker(void* arg) {
+  vf_worker_t* W = (vf_worker_t*)arg;
+  for (int64_t a = W->r0; a < W->r1; ++a)
+    for (int64_t b = 0; b < W->n; ++b) {
+      double v = 0.0;
+      if (a != b) {
+        v = vf_conductance(W->xyz + 12 * a, W->nv[a], W->xyz + 12 * b, W->nv[b]) / W->area[a];
+        if (v != v) v = 0.0; /* enclosureViewFactors3D.jl:42 */
+      }
+      W->F[a * W->n + b] = v;
+    }
+  return NULL;
+}
+
+/* F[n*n] row-major and area[n] (either may be NULL); rows over threads. */
+ORACLE_API int oracle_view_factors_3d(const double* xyz, const int32_t* nv, int64_t n, int nthreads, double* F,
+                                      double* area_out) {
+  if (!xyz || !nv || n < 1) return RTHX_EINVAL;
+  double* area = (double*)malloc(sizeof(double) * (size_t)n);
+  for (int64_t k = 0; k < n; ++k) area[k] = vf_area(xyz + 12 * k, nv[k]);
+  if (area_out) memcpy(area_out, area, sizeof(double) * (size_t)n);
+  if (F) {
+    if (nthreads <= 0) nthreads = (int)sysconf(_SC_NPROCESSORS_ONLN);
+    if (nthreads > n) nthreads = (int)n;
+    vf_worker_t* W = (vf_worker_t*)calloc((size_t)nthreads, sizeof(vf_worker_t));
+    pthread_t* th = (pthread_t*)calloc((size_t)nthreads, sizeof(pthread_t));
+    int64_t per = n / nthreads, rem = n % nthreads, start = 0;
+    for (int t = 0; t < nthreads; ++t) {
+      int64_t sz = per + (t < rem ? 1 : 0);
+      W[t].xyz = xyz; W[t].nv = nv; W[t].area = area; W[t].n = n; W[t].F = F;
+      W[t].r0 = start; W[t].r1 = start + sz;
+      start += sz;
+    }
+    for (int t = 1; t < nthreads; ++t) pthread_create(&th[t], NULL, vf_worker, &W[t]);
+    vf_worker(&W[0]);
+    for (int t = 1; t < nthreads; ++t) pthread_join(th[t], NULL);
+    free(W); free(th);
+  }
+  free(area);
+  return RTHX_OK;
+}

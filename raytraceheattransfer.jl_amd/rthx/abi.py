@@ -203,6 +203,19 @@ class DirectInfo(C.Structure):
         return {name: getattr(self, name) for name, _ in self._fields_}
 
 
+class Vf3dArgs(C.Structure):
+    """rthx_vf3d_args (include/rthx.h)."""
+    _fields_ = [("device", C.c_int32), ("reserved0", C.c_int32)]
+
+
+class Vf3dInfo(C.Structure):
+    """rthx_vf3d_info (include/rthx.h)."""
+    _fields_ = [("n", C.c_int64), ("pairs", C.c_int64), ("kernel_ms", C.c_double), ("total_ms", C.c_double)]
+
+    def as_dict(self) -> dict:
+        return {name: getattr(self, name) for name, _ in self._fields_}
+
+
 # Every symbol include/rthx.h declares (checked by tests/test_abi_symbols.py).
 EXPORTED_SYMBOLS = (
     "rthx_abi_version",
@@ -225,6 +238,7 @@ EXPORTED_SYMBOLS = (
     "rthx_solve_grey",
     "rthx_solve_grey_smoothed",
     "rthx_trace_direct",
+    "rthx_view_factors_3d",
 )
 
 

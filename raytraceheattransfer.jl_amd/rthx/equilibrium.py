@@ -190,9 +190,60 @@ def _write_results(dom, T, j, Abs, r):
 
 
 def solve_equilibrium(dom, F=None, device: int = 0, verbose: bool = False):
-    """solveEquilibrium! (solveEquilibrium.jl:1-26) for grey 2D domains; F
-    defaults to dom.F_smooth.  Spectral modes (equilibriumSpectral2D!) are not
-    part of this package."""
+    """solveEquilibrium! (solveEquilibrium.jl:1-26) for grey 2D domains and grey
+    3D surface enclosures; F defaults to dom.F_smooth.  Spectral modes
+    (equilibriumSpectral2D!, equilibriumSurfacesSpectral3D!) are not part of
+    this package."""
+    from .domain3d import ViewFactorDomain3D
+
     if dom.spectral_mode != "grey":
-        raise NotImplementedError("spectral GERT solve (equilibriumSpectral2D!) is out of scope")
+        raise NotImplementedError("spectral GERT solves (equilibriumSpectral2D!, ...Spectral3D!) are out of scope")
+    if isinstance(dom, ViewFactorDomain3D):  # solveEquilibrium.jl:13-22
+        return equilibrium_surfaces_grey_3d(dom, dom.F_smooth if F is None else F, device=device, verbose=verbose)
     return equilibrium_grey(dom, dom.F_smooth if F is None else F, device=device, verbose=verbose)
+
+
+def equilibrium_surfaces_grey_3d(domain, F, spectral_bin: int = 1, device: int = 0, verbose: bool = False,
+                                 info: Optional[dict] = None):
+    """equilibriumSurfacesGrey3D! (equilibriumSurfacesGrey3D.jl:40-132) with
+    populateWorkspace!(::SurfaceOnlyWorkspace, ::ViewFactorDomain3D)
+    (WorkspaceStructs.jl:120-141) and writeResultsToDomainGrey3D!
+    (writeResultsToDomain3D.jl:54-83).  The system (I - diag(coeff) F') j = h
+    runs on the device (rthx_solve_grey; the reference's dense `\\` is met
+    within the solver tolerance).  Returns (T, j, Abs, r)."""
+    subs = domain.subfaces()
+    n = len(subs)
+    b = spectral_bin - 1
+    area = np.array([s.area for s in subs])
+    eps = np.array([float(np.atleast_1d(s.epsilon)[min(b, np.size(s.epsilon) - 1)]) for s in subs])
+    Tw = np.array([s.T_in_w for s in subs])
+    qw = np.array([s.q_in_w for s in subs])
+    Q_known = (Tw < 0.0).astype(int)
+    E = np.where(Q_known == 0, eps * STEFAN_BOLTZMANN * area * Tw ** 4, 0.0)  # computeEmissivePowers! (:3-16)
+    h = np.where(Q_known == 1, qw, E)
+    coeff = np.where(Q_known == 1, 1.0, 1.0 - eps)
+    solve_info = {} if info is None else info
+    j, g = _solve(np.asarray(F)[:n, :n], coeff, h, device, solve_info)
+    if verbose:
+        print(f"GMRES: {solve_info['iterations']} iterations, residual {solve_info['residual']:.3e}")
+    Bv = 1.0 - eps  # getValueB(::SurfaceOnlyWorkspace) (WorkspaceStructs.jl:173-175)
+    Abs = (1.0 - Bv) * g
+    r = Bv * g
+    T = np.zeros(n)
+    for i in range(n):  # computeTemperatures! (:18-34)
+        e = max(j[i] - r[i], 0.0)
+        T[i] = (e / (eps[i] * STEFAN_BOLTZMANN * area[i])) ** 0.25 if eps[i] > 0.0 and area[i] > 0.0 else 0.0
+    T = np.nan_to_num(T, nan=0.0)
+    for i, s in enumerate(subs):  # writeResultsToDomainGrey3D!
+        e = max(j[i] - r[i], 0.0)
+        s.j_w, s.g_a_w, s.e_w, s.r_w = j[i], Abs[i], e, r[i]
+        s.g_w = Abs[i] + r[i]
+        s.i_w = j[i] / (math.pi * s.area)
+        if s.T_in_w < -0.1:
+            s.q_w = s.q_in_w
+            s.T_w = T[i]
+        else:
+            s.T_w = s.T_in_w
+            s.q_w = e - Abs[i]
+    domain.energy_error = float(np.sum(j - r - Abs))
+    return T, j, Abs, r

@@ -14,6 +14,12 @@ test files (parsed from /root/reference/test when it is present):
 oracle_c1_seed1.npz — CPU-restatement absorber counts for README Ex.1
 (11x11, kappa=1, 1e6 rays, seed 1): a regression fixture that the HIP path
 must reproduce exactly.
+
+reference_3d.json (`python tests/golden/make_golden.py 3d`) — the 3D view
+factor known answers of test/test_3d_viewfactors.jl (Narayanaswamy 2015
+examples :31-75 and the EES unit-cube table :101-143, tolerance VF_TOLERANCE
+:22, rotations :194-213) and the cube enclosure / tolerances of
+test/test_3d_heat_transfer.jl:22-23,29-205.
 """
 import json
 import math
@@ -92,5 +98,44 @@ def main():
     print("wrote fixtures; C1 nnz", info["nnz"])
 
 
+def parse_julia_matrix(body):
+    rows = [r.strip() for r in body.replace("\n", " ").split(";") if r.strip()]
+    return [[float(x) for x in r.split()] for r in rows]
+
+
+def main_3d():
+    ref = "/root/reference/test/test_3d_viewfactors.jl"
+    txt = open(ref).read()
+    cases = []
+    for m in re.finditer(r'name = "([^"]+)",\s*poly_A = \[(.*?)\],\s*poly_B = \[(.*?)\],\s*F_ref = ([0-9.eE+-]+)',
+                         txt, re.S):
+        cases.append({"name": m.group(1), "poly_A": parse_julia_matrix(m.group(2)),
+                      "poly_B": parse_julia_matrix(m.group(3)), "F_ref": float(m.group(4))})
+    ees = re.search(r"F_EES = \[(.*?)\]", txt, re.S).group(1)
+    points = re.search(r"points = \[(.*?)\]", txt, re.S).group(1)
+    faces = re.search(r"faces = \[(.*?)\]", re.sub(r"#[^\n]*", "", txt), re.S).group(1)
+    tol = float(re.search(r"VF_TOLERANCE = ([0-9.eE+-]+)", txt).group(1))
+    rot = [(a, eval(ang.replace("π", "math.pi"))) for a, ang in
+           re.findall(r"\(:(\w), (π/\d|π)[^)]*\)", txt.split("rotations = [")[1].split("]")[0])]
+    ht = open("/root/reference/test/test_3d_heat_transfer.jl").read()
+    out = {
+        "source": "test/test_3d_viewfactors.jl, test/test_3d_heat_transfer.jl",
+        "vf_tolerance": tol,
+        "narayanaswamy": cases,
+        "cube_points": parse_julia_matrix(points),
+        "cube_faces": [[int(v) for v in r] for r in parse_julia_matrix(faces)],
+        "F_EES": parse_julia_matrix(ees),
+        "rotations": [{"axis": a, "angle": ang} for a, ang in rot],
+        "temp_tolerance_K": float(re.search(r"TEMP_TOLERANCE = ([0-9.eE+-]+)", ht).group(1)),
+        "energy_tolerance_W": float(re.search(r"ENERGY_TOLERANCE = ([0-9.eE+-]+)", ht).group(1)),
+    }
+    with open(os.path.join(HERE, "reference_3d.json"), "w") as fh:
+        json.dump(out, fh, indent=1)
+    print("wrote reference_3d.json:", len(cases), "Narayanaswamy cases,", len(rot), "rotations")
+
+
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["3d"]:
+        main_3d()
+    else:
+        main()

@@ -16,7 +16,7 @@ HEADER = os.path.join(H.ROOT, "include", "rthx.h")
 
 def declared_functions():
     txt = open(HEADER).read()
-    return sorted(set(re.findall(r"\b(rthx_[A-Za-z_]+)\s*\(", txt)))
+    return sorted(set(re.findall(r"\b(rthx_[A-Za-z0-9_]+)\s*\(", txt)))
 
 
 @pytest.fixture(scope="module")
@@ -34,7 +34,7 @@ def test_header_and_python_mirror_agree():
 
 def test_every_declared_symbol_is_exported(lib):
     out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True, check=True).stdout
-    exported = set(re.findall(r"\b(rthx_[A-Za-z_]+)\b", out))
+    exported = set(re.findall(r"\b(rthx_[A-Za-z0-9_]+)\b", out))
     missing = [s for s in declared_functions() if s not in exported]
     assert not missing, missing
     for s in declared_functions():
@@ -58,7 +58,8 @@ _MIRRORS = [("rthx_grid_desc", abi.GridDesc), ("rthx_domain_desc", abi.DomainDes
             ("rthx_trace_args", abi.TraceArgs), ("rthx_result_info", abi.ResultInfo),
             ("rthx_smooth_args", abi.SmoothArgs), ("rthx_smooth_info", abi.SmoothInfo),
             ("rthx_solve_args", abi.SolveArgs), ("rthx_solve_info", abi.SolveInfo),
-            ("rthx_direct_args", abi.DirectArgs), ("rthx_direct_info", abi.DirectInfo)]
+            ("rthx_direct_args", abi.DirectArgs), ("rthx_direct_info", abi.DirectInfo),
+            ("rthx_vf3d_args", abi.Vf3dArgs), ("rthx_vf3d_info", abi.Vf3dInfo)]
 
 
 def test_struct_layouts_match_c_compiler(tmp_path):
