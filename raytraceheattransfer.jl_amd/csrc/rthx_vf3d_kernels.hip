@@ -23,6 +23,23 @@ constexpr double kTwoPi = 6.283185307179586;
 // almostZero = 10 eps(Float64), halfTol = 10 almostZero (viewFactor3D.jl:37-38)
 constexpr double kAlmostZero = 2.220446049250313e-15;
 constexpr double kHalfTol = 2.220446049250313e-14;
+constexpr double kClausenC0 = 3.596312591138855;  // 2 + log(pi^2 / 2) (Cl3D.jl:22), folded
+
+#ifndef RTHX_VF_WAVES
+#define RTHX_VF_WAVES 3  // A/B: 3 waves (168 VGPRs, small spill) beat 2 by 20 %
+#endif
+// Out-of-line bodies (one copy of the f3D / Im Li2 code instead of 4 / 12
+// inlined copies per edge pair: instruction-cache footprint).
+#if defined(RTHX_VF_NOINLINE_SKEW)
+#define RTHX_VF_SKEW_ATTR __attribute__((noinline))
+#else
+#define RTHX_VF_SKEW_ATTR
+#endif
+#if defined(RTHX_VF_NOINLINE_LI2)
+#define RTHX_VF_LI2_ATTR __attribute__((noinline))
+#else
+#define RTHX_VF_LI2_ATTR
+#endif
 
 struct V3 {
   double x, y, z;
@@ -59,13 +76,12 @@ __device__ double clausen(double theta) {
   cheb += 6.499672439854756e-8 * T9;
   cheb += 1.238143696612060e-9 * T11;
   cheb += 5.586505893753557e-13 * T13;
-  const double c0 = 2.0 + log(kPi * kPi / 2.0);
-  return (theta - kPi) * c0 + (kTwoPi - theta) * log((kTwoPi - theta) * (1.0 - kAlmostZero) + kAlmostZero) -
+  return (theta - kPi) * kClausenC0 + (kTwoPi - theta) * log((kTwoPi - theta) * (1.0 - kAlmostZero) + kAlmostZero) -
          theta * log(theta * (1.0 - kAlmostZero) + kAlmostZero) + cheb;
 }
 
 // imagLi2_3D.jl:7-17: Im Li2(mag e^{i angle}), Eq. (24).
-__device__ double imag_li2(double mag, double angle) {
+__device__ RTHX_VF_LI2_ATTR double imag_li2(double mag, double angle) {
   if (mag > kAlmostZero) {
     const double omega = atan2(mag * sin(angle), 1.0 - mag * cos(angle));
     return 0.5 * clausen(2.0 * angle) + 0.5 * clausen(2.0 * omega) - 0.5 * clausen(2.0 * omega + 2.0 * angle) +
@@ -75,7 +91,7 @@ __device__ double imag_li2(double mag, double angle) {
 }
 
 // f3D.jl:9-34, Eq. (22b).
-__device__ double f_skew(double s, double l, double alpha, double ca, double sa, double d) {
+__device__ RTHX_VF_SKEW_ATTR double f_skew(double s, double l, double alpha, double ca, double sa, double d) {
   const double s2 = s * s, l2 = l * l, d2 = d * d, sa2 = sa * sa;
   const double wsqrt = sqrt(s2 + d2 / sa2);
   const double psqrt = sqrt(l2 + d2 / sa2);
@@ -165,7 +181,7 @@ __device__ double conductance(const Poly3* __restrict__ A, const Poly3* __restri
 
 // F[a][b] for the rows [row_begin, row_begin + rows) (row-major, F[a][a] = 0,
 // NaN -> 0 as enclosureViewFactors3D.jl:42).  One lane per (a, b).
-__global__ __launch_bounds__(256) void view_factor_kernel(const Poly3* __restrict__ polys, const double* __restrict__ area,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RTHX_VF_WAVES))) void view_factor_kernel(const Poly3* __restrict__ polys, const double* __restrict__ area,
                                                           int64_t n, int64_t row_begin, int64_t rows,
                                                           double* __restrict__ F) {
   const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;

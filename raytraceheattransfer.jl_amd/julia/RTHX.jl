@@ -152,6 +152,18 @@ struct DirectInfo
     total_ms::Float64
 end
 
+struct Vf3dArgs
+    device::Int32
+    reserved0::Int32
+end
+
+struct Vf3dInfo
+    n::Int64
+    pairs::Int64
+    kernel_ms::Float64
+    total_ms::Float64
+end
+
 function check(rc::Integer)
     if rc != 0
         msg = unsafe_string(ccall((:rthx_last_error, LIB[]), Cstring, ()))
@@ -414,13 +426,49 @@ function directRayTracingSingleBin!(rtm, rays_tot::Integer, nudge, spectral_bin:
 end
 
 """
+    enclosureViewFactors3D(superFaces, parallel, max_iters=1000)
+
+Drop-in for enclosureViewFactors3D.jl:1-94: every ordered sub-face pair's
+viewFactor3D on the device (`rthx_view_factors_3d`, sub-faces in the
+reference's face-major linear order, fromLinear :96-100), areas written back
+to the sub-faces (:48-49), then the reference's own smooth_F with
+smooth_surfaces_only = true (:88-91).
+"""
+function enclosureViewFactors3D(superFaces, parallel::Bool, max_iters::Int = 1000)
+    RTHT = parentmodule(@__MODULE__).RayTraceHeatTransfer
+    subs = [sf for f in superFaces for sf in f.subFaces]
+    n = length(subs)
+    xyz = zeros(Float64, 12n); nv = zeros(Int32, n)
+    for (k, sf) in enumerate(subs)
+        nv[k] = length(sf.vertices)
+        for (i, v) in enumerate(sf.vertices), d in 1:3
+            xyz[12(k - 1) + 3(i - 1) + d] = v[d]
+        end
+    end
+    Ft = Matrix{Float64}(undef, n, n)      # row-major from the library = F' in Julia's layout
+    area = Vector{Float64}(undef, n)
+    info = Ref{Vf3dInfo}()
+    args = Ref(Vf3dArgs(DEVICE[], Int32(0)))
+    check(ccall((:rthx_view_factors_3d, LIB[]), Cint,
+                (Ptr{Float64}, Ptr{Int32}, Int64, Ptr{Vf3dArgs}, Ptr{Float64}, Ptr{Float64}, Ptr{Vf3dInfo}),
+                xyz, nv, n, args, Ft, area, info))
+    F_raw = permutedims(Ft)
+    for (k, sf) in enumerate(subs)
+        sf.area = area[k]
+    end
+    F_smooth = RTHT.smooth_F(F_raw, area, n; max_iters = max_iters, smooth_surfaces_only = true)
+    return F_raw, F_smooth
+end
+
+"""
     enable!(; lib, device=0, seed=1, faithful=false)
 
 Redirect RayTraceHeatTransfer's `computeExchangeFactorsBin` (and, with
-`direct = true`, `directRayTracingSingleBin!`) to the GPU.
+`direct = true`, `directRayTracingSingleBin!`; with `viewfactors3d = true`,
+`enclosureViewFactors3D`) to the GPU.
 """
 function enable!(; lib::AbstractString, device::Integer = 0, seed::Integer = 1, faithful::Bool = false,
-                 smoothing::Bool = false, direct::Bool = true)
+                 smoothing::Bool = false, direct::Bool = true, viewfactors3d::Bool = true)
     LIB[] = lib
     DEVICE[] = Int32(device)
     SEED[] = UInt64(seed)
@@ -435,6 +483,12 @@ function enable!(; lib::AbstractString, device::Integer = 0, seed::Integer = 1, 
         return $(RTHX).computeExchangeFactorsBin(rtm, rays_per_emitter, nudge, spectral_bin, surface_mapping,
                                                  volume_mapping, num_surfaces, num_volumes, num_emitters,
                                                  verbose, rec)
+    end
+    if viewfactors3d  # 3D enclosures: analytic view factors on the device
+        @eval RTHT function enclosureViewFactors3D(superFaces::Vector{PolyFace3D{G}}, parallel::Bool,
+                                                  max_iters::Int = 1000) where G
+            return $(RTHX).enclosureViewFactors3D(superFaces, parallel, max_iters)
+        end
     end
     if direct  # method=:direct on the device as well
         @eval RTHT function directRayTracingSingleBin!(rtm::RayTracingDomain2D, rays_tot::P, nudge::G,

@@ -142,7 +142,8 @@ def test_julia_shim_mirrors_header():
     for c_name, jl_name in [("rthx_grid_desc", "GridDesc"), ("rthx_domain_desc", "DomainDesc"),
                             ("rthx_trace_args", "TraceArgs"), ("rthx_result_info", "ResultInfo"),
                             ("rthx_smooth_args", "SmoothArgs"), ("rthx_smooth_info", "SmoothInfo"),
-                            ("rthx_direct_args", "DirectArgs"), ("rthx_direct_info", "DirectInfo")]:
+                            ("rthx_direct_args", "DirectArgs"), ("rthx_direct_info", "DirectInfo"),
+                            ("rthx_vf3d_args", "Vf3dArgs"), ("rthx_vf3d_info", "Vf3dInfo")]:
         assert _julia_struct_fields(jl, jl_name) == _c_struct_fields(c_name), c_name
     called = set(re.findall(r"ccall\(\(:(rthx_\w+)", jl))
     assert called and called <= set(declared_functions())
