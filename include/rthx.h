@@ -365,6 +365,27 @@ typedef struct rthx_vf3d_info {
 int rthx_view_factors_3d(const double* xyz, const int32_t* nv, int64_t n, const rthx_vf3d_args* args,
                          double* F_out, double* area_out, rthx_vf3d_info* info);
 
+/* ------------------------------------------------------------------------
+ * 3D Monte Carlo exchange factors (BASELINE config 4: cube
+ * + icosphere, Moeller-Trumbore).  The 3D counterpart of rthx_trace_exchange
+ * for surface enclosures with obstructions, which the reference's analytic
+ * view factors (enclosureViewFactors3D.jl) do not handle.  The scene is n
+ * planar polygons xyz[n][4][3] / nv[n] (as rthx_view_factors_3d) with, per
+ * polygon, a normal pointing to the side rays leave from (normal[n][3], any
+ * length; the polygon's own unit normal is oriented to agree with it).
+ * Each emitter traces rays_per_emitter rays: uniform point on the polygon,
+ * cosine-law direction, nearest polygon hit (the emitter itself excluded).
+ * Counts go into an rthx_result exactly as for rthx_trace_exchange (read them
+ * with rthx_result_get_info / rthx_result_copy_csr); F_ij = count_ij / R.
+ * rthx_trace_args: bin must be 0, n_record 0; nudge is unused.
+ * ------------------------------------------------------------------------ */
+typedef struct rthx_scene3d rthx_scene3d;
+
+int rthx_scene3d_create(const double* xyz, const int32_t* nv, const double* normal, int64_t n, int32_t device,
+                        rthx_scene3d** out);
+void rthx_scene3d_destroy(rthx_scene3d* scene);
+int rthx_trace_exchange_3d(rthx_scene3d* scene, const rthx_trace_args* args, rthx_result* res);
+
 #ifdef __cplusplus
 }
 #endif

@@ -59,6 +59,8 @@ def load() -> C.CDLL:
                                         C.POINTER(abi.DirectArgs), C.c_int, C.POINTER(C.c_uint64),
                                         C.POINTER(abi.DirectInfo)]
     lib.oracle_view_factors_3d.argtypes = [dp, C.POINTER(C.c_int32), C.c_int64, C.c_int, dp, dp]
+    lib.oracle_trace_exchange_3d.argtypes = [dp, C.POINTER(C.c_int32), dp, C.c_int64, C.POINTER(abi.TraceArgs), C.c_int,
+                                             C.POINTER(C.c_uint32), C.POINTER(C.c_int64)]
     lib.oracle_last_error.restype = C.c_char_p
     _lib = lib
     return lib
@@ -164,6 +166,23 @@ def view_factors_3d(xyz, nv, nthreads: int = 0, with_F: bool = True):
                                        abi.ptr(F, C.c_double) if with_F else None, abi.ptr(area, C.c_double))
     assert rc == 0
     return F, area
+
+
+def trace_exchange_3d(xyz, nv, normals, R, seed=1, begin=0, end=None, stride=1, nthreads: int = 0):
+    """The 3D tracer restated on the CPU: dense counts[rows, n] and lost rays."""
+    x = np.ascontiguousarray(xyz, dtype=np.float64).reshape(-1, 12)
+    k = np.ascontiguousarray(nv, dtype=np.int32)
+    nrm = np.ascontiguousarray(normals, dtype=np.float64).reshape(-1, 3)
+    n = len(k)
+    end = n if end is None else min(end, n)
+    rows = max(0, (end - begin + stride - 1) // stride)
+    args, _keep = make_args(0, R, 0.0, seed, begin, end, stride)
+    counts = np.zeros((max(rows, 1), n), dtype=np.uint32)
+    lost = C.c_int64(0)
+    rc = load().oracle_trace_exchange_3d(abi.ptr(x, C.c_double), abi.ptr(k, C.c_int32), abi.ptr(nrm, C.c_double), n,
+                                         C.byref(args), nthreads, abi.ptr(counts, C.c_uint32), C.byref(lost))
+    assert rc == 0
+    return counts[:rows], lost.value
 
 
 class OracleBackend:

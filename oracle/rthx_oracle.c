@@ -1301,3 +1301,155 @@ ORACLE_API int oracle_view_factors_3d(const double* xyz, const int32_t* nv, int6
   free(area);
   return RTHX_OK;
 }
+
+/* ======================================================================== */
+/* 3D Monte Carlo exchange factors (BASELINE config 4).   */
+/* The reference has no 3D ray tracer; this restates the library's 3D       */
+/* tracer (csrc/rthx_trace3d_kernels.hip) from its specification: uniform   */
+/* point on the polygon (quads split v0 v1 v2 / v2 v3 v0 by area, as        */
+/* emitVolumeRay2D.jl:6-18 splits quads), cosine-law direction about the    */
+/* oriented normal, nearest Moeller-Trumbore hit over ALL triangles in      */
+/* index order (ties on t to the lower index; the emitter's triangles are   */
+/* skipped).  Pinned by the analytic view factors (oracle_view_factors_3d,  */
+/* itself pinned by the reference's EES / Narayanaswamy tables) on convex   */
+/* enclosures, and by F(sphere -> cube) = 1 for a sphere inside a cube.     */
+/* ======================================================================== */
+typedef struct {
+  double v[4][3], n[3], t1[3], t2[3], tri_frac;
+  int nv;
+} t3_poly;
+
+typedef struct {
+  double v0[3], e1[3], e2[3];
+  int poly;
+} t3_tri;
+
+static double t3_dot(const double* a, const double* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+static void t3_cross(const double* a, const double* b, double* c) {
+  c[0] = a[1] * b[2] - a[2] * b[1];
+  c[1] = a[2] * b[0] - a[0] * b[2];
+  c[2] = a[0] * b[1] - a[1] * b[0];
+}
+
+static double t3_mt(const t3_tri* T, const double* o, const double* d) {
+  double p[3], q[3], s[3];
+  t3_cross(d, T->e2, p);
+  double det = t3_dot(T->e1, p);
+  if (det == 0.0) return -1.0;
+  double inv = 1.0 / det;
+  s[0] = o[0] - T->v0[0]; s[1] = o[1] - T->v0[1]; s[2] = o[2] - T->v0[2];
+  double u = t3_dot(s, p) * inv;
+  if (u < 0.0 || u > 1.0) return -1.0;
+  t3_cross(s, T->e1, q);
+  double v = t3_dot(d, q) * inv;
+  if (v < 0.0 || u + v > 1.0) return -1.0;
+  return t3_dot(T->e2, q) * inv;
+}
+
+typedef struct {
+  const t3_poly* polys;
+  const t3_tri* tris;
+  int64_t n_tri, n, R, k0, k1, begin, stride;
+  uint64_t seed;
+  uint32_t* counts; /* dense [rows][n] */
+  int64_t lost;
+} t3_worker_t;
+
+static void* t3_worker(void* arg) {
+  t3_worker_t* W = (t3_worker_t*)arg;
+  uint32_t key[2] = {(uint32_t)W->seed, (uint32_t)(W->seed >> 32)};
+  for (int64_t k = W->k0; k < W->k1; ++k) {
+    int64_t g = W->begin + k * W->stride;
+    const t3_poly* E = W->polys + g;
+    for (int64_t r = 0; r < W->R; ++r) {
+      draws_t rd;
+      draws_at(W->seed, (uint32_t)r, (uint32_t)g, 0u, 0x40000000u, &rd);
+      uint32_t cc[4] = {(uint32_t)r, (uint32_t)g, 1u, 0x40000000u}, c[4];
+      oracle_philox4x32_10(cc, key, c);
+      double s1 = sqrt(rd.R1);
+      double wa = 1.0 - s1, wb = s1 * (1.0 - rd.R2), wc = s1 * rd.R2;
+      int ia = 0, ib = 1, ic = 2;
+      if (E->nv == 4 && !(rd.sel < E->tri_frac)) { ia = 2; ib = 3; ic = 0; }
+      double o[3], d[3];
+      for (int q = 0; q < 3; ++q) o[q] = wa * E->v[ia][q] + wb * E->v[ib][q] + wc * E->v[ic][q];
+      double st = sqrt(rd.path), ct = sqrt(1.0 - rd.path);
+      double phi = TWO_PI * u32(c[3]);
+      double a = st * cos(phi), b = st * sin(phi);
+      for (int q = 0; q < 3; ++q) d[q] = a * E->t1[q] + b * E->t2[q] + ct * E->n[q];
+      double best_t = INFINITY;
+      int64_t best = -1;
+      for (int64_t t = 0; t < W->n_tri; ++t) { /* index order: ties keep the lower index */
+        if (W->tris[t].poly == g) continue;
+        double th = t3_mt(&W->tris[t], o, d);
+        if (th > 0.0 && th < best_t) { best_t = th; best = t; }
+      }
+      if (best < 0) { W->lost++; continue; }
+      W->counts[(size_t)k * (size_t)W->n + (size_t)W->tris[best].poly]++;
+    }
+  }
+  return NULL;
+}
+
+/* Dense counts[n_rows][n] of emitters g = emitter_begin + k * stride; returns
+ * the lost-ray total in *lost.  Polygons as rthx_scene3d_create. */
+ORACLE_API int oracle_trace_exchange_3d(const double* xyz, const int32_t* nv, const double* normal, int64_t n,
+                                        const rthx_trace_args* a, int nthreads, uint32_t* counts, int64_t* lost) {
+  if (!xyz || !nv || !normal || !a || !counts || n < 2) return RTHX_EINVAL;
+  t3_poly* P = (t3_poly*)calloc((size_t)n, sizeof(t3_poly));
+  t3_tri* T = (t3_tri*)calloc(2 * (size_t)n, sizeof(t3_tri));
+  int64_t nt = 0;
+  for (int64_t k = 0; k < n; ++k) {
+    int m = nv[k];
+    const double* p = xyz + 12 * k;
+    vf_v3 v[4];
+    for (int i = 0; i < 4; ++i) { int j = i < m ? i : m - 1; v[i] = vf_vertex(p, j); }
+    vf_v3 ng = v3_cross(v3_sub(v[1], v[0]), v3_sub(v[2], v[0]));
+    double a1 = v3_norm(ng) / 2;
+    double a2 = m == 4 ? v3_norm(v3_cross(v3_sub(v[3], v[2]), v3_sub(v[0], v[2]))) / 2 : 0.0;
+    vf_v3 un = {normal[3 * k], normal[3 * k + 1], normal[3 * k + 2]};
+    vf_v3 nn = v3_mul(ng, 1.0 / v3_norm(ng));
+    if (v3_dot(nn, un) < 0.0) nn = v3_mul(nn, -1.0);
+    vf_v3 e01 = v3_sub(v[1], v[0]);
+    vf_v3 t1 = v3_mul(e01, 1.0 / v3_norm(e01));
+    vf_v3 t2 = v3_cross(nn, t1);
+    t3_poly* E = &P[k];
+    for (int i = 0; i < 4; ++i) { E->v[i][0] = v[i].x; E->v[i][1] = v[i].y; E->v[i][2] = v[i].z; }
+    E->n[0] = nn.x; E->n[1] = nn.y; E->n[2] = nn.z;
+    E->t1[0] = t1.x; E->t1[1] = t1.y; E->t1[2] = t1.z;
+    E->t2[0] = t2.x; E->t2[1] = t2.y; E->t2[2] = t2.z;
+    E->tri_frac = m == 4 ? a1 / (a1 + a2) : 1.0;
+    E->nv = m;
+    static const int corners[2][3] = {{0, 1, 2}, {2, 3, 0}};
+    for (int h = 0; h < (m == 4 ? 2 : 1); ++h) {
+      vf_v3 A = v[corners[h][0]], B = v[corners[h][1]], Cc = v[corners[h][2]];
+      vf_v3 e1 = v3_sub(B, A), e2 = v3_sub(Cc, A);
+      t3_tri* t = &T[nt++];
+      t->v0[0] = A.x; t->v0[1] = A.y; t->v0[2] = A.z;
+      t->e1[0] = e1.x; t->e1[1] = e1.y; t->e1[2] = e1.z;
+      t->e2[0] = e2.x; t->e2[1] = e2.y; t->e2[2] = e2.z;
+      t->poly = (int)k;
+    }
+  }
+  int64_t end = a->emitter_end < n ? a->emitter_end : n;
+  int64_t rows = end > a->emitter_begin ? (end - a->emitter_begin + a->emitter_stride - 1) / a->emitter_stride : 0;
+  if (nthreads <= 0) nthreads = (int)sysconf(_SC_NPROCESSORS_ONLN);
+  if (nthreads > rows) nthreads = rows > 0 ? (int)rows : 1;
+  t3_worker_t* W = (t3_worker_t*)calloc((size_t)nthreads, sizeof(t3_worker_t));
+  pthread_t* th = (pthread_t*)calloc((size_t)nthreads, sizeof(pthread_t));
+  int64_t per = rows / nthreads, rem = rows % nthreads, start = 0;
+  for (int t = 0; t < nthreads; ++t) {
+    int64_t sz = per + (t < rem ? 1 : 0);
+    W[t].polys = P; W[t].tris = T; W[t].n_tri = nt; W[t].n = n; W[t].R = a->rays_per_emitter;
+    W[t].begin = a->emitter_begin; W[t].stride = a->emitter_stride; W[t].seed = a->seed;
+    W[t].k0 = start; W[t].k1 = start + sz; W[t].counts = counts;
+    start += sz;
+  }
+  for (int t = 1; t < nthreads; ++t) pthread_create(&th[t], NULL, t3_worker, &W[t]);
+  t3_worker(&W[0]);
+  for (int t = 1; t < nthreads; ++t) pthread_join(th[t], NULL);
+  int64_t lost_total = 0;
+  for (int t = 0; t < nthreads; ++t) lost_total += W[t].lost;
+  if (lost) *lost = lost_total;
+  free(th); free(W); free(P); free(T);
+  return RTHX_OK;
+}

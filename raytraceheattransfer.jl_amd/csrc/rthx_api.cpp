@@ -38,32 +38,32 @@ int fail(int code, const std::string& msg) {
   g_last_error = msg;
   return code;
 }
-}  // namespace rthx
 
-struct rthx_result {
-  int device = -1;
-  DevBuf stage_cols, stage_cnt, row_nnz, row_tallied, row_off, totals, cols, cnt, dense;
-  DevBuf rec_ids, rec_ok, rec_orig, rec_end;
-  bool valid = false;
-  bool host_csr = false;
-  bool host_row_off = false;
-  int64_t N = 0, R = 0, n_rows = 0, begin = 0, stride = 1, split = 1;
-  std::vector<int64_t> h_row_off;
-  HostBuf h_cols, h_cnt;  // pinned
-  std::vector<int64_t> rec_g;  // recorded emitters (ascending)
-  std::vector<uint8_t> h_ok;
-  std::vector<double> h_orig, h_end;
-  bool host_rec = false;
-  rthx_result_info info{};
-  ~rthx_result() {
-    if (device >= 0) (void)hipSetDevice(device);
-    DevBuf* all[] = {&stage_cols, &stage_cnt, &row_nnz,  &row_tallied, &row_off,  &totals, &cols,
-                     &cnt,        &dense,     &rec_ids,  &rec_ok,      &rec_orig, &rec_end};
-    for (DevBuf* b : all) b->release();
-    h_cols.release();
-    h_cnt.release();
+// Device lookup tables (rthx_device.h): cos/sin(2 pi j/256) for
+// cos_2pi_u32, and for neg_log_tab per entry i the centre c of its z interval
+// [0.6875 + ..), invc = fl(1/c) and ln(invc) split into hi + lo, evaluated in
+// long double.
+void fill_tables(double* t) {
+  for (int j = 0; j < rthx::kCosTable; ++j) {
+    const long double a = 2.0L * 3.141592653589793238462643383279502884L * j / rthx::kCosTable;
+    t[2 * j] = (double)cosl(a);
+    t[2 * j + 1] = (double)sinl(a);
   }
-};
+  double* L = t + rthx::kLogTableOffset;
+  for (int i = 0; i < rthx::kLogTable; ++i) {
+    const double z0 = rthx::bitsd(rthx::kLogOff + ((uint64_t)i << 45));
+    const double z1 = rthx::bitsd(rthx::kLogOff + ((uint64_t)(i + 1) << 45));
+    const double invc = (double)(2.0L / ((long double)z0 + (long double)z1));
+    const long double T = logl((long double)invc);
+    const double hi = (double)T;
+    L[4 * i] = invc;
+    L[4 * i + 1] = hi;
+    L[4 * i + 2] = (double)(T - (long double)hi);
+    L[4 * i + 3] = 0.0;
+  }
+}
+
+}  // namespace rthx
 
 namespace {
 
@@ -123,30 +123,6 @@ rthx::DevGrid add_grid(const int32_t* nv, const double* xy, int first, int count
   return g;
 }
 
-// Device lookup tables (rthx_device.h): cos/sin(2 pi j/256) for
-// cos_2pi_u32, and for neg_log_tab per entry i the centre c of its z interval
-// [0.6875 + ..), invc = fl(1/c) and ln(invc) split into hi + lo, evaluated in
-// long double.
-void fill_tables(double* t) {
-  for (int j = 0; j < rthx::kCosTable; ++j) {
-    const long double a = 2.0L * 3.141592653589793238462643383279502884L * j / rthx::kCosTable;
-    t[2 * j] = (double)cosl(a);
-    t[2 * j + 1] = (double)sinl(a);
-  }
-  double* L = t + rthx::kLogTableOffset;
-  for (int i = 0; i < rthx::kLogTable; ++i) {
-    const double z0 = rthx::bitsd(rthx::kLogOff + ((uint64_t)i << 45));
-    const double z1 = rthx::bitsd(rthx::kLogOff + ((uint64_t)(i + 1) << 45));
-    const double invc = (double)(2.0L / ((long double)z0 + (long double)z1));
-    const long double T = logl((long double)invc);
-    const double hi = (double)T;
-    L[4 * i] = invc;
-    L[4 * i + 1] = hi;
-    L[4 * i + 2] = (double)(T - (long double)hi);
-    L[4 * i + 3] = 0.0;
-  }
-}
-
 }  // namespace
 
 // Host evaluation of the device free-path log (tests/test_numerics.py); not
@@ -154,7 +130,7 @@ void fill_tables(double* t) {
 extern "C" __attribute__((visibility("default"))) int rthx_debug_neg_log(const double* u, int64_t n, double* out) {
   if ((!u || !out) && n > 0) return -1;
   std::vector<double> t(rthx::kTableDoubles);
-  fill_tables(t.data());
+  rthx::fill_tables(t.data());
   for (int64_t k = 0; k < n; ++k) out[k] = rthx::neg_log_tab(u[k], t.data() + rthx::kLogTableOffset);
   return 0;
 }
@@ -332,7 +308,7 @@ RTHX_EXPORT int rthx_domain_create(const rthx_domain_desc* desc, int32_t device,
   // (cos, sin)(2 pi j / 256) for the emission azimuth (cos_2pi_u32) and the
   // free-path log table (neg_log_tab)
   std::vector<double> tables(rthx::kTableDoubles);
-  fill_tables(tables.data());
+  rthx::fill_tables(tables.data());
   UP(cpoly.data(), nc, D.c_poly);
   UP(csolid.data(), nc, D.c_solid);
   UP(s.coarse_bbox, 4 * nc, D.c_bbox);

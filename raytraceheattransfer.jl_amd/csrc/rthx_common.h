@@ -17,6 +17,10 @@ namespace rthx {
 extern thread_local std::string g_last_error;
 int fail(int code, const std::string& msg);
 
+// The device lookup tables (rthx_device.h kTableDoubles: cos/sin of 2 pi j/256
+// and the free-path log table), rthx_api.cpp.
+void fill_tables(double* t);
+
 inline int hip_fail(hipError_t e, const char* what) {
   return fail(RTHX_EDEVICE, std::string(what) + ": " + hipGetErrorString(e));
 }

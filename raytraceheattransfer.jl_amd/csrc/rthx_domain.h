@@ -1,12 +1,18 @@
-// rthx_domain.h -- the opaque rthx_domain handle of include/rthx.h: the
-// uploaded domain (rthx_api.cpp rthx_domain_create) shared by the exchange
-// tracer (rthx_api.cpp) and the direct method (rthx_direct.cpp).
+// rthx_domain.h -- the opaque handles of include/rthx.h shared between
+// translation units: rthx_domain (the uploaded 2D domain, rthx_api.cpp
+// rthx_domain_create; used by the exchange tracer and the direct method,
+// rthx_direct.cpp) and rthx_result (an exchange trace's counts, filled by
+// rthx_trace_exchange and by the 3D tracer, rthx_trace3d.cpp).
 #pragma once
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <string>
 #include <vector>
+
+#include "../../include/rthx.h"
+#include "rthx_common.h"
 
 #include "rthx_device.h"
 
@@ -35,5 +41,30 @@ struct rthx_domain {
     for (auto& e : ev)
       if (e) (void)hipEventDestroy(e);
     if (stream) (void)hipStreamDestroy(stream);
+  }
+};
+
+struct rthx_result {
+  int device = -1;
+  rthx::DevBuf stage_cols, stage_cnt, row_nnz, row_tallied, row_off, totals, cols, cnt, dense;
+  rthx::DevBuf rec_ids, rec_ok, rec_orig, rec_end;
+  bool valid = false;
+  bool host_csr = false;
+  bool host_row_off = false;
+  int64_t N = 0, R = 0, n_rows = 0, begin = 0, stride = 1, split = 1;
+  std::vector<int64_t> h_row_off;
+  rthx::HostBuf h_cols, h_cnt;  // pinned
+  std::vector<int64_t> rec_g;  // recorded emitters (ascending)
+  std::vector<uint8_t> h_ok;
+  std::vector<double> h_orig, h_end;
+  bool host_rec = false;
+  rthx_result_info info{};
+  ~rthx_result() {
+    if (device >= 0) (void)hipSetDevice(device);
+    rthx::DevBuf* all[] = {&stage_cols, &stage_cnt, &row_nnz,  &row_tallied, &row_off,  &totals, &cols,
+                     &cnt,        &dense,     &rec_ids,  &rec_ok,      &rec_orig, &rec_end};
+    for (rthx::DevBuf* b : all) b->release();
+    h_cols.release();
+    h_cnt.release();
   }
 };

@@ -1,0 +1,58 @@
+// rthx_trace3d.h -- device scene and launcher of the 3D Monte Carlo
+// exchange-factor tracer (rthx_trace3d_kernels.hip, rthx_trace3d.cpp).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rthx_kernels.h"
+
+namespace rthx {
+
+// Emitting polygon (3 or 4 vertices): emission frame and area split.
+struct alignas(16) Emit3 {
+  double v[4][3];     // vertices (a triangle repeats vertex 2)
+  double n[3];        // unit normal on the emitting side
+  double t1[3];       // unit tangent (v1 - v0) / |v1 - v0|
+  double t2[3];       // n x t1
+  double tri_frac;    // area(v0 v1 v2) / area (quads; 1 for triangles)
+  int32_t nv;
+  int32_t reserved;
+};
+
+// Triangle for the Moeller-Trumbore test: v0, e1 = v1 - v0, e2 = v2 - v0.
+struct alignas(16) Tri3 {
+  double v0[3], e1[3], e2[3];
+  int32_t poly;       // polygon it belongs to (the absorber index)
+  int32_t id;         // triangle index before the BVH permutation (hit ties)
+};
+
+// BVH node: bounds; a >= 0: children a, b; a < 0: leaf, triangles [~a, ~a + b).
+struct alignas(16) BvhNode {
+  double lo[3], hi[3];
+  int32_t a, b;
+};
+
+struct DevScene3D {
+  int32_t n_poly, n_tri, n_nodes, reserved;
+  const Emit3* polys;
+  const Tri3* tris;
+  const BvhNode* nodes;
+  const double* tables;  // kTableDoubles (cos/sin table for the azimuth)
+};
+
+constexpr uint32_t kTrace3dTag = 0x40000000u;  // Philox counter word 3 of the 3D tracer
+constexpr int kBvhStack = 64;
+
+struct Trace3dLaunch {
+  const DevScene3D* S;
+  TraceParams P;        // R, g_begin, g_stride, key (bin / beta unused)
+  TallyParams T;        // split path: dense rows + row_tallied
+  size_t lds_bytes;
+  hipStream_t stream;
+  bool faithful;
+};
+
+hipError_t launch_trace3d(const Trace3dLaunch& L);
+
+}  // namespace rthx

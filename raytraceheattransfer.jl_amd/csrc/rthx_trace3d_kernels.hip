@@ -1,0 +1,187 @@
+// rthx_trace3d_kernels.hip -- Monte Carlo exchange factors of a 3D surface
+// enclosure on gfx950 (BASELINE config 4: cube + icosphere,
+// Moeller-Trumbore).
+//
+// The reference computes 3D view factors analytically
+// (ViewFactor3D/enclosureViewFactors3D.jl), which ignores occlusion; this
+// tracer is the 3D counterpart of the 2D exchange tracer (per-emitter rows of
+// absorber counts, parallelRayTracing.jl:64-159) for enclosures with
+// obstructions.  A workgroup traces a slice of one emitter's rays: uniform
+// point on the polygon (two triangles by area for a quad, as
+// emitVolumeRay2D.jl:6-18 splits quads), cosine-law direction about the
+// polygon normal, nearest hit by a BVH walk with the Moeller-Trumbore test
+// (fp64; ties on t go to the lower triangle index, so the walk order never
+// matters), and an LDS histogram of absorbing polygons flushed into the row's
+// dense count buffer.  The CPU restatement (oracle/rthx_oracle.c
+// oracle_trace_exchange_3d) tests every triangle in index order with the same
+// arithmetic, so counts compare exactly.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rthx_device.h"
+#include "rthx_trace3d.h"
+#include "rthx_wave.h"
+
+namespace rthx {
+namespace t3 {
+
+constexpr int kThreads = 256;
+
+__device__ __forceinline__ double dot3(const double* a, const double* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+__device__ __forceinline__ void cross3(const double* a, const double* b, double* c) {
+  c[0] = a[1] * b[2] - a[2] * b[1];
+  c[1] = a[2] * b[0] - a[0] * b[2];
+  c[2] = a[0] * b[1] - a[1] * b[0];
+}
+
+// Moeller-Trumbore (J. Graphics Tools 2(1), 1997): t of the hit or -1.
+__device__ __forceinline__ double moller_trumbore(const Tri3& T, const double* o, const double* d) {
+  double p[3], q[3], s[3];
+  cross3(d, T.e2, p);
+  const double det = dot3(T.e1, p);
+  if (det == 0.0) return -1.0;
+  const double inv = 1.0 / det;
+  s[0] = o[0] - T.v0[0];
+  s[1] = o[1] - T.v0[1];
+  s[2] = o[2] - T.v0[2];
+  const double u = dot3(s, p) * inv;
+  if (u < 0.0 || u > 1.0) return -1.0;
+  cross3(s, T.e1, q);
+  const double v = dot3(d, q) * inv;
+  if (v < 0.0 || u + v > 1.0) return -1.0;
+  return dot3(T.e2, q) * inv;
+}
+
+// Nearest triangle along o + t d (t > 0) not on polygon `skip`: the absorbing
+// polygon, or -1 if the ray leaves through a crack.
+__device__ int nearest_hit(const DevScene3D& S, const double* o, const double* d, int skip) {
+  const double inv[3] = {1.0 / d[0], 1.0 / d[1], 1.0 / d[2]};
+  double best_t = __builtin_inf();
+  int best_id = 0x7FFFFFFF, best_poly = -1;
+  int stack[kBvhStack];
+  int sp = 0;
+  stack[sp++] = 0;
+  while (sp > 0) {
+    const BvhNode nd = S.nodes[stack[--sp]];
+    double tn = 0.0, tf = best_t;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const double t0 = (nd.lo[k] - o[k]) * inv[k], t1 = (nd.hi[k] - o[k]) * inv[k];
+      tn = fmax(tn, fmin(t0, t1));
+      tf = fmin(tf, fmax(t0, t1));
+    }
+    if (tn > tf) continue;
+    if (nd.a < 0) {
+      const int first = ~nd.a;
+      for (int k = first; k < first + nd.b; ++k) {
+        const Tri3 T = S.tris[k];
+        if (T.poly == skip) continue;
+        const double t = moller_trumbore(T, o, d);
+        if (t > 0.0 && (t < best_t || (t == best_t && T.id < best_id))) {
+          best_t = t;
+          best_id = T.id;
+          best_poly = T.poly;
+        }
+      }
+    } else if (sp + 2 <= kBvhStack) {
+      stack[sp++] = nd.b;
+      stack[sp++] = nd.a;
+    }
+  }
+  return best_poly;
+}
+
+// One ray (g, r): emission point and cosine-law direction, then the walk.
+template <bool FAITHFUL>
+__device__ __forceinline__ int trace_ray(const DevScene3D& S, const Emit3& E, const double* tab, uint32_t g, uint32_t r,
+                                         uint32_t k0, uint32_t k1) {
+  const RayDraws rd(r, g, 0u, kTrace3dTag, k0, k1);
+  const double R1 = rd.R1(), R2 = rd.R2();
+  const double s1 = sqrt(R1);
+  const double wa = 1.0 - s1, wb = s1 * (1.0 - R2), wc = s1 * R2;
+  int ia = 0, ib = 1, ic = 2;
+  if (E.nv == 4 && !(rd.sel() < E.tri_frac)) {
+    ia = 2;
+    ib = 3;
+    ic = 0;
+  }
+  double o[3], d[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) o[k] = wa * E.v[ia][k] + wb * E.v[ib][k] + wc * E.v[ic][k];
+  const double u3 = rd.path();
+  const double st = sqrt(u3), ct = sqrt(1.0 - u3);
+  const uint32_t w = rd.c[3];
+  double cphi, sphi;
+  if (FAITHFUL) {
+    cphi = cos(RTHX_TWO_PI * u32(w));
+    sphi = sin(RTHX_TWO_PI * u32(w));
+  } else {
+    cphi = cos_2pi_u32(w, tab);
+    sphi = cos_2pi_u32(w - 0x40000000u, tab);  // cos(2 pi u - pi/2) = sin(2 pi u)
+  }
+  const double a = st * cphi, b = st * sphi;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) d[k] = a * E.t1[k] + b * E.t2[k] + ct * E.n[k];
+  return nearest_hit(S, o, d, (int)g);
+}
+
+// Grid: n_rows * split workgroups; workgroup (slot, part) traces rays
+// [part * chunk, ...) of emitter g = g_begin + slot * g_stride.
+template <bool FAITHFUL>
+__global__ __launch_bounds__(kThreads) void trace_exchange_3d_kernel(const DevScene3D* __restrict__ Sp, TraceParams P,
+                                                                    TallyParams T) {
+  extern __shared__ uint32_t hist[];
+  __shared__ double s_tab[kTableDoubles];
+  __shared__ Emit3 s_emit;
+  __shared__ uint32_t s_tallied;
+  const DevScene3D& S = *Sp;
+  const int tid = threadIdx.x;
+  const int64_t slot = blockIdx.x / T.split, part = blockIdx.x % T.split;
+  const int64_t chunk = (P.R + T.split - 1) / T.split;
+  const int64_t r_begin = part * chunk;
+  const int64_t r_end = r_begin + chunk < P.R ? r_begin + chunk : P.R;
+  const int64_t g = P.g_begin + slot * P.g_stride;
+  const int64_t N = T.n_emitters;
+  for (int64_t i = tid; i < N; i += kThreads) hist[i] = 0u;
+  if (!FAITHFUL)
+    for (int i = tid; i < kTableDoubles; i += kThreads) s_tab[i] = S.tables[i];
+  if (tid == 0) {
+    s_emit = S.polys[g];
+    s_tallied = 0u;
+  }
+  __syncthreads();
+  uint32_t tallied = 0;
+  for (int64_t r = r_begin + tid; r < r_end; r += kThreads) {
+    const Emit3 RTHX_LDS* em = lds_opaque(&s_emit);
+    const int a = trace_ray<FAITHFUL>(S, *(const Emit3*)em, (const double*)lds_opaque(&s_tab[0]), (uint32_t)g,
+                                      (uint32_t)r, P.key0, P.key1);
+    if (a >= 0) {
+      atomicAdd(&hist[a], 1u);
+      ++tallied;
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) tallied += __shfl_xor(tallied, off);
+  if (lane_id() == 0) atomicAdd(&s_tallied, tallied);
+  __syncthreads();
+  uint32_t* dense = T.dense + slot * N;
+  for (int64_t i = tid; i < N; i += kThreads) {
+    const uint32_t v = hist[i];
+    if (v) atomicAdd(&dense[i], v);
+  }
+  if (tid == 0) atomicAdd(&T.row_tallied[slot], s_tallied);
+}
+
+}  // namespace t3
+
+hipError_t launch_trace3d(const Trace3dLaunch& L) {
+  auto kern = L.faithful ? t3::trace_exchange_3d_kernel<true> : t3::trace_exchange_3d_kernel<false>;
+  if (L.lds_bytes > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.lds_bytes);
+    if (e != hipSuccess) return e;
+  }
+  const int64_t blocks = L.T.n_rows * L.T.split;
+  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(t3::kThreads), L.lds_bytes, L.stream, L.S, L.P, L.T);
+  return hipGetLastError();
+}
+
+}  // namespace rthx

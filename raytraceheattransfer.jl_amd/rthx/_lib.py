@@ -78,6 +78,10 @@ def load(path: Optional[str] = None) -> C.CDLL:
     lib.rthx_trace_direct.argtypes = [C.c_void_p, dp, dp, dp, C.POINTER(C.c_uint8), C.POINTER(abi.DirectArgs),
                                       C.POINTER(C.c_uint64), C.POINTER(abi.DirectInfo)]
     lib.rthx_debug_alias.argtypes = [dp, C.c_int64, C.POINTER(C.c_uint64)]
+    lib.rthx_scene3d_create.argtypes = [dp, C.POINTER(C.c_int32), dp, C.c_int64, C.c_int32, C.POINTER(C.c_void_p)]
+    lib.rthx_scene3d_destroy.argtypes = [C.c_void_p]
+    lib.rthx_scene3d_destroy.restype = None
+    lib.rthx_trace_exchange_3d.argtypes = [C.c_void_p, C.POINTER(abi.TraceArgs), C.c_void_p]
     lib.rthx_view_factors_3d.argtypes = [dp, C.POINTER(C.c_int32), C.c_int64, C.POINTER(abi.Vf3dArgs), dp, dp,
                                          C.POINTER(abi.Vf3dInfo)]
     if lib.rthx_abi_version() != abi.RTHX_ABI_VERSION:

@@ -239,6 +239,9 @@ EXPORTED_SYMBOLS = (
     "rthx_solve_grey_smoothed",
     "rthx_trace_direct",
     "rthx_view_factors_3d",
+    "rthx_scene3d_create",
+    "rthx_scene3d_destroy",
+    "rthx_trace_exchange_3d",
 )
 
 

@@ -194,15 +194,29 @@ class ViewFactorDomain3D:
             xyz[k, : nv[k]] = np.array(s.vertices)
         return xyz, nv
 
-    def __call__(self, parallel: bool = True, max_iters: int = 1000, device: int = 0, verbose: bool = False):
+    def __call__(self, parallel: bool = True, max_iters: int = 1000, device: int = 0, verbose: bool = False,
+                 method: str = "analytic", rays_tot: int = 0, seed: int = 1):
         """ViewFactorDomain3D functor (ViewFactorDomain3D.jl:92-101) ->
         enclosureViewFactors3D (enclosureViewFactors3D.jl:1-94): F_raw on the
         device, sub-face areas from viewFactor3D's formulas, then smooth_F with
-        smooth_surfaces_only = true."""
+        smooth_surfaces_only = true.  ``method="montecarlo"`` (an extension:
+        enclosures with obstructions) traces ``rays_tot`` rays instead
+        (rthx.trace3d, rays leave along each sub-face's inward normal)."""
         from .smoothing import smooth_F
 
         xyz, nv = self.polygon_arrays()
-        F_raw, area, info = view_factors_3d(xyz, nv, device=device)
+        if method == "montecarlo":
+            from .trace3d import exchange_factors_3d
+
+            _, area, _ = view_factors_3d(xyz, nv, device=device, with_F=False)
+            normals = np.array([s.inwardNormal for s in self.subfaces()])
+            R = max(1, int(rays_tot) // len(nv))
+            F_raw = exchange_factors_3d(xyz, nv, normals, R, seed=seed, device=device).toarray()
+            info = {"rays_per_emitter": R}
+        elif method == "analytic":
+            F_raw, area, info = view_factors_3d(xyz, nv, device=device)
+        else:
+            raise ValueError(f"unknown method {method!r}: 'analytic' or 'montecarlo'")
         for s, a in zip(self.subfaces(), area):
             s.area = float(a)  # enclosureViewFactors3D.jl:48-49
         self.F_raw = F_raw
@@ -215,7 +229,8 @@ class ViewFactorDomain3D:
 
 
 def view_factors_3d(xyz, nv, device: int = 0, with_F: bool = True):
-    """rthx_view_factors_3d: (F[n, n], area[n], info)."""
+    """rthx_view_factors_3d: (F[n, n], area[n], info); with_F=False computes
+    the areas only (no device needed)."""
     from ._lib import check, load
 
     lib = load()

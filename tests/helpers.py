@@ -261,3 +261,57 @@ def greenhouse_domain(n_layers=67, nx=201, ny=3, n_bins=8, scale_height=15_900.0
         f.T_in_g = -1.0
         faces.append(f)
     return RayTracingDomain2D(faces, [(nx, ny)] * n_layers)
+
+
+def icosphere(level=2, radius=0.3, center=(0.5, 0.5, 0.5)):
+    """Triangles of a subdivided icosahedron projected on a sphere:
+    20 * 4**level faces, counter-clockwise seen from outside."""
+    t = (1 + 5 ** 0.5) / 2
+    V = [(-1, t, 0), (1, t, 0), (-1, -t, 0), (1, -t, 0), (0, -1, t), (0, 1, t), (0, -1, -t), (0, 1, -t),
+         (t, 0, -1), (t, 0, 1), (-t, 0, -1), (-t, 0, 1)]
+    V = [np.array(v, dtype=float) / np.linalg.norm(v) for v in V]
+    F = [(0, 11, 5), (0, 5, 1), (0, 1, 7), (0, 7, 10), (0, 10, 11), (1, 5, 9), (5, 11, 4), (11, 10, 2), (10, 7, 6),
+         (7, 1, 8), (3, 9, 4), (3, 4, 2), (3, 2, 6), (3, 6, 8), (3, 8, 9), (4, 9, 5), (2, 4, 11), (6, 2, 10),
+         (8, 6, 7), (9, 8, 1)]
+    for _ in range(level):
+        cache = {}
+
+        def mid(a, b):
+            key = (min(a, b), max(a, b))
+            if key not in cache:
+                m = V[a] + V[b]
+                V.append(m / np.linalg.norm(m))
+                cache[key] = len(V) - 1
+            return cache[key]
+
+        F = [f for a, b, c in F for f in ((a, mid(a, b), mid(c, a)), (b, mid(b, c), mid(a, b)),
+                                          (c, mid(c, a), mid(b, c)), (mid(a, b), mid(b, c), mid(c, a)))]
+    c = np.asarray(center, dtype=float)
+    return np.array([[c + radius * V[i] for i in f] for f in F])
+
+
+def cube_icosphere_scene(ndim=10, level=3, radius=0.3):
+    """BASELINE configs[3]: the unit cube (faces split ndim x ndim, rays leave
+    inward) around a centred icosphere (rays leave outward).  Returns
+    (xyz[n][4][3], nv[n], normals[n][3], n_cube)."""
+    from rthx.domain3d import mesh_faces
+
+    ref = json.load(open(os.path.join(GOLDEN, "reference_3d.json")))
+    pts = np.array(ref["cube_points"])
+    faces = np.array(ref["cube_faces"]) - 1
+    polys, normals = [], []
+    centre = np.array([0.5, 0.5, 0.5])
+    for (p1, p2, p3, p4) in mesh_faces(pts, faces, ndim):
+        for k in range(len(p1)):
+            q = np.array([p1[k], p2[k], p3[k], p4[k]])
+            polys.append(q)
+            normals.append(centre - q.mean(axis=0))
+    n_cube = len(polys)
+    for tri in icosphere(level, radius):
+        q = np.zeros((4, 3))
+        q[:3] = tri
+        q[3] = tri[2]
+        polys.append(q)
+        normals.append(tri.mean(axis=0) - centre)
+    nv = np.array([4] * n_cube + [3] * (len(polys) - n_cube), dtype=np.int32)
+    return np.array(polys), nv, np.array(normals), n_cube
