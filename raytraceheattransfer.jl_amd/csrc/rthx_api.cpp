@@ -328,6 +328,53 @@ RTHX_EXPORT int rthx_domain_create(const rthx_domain_desc* desc, int32_t device,
   UP(s_face.data(), s_face.size(), D.s_face);
   UP(s_wall.data(), s_wall.size(), D.s_wall);
   UP(tables.data(), tables.size(), D.tables);
+  // Coarse mesh as the CLDS kernels stage it in LDS (rthx_device.h
+  // CoarseLayout), and per bin the beta every fine polygon of a coarse
+  // polygon shares (-1 when they differ).
+  {
+    const size_t ncells = (size_t)D.c_grid.nx * D.c_grid.ny;
+    auto a16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
+    rthx::CoarseLayout L{};
+    size_t off = a16(nc * sizeof(rthx::DevPoly));
+    L.off_fgrid = (int32_t)off;
+    off = a16(off + nc * sizeof(rthx::DevGrid));
+    L.off_bbox = (int32_t)off;
+    off = a16(off + nc * 4 * sizeof(double));
+    L.off_first = (int32_t)off;
+    off = a16(off + (nc + 1) * sizeof(int32_t));
+    L.off_solid = (int32_t)off;
+    off = a16(off + nc * sizeof(uint32_t));
+    L.off_cells = (int32_t)off;
+    off = a16(off + ncells * sizeof(rthx::CellRec));
+    L.off_beta = (int32_t)off;
+    L.blob_bytes = (int32_t)off;
+    off = a16(off + nc * sizeof(double));
+    if (nc >= 2 && D.c_grid.cell_base == 0 && off <= rthx::kMaxCoarseLdsBytes) {
+      L.bytes = (int32_t)off;
+      std::vector<uint4> blob((size_t)L.blob_bytes / 16);
+      char* b = reinterpret_cast<char*>(blob.data());
+      std::memset(b, 0, (size_t)L.blob_bytes);
+      std::memcpy(b, cpoly.data(), nc * sizeof(rthx::DevPoly));
+      std::memcpy(b + L.off_fgrid, fgrids.data(), nc * sizeof(rthx::DevGrid));
+      std::memcpy(b + L.off_bbox, s.coarse_bbox, nc * 4 * sizeof(double));
+      std::memcpy(b + L.off_first, s.fine_offset, (nc + 1) * sizeof(int32_t));
+      std::memcpy(b + L.off_solid, csolid.data(), nc * sizeof(uint32_t));
+      std::memcpy(b + L.off_cells, gcells.data(), ncells * sizeof(rthx::CellRec));
+      std::vector<double> cbeta((size_t)s.n_bins * nc, -1.0);
+      for (int bn = 0; bn < s.n_bins; ++bn)
+        for (size_t c = 0; c < nc; ++c) {
+          const int f0 = s.fine_offset[c], f1 = s.fine_offset[c + 1];
+          if (f1 <= f0) continue;
+          const double* bb = s.beta + (size_t)bn * nf;
+          bool same = true;
+          for (int f = f0 + 1; f < f1 && same; ++f) same = bb[f] == bb[f0];
+          if (same) cbeta[(size_t)bn * nc + c] = bb[f0];
+        }
+      UP(blob.data(), blob.size(), D.c_blob);
+      UP(cbeta.data(), cbeta.size(), D.c_beta);
+    }
+    D.cl = L;
+  }
 #undef UP
   {
     int r3 = upload(d, &d->D, 1, &d->d_dom, "domain record");
@@ -384,9 +431,16 @@ RTHX_EXPORT int rthx_trace_exchange(rthx_domain* dom, const rthx_trace_args* a, 
   const int64_t rays_per_block = split > 1 ? (R + split - 1) / split : R;
   const bool pack16 = rays_per_block < 65536;
   const int64_t words = pack16 ? (N + 1) / 2 : N;
-  const size_t lds_bytes = (size_t)words * 4;
+  size_t lds_bytes = (size_t)words * 4;
   if (lds_bytes + rthx::kStaticLdsBytes > rthx::kMaxLdsBytes)
     return fail(RTHX_ERANGE, "N too large for the LDS row histogram of this build (N <= 76800)");
+  // multi-polygon domains: the coarse mesh goes behind the histogram in LDS
+  // when it fits (CLDS kernels, rthx_device.h segment_cl)
+  const size_t cl_offset = (lds_bytes + 15) & ~(size_t)15;
+  const bool clds = !dom->single_convex && dom->D.cl.bytes > 0 &&
+                    cl_offset + (size_t)dom->D.cl.bytes + rthx::kStaticLdsBytes <= rthx::kMaxLdsBytes &&
+                    !(getenv("RTHX_NO_CLDS") && getenv("RTHX_NO_CLDS")[0] == '1');
+  if (clds) lds_bytes = cl_offset + (size_t)dom->D.cl.bytes;
   const int64_t row_cap = std::max<int64_t>(1, std::min<int64_t>(N, R));
 
   res->valid = false;
@@ -457,6 +511,7 @@ RTHX_EXPORT int rthx_trace_exchange(rthx_domain* dom, const rthx_trace_args* a, 
   T.n_rows = n_rows;
   T.row_cap = row_cap;
   T.split = (int32_t)split;
+  T.cl_offset = clds ? (int32_t)cl_offset : 0;
   T.stage_cols = res->stage_cols.as<uint32_t>();
   T.stage_cnt = res->stage_cnt.as<uint32_t>();
   T.row_nnz = res->row_nnz.as<uint32_t>();
@@ -481,6 +536,7 @@ RTHX_EXPORT int rthx_trace_exchange(rthx_domain* dom, const rthx_trace_args* a, 
     L.pack16 = pack16;
     L.faithful = (a->flags & RTHX_FLAG_FAITHFUL_SAMPLING) != 0;
     L.single = dom->single_convex;
+    L.clds = clds;
     L.axis = dom->axis_rect && !(getenv("RTHX_NO_AXIS") && getenv("RTHX_NO_AXIS")[0] == '1');
     HIP_TRY(rthx::launch_trace(L), "trace_exchange_kernel launch");
   }

@@ -63,6 +63,17 @@ constexpr int kLogTable = 128;  // neg_log_tab entries
 constexpr int kLogTableOffset = 2 * kCosTable;
 constexpr int kTableDoubles = kLogTableOffset + 4 * kLogTable;
 
+// Byte layout of the coarse mesh as multi-polygon trace kernels stage it in
+// LDS (CLDS kernels): DevPoly records at 0, then fine grids,
+// bounding boxes, fine-polygon offsets, solid-wall masks, the coarse grid's
+// cell records and one beta per coarse polygon for the traced bin.  Every
+// offset is a multiple of 16.  bytes == 0: not staged (too large).
+struct CoarseLayout {
+  int32_t bytes;      // whole LDS block, beta included
+  int32_t blob_bytes; // copied from c_blob (everything before beta)
+  int32_t off_fgrid, off_bbox, off_first, off_solid, off_cells, off_beta;
+};
+
 struct DevDomain {
   int32_t n_coarse, n_fine, n_surfaces, n_bins;
   // coarse polygons
@@ -92,6 +103,11 @@ struct DevDomain {
   // kTableDoubles doubles: cos(2 pi j/256), sin(2 pi j/256) pairs, j < 256
   // (emission azimuth), then kLogTable (invc, ln(invc) hi, lo, 0) quads
   const double RTHX_GLOBAL* tables;
+  // coarse mesh for LDS staging (CoarseLayout) and the per-bin beta of each
+  // coarse polygon when all its fine polygons share it, else -1
+  const uint4 RTHX_GLOBAL* c_blob;     // [cl.blob_bytes / 16]
+  const double RTHX_GLOBAL* c_beta;    // [n_bins][n_coarse]
+  CoarseLayout cl;
 };
 
 struct TraceParams {
@@ -343,15 +359,16 @@ __device__ __forceinline__ bool point_in_polygon(double px, double py, const Pol
 // not fit fall back to their candidate list and the point-in-polygon loop.
 // A point outside every polygon of the cell ends, as in the reference, in the
 // bbox-prefiltered scan in index order.
-template <class Grid>
-__device__ __forceinline__ int locate(const Grid& g, const DevDomain& D, const DevPoly RTHX_GLOBAL* __restrict__ polys,
-                                      const double RTHX_GLOBAL* __restrict__ bbox, int first, int count, double px,
-                                      double py) {
+// `cells`, `polys` and `bbox` point into global memory or LDS (the coarse
+// mesh of CLDS kernels); cells[g.cell_base + local cell].
+template <class Grid, class CellP, class PolyP, class BoxP>
+__device__ __forceinline__ int locate(const Grid& g, const DevDomain& D, CellP cells, PolyP polys, BoxP bbox, int first,
+                                      int count, double px, double py) {
   double fi = floor(__dmul_rn(px - g.ox, g.inv_x));
   double fj = floor(__dmul_rn(py - g.oy, g.inv_y));
   if (fi >= 0.0 && fi < (double)g.nx && fj >= 0.0 && fj < (double)g.ny) {
     const int cell = g.cell_base + (int)fj * g.nx + (int)fi;
-    const DevCell c = D.grid_cells[cell];
+    const DevCell c = ld(cells + cell);
     double s0 = __dmul_rn(c.a0, px) + __dmul_rn(c.b0, py) + c.c0;
     double s1 = __dmul_rn(c.a1, px) + __dmul_rn(c.b1, py) + c.c1;
     int leaf = s1 < 0.0 ? (s0 < 0.0 ? c.leaf[3] : c.leaf[2]) : (s0 < 0.0 ? c.leaf[1] : c.leaf[0]);
@@ -366,7 +383,7 @@ __device__ __forceinline__ int locate(const Grid& g, const DevDomain& D, const D
     }
   }
   for (int f = 0; f < count; ++f) {
-    const double RTHX_GLOBAL* b = bbox + 4 * (size_t)(first + f);
+    const auto b = bbox + 4 * (size_t)(first + f);
     if (b[0] <= px && px <= b[1] && b[2] <= py && py <= b[3]) {
       if (point_in_polygon(px, py, polys[first + f])) return f;
     }
@@ -377,11 +394,11 @@ __device__ __forceinline__ int locate(const Grid& g, const DevDomain& D, const D
 template <class Grid>
 __device__ __forceinline__ int locate_fine(const DevDomain& D, const Grid& g, int first, int count, double px,
                                            double py) {
-  return locate(g, D, D.f_poly, D.f_bbox, first, count, px, py);
+  return locate(g, D, D.grid_cells, D.f_poly, D.f_bbox, first, count, px, py);
 }
 
 __device__ __forceinline__ int locate_coarse(const DevDomain& D, double px, double py) {
-  return locate(D.c_grid, D, D.c_poly, D.c_bbox, 0, D.n_coarse, px, py);
+  return locate(D.c_grid, D, D.grid_cells, D.c_poly, D.c_bbox, 0, D.n_coarse, px, py);
 }
 
 // ---------------------------------------------------------------------------
@@ -607,6 +624,98 @@ __device__ __forceinline__ int segment(const DevDomain& D, const TraceParams& P,
   py = py + __dmul_rn(t, dy);
   if (UNIFORM) S -= u; else acc += tau_b;
   c = locate_coarse(D, px, py);
+  return c < 0 ? -1 : kRayContinue;
+}
+
+// ---------------------------------------------------------------------------
+// CLDS kernels: the coarse mesh of a multi-polygon domain staged in LDS
+// (CoarseLayout), so that the per-segment chain -- locate the coarse polygon,
+// read its record, walls and fine grid, read beta -- runs on LDS latency
+// instead of four dependent L2 round trips.
+// ---------------------------------------------------------------------------
+#ifndef RTHX_LDS
+#define RTHX_LDS __attribute__((address_space(3)))
+#endif
+
+// Copy of an object in LDS or global memory (the implicit copy constructor
+// takes a generic-address-space reference).
+template <class T>
+__device__ __forceinline__ T ld(const T RTHX_LDS* p) { return *(const T*)p; }
+template <class T>
+__device__ __forceinline__ T ld(const T RTHX_GLOBAL* p) { return *p; }
+
+struct CoarseLds {
+  const DevPoly RTHX_LDS* poly;
+  const DevGrid RTHX_LDS* fgrid;
+  const double RTHX_LDS* bbox;
+  const int32_t RTHX_LDS* first;
+  const uint32_t RTHX_LDS* solid;
+  const DevCell RTHX_LDS* cells;  // coarse grid (cell_base 0)
+  const double RTHX_LDS* beta;    // this bin; -1: the fine polygons' betas differ
+};
+
+__device__ __forceinline__ CoarseLds coarse_lds_view(const char RTHX_LDS* base, const CoarseLayout& L) {
+  CoarseLds v;
+  v.poly = (const DevPoly RTHX_LDS*)base;
+  v.fgrid = (const DevGrid RTHX_LDS*)(base + L.off_fgrid);
+  v.bbox = (const double RTHX_LDS*)(base + L.off_bbox);
+  v.first = (const int32_t RTHX_LDS*)(base + L.off_first);
+  v.solid = (const uint32_t RTHX_LDS*)(base + L.off_solid);
+  v.cells = (const DevCell RTHX_LDS*)(base + L.off_cells);
+  v.beta = (const double RTHX_LDS*)(base + L.off_beta);
+  return v;
+}
+
+// segment() with the coarse mesh in LDS.  One more shortcut of the variable
+// path (traceRay.jl:87-103): when every fine polygon of coarse c has the same
+// beta in this bin (the greenhouse's layers), beta is that value whichever
+// fine polygon holds the segment start, so the start is not located.  The
+// reference would lose a ray whose start lies in no fine polygon of c; such a
+// point lies within rounding of c's boundary (the fine polygons tile c), and
+// here that ray continues.
+template <bool UNIFORM, bool AXIS>
+__device__ __forceinline__ int segment_cl(const DevDomain& D, const TraceParams& P, const CoarseLds& L, int& c,
+                                          double& px, double& py, double dx, double dy, double& S, double& acc) {
+  const double eta = P.eta;
+  int k;
+  const int first = L.first[c];
+  const int count = L.first[c + 1] - first;
+  const double u = dist_to_cell<AXIS>(px, py, dx, dy, L.poly[c], k);
+  const uint32_t solid = L.solid[c];
+  bool gas;
+  double beta = 0.0, tau_b = 0.0;
+  if (UNIFORM) {
+    gas = S < u;
+  } else {
+    beta = L.beta[c];
+    if (beta < 0.0) {
+      const DevGrid fg = ld(L.fgrid + c);
+      const int f0 = locate_fine(D, fg, first, count, px, py);
+      if (f0 < 0) return -1;
+      beta = D.beta[(size_t)P.bin * D.n_fine + first + f0];
+    }
+    tau_b = __dmul_rn(beta, u);
+    gas = acc + tau_b >= S;
+  }
+  const bool wall = !gas && ((solid >> k) & 1u);
+  if (gas || wall) {
+    const double t = gas ? (UNIFORM ? S : (S - acc) / beta) - eta : u - eta;
+    px = px + __dmul_rn(t, dx);
+    py = py + __dmul_rn(t, dy);
+    const DevGrid fg = ld(L.fgrid + c);
+    const int f = locate_fine(D, fg, first, count, px, py);
+    if (f < 0) return -1;
+    const int fg_idx = first + f;
+    if (gas) return D.n_surfaces + fg_idx;
+    int w;
+    dist_to_cell<AXIS>(px, py, dx, dy, D.f_poly[fg_idx], w);
+    return D.f_surf[4 * fg_idx + w];
+  }
+  const double t = u + eta;
+  px = px + __dmul_rn(t, dx);
+  py = py + __dmul_rn(t, dy);
+  if (UNIFORM) S -= u; else acc += tau_b;
+  c = locate(D.c_grid, D, L.cells, L.poly, L.bbox, 0, D.n_coarse, px, py);
   return c < 0 ? -1 : kRayContinue;
 }
 

@@ -13,6 +13,7 @@ constexpr int kTraceThreads = 256;               // default workgroup: 4 waves o
 constexpr int kMaxTraceThreads = 1024;           // large-N rows (LDS-bound occupancy) use up to 16 waves
 constexpr size_t kMaxLdsBytes = 160 * 1024;      // gfx950 LDS per CU
 constexpr int64_t kStaticLdsBytes = 10240;      // the trace kernel's static LDS (emitter, coarse, tables, ...)
+constexpr size_t kMaxCoarseLdsBytes = 48 * 1024; // largest coarse mesh the CLDS kernels stage in LDS
 
 struct RecordParams {
   int32_t n;            // recorded emitters in this call
@@ -31,7 +32,7 @@ struct TallyParams {
   int64_t n_rows;
   int64_t row_cap;      // min(N, R)
   int32_t split;        // workgroups per row (>= 1)
-  int32_t reserved;
+  int32_t cl_offset;    // CLDS kernels: byte offset of the coarse mesh in dynamic LDS
   uint32_t* stage_cols;
   uint32_t* stage_cnt;
   uint32_t* row_nnz;
@@ -46,7 +47,7 @@ struct LaunchCfg {
   RecordParams rec;
   size_t lds_bytes;
   hipStream_t stream;
-  bool uniform, pack16, faithful, single, axis;
+  bool uniform, pack16, faithful, single, axis, clds;
 };
 
 hipError_t launch_trace(const LaunchCfg& L);

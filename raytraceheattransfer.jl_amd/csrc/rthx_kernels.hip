@@ -76,7 +76,7 @@ __device__ __forceinline__ uint32_t compact_row(int64_t n_words, F count2, uint3
   return total;
 }
 
-template <bool UNIFORM, bool PACK16, bool FAITHFUL, bool SINGLE, bool REC, bool SPLIT, bool AXIS>
+template <bool UNIFORM, bool PACK16, bool FAITHFUL, bool SINGLE, bool REC, bool SPLIT, bool AXIS, bool CLDS>
 __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_exchange_kernel(const DevDomain* __restrict__ Dp,
                                                                      TraceParams P, TallyParams T,
                                                                      RecordParams rec) {
@@ -105,6 +105,15 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
 
   const int nthr = (int)blockDim.x;  // 256, 512 or 1024 (launch_trace_t)
   for (int64_t w = tid; w < n_words; w += nthr) hist[w] = 0u;
+  // CLDS: the coarse mesh behind the histogram (T.cl_offset bytes in), and
+  // this bin's coarse betas
+  char RTHX_LDS* cl_base = (char RTHX_LDS*)hist + T.cl_offset;
+  if (CLDS) {
+    uint4* dst = (uint4*)cl_base;  // generic view (HIP vector assignment); stores stay ds_write
+    for (int i = tid; i < D.cl.blob_bytes / 16; i += nthr) dst[i] = D.c_blob[i];
+    double RTHX_LDS* cb = (double RTHX_LDS*)(cl_base + D.cl.off_beta);
+    for (int i = tid; i < D.n_coarse; i += nthr) cb[i] = D.c_beta[(size_t)P.bin * D.n_coarse + i];
+  }
   if (!FAITHFUL)
     for (int i = tid; i < kTableDoubles; i += nthr) s_tab[i] = D.tables[i];
   if (tid == 0) {
@@ -195,7 +204,15 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
       }
       if (__ballot(live) == 0ull) break;
       if (live) {
-        int a = it < 10000 ? segment<UNIFORM, false, AXIS>(D, P, s_single, c, px, py, dx, dy, S, acc) : -1;
+        int a = -1;
+        if (it < 10000) {
+          if (CLDS) {
+            const CoarseLds L = coarse_lds_view(lds_opaque(cl_base), D.cl);
+            a = segment_cl<UNIFORM, AXIS>(D, P, L, c, px, py, dx, dy, S, acc);
+          } else {
+            a = segment<UNIFORM, false, AXIS>(D, P, s_single, c, px, py, dx, dy, S, acc);
+          }
+        }
         ++it;
         if (a != kRayContinue) {
           tally(a);
@@ -346,9 +363,9 @@ __global__ __launch_bounds__(256) void csr_pack_kernel(const uint32_t* __restric
 // ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
-template <bool UNIFORM, bool PACK16, bool FAITHFUL, bool SINGLE, bool REC, bool SPLIT, bool AXIS>
+template <bool UNIFORM, bool PACK16, bool FAITHFUL, bool SINGLE, bool REC, bool SPLIT, bool AXIS, bool CLDS = false>
 static hipError_t launch_trace_t(const LaunchCfg& L) {
-  auto kern = trace_exchange_kernel<UNIFORM, PACK16, FAITHFUL, SINGLE, REC, SPLIT, AXIS>;
+  auto kern = trace_exchange_kernel<UNIFORM, PACK16, FAITHFUL, SINGLE, REC, SPLIT, AXIS, CLDS>;
   if (L.lds_bytes > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)L.lds_bytes);
@@ -376,9 +393,11 @@ template <bool UNIFORM, bool PACK16, bool FAITHFUL, bool AXIS>
 static hipError_t launch_trace_a(const LaunchCfg& L) {
   if (L.T.split > 1) {
     if (L.single) return launch_trace_t<UNIFORM, PACK16, FAITHFUL, true, false, true, AXIS>(L);
+    if (L.clds) return launch_trace_t<UNIFORM, PACK16, FAITHFUL, false, false, true, AXIS, true>(L);
     return launch_trace_t<UNIFORM, PACK16, FAITHFUL, false, false, true, AXIS>(L);
   }
   if (L.single) return launch_trace_t<UNIFORM, PACK16, FAITHFUL, true, false, false, AXIS>(L);
+  if (L.clds) return launch_trace_t<UNIFORM, PACK16, FAITHFUL, false, false, false, AXIS, true>(L);
   return launch_trace_t<UNIFORM, PACK16, FAITHFUL, false, false, false, AXIS>(L);
 }
 

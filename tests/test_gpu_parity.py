@@ -134,6 +134,35 @@ def test_spectral_variable_bins_exact(hip):
         assert_same(gpu_trace(hip, flat, args), oracle.trace_exchange(flat, args, 16))
 
 
+@pytest.mark.parametrize("case", ["greenhouse_checker", "wedges"])
+def test_coarse_lds_kernels_match_global_kernels(hip, case, monkeypatch):
+    """Multi-polygon domains stage the coarse mesh in LDS (CLDS kernels,
+    rthx_device.h segment_cl) and take beta from the coarse polygon when all
+    its fine polygons share it; RTHX_NO_CLDS=1 forces the global-memory
+    kernels.  Both must equal the oracle -- including layers whose fine betas
+    differ (a checkerboard of kappa), where the segment start is located."""
+    if case == "wedges":
+        dom, bins = H.wedge_domain(16, 4), (0,)
+    else:
+        dom, bins = H.greenhouse_domain(n_layers=6, nx=9, ny=3, n_bins=8), (0, 3, 7)
+        for c in (1, 4):
+            for k, f in enumerate(dom.fine_mesh[c]):
+                if k % 2:
+                    f.kappa_g = np.asarray(f.kappa_g) * 1.7
+    flat = dom.flat()
+    if case != "wedges":
+        beta = flat.beta.reshape(8, -1)
+        assert len(np.unique(beta[0])) == 8  # 6 layers, two of them with two betas each
+    for b in bins:
+        args, _k = _args(hip, flat, 1500, seed=7, bin0=b)
+        a = gpu_trace(hip, flat, args)
+        monkeypatch.setenv("RTHX_NO_CLDS", "1")
+        g = gpu_trace(hip, flat, args)
+        monkeypatch.delenv("RTHX_NO_CLDS")
+        assert_same(a, g)
+        assert_same(a, oracle.trace_exchange(flat, args, 16))
+
+
 def test_recorder_exact(hip):
     dom = H.wedge_domain(8, 3)
     flat = dom.flat()
