@@ -359,23 +359,43 @@ __device__ __forceinline__ bool point_in_polygon(double px, double py, const Pol
 // not fit fall back to their candidate list and the point-in-polygon loop.
 // A point outside every polygon of the cell ends, as in the reference, in the
 // bbox-prefiltered scan in index order.
-// `cells`, `polys` and `bbox` point into global memory or LDS (the coarse
-// mesh of CLDS kernels); cells[g.cell_base + local cell].
-template <class Grid, class CellP, class PolyP, class BoxP>
-__device__ __forceinline__ int locate(const Grid& g, const DevDomain& D, CellP cells, PolyP polys, BoxP bbox, int first,
-                                      int count, double px, double py) {
-  double fi = floor(__dmul_rn(px - g.ox, g.inv_x));
-  double fj = floor(__dmul_rn(py - g.oy, g.inv_y));
-  if (fi >= 0.0 && fi < (double)g.nx && fj >= 0.0 && fj < (double)g.ny) {
-    const int cell = g.cell_base + (int)fj * g.nx + (int)fi;
-    const DevCell c = ld(cells + cell);
-    double s0 = __dmul_rn(c.a0, px) + __dmul_rn(c.b0, py) + c.c0;
-    double s1 = __dmul_rn(c.a1, px) + __dmul_rn(c.b1, py) + c.c1;
-    int leaf = s1 < 0.0 ? (s0 < 0.0 ? c.leaf[3] : c.leaf[2]) : (s0 < 0.0 ? c.leaf[1] : c.leaf[0]);
-    if (RTHX_ABLATE & 8) return leaf < 0 ? 0 : leaf;
+// locate() in two halves: the cell record of the point (cell 0's, ignored,
+// for a point outside the grid), then the decision.
+struct CellFetch {
+  double a0, b0, c0, a1, b1, c1;
+  int4 leaf;
+  int cell;
+  bool in_range;
+};
+
+template <class Grid, class CellP>
+__device__ __forceinline__ CellFetch locate_fetch(const Grid& g, CellP cells, double px, double py) {
+  const double fi = floor(__dmul_rn(px - g.ox, g.inv_x));
+  const double fj = floor(__dmul_rn(py - g.oy, g.inv_y));
+  CellFetch f;
+  f.in_range = fi >= 0.0 && fi < (double)g.nx && fj >= 0.0 && fj < (double)g.ny;
+  f.cell = g.cell_base + (f.in_range ? (int)fj * g.nx + (int)fi : 0);
+  const auto r = cells + f.cell;
+  f.a0 = r->a0; f.b0 = r->b0; f.c0 = r->c0;
+  f.a1 = r->a1; f.b1 = r->b1; f.c1 = r->c1;
+  f.leaf.x = r->leaf[0]; f.leaf.y = r->leaf[1]; f.leaf.z = r->leaf[2]; f.leaf.w = r->leaf[3];
+  return f;
+}
+
+template <class PolyP, class BoxP>
+__device__ __forceinline__ int locate_finish(const CellFetch& cf, const DevDomain& D, PolyP polys, BoxP bbox,
+                                             int first, int count, double px, double py) {
+  if (cf.in_range) {
+    double s0 = __dmul_rn(cf.a0, px) + __dmul_rn(cf.b0, py) + cf.c0;
+    double s1 = __dmul_rn(cf.a1, px) + __dmul_rn(cf.b1, py) + cf.c1;
+    // opaque copies: the choice stays a select of values; a select between
+    // fields of the record becomes a dynamically indexed scratch load
+    int l0 = cf.leaf.x, l1 = cf.leaf.y, l2 = cf.leaf.z, l3 = cf.leaf.w;
+    __asm__ volatile("" : "+v"(l0), "+v"(l1), "+v"(l2), "+v"(l3));
+    int leaf = s1 < 0.0 ? (s0 < 0.0 ? l3 : l2) : (s0 < 0.0 ? l1 : l0);
     if (leaf >= 0) return leaf;
     if (leaf == -2) {
-      const int k0 = D.grid_lists[2 * cell], k1 = k0 + D.grid_lists[2 * cell + 1];
+      const int k0 = D.grid_lists[2 * cf.cell], k1 = k0 + D.grid_lists[2 * cf.cell + 1];
       for (int k = k0; k < k1; ++k) {
         int f = D.grid_items[k];
         if (point_in_polygon(px, py, polys[first + f])) return f;
@@ -389,6 +409,14 @@ __device__ __forceinline__ int locate(const Grid& g, const DevDomain& D, CellP c
     }
   }
   return -1;
+}
+
+// `cells`, `polys` and `bbox` point into global memory or LDS (the coarse
+// mesh of CLDS kernels); cells[g.cell_base + local cell].
+template <class Grid, class CellP, class PolyP, class BoxP>
+__device__ __forceinline__ int locate(const Grid& g, const DevDomain& D, CellP cells, PolyP polys, BoxP bbox, int first,
+                                      int count, double px, double py) {
+  return locate_finish(locate_fetch(g, cells, px, py), D, polys, bbox, first, count, px, py);
 }
 
 template <class Grid>
