@@ -4,10 +4,11 @@
 //
 // rthx_scene3d_create validates the polygons, orients each emission frame by
 // the caller's normal, splits quads into two triangles (v0 v1 v2, v2 v3 v0 --
-// the same split the emission uses), builds a BVH on the host (median split
-// on the longest centroid axis, leaves of <= 4 triangles, bounds padded by
-// 1e-9 of the scene size so the fp64 slab test never drops a hit) and uploads
-// it.  rthx_trace_exchange_3d traces R rays per emitter polygon into the
+// the same split the emission uses), builds a two-child BVH on the host
+// (binned SAH, leaves of <= 4 triangles, both children's bounds in each node
+// as fp32 padded outward by kBoxPad of the scene scale, so the device's fp32
+// slab tests never drop a hit the fp64 Moeller-Trumbore test would find) and
+// uploads it.  rthx_trace_exchange_3d traces R rays per emitter polygon into the
 // caller's rthx_result exactly like the 2D split-row path: dense per-row
 // counts, row_compact_kernel, row_scan_kernel, csr_pack_kernel.
 #define RTHX_HOST_ONLY_TU 1
@@ -63,47 +64,161 @@ struct BuildTri {
   double lo[3], hi[3], c[3];
 };
 
-// Median-split BVH over tri indices [b, e) of `order`; returns the node index.
-int build_bvh(std::vector<rthx::BvhNode>& nodes, std::vector<int>& order, const std::vector<BuildTri>& bt, int b, int e,
-              double pad) {
-  rthx::BvhNode nd{};
-  double clo[3] = {1e300, 1e300, 1e300}, chi[3] = {-1e300, -1e300, -1e300};
-  for (int k = 0; k < 3; ++k) {
-    nd.lo[k] = 1e300;
-    nd.hi[k] = -1e300;
-  }
-  for (int i = b; i < e; ++i) {
-    const BuildTri& t = bt[order[i]];
+struct Box {
+  double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
+  void grow(const double* l, const double* h) {
     for (int k = 0; k < 3; ++k) {
-      nd.lo[k] = std::min(nd.lo[k], t.lo[k]);
-      nd.hi[k] = std::max(nd.hi[k], t.hi[k]);
-      clo[k] = std::min(clo[k], t.c[k]);
-      chi[k] = std::max(chi[k], t.c[k]);
+      lo[k] = std::min(lo[k], l[k]);
+      hi[k] = std::max(hi[k], h[k]);
     }
   }
-  for (int k = 0; k < 3; ++k) {
-    nd.lo[k] -= pad;
-    nd.hi[k] += pad;
+  double area() const {
+    const double x = hi[0] - lo[0], y = hi[1] - lo[1], z = hi[2] - lo[2];
+    return x < 0 ? 0.0 : 2.0 * (x * y + y * z + z * x);
   }
-  const int idx = (int)nodes.size();
-  nodes.push_back(nd);
-  if (e - b <= kLeafTris) {
-    nodes[idx].a = ~b;
-    nodes[idx].b = e - b;
+};
+
+// fp32 bound below x - pad / above x + pad (rounded outward)
+float down32(double x) {
+  float f = (float)x;
+  while ((double)f > x) f = std::nextafter(f, -HUGE_VALF);
+  return f;
+}
+float up32(double x) {
+  float f = (float)x;
+  while ((double)f < x) f = std::nextafter(f, HUGE_VALF);
+  return f;
+}
+
+int32_t leaf_ref(int first, int count) { return ~((first << rthx::kLeafBits) | count); }
+
+// Binary BVH over triangle indices order[b, e): binned SAH (16 bins per axis
+// over the centroid bounds; `median` forces median splits on the longest
+// centroid axis).  Leaves hold <= kLeafTris triangles.  Returns the child
+// reference of the range and its bounds; `depth` tracks the deepest inner
+// node (stack bound of the walk).
+struct Bvh2Builder {
+  std::vector<rthx::Bvh2Node>& nodes;
+  std::vector<int>& order;
+  const std::vector<BuildTri>& bt;
+  double pad;
+  bool median;
+  int depth = 0;
+
+  void set_child(int idx, int slot, int32_t ref, const Box& bx) {
+    rthx::Bvh2Node& nd = nodes[idx];
+    nd.child[slot] = ref;
+    for (int k = 0; k < 3; ++k) {
+      nd.lo[slot][k] = down32(bx.lo[k] - pad);
+      nd.hi[slot][k] = up32(bx.hi[k] + pad);
+    }
+  }
+
+  int32_t build(int b, int e, int level, Box& out) {
+    Box bx, cb;
+    for (int i = b; i < e; ++i) {
+      const BuildTri& t = bt[order[i]];
+      bx.grow(t.lo, t.hi);
+      cb.grow(t.c, t.c);
+    }
+    out = bx;
+    if (e - b <= kLeafTris) return leaf_ref(b, e - b);
+    depth = std::max(depth, level + 1);
+    int axis = 0;
+    for (int k = 1; k < 3; ++k)
+      if (cb.hi[k] - cb.lo[k] > cb.hi[axis] - cb.lo[axis]) axis = k;
+    int mid = b + (e - b) / 2;
+    bool done = false;
+    if (!median) {
+      constexpr int kBins = 16;
+      double best = 1e300;
+      int best_axis = -1, best_bin = -1;
+      for (int k = 0; k < 3; ++k) {
+        const double ext = cb.hi[k] - cb.lo[k];
+        if (!(ext > 0.0)) continue;
+        Box bin_box[kBins];
+        int bin_n[kBins] = {0};
+        for (int i = b; i < e; ++i) {
+          const BuildTri& t = bt[order[i]];
+          int j = (int)((t.c[k] - cb.lo[k]) / ext * kBins);
+          j = std::min(kBins - 1, std::max(0, j));
+          bin_box[j].grow(t.lo, t.hi);
+          ++bin_n[j];
+        }
+        Box left[kBins];
+        int nl[kBins];
+        Box acc;
+        int n = 0;
+        for (int j = 0; j < kBins; ++j) {
+          acc.grow(bin_box[j].lo, bin_box[j].hi);
+          n += bin_n[j];
+          left[j] = acc;
+          nl[j] = n;
+        }
+        Box racc;
+        int nr = 0;
+        for (int j = kBins - 1; j > 0; --j) {
+          racc.grow(bin_box[j].lo, bin_box[j].hi);
+          nr += bin_n[j];
+          if (nl[j - 1] == 0 || nr == 0) continue;
+          const double cost = left[j - 1].area() * nl[j - 1] + racc.area() * nr;
+          if (cost < best) {
+            best = cost;
+            best_axis = k;
+            best_bin = j;
+          }
+        }
+      }
+      if (best_axis >= 0) {
+        const int k = best_axis;
+        const double ext = cb.hi[k] - cb.lo[k];
+        auto in_left = [&](int ti) {
+          int j = (int)((bt[ti].c[k] - cb.lo[k]) / ext * kBins);
+          j = std::min(kBins - 1, std::max(0, j));
+          return j < best_bin;
+        };
+        // stable partition: deterministic order of equal keys
+        mid = (int)(std::stable_partition(order.begin() + b, order.begin() + e, in_left) - order.begin());
+        done = mid > b && mid < e;
+      }
+    }
+    if (!done) {
+      mid = b + (e - b) / 2;
+      std::nth_element(order.begin() + b, order.begin() + mid, order.begin() + e, [&](int x, int y) {
+        return bt[x].c[axis] < bt[y].c[axis] || (bt[x].c[axis] == bt[y].c[axis] && x < y);
+      });
+    }
+    const int idx = (int)nodes.size();
+    nodes.push_back(rthx::Bvh2Node{});
+    Box lb, rb;
+    const int32_t l = build(b, mid, level + 1, lb);
+    const int32_t r = build(mid, e, level + 1, rb);
+    set_child(idx, 0, l, lb);
+    set_child(idx, 1, r, rb);
     return idx;
   }
-  int axis = 0;
-  for (int k = 1; k < 3; ++k)
-    if (chi[k] - clo[k] > chi[axis] - clo[axis]) axis = k;
-  const int mid = b + (e - b) / 2;
-  std::nth_element(order.begin() + b, order.begin() + mid, order.begin() + e, [&](int x, int y) {
-    return bt[x].c[axis] < bt[y].c[axis] || (bt[x].c[axis] == bt[y].c[axis] && x < y);
-  });
-  const int left = build_bvh(nodes, order, bt, b, mid, pad);
-  const int right = build_bvh(nodes, order, bt, mid, e, pad);
-  nodes[idx].a = left;
-  nodes[idx].b = right;
-  return idx;
+};
+
+// Builds the two-child BVH; the root is always inner node 0 (a scene of
+// <= kLeafTris triangles gets one leaf and one empty child).  Returns the
+// inner-node depth.
+int build_bvh2(std::vector<rthx::Bvh2Node>& nodes, std::vector<int>& order, const std::vector<BuildTri>& bt, double pad,
+               bool median) {
+  nodes.clear();
+  std::iota(order.begin(), order.end(), 0);
+  Bvh2Builder B{nodes, order, bt, pad, median};
+  const int n = (int)order.size();
+  if (n <= kLeafTris) {
+    nodes.push_back(rthx::Bvh2Node{});
+    Box bx, empty;
+    for (int i = 0; i < n; ++i) bx.grow(bt[i].lo, bt[i].hi);
+    B.set_child(0, 0, leaf_ref(0, n), bx);
+    B.set_child(0, 1, leaf_ref(0, 0), empty);
+    return 1;
+  }
+  Box root;
+  B.build(0, n, 0, root);
+  return B.depth;
 }
 
 }  // namespace
@@ -184,25 +299,17 @@ RTHX_EXPORT int rthx_scene3d_create(const double* xyz, const int32_t* nv, const 
       bt.push_back(B);
     }
   }
-  const double extent = std::max({shi[0] - slo[0], shi[1] - slo[1], shi[2] - slo[2]});
+  // fp32 box padding: covers the rounding of the fp32 slab test for any ray
+  // that stays within the scene scale
+  double scale = 0.0;
+  for (int k = 0; k < 3; ++k) scale = std::max({scale, std::fabs(slo[k]), std::fabs(shi[k]), shi[k] - slo[k]});
   std::vector<int> order(tris.size());
-  std::iota(order.begin(), order.end(), 0);
-  std::vector<rthx::BvhNode> nodes;
-  nodes.reserve(2 * tris.size());
-  build_bvh(nodes, order, bt, 0, (int)tris.size(), 1e-9 * extent);
-  // depth bound for the fixed device stack
-  std::vector<std::pair<int, int>> st{{0, 1}};
-  int depth = 0;
-  while (!st.empty()) {
-    auto [i, dpt] = st.back();
-    st.pop_back();
-    depth = std::max(depth, dpt);
-    if (nodes[i].a >= 0) {
-      st.push_back({nodes[i].a, dpt + 1});
-      st.push_back({nodes[i].b, dpt + 1});
-    }
-  }
-  if (depth + 1 >= rthx::kBvhStack) return fail(RTHX_ERANGE, "BVH too deep");
+  std::vector<rthx::Bvh2Node> nodes;
+  nodes.reserve(tris.size());
+  int depth = build_bvh2(nodes, order, bt, rthx::kBoxPad * scale, false);
+  if (depth > rthx::kBvhStack) depth = build_bvh2(nodes, order, bt, rthx::kBoxPad * scale, true);
+  if (depth > rthx::kBvhStack) return fail(RTHX_ERANGE, "BVH too deep for the traversal stack");
+  if (tris.size() >= (size_t(1) << (30 - rthx::kLeafBits))) return fail(RTHX_ERANGE, "too many triangles");
   std::vector<rthx::Tri3> tris_sorted(tris.size());
   for (size_t i = 0; i < order.size(); ++i) tris_sorted[i] = tris[order[i]];
   std::vector<double> tables(rthx::kTableDoubles);
@@ -229,7 +336,7 @@ RTHX_EXPORT int rthx_scene3d_create(const double* xyz, const int32_t* nv, const 
   };
   if (!up(s->polys, polys.data(), polys.size() * sizeof(rthx::Emit3)) ||
       !up(s->tris, tris_sorted.data(), tris_sorted.size() * sizeof(rthx::Tri3)) ||
-      !up(s->nodes, nodes.data(), nodes.size() * sizeof(rthx::BvhNode)) ||
+      !up(s->nodes, nodes.data(), nodes.size() * sizeof(rthx::Bvh2Node)) ||
       !up(s->tables, tables.data(), tables.size() * 8))
     return bail(fail(RTHX_ENOMEM, "uploading the 3D scene"));
   s->S.n_poly = (int32_t)n;
@@ -237,7 +344,7 @@ RTHX_EXPORT int rthx_scene3d_create(const double* xyz, const int32_t* nv, const 
   s->S.n_nodes = (int32_t)nodes.size();
   s->S.polys = s->polys.as<rthx::Emit3>();
   s->S.tris = s->tris.as<rthx::Tri3>();
-  s->S.nodes = s->nodes.as<rthx::BvhNode>();
+  s->S.nodes = s->nodes.as<rthx::Bvh2Node>();
   s->S.tables = s->tables.as<double>();
   if (!up(s->scene, &s->S, sizeof(s->S))) return bail(fail(RTHX_ENOMEM, "uploading the 3D scene"));
   *out = s;
@@ -262,8 +369,8 @@ RTHX_EXPORT int rthx_trace_exchange_3d(rthx_scene3d* sc, const rthx_trace_args* 
   const int64_t end = std::min<int64_t>(a->emitter_end, N);
   const int64_t n_rows = end > a->emitter_begin ? (end - a->emitter_begin + a->emitter_stride - 1) / a->emitter_stride : 0;
   const size_t lds_bytes = (size_t)N * 4;
-  if (lds_bytes + rthx::kTableDoubles * 8 + 512 > rthx::kMaxLdsBytes)
-    return fail(RTHX_ERANGE, "N too large for the LDS row histogram of the 3D tracer (N <= 38600)");
+  if (lds_bytes + rthx::kTrace3dStaticLds > rthx::kMaxLdsBytes)
+    return fail(RTHX_ERANGE, "N too large for the LDS row histogram of the 3D tracer (N <= 33700)");
   int64_t split = 1;
   if (n_rows > 0 && R >= 2 * kSplitMinRays)
     split = std::max<int64_t>(1, std::min<int64_t>((kSplitTargetBlocks + n_rows - 1) / n_rows, R / kSplitMinRays));

@@ -27,22 +27,36 @@ struct alignas(16) Tri3 {
   int32_t id;         // triangle index before the BVH permutation (hit ties)
 };
 
-// BVH node: bounds; a >= 0: children a, b; a < 0: leaf, triangles [~a, ~a + b).
-struct alignas(16) BvhNode {
-  double lo[3], hi[3];
-  int32_t a, b;
+// Binary BVH node holding both children's bounds (the walk tests both
+// children of the node it reads and descends into the nearer).  Bounds are
+// fp32, padded outward by kBoxPad of the scene scale and rounded outward, so
+// the fp32 slab test never rejects a box that the exact ray enters before the
+// best hit so far.  Child reference: >= 0 an inner node;
+// < 0 a leaf ~(first << 3 | count), triangles [first, first + count).
+struct alignas(16) Bvh2Node {
+  float lo[2][3], hi[2][3];
+  int32_t child[2];
+  int32_t pad[2];
 };
+static_assert(sizeof(Bvh2Node) == 64, "Bvh2Node is one 64-byte record");
+
+constexpr int kLeafBits = 3;       // up to 7 triangles per leaf reference
+constexpr double kBoxPad = 1e-5;   // fp32 box padding, relative to the scene scale
 
 struct DevScene3D {
   int32_t n_poly, n_tri, n_nodes, reserved;
   const Emit3* polys;
   const Tri3* tris;
-  const BvhNode* nodes;
+  const Bvh2Node* nodes;
   const double* tables;  // kTableDoubles (cos/sin table for the azimuth)
 };
 
 constexpr uint32_t kTrace3dTag = 0x40000000u;  // Philox counter word 3 of the 3D tracer
-constexpr int kBvhStack = 64;
+constexpr int kBvhStack = 24;  // per-lane traversal stack in LDS (entries); deeper BVHs are rebuilt balanced
+
+constexpr int kTrace3dThreads = 256;
+// static LDS of the 3D kernel: walk stacks, cos table, emitter, counters
+constexpr size_t kTrace3dStaticLds = 4 * kBvhStack * kTrace3dThreads + 16 * kCosTable + 512;
 
 struct Trace3dLaunch {
   const DevScene3D* S;

@@ -25,7 +25,11 @@
 namespace rthx {
 namespace t3 {
 
-constexpr int kThreads = 256;
+constexpr int kThreads = kTrace3dThreads;
+
+#ifndef RTHX_T3_REFILL
+#define RTHX_T3_REFILL 0
+#endif
 
 __device__ __forceinline__ double dot3(const double* a, const double* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
 __device__ __forceinline__ void cross3(const double* a, const double* b, double* c) {
@@ -52,49 +56,92 @@ __device__ __forceinline__ double moller_trumbore(const Tri3& T, const double* o
   return dot3(T.e2, q) * inv;
 }
 
-// Nearest triangle along o + t d (t > 0) not on polygon `skip`: the absorbing
-// polygon, or -1 if the ray leaves through a crack.
-__device__ int nearest_hit(const DevScene3D& S, const double* o, const double* d, int skip) {
-  const double inv[3] = {1.0 / d[0], 1.0 / d[1], 1.0 / d[2]};
-  double best_t = __builtin_inf();
-  int best_id = 0x7FFFFFFF, best_poly = -1;
-  int stack[kBvhStack];
-  int sp = 0;
-  stack[sp++] = 0;
-  while (sp > 0) {
-    const BvhNode nd = S.nodes[stack[--sp]];
-    double tn = 0.0, tf = best_t;
+constexpr int kWalkDone = INT32_MIN;  // empty stack (leaf references are > INT32_MIN)
+
+// Nearest-hit walk of one ray along o + t d (t > 0), skipping the triangles
+// of polygon `skip` (the emitter): the absorbing polygon, or -1 if the ray
+// leaves through a crack.  Two-child BVH (Bvh2Node): both children of a node
+// are slab-tested in fp32 against the padded boxes, the nearer hit child is
+// visited next and the farther one goes on the lane's stack in LDS
+// (stk[level * kThreads], conflict-free across the wave); leaves run the
+// fp64 Moeller-Trumbore test.  Pruning only drops boxes that no hit at
+// t <= best_t can lie in, and ties on t go to the lower triangle index, so
+// the result is the brute-force nearest hit of the oracle.
+struct Walk {
+  double o[3], d[3];
+  float inv[3], oi[3];
+  double best_t;
+  float best_tf;  // fp32 upper bound of best_t
+  int best_id, best_poly, node, sp;
+
+  __device__ __forceinline__ void init(const double* o_, const double* d_) {
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-      const double t0 = (nd.lo[k] - o[k]) * inv[k], t1 = (nd.hi[k] - o[k]) * inv[k];
-      tn = fmax(tn, fmin(t0, t1));
-      tf = fmin(tf, fmax(t0, t1));
+      o[k] = o_[k];
+      d[k] = d_[k];
+      inv[k] = 1.0f / (float)d[k];
+      oi[k] = (float)o[k] * inv[k];
     }
-    if (tn > tf) continue;
-    if (nd.a < 0) {
-      const int first = ~nd.a;
-      for (int k = first; k < first + nd.b; ++k) {
-        const Tri3 T = S.tris[k];
-        if (T.poly == skip) continue;
-        const double t = moller_trumbore(T, o, d);
-        if (t > 0.0 && (t < best_t || (t == best_t && T.id < best_id))) {
-          best_t = t;
-          best_id = T.id;
-          best_poly = T.poly;
-        }
-      }
-    } else if (sp + 2 <= kBvhStack) {
-      stack[sp++] = nd.b;
-      stack[sp++] = nd.a;
-    }
+    best_t = __builtin_inf();
+    best_tf = __builtin_inff();
+    best_id = 0x7FFFFFFF;
+    best_poly = -1;
+    node = 0;
+    sp = 0;
   }
-  return best_poly;
-}
 
-// One ray (g, r): emission point and cosine-law direction, then the walk.
+  // Descends to the next leaf and tests its triangles; false once the walk
+  // is over (best_poly is then the result).
+  __device__ __forceinline__ bool step(const DevScene3D& S, int skip, int RTHX_LDS* stk) {
+    while (node >= 0) {
+      const Bvh2Node nd = S.nodes[node];
+      float tn[2], tf[2];
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const float a0 = __builtin_fmaf(nd.lo[c][0], inv[0], -oi[0]), b0 = __builtin_fmaf(nd.hi[c][0], inv[0], -oi[0]);
+        const float a1 = __builtin_fmaf(nd.lo[c][1], inv[1], -oi[1]), b1 = __builtin_fmaf(nd.hi[c][1], inv[1], -oi[1]);
+        const float a2 = __builtin_fmaf(nd.lo[c][2], inv[2], -oi[2]), b2 = __builtin_fmaf(nd.hi[c][2], inv[2], -oi[2]);
+        // NaN (0 * inf on an axis the ray runs parallel to) drops out of
+        // fminf/fmaxf: that axis then does not prune (conservative)
+        tn[c] = fmaxf(fmaxf(fminf(a0, b0), fminf(a1, b1)), fmaxf(fminf(a2, b2), 0.0f));
+        tf[c] = fminf(fminf(fmaxf(a0, b0), fmaxf(a1, b1)), fminf(fmaxf(a2, b2), best_tf));
+      }
+      const bool h0 = tn[0] <= tf[0], h1 = tn[1] <= tf[1];
+      if (h0 && h1) {
+        const bool near0 = tn[0] <= tn[1];
+        stk[sp * kThreads] = near0 ? nd.child[1] : nd.child[0];
+        ++sp;
+        node = near0 ? nd.child[0] : nd.child[1];
+      } else if (h0 || h1) {
+        node = h0 ? nd.child[0] : nd.child[1];
+      } else {
+        node = sp > 0 ? stk[--sp * kThreads] : kWalkDone;
+      }
+    }
+    if (node == kWalkDone) return false;
+    const int ref = ~node;
+    const int first = ref >> kLeafBits, last = first + (ref & ((1 << kLeafBits) - 1));
+    for (int k = first; k < last; ++k) {
+      const Tri3 T = S.tris[k];
+      if (T.poly == skip) continue;
+      const double t = moller_trumbore(T, o, d);
+      if (t > 0.0 && (t < best_t || (t == best_t && T.id < best_id))) {
+        best_t = t;
+        best_id = T.id;
+        best_poly = T.poly;
+        best_tf = (float)(best_t * (1.0 + 1e-6));
+      }
+    }
+    node = sp > 0 ? stk[--sp * kThreads] : kWalkDone;
+    return node != kWalkDone;
+  }
+};
+
+// Emission of ray (g, r): a uniform point on the polygon and a cosine-law
+// direction about its normal.
 template <bool FAITHFUL>
-__device__ __forceinline__ int trace_ray(const DevScene3D& S, const Emit3& E, const double* tab, uint32_t g, uint32_t r,
-                                         uint32_t k0, uint32_t k1) {
+__device__ __forceinline__ void emit_ray(const Emit3& E, const double* tab, uint32_t g, uint32_t r, uint32_t k0,
+                                         uint32_t k1, double* o, double* d) {
   const RayDraws rd(r, g, 0u, kTrace3dTag, k0, k1);
   const double R1 = rd.R1(), R2 = rd.R2();
   const double s1 = sqrt(R1);
@@ -105,7 +152,6 @@ __device__ __forceinline__ int trace_ray(const DevScene3D& S, const Emit3& E, co
     ib = 3;
     ic = 0;
   }
-  double o[3], d[3];
 #pragma unroll
   for (int k = 0; k < 3; ++k) o[k] = wa * E.v[ia][k] + wb * E.v[ib][k] + wc * E.v[ic][k];
   const double u3 = rd.path();
@@ -122,7 +168,6 @@ __device__ __forceinline__ int trace_ray(const DevScene3D& S, const Emit3& E, co
   const double a = st * cphi, b = st * sphi;
 #pragma unroll
   for (int k = 0; k < 3; ++k) d[k] = a * E.t1[k] + b * E.t2[k] + ct * E.n[k];
-  return nearest_hit(S, o, d, (int)g);
 }
 
 // Grid: n_rows * split workgroups; workgroup (slot, part) traces rays
@@ -131,9 +176,11 @@ template <bool FAITHFUL>
 __global__ __launch_bounds__(kThreads) void trace_exchange_3d_kernel(const DevScene3D* __restrict__ Sp, TraceParams P,
                                                                     TallyParams T) {
   extern __shared__ uint32_t hist[];
-  __shared__ double s_tab[kTableDoubles];
+  __shared__ double s_tab[2 * kCosTable];        // (cos, sin)(2 pi j / 256)
+  __shared__ int s_stack[kBvhStack * kThreads];  // per-lane BVH walk stacks, [level][lane]
   __shared__ Emit3 s_emit;
   __shared__ uint32_t s_tallied;
+  __shared__ uint32_t s_next;  // next ray of the slice (RTHX_T3_REFILL)
   const DevScene3D& S = *Sp;
   const int tid = threadIdx.x;
   const int64_t slot = blockIdx.x / T.split, part = blockIdx.x % T.split;
@@ -144,20 +191,62 @@ __global__ __launch_bounds__(kThreads) void trace_exchange_3d_kernel(const DevSc
   const int64_t N = T.n_emitters;
   for (int64_t i = tid; i < N; i += kThreads) hist[i] = 0u;
   if (!FAITHFUL)
-    for (int i = tid; i < kTableDoubles; i += kThreads) s_tab[i] = S.tables[i];
+    for (int i = tid; i < 2 * kCosTable; i += kThreads) s_tab[i] = S.tables[i];
   if (tid == 0) {
     s_emit = S.polys[g];
     s_tallied = 0u;
+    s_next = (uint32_t)r_begin;
   }
   __syncthreads();
   uint32_t tallied = 0;
-  for (int64_t r = r_begin + tid; r < r_end; r += kThreads) {
-    const Emit3 RTHX_LDS* em = lds_opaque(&s_emit);
-    const int a = trace_ray<FAITHFUL>(S, *(const Emit3*)em, (const double*)lds_opaque(&s_tab[0]), (uint32_t)g,
-                                      (uint32_t)r, P.key0, P.key1);
+  int RTHX_LDS* stk = (int RTHX_LDS*)&s_stack[tid];
+  auto tally = [&](int a) {
     if (a >= 0) {
       atomicAdd(&hist[a], 1u);
       ++tallied;
+    }
+  };
+  if (RTHX_T3_REFILL) {
+    // Ray regeneration: a lane whose walk has ended takes the row's next ray
+    // from an LDS counter (batched: once kRefill lanes of the wave idle), so
+    // waves do not idle until their longest walk ends.
+    constexpr int kRefill = 16;
+    Walk w;
+    bool live = false, more = true;
+    while (true) {
+      if (more) {
+        if (__popcll(__ballot(!live)) >= kRefill || __ballot(live) == 0ull) {
+          if (!live) {
+            const uint32_t r = atomicAdd(&s_next, 1u);
+            if (r < (uint32_t)r_end) {
+              const Emit3 RTHX_LDS* em = lds_opaque(&s_emit);
+              double o[3], d[3];
+              emit_ray<FAITHFUL>(*(const Emit3*)em, (const double*)lds_opaque(&s_tab[0]), (uint32_t)g, r, P.key0,
+                                 P.key1, o, d);
+              w.init(o, d);
+              live = true;
+            }
+          }
+          more = __ballot(!live) == 0ull;
+        }
+      }
+      if (__ballot(live) == 0ull) break;
+      if (live && !w.step(S, (int)g, stk)) {
+        tally(w.best_poly);
+        live = false;
+      }
+    }
+  } else {
+    for (int64_t r = r_begin + tid; r < r_end; r += kThreads) {
+      const Emit3 RTHX_LDS* em = lds_opaque(&s_emit);
+      double o[3], d[3];
+      emit_ray<FAITHFUL>(*(const Emit3*)em, (const double*)lds_opaque(&s_tab[0]), (uint32_t)g, (uint32_t)r, P.key0,
+                         P.key1, o, d);
+      Walk w;
+      w.init(o, d);
+      while (w.step(S, (int)g, stk)) {
+      }
+      tally(w.best_poly);
     }
   }
   for (int off = 32; off > 0; off >>= 1) tallied += __shfl_xor(tallied, off);

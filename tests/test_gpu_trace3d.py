@@ -92,3 +92,31 @@ def test_errors(hip):
         assert info["nnz"] == 0 and rp[-1] == 0
     finally:
         s.close()
+
+
+def test_far_from_origin_and_single_leaf_scenes(hip):
+    """The walk tests fp32 boxes padded relative to the scene scale
+    (rthx_trace3d.h kBoxPad): a config-4 scene moved far from the origin and
+    shrunk must still give the brute-force counts, and so must a tetrahedron
+    (4 triangles: one leaf under the root)."""
+    xyz, nv, nrm, nc = H.cube_icosphere_scene(ndim=3, level=2)
+    moved = np.ascontiguousarray(xyz * 1e-3 + np.array([250.0, -1000.0, 37.5]))
+    D, info = gpu_dense(moved, nv, nrm, 3000, seed=9)
+    C, lost = oracle.trace_exchange_3d(moved, nv, nrm, 3000, seed=9, nthreads=16)
+    assert np.array_equal(D, C) and info["lost_total"] == lost
+    v = np.array([[0.0, 0.0, 0.0], [1.0, 0.0, 0.0], [0.0, 1.0, 0.0], [0.0, 0.0, 1.0]])
+    faces = [(0, 1, 2), (0, 1, 3), (0, 2, 3), (1, 2, 3)]
+    cen = v.mean(axis=0)
+    xyz4 = np.zeros((4, 4, 3))
+    nrm4 = np.zeros((4, 3))
+    for i, f in enumerate(faces):
+        p = v[list(f)]
+        xyz4[i, :3] = p
+        xyz4[i, 3] = p[2]
+        n = np.cross(p[1] - p[0], p[2] - p[0])
+        nrm4[i] = n if np.dot(n, cen - p.mean(axis=0)) > 0 else -n
+    nv4 = np.full(4, 3, dtype=np.int32)
+    D4, info4 = gpu_dense(xyz4, nv4, nrm4, 20000, seed=10)
+    C4, lost4 = oracle.trace_exchange_3d(xyz4, nv4, nrm4, 20000, seed=10, nthreads=16)
+    assert np.array_equal(D4, C4) and info4["lost_total"] == lost4
+    assert np.all(np.diag(D4) == 0) and lost4 == 0
