@@ -1324,26 +1324,29 @@ typedef struct {
   int poly;
 } t3_tri;
 
-static double t3_dot(const double* a, const double* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+/* Products fused with fma() exactly where the device kernel fuses them
+ * (csrc/rthx_trace3d_kernels.hip dot3 / cross3); the rest uncontracted. */
+static double t3_dot(const double* a, const double* b) { return fma(a[0], b[0], fma(a[1], b[1], a[2] * b[2])); }
 static void t3_cross(const double* a, const double* b, double* c) {
-  c[0] = a[1] * b[2] - a[2] * b[1];
-  c[1] = a[2] * b[0] - a[0] * b[2];
-  c[2] = a[0] * b[1] - a[1] * b[0];
+  c[0] = fma(a[1], b[2], -(a[2] * b[1]));
+  c[1] = fma(a[2], b[0], -(a[0] * b[2]));
+  c[2] = fma(a[0], b[1], -(a[1] * b[0]));
 }
 
+/* Moeller-Trumbore with the division deferred (the paper's culling branch):
+ * U = s.p, V = d.q, W = e2.q against det with signs normalised to det > 0;
+ * t = W / det only for a hit.  Returns t or -1. */
 static double t3_mt(const t3_tri* T, const double* o, const double* d) {
   double p[3], q[3], s[3];
   t3_cross(d, T->e2, p);
   double det = t3_dot(T->e1, p);
-  if (det == 0.0) return -1.0;
-  double inv = 1.0 / det;
   s[0] = o[0] - T->v0[0]; s[1] = o[1] - T->v0[1]; s[2] = o[2] - T->v0[2];
-  double u = t3_dot(s, p) * inv;
-  if (u < 0.0 || u > 1.0) return -1.0;
+  double U = t3_dot(s, p);
   t3_cross(s, T->e1, q);
-  double v = t3_dot(d, q) * inv;
-  if (v < 0.0 || u + v > 1.0) return -1.0;
-  return t3_dot(T->e2, q) * inv;
+  double V = t3_dot(d, q), W = t3_dot(T->e2, q);
+  if (det < 0.0) { det = -det; U = -U; V = -V; W = -W; }
+  if (!(det > 0.0) || !(U >= 0.0) || !(V >= 0.0) || !(U + V <= det) || !(W > 0.0)) return -1.0;
+  return W / det;
 }
 
 typedef struct {

@@ -342,6 +342,7 @@ RTHX_EXPORT int rthx_scene3d_create(const double* xyz, const int32_t* nv, const 
   s->S.n_poly = (int32_t)n;
   s->S.n_tri = (int32_t)tris.size();
   s->S.n_nodes = (int32_t)nodes.size();
+  s->S.stack = depth;
   s->S.polys = s->polys.as<rthx::Emit3>();
   s->S.tris = s->tris.as<rthx::Tri3>();
   s->S.nodes = s->nodes.as<rthx::Bvh2Node>();
@@ -368,9 +369,9 @@ RTHX_EXPORT int rthx_trace_exchange_3d(rthx_scene3d* sc, const rthx_trace_args* 
   const int64_t N = sc->n_poly, R = a->rays_per_emitter;
   const int64_t end = std::min<int64_t>(a->emitter_end, N);
   const int64_t n_rows = end > a->emitter_begin ? (end - a->emitter_begin + a->emitter_stride - 1) / a->emitter_stride : 0;
-  const size_t lds_bytes = (size_t)N * 4;
+  const size_t lds_bytes = rthx::trace3d_dynamic_lds(N, sc->S.stack);
   if (lds_bytes + rthx::kTrace3dStaticLds > rthx::kMaxLdsBytes)
-    return fail(RTHX_ERANGE, "N too large for the LDS row histogram of the 3D tracer (N <= 33700)");
+    return fail(RTHX_ERANGE, "N too large for the LDS row histogram and walk stacks of the 3D tracer");
   int64_t split = 1;
   if (n_rows > 0 && R >= 2 * kSplitMinRays)
     split = std::max<int64_t>(1, std::min<int64_t>((kSplitTargetBlocks + n_rows - 1) / n_rows, R / kSplitMinRays));

@@ -44,7 +44,8 @@ constexpr int kLeafBits = 3;       // up to 7 triangles per leaf reference
 constexpr double kBoxPad = 1e-5;   // fp32 box padding, relative to the scene scale
 
 struct DevScene3D {
-  int32_t n_poly, n_tri, n_nodes, reserved;
+  int32_t n_poly, n_tri, n_nodes;
+  int32_t stack;  // walk stack entries a lane needs (inner-node depth of the BVH)
   const Emit3* polys;
   const Tri3* tris;
   const Bvh2Node* nodes;
@@ -52,11 +53,18 @@ struct DevScene3D {
 };
 
 constexpr uint32_t kTrace3dTag = 0x40000000u;  // Philox counter word 3 of the 3D tracer
-constexpr int kBvhStack = 24;  // per-lane traversal stack in LDS (entries); deeper BVHs are rebuilt balanced
+// Per-lane walk stack in LDS: the scene's inner-node depth of entries (a
+// deeper SAH tree is rebuilt with median splits; deeper still is an error).
+constexpr int kBvhStack = 32;
 
 constexpr int kTrace3dThreads = 256;
-// static LDS of the 3D kernel: walk stacks, cos table, emitter, counters
-constexpr size_t kTrace3dStaticLds = 4 * kBvhStack * kTrace3dThreads + 16 * kCosTable + 512;
+// static LDS of the 3D kernel: cos table, emitter, counters
+constexpr size_t kTrace3dStaticLds = 16 * kCosTable + 512;
+// dynamic LDS: the row histogram (N words, padded to 64) then the stacks
+__host__ __device__ constexpr size_t trace3d_stack_offset(int64_t n) { return (size_t)((n + 63) & ~int64_t(63)); }
+__host__ __device__ constexpr size_t trace3d_dynamic_lds(int64_t n, int stack) {
+  return 4 * (trace3d_stack_offset(n) + (size_t)stack * kTrace3dThreads);
+}
 
 struct Trace3dLaunch {
   const DevScene3D* S;

@@ -27,33 +27,39 @@ namespace t3 {
 
 constexpr int kThreads = kTrace3dThreads;
 
-#ifndef RTHX_T3_REFILL
-#define RTHX_T3_REFILL 0
-#endif
-
-__device__ __forceinline__ double dot3(const double* a, const double* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+// Products are fused exactly where the CPU restatement fuses them (fma() in
+// oracle/rthx_oracle.c t3_mt); everything else is built uncontracted.
+__device__ __forceinline__ double dot3(const double* a, const double* b) {
+  return __builtin_fma(a[0], b[0], __builtin_fma(a[1], b[1], a[2] * b[2]));
+}
 __device__ __forceinline__ void cross3(const double* a, const double* b, double* c) {
-  c[0] = a[1] * b[2] - a[2] * b[1];
-  c[1] = a[2] * b[0] - a[0] * b[2];
-  c[2] = a[0] * b[1] - a[1] * b[0];
+  c[0] = __builtin_fma(a[1], b[2], -(a[2] * b[1]));
+  c[1] = __builtin_fma(a[2], b[0], -(a[0] * b[2]));
+  c[2] = __builtin_fma(a[0], b[1], -(a[1] * b[0]));
 }
 
-// Moeller-Trumbore (J. Graphics Tools 2(1), 1997): t of the hit or -1.
+// Moeller-Trumbore (J. Graphics Tools 2(1), 1997) with the division
+// deferred, as in the paper's culling branch: U = s.p, V = d.q, T = e2.q are
+// compared against det (signs normalised to det > 0) and t = T / det is
+// formed only for a hit.  Returns t, or -1 for a miss.
 __device__ __forceinline__ double moller_trumbore(const Tri3& T, const double* o, const double* d) {
   double p[3], q[3], s[3];
   cross3(d, T.e2, p);
-  const double det = dot3(T.e1, p);
-  if (det == 0.0) return -1.0;
-  const double inv = 1.0 / det;
+  double det = dot3(T.e1, p);
   s[0] = o[0] - T.v0[0];
   s[1] = o[1] - T.v0[1];
   s[2] = o[2] - T.v0[2];
-  const double u = dot3(s, p) * inv;
-  if (u < 0.0 || u > 1.0) return -1.0;
+  double U = dot3(s, p);
   cross3(s, T.e1, q);
-  const double v = dot3(d, q) * inv;
-  if (v < 0.0 || u + v > 1.0) return -1.0;
-  return dot3(T.e2, q) * inv;
+  double V = dot3(d, q), W = dot3(T.e2, q);
+  if (det < 0.0) {
+    det = -det;
+    U = -U;
+    V = -V;
+    W = -W;
+  }
+  if (!(det > 0.0) || !(U >= 0.0) || !(V >= 0.0) || !(U + V <= det) || !(W > 0.0)) return -1.0;
+  return W / det;
 }
 
 constexpr int kWalkDone = INT32_MIN;  // empty stack (leaf references are > INT32_MIN)
@@ -67,12 +73,17 @@ constexpr int kWalkDone = INT32_MIN;  // empty stack (leaf references are > INT3
 // fp64 Moeller-Trumbore test.  Pruning only drops boxes that no hit at
 // t <= best_t can lie in, and ties on t go to the lower triangle index, so
 // the result is the brute-force nearest hit of the oracle.
+//
+// Speculative traversal (Aila & Laine, HPG 2009): a lane that reaches a leaf
+// postpones it and keeps walking until every lane of the wave holds a leaf
+// (or is done); the leaves are then tested together, so the fp64 triangle
+// tests run with most lanes active instead of one lane at a time.
 struct Walk {
   double o[3], d[3];
   float inv[3], oi[3];
   double best_t;
   float best_tf;  // fp32 upper bound of best_t
-  int best_id, best_poly, node, sp;
+  int best_id, best_poly;
 
   __device__ __forceinline__ void init(const double* o_, const double* d_) {
 #pragma unroll
@@ -86,40 +97,10 @@ struct Walk {
     best_tf = __builtin_inff();
     best_id = 0x7FFFFFFF;
     best_poly = -1;
-    node = 0;
-    sp = 0;
   }
 
-  // Descends to the next leaf and tests its triangles; false once the walk
-  // is over (best_poly is then the result).
-  __device__ __forceinline__ bool step(const DevScene3D& S, int skip, int RTHX_LDS* stk) {
-    while (node >= 0) {
-      const Bvh2Node nd = S.nodes[node];
-      float tn[2], tf[2];
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        const float a0 = __builtin_fmaf(nd.lo[c][0], inv[0], -oi[0]), b0 = __builtin_fmaf(nd.hi[c][0], inv[0], -oi[0]);
-        const float a1 = __builtin_fmaf(nd.lo[c][1], inv[1], -oi[1]), b1 = __builtin_fmaf(nd.hi[c][1], inv[1], -oi[1]);
-        const float a2 = __builtin_fmaf(nd.lo[c][2], inv[2], -oi[2]), b2 = __builtin_fmaf(nd.hi[c][2], inv[2], -oi[2]);
-        // NaN (0 * inf on an axis the ray runs parallel to) drops out of
-        // fminf/fmaxf: that axis then does not prune (conservative)
-        tn[c] = fmaxf(fmaxf(fminf(a0, b0), fminf(a1, b1)), fmaxf(fminf(a2, b2), 0.0f));
-        tf[c] = fminf(fminf(fmaxf(a0, b0), fmaxf(a1, b1)), fminf(fmaxf(a2, b2), best_tf));
-      }
-      const bool h0 = tn[0] <= tf[0], h1 = tn[1] <= tf[1];
-      if (h0 && h1) {
-        const bool near0 = tn[0] <= tn[1];
-        stk[sp * kThreads] = near0 ? nd.child[1] : nd.child[0];
-        ++sp;
-        node = near0 ? nd.child[0] : nd.child[1];
-      } else if (h0 || h1) {
-        node = h0 ? nd.child[0] : nd.child[1];
-      } else {
-        node = sp > 0 ? stk[--sp * kThreads] : kWalkDone;
-      }
-    }
-    if (node == kWalkDone) return false;
-    const int ref = ~node;
+  __device__ __forceinline__ void leaf(const DevScene3D& S, int skip, int ref) {
+    ref = ~ref;
     const int first = ref >> kLeafBits, last = first + (ref & ((1 << kLeafBits) - 1));
     for (int k = first; k < last; ++k) {
       const Tri3 T = S.tris[k];
@@ -132,8 +113,51 @@ struct Walk {
         best_tf = (float)(best_t * (1.0 + 1e-6));
       }
     }
-    node = sp > 0 ? stk[--sp * kThreads] : kWalkDone;
-    return node != kWalkDone;
+  }
+
+  __device__ __forceinline__ void run(const DevScene3D& S, int skip, int RTHX_LDS* stk) {
+    int node = 0, sp = 0;
+    int pending = 0;  // postponed leaf reference (< 0), 0 = none
+    while (node != kWalkDone) {
+      while (node >= 0) {
+        const Bvh2Node nd = S.nodes[node];
+        float tn[2], tf[2];
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          const float a0 = __builtin_fmaf(nd.lo[c][0], inv[0], -oi[0]), b0 = __builtin_fmaf(nd.hi[c][0], inv[0], -oi[0]);
+          const float a1 = __builtin_fmaf(nd.lo[c][1], inv[1], -oi[1]), b1 = __builtin_fmaf(nd.hi[c][1], inv[1], -oi[1]);
+          const float a2 = __builtin_fmaf(nd.lo[c][2], inv[2], -oi[2]), b2 = __builtin_fmaf(nd.hi[c][2], inv[2], -oi[2]);
+          // NaN (0 * inf on an axis the ray runs parallel to) drops out of
+          // fminf/fmaxf: that axis then does not prune (conservative)
+          tn[c] = fmaxf(fmaxf(fminf(a0, b0), fminf(a1, b1)), fmaxf(fminf(a2, b2), 0.0f));
+          tf[c] = fminf(fminf(fmaxf(a0, b0), fmaxf(a1, b1)), fminf(fmaxf(a2, b2), best_tf));
+        }
+        const bool h0 = tn[0] <= tf[0], h1 = tn[1] <= tf[1];
+        if (h0 && h1) {
+          const bool near0 = tn[0] <= tn[1];
+          stk[sp * kThreads] = near0 ? nd.child[1] : nd.child[0];
+          ++sp;
+          node = near0 ? nd.child[0] : nd.child[1];
+        } else if (h0 || h1) {
+          node = h0 ? nd.child[0] : nd.child[1];
+        } else {
+          node = sp > 0 ? stk[--sp * kThreads] : kWalkDone;
+        }
+        if (node < 0 && node != kWalkDone && pending == 0) {
+          pending = node;
+          node = sp > 0 ? stk[--sp * kThreads] : kWalkDone;
+        }
+        if (__ballot(pending == 0) == 0ull) break;
+      }
+      while (pending < 0) {
+        leaf(S, skip, pending);
+        pending = 0;
+        if (node < 0 && node != kWalkDone) {
+          pending = node;
+          node = sp > 0 ? stk[--sp * kThreads] : kWalkDone;
+        }
+      }
+    }
   }
 };
 
@@ -177,10 +201,8 @@ __global__ __launch_bounds__(kThreads) void trace_exchange_3d_kernel(const DevSc
                                                                     TallyParams T) {
   extern __shared__ uint32_t hist[];
   __shared__ double s_tab[2 * kCosTable];        // (cos, sin)(2 pi j / 256)
-  __shared__ int s_stack[kBvhStack * kThreads];  // per-lane BVH walk stacks, [level][lane]
   __shared__ Emit3 s_emit;
   __shared__ uint32_t s_tallied;
-  __shared__ uint32_t s_next;  // next ray of the slice (RTHX_T3_REFILL)
   const DevScene3D& S = *Sp;
   const int tid = threadIdx.x;
   const int64_t slot = blockIdx.x / T.split, part = blockIdx.x % T.split;
@@ -195,58 +217,21 @@ __global__ __launch_bounds__(kThreads) void trace_exchange_3d_kernel(const DevSc
   if (tid == 0) {
     s_emit = S.polys[g];
     s_tallied = 0u;
-    s_next = (uint32_t)r_begin;
   }
   __syncthreads();
   uint32_t tallied = 0;
-  int RTHX_LDS* stk = (int RTHX_LDS*)&s_stack[tid];
-  auto tally = [&](int a) {
-    if (a >= 0) {
-      atomicAdd(&hist[a], 1u);
-      ++tallied;
-    }
-  };
-  if (RTHX_T3_REFILL) {
-    // Ray regeneration: a lane whose walk has ended takes the row's next ray
-    // from an LDS counter (batched: once kRefill lanes of the wave idle), so
-    // waves do not idle until their longest walk ends.
-    constexpr int kRefill = 16;
+  int RTHX_LDS* stk = (int RTHX_LDS*)(hist + trace3d_stack_offset(N)) + tid;
+  for (int64_t r = r_begin + tid; r < r_end; r += kThreads) {
+    const Emit3 RTHX_LDS* em = lds_opaque(&s_emit);
+    double o[3], d[3];
+    emit_ray<FAITHFUL>(*(const Emit3*)em, (const double*)lds_opaque(&s_tab[0]), (uint32_t)g, (uint32_t)r, P.key0,
+                       P.key1, o, d);
     Walk w;
-    bool live = false, more = true;
-    while (true) {
-      if (more) {
-        if (__popcll(__ballot(!live)) >= kRefill || __ballot(live) == 0ull) {
-          if (!live) {
-            const uint32_t r = atomicAdd(&s_next, 1u);
-            if (r < (uint32_t)r_end) {
-              const Emit3 RTHX_LDS* em = lds_opaque(&s_emit);
-              double o[3], d[3];
-              emit_ray<FAITHFUL>(*(const Emit3*)em, (const double*)lds_opaque(&s_tab[0]), (uint32_t)g, r, P.key0,
-                                 P.key1, o, d);
-              w.init(o, d);
-              live = true;
-            }
-          }
-          more = __ballot(!live) == 0ull;
-        }
-      }
-      if (__ballot(live) == 0ull) break;
-      if (live && !w.step(S, (int)g, stk)) {
-        tally(w.best_poly);
-        live = false;
-      }
-    }
-  } else {
-    for (int64_t r = r_begin + tid; r < r_end; r += kThreads) {
-      const Emit3 RTHX_LDS* em = lds_opaque(&s_emit);
-      double o[3], d[3];
-      emit_ray<FAITHFUL>(*(const Emit3*)em, (const double*)lds_opaque(&s_tab[0]), (uint32_t)g, (uint32_t)r, P.key0,
-                         P.key1, o, d);
-      Walk w;
-      w.init(o, d);
-      while (w.step(S, (int)g, stk)) {
-      }
-      tally(w.best_poly);
+    w.init(o, d);
+    w.run(S, (int)g, stk);
+    if (w.best_poly >= 0) {
+      atomicAdd(&hist[w.best_poly], 1u);
+      ++tallied;
     }
   }
   for (int off = 32; off > 0; off >>= 1) tallied += __shfl_xor(tallied, off);
