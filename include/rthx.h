@@ -384,6 +384,12 @@ typedef struct rthx_scene3d rthx_scene3d;
 int rthx_scene3d_create(const double* xyz, const int32_t* nv, const double* normal, int64_t n, int32_t device,
                         rthx_scene3d** out);
 void rthx_scene3d_destroy(rthx_scene3d* scene);
+/* Acceleration-structure statistics of a scene (any pointer may be NULL):
+ * Moeller-Trumbore triangles, BVH inner nodes, inner-node depth (the walk
+ * stack a lane needs) and the LDS bytes one 256-lane workgroup of
+ * rthx_trace_exchange_3d takes (row histogram + walk stacks + tables). */
+int rthx_scene3d_stats(const rthx_scene3d* scene, int64_t* n_tri, int64_t* n_nodes, int32_t* depth,
+                       int64_t* lds_bytes);
 int rthx_trace_exchange_3d(rthx_scene3d* scene, const rthx_trace_args* args, rthx_result* res);
 
 #ifdef __cplusplus

@@ -37,6 +37,7 @@ struct rthx_scene3d {
   DevBuf polys, tris, nodes, tables, scene;
   rthx::DevScene3D S{};
   int64_t n_poly = 0;
+  int top_choice[4] = {-1, -1, -1, -1};  // LDS node-cache size per kernel variant (launch_trace3d)
   ~rthx_scene3d() {
     (void)hipSetDevice(device);
     for (auto& e : ev)
@@ -221,6 +222,59 @@ int build_bvh2(std::vector<rthx::Bvh2Node>& nodes, std::vector<int>& order, cons
   return B.depth;
 }
 
+// Node layout: the top kTopNodes inner nodes in breadth-first order at the
+// start of the array (the hottest nodes contiguous; the kernel may stage them
+// in LDS), every subtree below them depth-first (a walk descending one path
+// reads neighbouring records).  Child references are remapped; leaf
+// references are unchanged.  The root stays node 0.
+void layout_nodes(std::vector<rthx::Bvh2Node>& nodes) {
+  const int n = (int)nodes.size();
+  std::vector<int> order;
+  order.reserve(n);
+  std::vector<char> taken(n, 0);
+  std::vector<int> frontier{0};
+  taken[0] = 1;
+  for (size_t h = 0; h < frontier.size() && (int)order.size() < rthx::kTopNodes; ++h) {
+    const int i = frontier[h];
+    order.push_back(i);
+    for (int c = 0; c < 2; ++c) {
+      const int ch = nodes[i].child[c];
+      if (ch >= 0 && !taken[ch]) {
+        taken[ch] = 1;
+        frontier.push_back(ch);
+      }
+    }
+  }
+  std::vector<char> placed(n, 0);
+  for (int i : order) placed[i] = 1;
+  // depth-first below the breadth-first top, in frontier order
+  std::vector<int> st;
+  for (int f : frontier) {
+    if (placed[f]) continue;
+    st.push_back(f);
+    while (!st.empty()) {
+      const int i = st.back();
+      st.pop_back();
+      if (placed[i]) continue;
+      placed[i] = 1;
+      order.push_back(i);
+      for (int c = 1; c >= 0; --c) {
+        const int ch = nodes[i].child[c];
+        if (ch >= 0 && !placed[ch]) st.push_back(ch);
+      }
+    }
+  }
+  std::vector<int> pos(n);
+  for (int k = 0; k < n; ++k) pos[order[k]] = k;
+  std::vector<rthx::Bvh2Node> out(n);
+  for (int k = 0; k < n; ++k) {
+    out[k] = nodes[order[k]];
+    for (int c = 0; c < 2; ++c)
+      if (out[k].child[c] >= 0) out[k].child[c] = pos[out[k].child[c]];
+  }
+  nodes.swap(out);
+}
+
 }  // namespace
 
 RTHX_EXPORT int rthx_scene3d_create(const double* xyz, const int32_t* nv, const double* normal, int64_t n,
@@ -310,6 +364,7 @@ RTHX_EXPORT int rthx_scene3d_create(const double* xyz, const int32_t* nv, const 
   if (depth > rthx::kBvhStack) depth = build_bvh2(nodes, order, bt, rthx::kBoxPad * scale, true);
   if (depth > rthx::kBvhStack) return fail(RTHX_ERANGE, "BVH too deep for the traversal stack");
   if (tris.size() >= (size_t(1) << (30 - rthx::kLeafBits))) return fail(RTHX_ERANGE, "too many triangles");
+  layout_nodes(nodes);
   std::vector<rthx::Tri3> tris_sorted(tris.size());
   for (size_t i = 0; i < order.size(); ++i) tris_sorted[i] = tris[order[i]];
   std::vector<double> tables(rthx::kTableDoubles);
@@ -354,6 +409,16 @@ RTHX_EXPORT int rthx_scene3d_create(const double* xyz, const int32_t* nv, const 
 
 RTHX_EXPORT void rthx_scene3d_destroy(rthx_scene3d* s) { delete s; }
 
+RTHX_EXPORT int rthx_scene3d_stats(const rthx_scene3d* sc, int64_t* n_tri, int64_t* n_nodes, int32_t* depth,
+                                   int64_t* lds_bytes) {
+  if (!sc) return fail(RTHX_EINVAL, "null scene");
+  if (n_tri) *n_tri = sc->S.n_tri;
+  if (n_nodes) *n_nodes = sc->S.n_nodes;
+  if (depth) *depth = sc->S.stack;
+  if (lds_bytes) *lds_bytes = (int64_t)(rthx::trace3d_dynamic_lds(sc->n_poly, sc->S.stack) + rthx::kTrace3dStaticLds);
+  return RTHX_OK;
+}
+
 RTHX_EXPORT int rthx_trace_exchange_3d(rthx_scene3d* sc, const rthx_trace_args* a, rthx_result* res) {
   const double t0 = now_ms();
   if (!sc || !a || !res) return fail(RTHX_EINVAL, "null argument");
@@ -369,12 +434,13 @@ RTHX_EXPORT int rthx_trace_exchange_3d(rthx_scene3d* sc, const rthx_trace_args* 
   const int64_t N = sc->n_poly, R = a->rays_per_emitter;
   const int64_t end = std::min<int64_t>(a->emitter_end, N);
   const int64_t n_rows = end > a->emitter_begin ? (end - a->emitter_begin + a->emitter_stride - 1) / a->emitter_stride : 0;
-  const size_t lds_bytes = rthx::trace3d_dynamic_lds(N, sc->S.stack);
-  if (lds_bytes + rthx::kTrace3dStaticLds > rthx::kMaxLdsBytes)
-    return fail(RTHX_ERANGE, "N too large for the LDS row histogram and walk stacks of the 3D tracer");
   int64_t split = 1;
   if (n_rows > 0 && R >= 2 * kSplitMinRays)
     split = std::max<int64_t>(1, std::min<int64_t>((kSplitTargetBlocks + n_rows - 1) / n_rows, R / kSplitMinRays));
+  const bool pack16 = (R + split - 1) / split < 65536;
+  const size_t lds_bytes = rthx::trace3d_dynamic_lds(pack16 ? (N + 1) / 2 : N, sc->S.stack);
+  if (lds_bytes + rthx::kTrace3dStaticLds > rthx::kMaxLdsBytes)
+    return fail(RTHX_ERANGE, "N too large for the LDS row histogram and walk stacks of the 3D tracer");
   if (n_rows * split >= (int64_t(1) << 31)) return fail(RTHX_ERANGE, "too many rows in one call");
   const int64_t row_cap = std::max<int64_t>(1, std::min<int64_t>(N, R));
   res->valid = false;
@@ -432,6 +498,8 @@ RTHX_EXPORT int rthx_trace_exchange_3d(rthx_scene3d* sc, const rthx_trace_args* 
     L.lds_bytes = lds_bytes;
     L.stream = st;
     L.faithful = (a->flags & RTHX_FLAG_FAITHFUL_SAMPLING) != 0;
+    L.pack16 = pack16;
+    L.top_choice = sc->top_choice;
     HIP_TRY(rthx::launch_trace3d(L), "trace_exchange_3d_kernel launch");
   }
   HIP_TRY(hipEventRecord(sc->ev[1], st), "hipEventRecord");

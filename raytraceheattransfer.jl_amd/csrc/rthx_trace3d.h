@@ -46,10 +46,10 @@ constexpr double kBoxPad = 1e-5;   // fp32 box padding, relative to the scene sc
 struct DevScene3D {
   int32_t n_poly, n_tri, n_nodes;
   int32_t stack;  // walk stack entries a lane needs (inner-node depth of the BVH)
-  const Emit3* polys;
-  const Tri3* tris;
-  const Bvh2Node* nodes;
-  const double* tables;  // kTableDoubles (cos/sin table for the azimuth)
+  const Emit3 RTHX_GLOBAL* polys;
+  const Tri3 RTHX_GLOBAL* tris;
+  const Bvh2Node RTHX_GLOBAL* nodes;
+  const double RTHX_GLOBAL* tables;  // kTableDoubles (cos/sin table for the azimuth)
 };
 
 constexpr uint32_t kTrace3dTag = 0x40000000u;  // Philox counter word 3 of the 3D tracer
@@ -57,13 +57,21 @@ constexpr uint32_t kTrace3dTag = 0x40000000u;  // Philox counter word 3 of the 3
 // deeper SAH tree is rebuilt with median splits; deeper still is an error).
 constexpr int kBvhStack = 32;
 
-constexpr int kTrace3dThreads = 256;
-// static LDS of the 3D kernel: cos table, emitter, counters
-constexpr size_t kTrace3dStaticLds = 16 * kCosTable + 512;
-// dynamic LDS: the row histogram (N words, padded to 64) then the stacks
-__host__ __device__ constexpr size_t trace3d_stack_offset(int64_t n) { return (size_t)((n + 63) & ~int64_t(63)); }
-__host__ __device__ constexpr size_t trace3d_dynamic_lds(int64_t n, int stack) {
-  return 4 * (trace3d_stack_offset(n) + (size_t)stack * kTrace3dThreads);
+#ifndef RTHX_T3_THREADS
+#define RTHX_T3_THREADS 256
+#endif
+constexpr int kTrace3dThreads = RTHX_T3_THREADS;  // lanes per workgroup
+// Breadth-first top of the node array (rthx_trace3d.cpp layout_nodes): the
+// kernel stages the first 64 or 128 nodes in LDS (launch_trace3d).
+constexpr int kTopNodes = 128;
+// static LDS of the 3D kernel: cos table, emitter, counters and (at least)
+// the 64-node cache
+constexpr size_t kTrace3dStaticLds = 16 * kCosTable + 512 + 64 * 64;
+// dynamic LDS: the row histogram (`words` = N, or (N + 1) / 2 packed u16,
+// padded to 64), then the stacks
+__host__ __device__ constexpr size_t trace3d_stack_offset(int64_t words) { return (size_t)((words + 63) & ~int64_t(63)); }
+__host__ __device__ constexpr size_t trace3d_dynamic_lds(int64_t words, int stack) {
+  return 4 * (trace3d_stack_offset(words) + (size_t)stack * kTrace3dThreads);
 }
 
 struct Trace3dLaunch {
@@ -73,6 +81,8 @@ struct Trace3dLaunch {
   size_t lds_bytes;
   hipStream_t stream;
   bool faithful;
+  bool pack16;  // < 65536 rays per workgroup: u16 row-histogram counters
+  int* top_choice;  // [faithful * 2 + pack16]: LDS node-cache size (64 / 128), -1 = not chosen yet
 };
 
 hipError_t launch_trace3d(const Trace3dLaunch& L);

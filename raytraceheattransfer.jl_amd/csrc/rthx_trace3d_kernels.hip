@@ -18,6 +18,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "rthx_device.h"
 #include "rthx_trace3d.h"
 #include "rthx_wave.h"
@@ -26,6 +28,15 @@ namespace rthx {
 namespace t3 {
 
 constexpr int kThreads = kTrace3dThreads;
+
+#ifndef RTHX_T3_WAVES
+#define RTHX_T3_WAVES 0  // > 0: amdgpu_waves_per_eu floor (register budget) for variants
+#endif
+#if RTHX_T3_WAVES > 0
+#define RTHX_T3_ATTR __attribute__((amdgpu_waves_per_eu(RTHX_T3_WAVES)))
+#else
+#define RTHX_T3_ATTR
+#endif
 
 // Products are fused exactly where the CPU restatement fuses them (fma() in
 // oracle/rthx_oracle.c t3_mt); everything else is built uncontracted.
@@ -115,12 +126,20 @@ struct Walk {
     }
   }
 
-  __device__ __forceinline__ void run(const DevScene3D& S, int skip, int RTHX_LDS* stk) {
+  __device__ __forceinline__ void run(const DevScene3D& S, const Bvh2Node RTHX_LDS* top, int n_top, int skip,
+                                     int RTHX_LDS* stk) {
     int node = 0, sp = 0;
     int pending = 0;  // postponed leaf reference (< 0), 0 = none
     while (node != kWalkDone) {
       while (node >= 0) {
-        const Bvh2Node nd = S.nodes[node];
+        Bvh2Node nd;
+        if (node < n_top) {
+          typedef float f4 __attribute__((ext_vector_type(4)));
+          const f4 RTHX_LDS* q = (const f4 RTHX_LDS*)(top + node);
+          const f4 w[4] = {q[0], q[1], q[2], q[3]};
+          __builtin_memcpy(&nd, w, sizeof(nd));
+        } else
+          nd = S.nodes[node];
         float tn[2], tf[2];
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
@@ -196,10 +215,18 @@ __device__ __forceinline__ void emit_ray(const Emit3& E, const double* tab, uint
 
 // Grid: n_rows * split workgroups; workgroup (slot, part) traces rays
 // [part * chunk, ...) of emitter g = g_begin + slot * g_stride.
-template <bool FAITHFUL>
-__global__ __launch_bounds__(kThreads) void trace_exchange_3d_kernel(const DevScene3D* __restrict__ Sp, TraceParams P,
-                                                                    TallyParams T) {
+// TOP: breadth-first top nodes of the BVH (rthx_trace3d.cpp layout_nodes)
+// staged in static LDS; the walk reads nodes < TOP there.  A small cache
+// serves the nodes most lanes share (larger ones measured slower: lanes
+// reading different deep nodes conflict in LDS banks).
+template <bool FAITHFUL, bool PACK16, int TOP>
+__global__ __launch_bounds__(kThreads) RTHX_T3_ATTR void trace_exchange_3d_kernel(const DevScene3D* __restrict__ Sp,
+                                                                                  TraceParams P, TallyParams T) {
+  // dynamic LDS: [row histogram][walk stacks]
   extern __shared__ uint32_t hist[];
+  __shared__ Bvh2Node s_top[TOP];
+  Bvh2Node RTHX_LDS* top = (Bvh2Node RTHX_LDS*)&s_top[0];
+  const int n_top = TOP < Sp->n_nodes ? TOP : Sp->n_nodes;
   __shared__ double s_tab[2 * kCosTable];        // (cos, sin)(2 pi j / 256)
   __shared__ Emit3 s_emit;
   __shared__ uint32_t s_tallied;
@@ -211,16 +238,25 @@ __global__ __launch_bounds__(kThreads) void trace_exchange_3d_kernel(const DevSc
   const int64_t r_end = r_begin + chunk < P.R ? r_begin + chunk : P.R;
   const int64_t g = P.g_begin + slot * P.g_stride;
   const int64_t N = T.n_emitters;
-  for (int64_t i = tid; i < N; i += kThreads) hist[i] = 0u;
+  // PACK16 (fewer than 65536 rays per workgroup): two u16 counters per word
+  const int64_t words = PACK16 ? (N + 1) / 2 : N;
+  for (int64_t i = tid; i < words; i += kThreads) hist[i] = 0u;
   if (!FAITHFUL)
     for (int i = tid; i < 2 * kCosTable; i += kThreads) s_tab[i] = S.tables[i];
+  // breadth-first top of the BVH (rthx_trace3d.cpp layout_nodes)
+  {
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    const f4 RTHX_GLOBAL* src = (const f4 RTHX_GLOBAL*)S.nodes;
+    f4 RTHX_LDS* dst = (f4 RTHX_LDS*)top;
+    for (int i = tid; i < 4 * n_top; i += kThreads) dst[i] = src[i];
+  }
   if (tid == 0) {
     s_emit = S.polys[g];
     s_tallied = 0u;
   }
   __syncthreads();
   uint32_t tallied = 0;
-  int RTHX_LDS* stk = (int RTHX_LDS*)(hist + trace3d_stack_offset(N)) + tid;
+  int RTHX_LDS* stk = (int RTHX_LDS*)(hist + trace3d_stack_offset(words)) + tid;
   for (int64_t r = r_begin + tid; r < r_end; r += kThreads) {
     const Emit3 RTHX_LDS* em = lds_opaque(&s_emit);
     double o[3], d[3];
@@ -228,9 +264,12 @@ __global__ __launch_bounds__(kThreads) void trace_exchange_3d_kernel(const DevSc
                        P.key1, o, d);
     Walk w;
     w.init(o, d);
-    w.run(S, (int)g, stk);
+    w.run(S, (const Bvh2Node RTHX_LDS*)lds_opaque((const Bvh2Node*)top), n_top, (int)g, stk);
     if (w.best_poly >= 0) {
-      atomicAdd(&hist[w.best_poly], 1u);
+      if (PACK16)
+        atomicAdd(&hist[w.best_poly >> 1], 1u << ((w.best_poly & 1) * 16));
+      else
+        atomicAdd(&hist[w.best_poly], 1u);
       ++tallied;
     }
   }
@@ -239,7 +278,7 @@ __global__ __launch_bounds__(kThreads) void trace_exchange_3d_kernel(const DevSc
   __syncthreads();
   uint32_t* dense = T.dense + slot * N;
   for (int64_t i = tid; i < N; i += kThreads) {
-    const uint32_t v = hist[i];
+    const uint32_t v = PACK16 ? (hist[i >> 1] >> ((i & 1) * 16)) & 0xFFFFu : hist[i];
     if (v) atomicAdd(&dense[i], v);
   }
   if (tid == 0) atomicAdd(&T.row_tallied[slot], s_tallied);
@@ -247,8 +286,26 @@ __global__ __launch_bounds__(kThreads) void trace_exchange_3d_kernel(const DevSc
 
 }  // namespace t3
 
-hipError_t launch_trace3d(const Trace3dLaunch& L) {
-  auto kern = L.faithful ? t3::trace_exchange_3d_kernel<true> : t3::trace_exchange_3d_kernel<false>;
+namespace {
+
+template <bool FAITHFUL, bool PACK16>
+hipError_t launch_variant(const Trace3dLaunch& L) {
+  // The 128-node cache when it costs no workgroup per CU against the 64-node
+  // one (occupancy queries are slow host calls: the choice is kept per scene
+  // and kernel variant in L.top_choice).
+  int& top = L.top_choice[(FAITHFUL ? 2 : 0) + (PACK16 ? 1 : 0)];
+  if (top < 0) {
+    int pc64 = 0, pc128 = 0;
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &pc64, (const void*)t3::trace_exchange_3d_kernel<FAITHFUL, PACK16, 64>, t3::kThreads, L.lds_bytes);
+    if (e != hipSuccess) return e;
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &pc128, (const void*)t3::trace_exchange_3d_kernel<FAITHFUL, PACK16, 128>, t3::kThreads, L.lds_bytes);
+    if (e != hipSuccess) return e;
+    top = pc128 > 0 && pc128 >= pc64 ? 128 : 64;
+  }
+  auto kern = top == 128 ? t3::trace_exchange_3d_kernel<FAITHFUL, PACK16, 128>
+                         : t3::trace_exchange_3d_kernel<FAITHFUL, PACK16, 64>;
   if (L.lds_bytes > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.lds_bytes);
     if (e != hipSuccess) return e;
@@ -256,6 +313,13 @@ hipError_t launch_trace3d(const Trace3dLaunch& L) {
   const int64_t blocks = L.T.n_rows * L.T.split;
   hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(t3::kThreads), L.lds_bytes, L.stream, L.S, L.P, L.T);
   return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t launch_trace3d(const Trace3dLaunch& L) {
+  if (L.faithful) return L.pack16 ? launch_variant<true, true>(L) : launch_variant<true, false>(L);
+  return L.pack16 ? launch_variant<false, true>(L) : launch_variant<false, false>(L);
 }
 
 }  // namespace rthx

@@ -81,6 +81,9 @@ def load(path: Optional[str] = None) -> C.CDLL:
     lib.rthx_scene3d_create.argtypes = [dp, C.POINTER(C.c_int32), dp, C.c_int64, C.c_int32, C.POINTER(C.c_void_p)]
     lib.rthx_scene3d_destroy.argtypes = [C.c_void_p]
     lib.rthx_scene3d_destroy.restype = None
+    if hasattr(lib, "rthx_scene3d_stats"):  # (older A/B variant libraries lack it)
+        lib.rthx_scene3d_stats.argtypes = [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int64),
+                                           C.POINTER(C.c_int32), C.POINTER(C.c_int64)]
     lib.rthx_trace_exchange_3d.argtypes = [C.c_void_p, C.POINTER(abi.TraceArgs), C.c_void_p]
     lib.rthx_view_factors_3d.argtypes = [dp, C.POINTER(C.c_int32), C.c_int64, C.POINTER(abi.Vf3dArgs), dp, dp,
                                          C.POINTER(abi.Vf3dInfo)]

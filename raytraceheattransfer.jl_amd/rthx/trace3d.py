@@ -57,6 +57,15 @@ class Scene3D:
             res.close()
         return rp, cols, cnt, info
 
+    def stats(self) -> dict:
+        """rthx_scene3d_stats: triangles, BVH inner nodes, depth, LDS bytes per workgroup."""
+        from ._lib import check
+
+        nt, nn, ln = C.c_int64(), C.c_int64(), C.c_int64()
+        dp = C.c_int32()
+        check(self._lib.rthx_scene3d_stats(self.handle, C.byref(nt), C.byref(nn), C.byref(dp), C.byref(ln)))
+        return {"n_tri": nt.value, "n_nodes": nn.value, "depth": dp.value, "lds_bytes": ln.value}
+
     def close(self) -> None:
         if getattr(self, "handle", None):
             self._lib.rthx_scene3d_destroy(self.handle)

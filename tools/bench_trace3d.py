@@ -44,12 +44,16 @@ def main():
         _, _, _, info = scene.trace(R, device_only=True)
         cs.append(time.perf_counter() - t)
         ks.append(info["trace_ms"])
+    try:
+        stats = scene.stats()
+    except AttributeError:  # a variant library without rthx_scene3d_stats
+        stats = {}
     k = float(np.median(ks))
     c = float(np.median(cs)) * 1e3
     rays = n * R
     line = (f"config4 cube {args.ndim}x{args.ndim}/face + icosphere L{args.level} (n={n}, {n - nc} triangles, "
             f"{int(np.sum(np.where(nv == 4, 2, 1)))} MT triangles)  R={R} rays={rays:.3e}  scene build {t_build * 1e3:.0f} ms  "
-            f"kernel {k:.2f} ms ({rays / k / 1e6:.2f} Grays/s)  call {c:.2f} ms  lost {info['lost_total']}  nnz {info['nnz']}")
+            f"BVH {stats}  kernel {k:.2f} ms ({rays / k / 1e6:.2f} Grays/s)  call {c:.2f} ms  lost {info['lost_total']}  nnz {info['nnz']}")
     if args.cpu_rows > 0:
         from oracle import oracle
 
