@@ -135,6 +135,38 @@ def read_fp64_flops_per_ray():
         return None
 
 
+def read_valu_issue_per_ray():
+    """VALU issue time floor per traced ray of the trace kernel (seconds of
+    whole-chip issue): the committed SQ counters (profiles/round1/pmc_sq.json)
+    split into full-rate fp64 (ADD/MUL/FMA), fp64 transcendentals and every
+    other VALU instruction, each priced at the chip-wide issue rate that
+    tools/probe/valu_probe.hip measured for v_fma_f64, v_rcp_f64 and
+    v_fma_f32 (profiles/round1/valu_probe.json).  Instructions are per wave,
+    so one covers the 64 rays of its lanes.  Returns (seconds per ray,
+    fp64-FMA-equivalent wave-instructions per ray, peak fp64-FMA wave-instr/s)
+    or None."""
+    pq = os.path.join(ROOT, "profiles", "round1", "pmc_sq.json")
+    pp = os.path.join(ROOT, "profiles", "round1", "valu_probe.json")
+    if not (os.path.exists(pq) and os.path.exists(pp)):
+        return None
+    try:
+        with open(pq) as fh:
+            d = json.load(fh)
+        with open(pp) as fh:
+            rates = json.load(fh)["rates_wave_instr_per_s"]
+        k = next(x for x in d if TRACE_KERNEL in x)
+        c = {n: v["mean"] for n, v in d[k].items()}
+        wave_rays = float(d.get("_rays_per_launch", 99994545)) / 64.0
+        f64 = c["SQ_INSTS_VALU_ADD_F64"] + c["SQ_INSTS_VALU_MUL_F64"] + c["SQ_INSTS_VALU_FMA_F64"]
+        trans = c["SQ_INSTS_VALU_TRANS_F64"]
+        other = c["SQ_INSTS_VALU"] - f64 - trans
+        t = f64 / rates["v_fma_f64"] + trans / rates["v_rcp_f64"] + other / rates["v_fma_f32"]
+        per_ray = t / wave_rays / 64.0
+        return per_ray, per_ray * 64.0 * rates["v_fma_f64"], rates["v_fma_f64"]
+    except Exception:
+        return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -253,6 +285,18 @@ def main():
                          "unit": "TFLOP/s", "frac": round(tf / FP64_VECTOR_PEAK_TFLOPS, 4),
                          "flop_per_ray": round(fpr, 1),
                          "note": "fp64 VALU instructions per ray from profiles/round1/pmc_sq.json (SQ counters)"}
+        vi = read_valu_issue_per_ray()
+        valu_roof = None
+        if vi is not None:
+            per_ray_s, eq_per_wave_ray, peak_rate = vi
+            floor_ms = rays_rank * per_ray_s * 1e3
+            ach = rays_rank / 64.0 * eq_per_wave_ray / (avg_trace_ms * 1e-3)
+            valu_roof = {"bound": "valu-issue", "achieved": round(ach / 1e9, 2), "peak": round(peak_rate / 1e9, 2),
+                         "unit": "G wave-instr/s (v_fma_f64-equivalent)", "frac": round(floor_ms / avg_trace_ms, 4),
+                         "issue_floor_ms": round(floor_ms, 4),
+                         "note": ("SQ instruction counts (profiles/round1/pmc_sq.json) priced at the issue rates "
+                                  "tools/probe/valu_probe.hip measured (profiles/round1/valu_probe.json): the "
+                                  "binding roofline of this kernel")}
         out = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -287,10 +331,11 @@ def main():
                 "kernel": TRACE_KERNEL,
                 "avg_kernel_ms": round(avg_trace_ms, 4),
                 "alg_bytes_per_launch": b_alg,
-                "note": "latency/fp64-VALU bound path; HBM fraction reported as mandated (DESIGN.md)",
+                "note": "VALU-issue bound path (roofline_valu); HBM fraction reported as mandated (DESIGN.md §6)",
             },
             "pack_ms": round(float(np.mean(pack_ms)), 4),
             "roofline_fp64": fp64_roof,
+            "roofline_valu": valu_roof,
             "e2e_with_d2h_mrays_s": round(e2e, 3) if e2e else None,
         }
         if args.emulate_world > 1:
