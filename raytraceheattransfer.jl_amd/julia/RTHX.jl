@@ -461,6 +461,75 @@ function enclosureViewFactors3D(superFaces, parallel::Bool, max_iters::Int = 100
 end
 
 """
+    enclosureViewFactorsMC3D(superFaces, rays_tot; max_iters=1000)
+
+Monte Carlo counterpart of enclosureViewFactors3D for enclosures with
+obstructions (BASELINE config 4: a sphere inside a cube), where the analytic
+pair view factors (which assume every pair sees each other) do not hold.
+Sub-faces in the same face-major order; each leaves along its inwardNormal.
+`rays_tot` rays in total, div(rays_tot, n) per sub-face as the 2D tracer
+(parallelRayTracing.jl:6).  F_raw = counts / R, row-normalised like the 2D
+path (row_normalize!), then the reference's smooth_F with
+smooth_surfaces_only = true (enclosureViewFactors3D.jl:88-91).
+"""
+function enclosureViewFactorsMC3D(superFaces, rays_tot::Integer; max_iters::Int = 1000, verbose::Bool = false)
+    RTHT = parentmodule(@__MODULE__).RayTraceHeatTransfer
+    subs = [sf for f in superFaces for sf in f.subFaces]
+    n = length(subs)
+    xyz = zeros(Float64, 12n); nv = zeros(Int32, n); nrm = zeros(Float64, 3n)
+    for (k, sf) in enumerate(subs)
+        nv[k] = length(sf.vertices)
+        for (i, v) in enumerate(sf.vertices), d in 1:3
+            xyz[12(k - 1) + 3(i - 1) + d] = v[d]
+        end
+        for d in 1:3
+            nrm[3(k - 1) + d] = sf.inwardNormal[d]
+        end
+    end
+    R = div(rays_tot, n)
+    scene = Ref{Ptr{Cvoid}}(C_NULL)
+    check(ccall((:rthx_scene3d_create, LIB[]), Cint,
+                (Ptr{Float64}, Ptr{Int32}, Ptr{Float64}, Int64, Int32, Ptr{Ptr{Cvoid}}),
+                xyz, nv, nrm, n, DEVICE[], scene))
+    res = Ref{Ptr{Cvoid}}(C_NULL)
+    try
+        check(ccall((:rthx_result_create, LIB[]), Cint, (Ptr{Ptr{Cvoid}},), res))
+        args = Ref(TraceArgs(Int32(0), FAITHFUL[] ? RTHX_FLAG_FAITHFUL_SAMPLING : UInt32(0), Int64(R), 0.0,
+                             SEED[], 0, Int64(n), 1, DEVICE[], Int32(0), Ptr{Int64}(C_NULL), Int32(0), Int32(0)))
+        check(ccall((:rthx_trace_exchange_3d, LIB[]), Cint, (Ptr{Cvoid}, Ptr{TraceArgs}, Ptr{Cvoid}),
+                    scene[], args, res[]))
+        info = Ref{ResultInfo}()
+        check(ccall((:rthx_result_get_info, LIB[]), Cint, (Ptr{Cvoid}, Ptr{ResultInfo}), res[], info))
+        nnz = info[].nnz
+        rowptr = Vector{Int64}(undef, n + 1)
+        cols = Vector{Int32}(undef, max(nnz, 1))
+        counts = Vector{UInt32}(undef, max(nnz, 1))
+        check(ccall((:rthx_result_copy_csr, LIB[]), Cint, (Ptr{Cvoid}, Ptr{Int64}, Ptr{Int32}, Ptr{UInt32}),
+                    res[], rowptr, cols, counts))
+        verbose && println("  rthx 3D: $(info[].rays_traced) rays, lost $(info[].lost_total), trace $(round(info[].trace_ms; digits=3)) ms")
+        Ft = SparseMatrixCSC(n, n, rowptr .+ 1, Int64.(cols[1:nnz]) .+ 1, Float64.(counts[1:nnz]) ./ R)
+        F_raw = Matrix(transpose(Ft))
+        F_raw = Matrix(RTHT.row_normalize!(sparse(F_raw), R))
+        # polygon areas as viewFactor3D.jl:47-76 (triangle |n|/2, quad |(P3-P1) x (P4-P2)|/2), written
+        # back to the sub-faces like enclosureViewFactors3D.jl:48-49
+        cr(a, b) = (a[2]b[3] - a[3]b[2], a[3]b[1] - a[1]b[3], a[1]b[2] - a[2]b[1])
+        nrm2(v) = sqrt(v[1]^2 + v[2]^2 + v[3]^2)
+        area = map(subs) do sf
+            P = sf.vertices
+            length(P) == 3 ? nrm2(cr(P[2] .- P[1], P[3] .- P[1])) / 2 : nrm2(cr(P[3] .- P[1], P[4] .- P[2])) / 2
+        end
+        for (k, sf) in enumerate(subs)
+            sf.area = area[k]
+        end
+        F_smooth = RTHT.smooth_F(F_raw, area, n; max_iters = max_iters, smooth_surfaces_only = true)
+        return F_raw, F_smooth
+    finally
+        res[] != C_NULL && ccall((:rthx_result_destroy, LIB[]), Cvoid, (Ptr{Cvoid},), res[])
+        ccall((:rthx_scene3d_destroy, LIB[]), Cvoid, (Ptr{Cvoid},), scene[])
+    end
+end
+
+"""
     enable!(; lib, device=0, seed=1, faithful=false)
 
 Redirect RayTraceHeatTransfer's `computeExchangeFactorsBin` (and, with
