@@ -5,7 +5,7 @@
 // rthx_scene3d_create validates the polygons, orients each emission frame by
 // the caller's normal, splits quads into two triangles (v0 v1 v2, v2 v3 v0 --
 // the same split the emission uses), builds a two-child BVH on the host
-// (binned SAH, leaves of <= 4 triangles, both children's bounds in each node
+// (binned SAH, leaves of <= 2 triangles, both children's bounds in each node
 // as fp32 padded outward by kBoxPad of the scene scale, so the device's fp32
 // slab tests never drop a hit the fp64 Moeller-Trumbore test would find) and
 // uploads it.  rthx_trace_exchange_3d traces R rays per emitter polygon into the
@@ -57,7 +57,10 @@ double dot(V a, V b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 double norm(V a) { return std::sqrt(dot(a, a)); }
 V scale(V a, double s) { return {a.x * s, a.y * s, a.z * s}; }
 
-constexpr int kLeafTris = 4;
+#ifndef RTHX_T3_LEAF
+#define RTHX_T3_LEAF 2
+#endif
+constexpr int kLeafTris = RTHX_T3_LEAF;  // triangles per BVH leaf (at most)
 constexpr int64_t kSplitTargetBlocks = 8192;
 constexpr int64_t kSplitMinRays = 1024;
 

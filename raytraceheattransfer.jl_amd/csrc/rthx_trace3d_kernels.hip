@@ -29,6 +29,9 @@ namespace t3 {
 
 constexpr int kThreads = kTrace3dThreads;
 
+#ifndef RTHX_T3_REFILL
+#define RTHX_T3_REFILL 16  // ray regeneration: refill batch (lanes); 0 = one ray per lane per pass
+#endif
 #ifndef RTHX_T3_WAVES
 #define RTHX_T3_WAVES 0  // > 0: amdgpu_waves_per_eu floor (register budget) for variants
 #endif
@@ -95,6 +98,8 @@ struct Walk {
   double best_t;
   float best_tf;  // fp32 upper bound of best_t
   int best_id, best_poly;
+  int node, sp;
+  int pending;  // postponed leaf reference (< 0), 0 = none
 
   __device__ __forceinline__ void init(const double* o_, const double* d_) {
 #pragma unroll
@@ -108,6 +113,9 @@ struct Walk {
     best_tf = __builtin_inff();
     best_id = 0x7FFFFFFF;
     best_poly = -1;
+    node = 0;
+    sp = 0;
+    pending = 0;
   }
 
   __device__ __forceinline__ void leaf(const DevScene3D& S, int skip, int ref) {
@@ -126,57 +134,57 @@ struct Walk {
     }
   }
 
-  __device__ __forceinline__ void run(const DevScene3D& S, const Bvh2Node RTHX_LDS* top, int n_top, int skip,
-                                     int RTHX_LDS* stk) {
-    int node = 0, sp = 0;
-    int pending = 0;  // postponed leaf reference (< 0), 0 = none
-    while (node != kWalkDone) {
-      while (node >= 0) {
-        Bvh2Node nd;
-        if (node < n_top) {
-          typedef float f4 __attribute__((ext_vector_type(4)));
-          const f4 RTHX_LDS* q = (const f4 RTHX_LDS*)(top + node);
-          const f4 w[4] = {q[0], q[1], q[2], q[3]};
-          __builtin_memcpy(&nd, w, sizeof(nd));
-        } else
-          nd = S.nodes[node];
-        float tn[2], tf[2];
+  // One round of the walk: descend (speculatively) until every live lane of
+  // the wave holds a leaf, then test the leaves; false once this lane's walk
+  // is over.
+  __device__ __forceinline__ bool step(const DevScene3D& S, const Bvh2Node RTHX_LDS* top, int n_top, int skip,
+                                       int RTHX_LDS* stk) {
+    while (node >= 0) {
+      Bvh2Node nd;
+      if (node < n_top) {
+        typedef float f4 __attribute__((ext_vector_type(4)));
+        const f4 RTHX_LDS* q = (const f4 RTHX_LDS*)(top + node);
+        const f4 w[4] = {q[0], q[1], q[2], q[3]};
+        __builtin_memcpy(&nd, w, sizeof(nd));
+      } else
+        nd = S.nodes[node];
+      float tn[2], tf[2];
 #pragma unroll
-        for (int c = 0; c < 2; ++c) {
-          const float a0 = __builtin_fmaf(nd.lo[c][0], inv[0], -oi[0]), b0 = __builtin_fmaf(nd.hi[c][0], inv[0], -oi[0]);
-          const float a1 = __builtin_fmaf(nd.lo[c][1], inv[1], -oi[1]), b1 = __builtin_fmaf(nd.hi[c][1], inv[1], -oi[1]);
-          const float a2 = __builtin_fmaf(nd.lo[c][2], inv[2], -oi[2]), b2 = __builtin_fmaf(nd.hi[c][2], inv[2], -oi[2]);
-          // NaN (0 * inf on an axis the ray runs parallel to) drops out of
-          // fminf/fmaxf: that axis then does not prune (conservative)
-          tn[c] = fmaxf(fmaxf(fminf(a0, b0), fminf(a1, b1)), fmaxf(fminf(a2, b2), 0.0f));
-          tf[c] = fminf(fminf(fmaxf(a0, b0), fmaxf(a1, b1)), fminf(fmaxf(a2, b2), best_tf));
-        }
-        const bool h0 = tn[0] <= tf[0], h1 = tn[1] <= tf[1];
-        if (h0 && h1) {
-          const bool near0 = tn[0] <= tn[1];
-          stk[sp * kThreads] = near0 ? nd.child[1] : nd.child[0];
-          ++sp;
-          node = near0 ? nd.child[0] : nd.child[1];
-        } else if (h0 || h1) {
-          node = h0 ? nd.child[0] : nd.child[1];
-        } else {
-          node = sp > 0 ? stk[--sp * kThreads] : kWalkDone;
-        }
-        if (node < 0 && node != kWalkDone && pending == 0) {
-          pending = node;
-          node = sp > 0 ? stk[--sp * kThreads] : kWalkDone;
-        }
-        if (__ballot(pending == 0) == 0ull) break;
+      for (int c = 0; c < 2; ++c) {
+        const float a0 = __builtin_fmaf(nd.lo[c][0], inv[0], -oi[0]), b0 = __builtin_fmaf(nd.hi[c][0], inv[0], -oi[0]);
+        const float a1 = __builtin_fmaf(nd.lo[c][1], inv[1], -oi[1]), b1 = __builtin_fmaf(nd.hi[c][1], inv[1], -oi[1]);
+        const float a2 = __builtin_fmaf(nd.lo[c][2], inv[2], -oi[2]), b2 = __builtin_fmaf(nd.hi[c][2], inv[2], -oi[2]);
+        // NaN (0 * inf on an axis the ray runs parallel to) drops out of
+        // fminf/fmaxf: that axis then does not prune (conservative)
+        tn[c] = fmaxf(fmaxf(fminf(a0, b0), fminf(a1, b1)), fmaxf(fminf(a2, b2), 0.0f));
+        tf[c] = fminf(fminf(fmaxf(a0, b0), fmaxf(a1, b1)), fminf(fmaxf(a2, b2), best_tf));
       }
-      while (pending < 0) {
-        leaf(S, skip, pending);
-        pending = 0;
-        if (node < 0 && node != kWalkDone) {
-          pending = node;
-          node = sp > 0 ? stk[--sp * kThreads] : kWalkDone;
-        }
+      const bool h0 = tn[0] <= tf[0], h1 = tn[1] <= tf[1];
+      if (h0 && h1) {
+        const bool near0 = tn[0] <= tn[1];
+        stk[sp * kThreads] = near0 ? nd.child[1] : nd.child[0];
+        ++sp;
+        node = near0 ? nd.child[0] : nd.child[1];
+      } else if (h0 || h1) {
+        node = h0 ? nd.child[0] : nd.child[1];
+      } else {
+        node = sp > 0 ? stk[--sp * kThreads] : kWalkDone;
+      }
+      if (node < 0 && node != kWalkDone && pending == 0) {
+        pending = node;
+        node = sp > 0 ? stk[--sp * kThreads] : kWalkDone;
+      }
+      if (__ballot(pending == 0) == 0ull) break;
+    }
+    while (pending < 0) {
+      leaf(S, skip, pending);
+      pending = 0;
+      if (node < 0 && node != kWalkDone) {
+        pending = node;
+        node = sp > 0 ? stk[--sp * kThreads] : kWalkDone;
       }
     }
+    return node != kWalkDone;
   }
 };
 
@@ -230,6 +238,9 @@ __global__ __launch_bounds__(kThreads) RTHX_T3_ATTR void trace_exchange_3d_kerne
   __shared__ double s_tab[2 * kCosTable];        // (cos, sin)(2 pi j / 256)
   __shared__ Emit3 s_emit;
   __shared__ uint32_t s_tallied;
+#if RTHX_T3_REFILL
+  __shared__ uint32_t s_next;  // next ray of the slice
+#endif
   const DevScene3D& S = *Sp;
   const int tid = threadIdx.x;
   const int64_t slot = blockIdx.x / T.split, part = blockIdx.x % T.split;
@@ -253,10 +264,50 @@ __global__ __launch_bounds__(kThreads) RTHX_T3_ATTR void trace_exchange_3d_kerne
   if (tid == 0) {
     s_emit = S.polys[g];
     s_tallied = 0u;
+#if RTHX_T3_REFILL
+    s_next = (uint32_t)r_begin;
+#endif
   }
   __syncthreads();
   uint32_t tallied = 0;
   int RTHX_LDS* stk = (int RTHX_LDS*)(hist + trace3d_stack_offset(words)) + tid;
+  auto tally = [&](int a) {
+    if (a >= 0) {
+      if (PACK16)
+        atomicAdd(&hist[a >> 1], 1u << ((a & 1) * 16));
+      else
+        atomicAdd(&hist[a], 1u);
+      ++tallied;
+    }
+  };
+  const Bvh2Node RTHX_LDS* topo = (const Bvh2Node RTHX_LDS*)lds_opaque((const Bvh2Node*)top);
+#if RTHX_T3_REFILL
+  // Ray regeneration: a lane whose walk has ended takes the slice's next ray
+  // from an LDS counter (batched: once kRefill lanes of the wave are idle).
+  constexpr int kRefill = RTHX_T3_REFILL;
+  Walk w;
+  bool live = false;
+  while (true) {
+    if (__popcll(__ballot(!live)) >= kRefill || __ballot(live) == 0ull) {
+      if (!live) {
+        const uint32_t r = atomicAdd(&s_next, 1u);
+        if (r < (uint32_t)r_end) {
+          const Emit3 RTHX_LDS* em = lds_opaque(&s_emit);
+          double o[3], d[3];
+          emit_ray<FAITHFUL>(*(const Emit3*)em, (const double*)lds_opaque(&s_tab[0]), (uint32_t)g, r, P.key0, P.key1,
+                             o, d);
+          w.init(o, d);
+          live = true;
+        }
+      }
+    }
+    if (__ballot(live) == 0ull) break;
+    if (live && !w.step(S, topo, n_top, (int)g, stk)) {
+      tally(w.best_poly);
+      live = false;
+    }
+  }
+#else
   for (int64_t r = r_begin + tid; r < r_end; r += kThreads) {
     const Emit3 RTHX_LDS* em = lds_opaque(&s_emit);
     double o[3], d[3];
@@ -264,15 +315,11 @@ __global__ __launch_bounds__(kThreads) RTHX_T3_ATTR void trace_exchange_3d_kerne
                        P.key1, o, d);
     Walk w;
     w.init(o, d);
-    w.run(S, (const Bvh2Node RTHX_LDS*)lds_opaque((const Bvh2Node*)top), n_top, (int)g, stk);
-    if (w.best_poly >= 0) {
-      if (PACK16)
-        atomicAdd(&hist[w.best_poly >> 1], 1u << ((w.best_poly & 1) * 16));
-      else
-        atomicAdd(&hist[w.best_poly], 1u);
-      ++tallied;
+    while (w.step(S, topo, n_top, (int)g, stk)) {
     }
+    tally(w.best_poly);
   }
+#endif
   for (int off = 32; off > 0; off >>= 1) tallied += __shfl_xor(tallied, off);
   if (lane_id() == 0) atomicAdd(&s_tallied, tallied);
   __syncthreads();
