@@ -61,6 +61,9 @@ V scale(V a, double s) { return {a.x * s, a.y * s, a.z * s}; }
 #define RTHX_T3_LEAF 2
 #endif
 constexpr int kLeafTris = RTHX_T3_LEAF;  // triangles per BVH leaf (at most)
+#ifndef RTHX_T3_SAH_BINS
+#define RTHX_T3_SAH_BINS 16
+#endif
 constexpr int64_t kSplitTargetBlocks = 8192;
 constexpr int64_t kSplitMinRays = 1024;
 
@@ -134,7 +137,7 @@ struct Bvh2Builder {
     int mid = b + (e - b) / 2;
     bool done = false;
     if (!median) {
-      constexpr int kBins = 16;
+      constexpr int kBins = RTHX_T3_SAH_BINS;
       double best = 1e300;
       int best_axis = -1, best_bin = -1;
       for (int k = 0; k < 3; ++k) {
