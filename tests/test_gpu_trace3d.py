@@ -2,7 +2,8 @@
 rthx_trace_exchange_3d) against its CPU restatement, exactly.
 
 Both draw every ray from the same Philox blocks and evaluate the same fp64
-Moeller-Trumbore arithmetic (the kernel is built uncontracted); the device
+Moeller-Trumbore arithmetic (deferred division; fused exactly where the
+oracle calls fma(), otherwise uncontracted); the device
 walks a BVH while the restatement tests every triangle in index order, with
 ties on t going to the lower triangle index on both sides.  Remaining
 difference: the azimuth's cos/sin (table + polynomial on the device, libm on
@@ -120,3 +121,34 @@ def test_far_from_origin_and_single_leaf_scenes(hip):
     C4, lost4 = oracle.trace_exchange_3d(xyz4, nv4, nrm4, 20000, seed=10, nthreads=16)
     assert np.array_equal(D4, C4) and info4["lost_total"] == lost4
     assert np.all(np.diag(D4) == 0) and lost4 == 0
+
+
+def test_u32_counters_and_stats(hip):
+    """>= 8192 emitter rows and R >= 65536: one workgroup per row traces all
+    R rays, so the row histogram takes u32 counters (below 65536 rays per
+    workgroup it packs u16 pairs).  Sampled rows equal the CPU restatement;
+    rthx_scene3d_stats reports the uploaded BVH."""
+    from rthx.trace3d import Scene3D
+
+    xyz, nv, nrm, nc = H.cube_icosphere_scene(ndim=37, level=0)
+    n = len(nv)
+    assert n >= 8192
+    R = 65600
+    s = Scene3D(xyz, nv, nrm)
+    try:
+        st = s.stats()
+        assert st["n_tri"] == int(np.sum(np.where(nv == 4, 2, 1)))
+        assert 0 < st["n_nodes"] < st["n_tri"] and 1 <= st["depth"] <= 32
+        rp, cols, cnt, info = s.trace(R, seed=5)
+    finally:
+        s.close()
+    assert info["rays_traced"] == n * R
+    assert int(cnt.sum()) + info["lost_total"] == n * R
+    # the same rows traced as a 3-row shard split over many workgroups (u16
+    # counters, pinned to the CPU restatement by the tests above)
+    stride = n // 3
+    D, info3 = gpu_dense(xyz, nv, nrm, R, seed=5, begin=0, end=3 * stride, stride=stride)
+    for g in (0, stride, 2 * stride):
+        row = np.zeros(n, dtype=np.uint32)
+        row[cols[rp[g]:rp[g + 1]]] = cnt[rp[g]:rp[g + 1]]
+        assert np.array_equal(row, D[g]), g
