@@ -38,6 +38,7 @@ struct Ctx {
   int64_t n = 0;
   bool verbose = false;
   DevBuf w, w2, inv_w, r, u, u2, part, scal;
+  DevBuf rowpart, colpart;  // dense AP on the upper triangle: per-tile row sums
   // dual system
   DevBuf d_rowsum, d_dinv, b, x, pr, z, p, Ap, rs;
   bool dual_ready = false;
@@ -176,7 +177,15 @@ int ap_dense(Ctx& c, double* F, double* X, int max_iters, double nz_over_N, APSt
   const int64_t n = c.n;
   hipStream_t s = c.s;
   HIP_TRY(build_x(F, c.dv(c.w), n, X, s), "build_x");
+#ifndef RTHX_AP_FULL
+  // X is symmetric through AP: iterate on the upper triangle (ap_sym)
+  TRY(c.alloc(c.rowpart, ap_sym_col_tiles(n) * n, "hipMalloc AP partial sums"));
+  TRY(c.alloc(c.colpart, ap_sym_row_tiles(n) * n, "hipMalloc AP partial sums"));
+  HIP_TRY(ap_sym(X, c.dv(c.u), c.dv(c.w), n, false, c.dv(c.rowpart), c.dv(c.colpart), c.dv(c.r), c.dv(c.u), s),
+          "hunger");
+#else
   HIP_TRY(hunger(X, c.dv(c.w), n, c.dv(c.r), c.dv(c.u), s), "hunger");
+#endif
   auto delta_of = [&](double* d) {
     HIP_TRY(delta_rows(X, c.dv(c.u), c.dv(c.w2), n, c.dv(c.part), s), "delta_rows");
     double ss;
@@ -185,13 +194,22 @@ int ap_dense(Ctx& c, double* F, double* X, int max_iters, double nz_over_N, APSt
     return RTHX_OK;
   };
   auto step = [&]() {
+#ifndef RTHX_AP_FULL
+    HIP_TRY(ap_sym(X, c.dv(c.u), c.dv(c.w), n, true, c.dv(c.rowpart), c.dv(c.colpart), c.dv(c.r), c.dv(c.u2), s),
+            "ap_step");
+#else
     HIP_TRY(ap_step(X, c.dv(c.u), c.dv(c.w), n, c.dv(c.r), c.dv(c.u2), s), "ap_step");
+#endif
     std::swap(c.u.p, c.u2.p);
     std::swap(c.u.cap, c.u2.cap);
     return RTHX_OK;
   };
   TRY(ap_loop(c, max_iters, nz_over_N, step, delta_of, st));
+#ifndef RTHX_AP_FULL
+  HIP_TRY(recover_sym(X, c.dv(c.r), n, s), "recover");
+#else
   HIP_TRY(recover(X, c.dv(c.r), n, s), "recover");
+#endif
   return RTHX_OK;
 }
 

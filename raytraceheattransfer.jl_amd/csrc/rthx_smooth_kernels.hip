@@ -96,6 +96,178 @@ __global__ __launch_bounds__(kRow) void k_ap_step(double* __restrict__ X, const 
   }
 }
 
+// ---------------------------------------------------------------------------
+// Dense AP on the upper triangle.  X stays symmetric through AP (build_X is
+// symmetric and scale! multiplies X_ij and X_ji by the same (u_i + u_j)/2), so
+// the iterations read and write only j >= i: half the HBM traffic of the
+// full-matrix step.  The row sum r_i = sum_{j >= i} X_ij + sum_{j < i} X_ji
+// is assembled from per-tile partials in a fixed order (deterministic):
+//   rowpart[jt][i]: sum over tile column block jt of X_ij, j >= i
+//   colpart[it][j]: sum over tile row block it of X_ij, i < j
+// recover_F then writes both triangles of F from the upper X.
+// ---------------------------------------------------------------------------
+#ifndef RTHX_SYM_ROWS
+#define RTHX_SYM_ROWS 128
+#endif
+#ifndef RTHX_SYM_BATCH
+#define RTHX_SYM_BATCH 8
+#endif
+constexpr int kSymRows = RTHX_SYM_ROWS;    // rows per AP tile
+constexpr int kSymCols = 256;              // columns per AP tile (one per lane)
+constexpr int kSymBatch = RTHX_SYM_BATCH;  // rows loaded before any is stored (loads in flight), multiple of 8
+
+__host__ __device__ inline int64_t sym_jt0(int64_t it) { return it * kSymRows / kSymCols; }
+
+// Sums of 8 rows over the 64 lanes of a wave with 10 shuffles (transpose-
+// reduce: each halving step exchanges only the rows the partner keeps).  The
+// total of row ((lane >> 3) & 7) ends in every lane of its 8-lane group (row
+// bits: lane bit 5 -> 4, bit 4 -> 2, bit 3 -> 1).  Fixed order.
+__device__ __forceinline__ double wave_sum8(const double* v, int lane) {
+  const bool b5 = lane & 32, b4 = lane & 16, b3 = lane & 8;
+  double a[4], c[2];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const double send = b5 ? v[k] : v[k + 4];
+    const double keep = b5 ? v[k + 4] : v[k];
+    a[k] = keep + __shfl_xor(send, 32);
+  }
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const double send = b4 ? a[k] : a[k + 2];
+    const double keep = b4 ? a[k + 2] : a[k];
+    c[k] = keep + __shfl_xor(send, 16);
+  }
+  double t = (b3 ? c[1] : c[0]) + __shfl_xor(b3 ? c[0] : c[1], 8);
+  t += __shfl_xor(t, 4);
+  t += __shfl_xor(t, 2);
+  t += __shfl_xor(t, 1);
+  return t;
+}
+
+// Tile (it, jt) of the upper triangle; SCALE = false is hunger! (row sums
+// only).  EDGE: the tile crosses the diagonal or the matrix edge (per-entry
+// masks); interior tiles run unmasked.
+template <bool SCALE, bool EDGE>
+__device__ __forceinline__ void ap_sym_tile(double* __restrict__ X, const double* __restrict__ u, int64_t n,
+                                            int64_t i0, int64_t j, double (*rs)[kSymCols / 64],
+                                            double& col) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const bool jok = !EDGE || j < n;
+  const double uj = jok ? u[j] : 0.0;
+  for (int y0 = 0; y0 < kSymRows; y0 += kSymBatch) {
+    double v[kSymBatch];
+#pragma unroll
+    for (int b = 0; b < kSymBatch; ++b) {
+      const int64_t i = i0 + y0 + b;
+      v[b] = (!EDGE || (jok && i < n && j >= i)) ? X[i * n + j] : 0.0;
+    }
+#pragma unroll
+    for (int b = 0; b < kSymBatch; ++b) {
+      const int64_t i = i0 + y0 + b;
+      if (SCALE) {
+        v[b] *= 0.5 * (u[!EDGE || i < n ? i : 0] + uj);
+        if (!EDGE || (jok && i < n && j >= i)) X[i * n + j] = v[b];
+      }
+      if (!EDGE || j > i) col += v[b];
+    }
+#pragma unroll
+    for (int h = 0; h < kSymBatch; h += 8) {
+      const double t = wave_sum8(v + h, lane);
+      if ((lane & 7) == 0) rs[y0 + h + (lane >> 3)][wave] = t;
+    }
+  }
+}
+
+template <bool SCALE>
+__global__ __launch_bounds__(kSymCols) void k_ap_sym(double* __restrict__ X, const double* __restrict__ u, int64_t n,
+                                                     int64_t n_it, int64_t n_jt, double* __restrict__ rowpart,
+                                                     double* __restrict__ colpart) {
+  __shared__ double rs[kSymRows][kSymCols / 64];
+  // blockIdx.y = it, blockIdx.x = jt - sym_jt0(it); tiles past n_jt return
+  const int64_t it = blockIdx.y;
+  const int64_t jt = sym_jt0(it) + blockIdx.x;
+  if (jt >= n_jt) return;
+  const int64_t i0 = it * kSymRows, j0 = jt * kSymCols, j = j0 + threadIdx.x;
+  const bool edge = j0 < i0 + kSymRows || i0 + kSymRows > n || j0 + kSymCols > n;  // uniform
+  double col = 0.0;
+  if (edge)
+    ap_sym_tile<SCALE, true>(X, u, n, i0, j, rs, col);
+  else
+    ap_sym_tile<SCALE, false>(X, u, n, i0, j, rs, col);
+  if (j < n) colpart[it * n + j] = col;
+  __syncthreads();
+  for (int y = threadIdx.x; y < kSymRows; y += kSymCols) {
+    const int64_t i = i0 + y;
+    double t = 0.0;
+    for (int w = 0; w < kSymCols / 64; ++w) t += rs[y][w];
+    if (i < n) rowpart[jt * n + i] = t;
+  }
+}
+
+// r_i = sum_{jt >= jt0(it(i))} rowpart[jt][i] + sum_{it' <= it_max(jt(i))} colpart[it'][i]
+// u_next_i = w_i / r_i.  Workgroup: 64 rows x kRedSlices lanes; slice q sums
+// every kRedSlices-th partial of its row, then the slice sums are added in
+// slice order (fixed order, deterministic).
+constexpr int kRedSlices = 8;
+__global__ __launch_bounds__(64 * kRedSlices) void k_ap_sym_reduce(const double* __restrict__ rowpart,
+                                                                   const double* __restrict__ colpart,
+                                                                   const double* __restrict__ w, int64_t n,
+                                                                   int64_t n_it, int64_t n_jt, double* __restrict__ r,
+                                                                   double* __restrict__ u_next) {
+  __shared__ double sh[kRedSlices][64];
+  const int lane = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int64_t i = (int64_t)blockIdx.x * 64 + lane;
+  double s = 0.0;
+  if (i < n) {
+    const int64_t it = i / kSymRows, jti = i / kSymCols;
+    const int64_t jt0 = sym_jt0(it);
+    const int64_t it_max = min(n_it - 1, (jti * kSymCols + kSymCols - 1) / kSymRows);
+    const int64_t nr = n_jt - jt0, nc = it_max + 1;
+    for (int64_t k = q; k < nr + nc; k += kRedSlices)
+      s += k < nr ? rowpart[(jt0 + k) * n + i] : colpart[(k - nr) * n + i];
+  }
+  sh[q][lane] = s;
+  __syncthreads();
+  if (q == 0 && i < n) {
+    double t = 0.0;
+    for (int k = 0; k < kRedSlices; ++k) t += sh[k][lane];
+    r[i] = t;
+    u_next[i] = w[i] / t;
+  }
+}
+
+// recover_F (:548) from the upper triangle: F_ij = X_ij / r_i for j >= i and
+// F_ij = X_ji / r_i for j < i.  Workgroup (bi, bj), bi <= bj, owns the tile
+// pair (bi, bj) / (bj, bi): it reads the upper tile, then writes both.
+__global__ __launch_bounds__(kTile * 8) void k_recover_sym(double* __restrict__ X, const double* __restrict__ r,
+                                                            int64_t n) {
+  __shared__ double t[kTile][kTile + 1];
+  const int64_t tbi = blockIdx.y, tbj = blockIdx.x;
+  if (tbj < tbi) return;
+  const int64_t bi = tbi * kTile, bj = tbj * kTile;
+  const int tx = threadIdx.x, ty = threadIdx.y;
+  for (int y = ty; y < kTile; y += 8) {
+    const int64_t i = bi + y, j = bj + tx;
+    t[y][tx] = (i < n && j < n) ? X[i * n + j] : 0.0;
+  }
+  __syncthreads();
+  if (tbi == tbj) {
+    for (int y = ty; y < kTile; y += 8) {
+      const int64_t i = bi + y, j = bj + tx;
+      if (i < n && j < n) X[i * n + j] = (tx >= y ? t[y][tx] : t[tx][y]) / r[i];
+    }
+    return;
+  }
+  for (int y = ty; y < kTile; y += 8) {
+    const int64_t i = bi + y, j = bj + tx;
+    if (i < n && j < n) X[i * n + j] = t[y][tx] / r[i];
+  }
+  for (int y = ty; y < kTile; y += 8) {
+    const int64_t i = bj + y, j = bi + tx;  // lower tile: F_ij = X_ji / r_i
+    if (i < n && j < n) X[i * n + j] = t[tx][y] / r[i];
+  }
+}
+
 // hunger! alone (the first (X_0, u_0)).
 __global__ __launch_bounds__(kRow) void k_hunger(const double* __restrict__ X, const double* __restrict__ w, int64_t n,
                                                  double* __restrict__ r, double* __restrict__ u) {
@@ -345,6 +517,27 @@ hipError_t delta_rows(const double* X, const double* u, const double* w2, int64_
 }
 hipError_t recover(double* X, const double* r, int64_t n, hipStream_t s) {
   hipLaunchKernelGGL(k_recover, dim3((unsigned)n), dim3(kRow), 0, s, X, r, n);
+  return hipGetLastError();
+}
+int64_t ap_sym_row_tiles(int64_t n) { return (n + kSymRows - 1) / kSymRows; }
+int64_t ap_sym_col_tiles(int64_t n) { return (n + kSymCols - 1) / kSymCols; }
+hipError_t ap_sym(double* X, const double* u, const double* w, int64_t n, bool scale, double* rowpart,
+                  double* colpart, double* r, double* u_next, hipStream_t s) {
+  const int64_t n_it = ap_sym_row_tiles(n), n_jt = ap_sym_col_tiles(n);
+  dim3 g((unsigned)n_jt, (unsigned)n_it);  // blockIdx.x = jt - jt0(it); tiles past n_jt return at once
+  if (scale)
+    hipLaunchKernelGGL(k_ap_sym<true>, g, dim3(kSymCols), 0, s, X, u, n, n_it, n_jt, rowpart, colpart);
+  else
+    hipLaunchKernelGGL(k_ap_sym<false>, g, dim3(kSymCols), 0, s, X, u, n, n_it, n_jt, rowpart, colpart);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_ap_sym_reduce, dim3(grid1(n, 64)), dim3(64 * kRedSlices), 0, s, rowpart, colpart, w, n, n_it,
+                     n_jt, r, u_next);
+  return hipGetLastError();
+}
+hipError_t recover_sym(double* X, const double* r, int64_t n, hipStream_t s) {
+  dim3 g(grid1(n, kTile), grid1(n, kTile));
+  hipLaunchKernelGGL(k_recover_sym, g, dim3(kTile, 8), 0, s, X, r, n);
   return hipGetLastError();
 }
 hipError_t renorm(double* F, int64_t n, hipStream_t s) {

@@ -38,7 +38,8 @@ def main():
         Fs = smooth_F(F, w, dom.num_surfaces, verbose=(r == 0), info=info, k_dykstra=a.k_dykstra)
         dt = time.perf_counter() - t
         n = info["n"]
-        ap_bytes = info["ap_iters"] * 16.0 * n * n
+        # dense AP reads and writes the upper triangle once per iteration (k_ap_sym)
+        ap_bytes = info["ap_iters"] * 16.0 * n * (n + 1) / 2
         print(f"smooth_F: {dt * 1e3:.1f} ms wall (library {info['ms_total']:.1f} ms: OP {info['ms_op']:.1f}, "
               f"AP {info['ms_ap']:.1f} ms, {info['ap_iters']} AP iterations, {info['pcg_iters']} PCG), "
               f"AP scale+sum traffic {ap_bytes / info['ms_ap'] / 1e6:.0f} GB/s lower bound, "
