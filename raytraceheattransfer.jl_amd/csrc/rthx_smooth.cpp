@@ -171,45 +171,37 @@ int ap_loop(Ctx& c, int max_iters, double nz_over_N, Step step, Delta delta_of, 
 }
 
 // Dense AP (:550-611 with the dense build_X / hunger! / scale! / delta_R_X /
-// recover_F).  F (n*n) is consumed; the result is left in X.
+// recover_F).  X is symmetric through AP, so the iterations run on its upper
+// triangle (ap_sym) with an even leading dimension (16-byte accesses); X needs
+// n * ap_dense_ld(n) doubles.  F (n*n) is consumed by build_X and receives
+// the result.
+int64_t ap_dense_ld(int64_t n) { return n + (n & 1); }
+
 int ap_dense(Ctx& c, double* F, double* X, int max_iters, double nz_over_N, APState& st) {
   using namespace rthx::sm;
-  const int64_t n = c.n;
+  const int64_t n = c.n, ld = ap_dense_ld(n);
   hipStream_t s = c.s;
-  HIP_TRY(build_x(F, c.dv(c.w), n, X, s), "build_x");
-#ifndef RTHX_AP_FULL
-  // X is symmetric through AP: iterate on the upper triangle (ap_sym)
+  HIP_TRY(build_x(F, c.dv(c.w), n, ld, X, s), "build_x");
   TRY(c.alloc(c.rowpart, ap_sym_col_tiles(n) * n, "hipMalloc AP partial sums"));
   TRY(c.alloc(c.colpart, ap_sym_row_tiles(n) * n, "hipMalloc AP partial sums"));
-  HIP_TRY(ap_sym(X, c.dv(c.u), c.dv(c.w), n, false, c.dv(c.rowpart), c.dv(c.colpart), c.dv(c.r), c.dv(c.u), s),
+  HIP_TRY(ap_sym(X, ld, c.dv(c.u), c.dv(c.w), n, false, c.dv(c.rowpart), c.dv(c.colpart), c.dv(c.r), c.dv(c.u), s),
           "hunger");
-#else
-  HIP_TRY(hunger(X, c.dv(c.w), n, c.dv(c.r), c.dv(c.u), s), "hunger");
-#endif
   auto delta_of = [&](double* d) {
-    HIP_TRY(delta_rows(X, c.dv(c.u), c.dv(c.w2), n, c.dv(c.part), s), "delta_rows");
+    HIP_TRY(delta_rows(X, ld, c.dv(c.u), c.dv(c.w2), n, c.dv(c.part), s), "delta_rows");
     double ss;
     TRY(c.dot(c.dv(c.part), nullptr, n, &ss));
     *d = std::sqrt(ss);
     return RTHX_OK;
   };
   auto step = [&]() {
-#ifndef RTHX_AP_FULL
-    HIP_TRY(ap_sym(X, c.dv(c.u), c.dv(c.w), n, true, c.dv(c.rowpart), c.dv(c.colpart), c.dv(c.r), c.dv(c.u2), s),
+    HIP_TRY(ap_sym(X, ld, c.dv(c.u), c.dv(c.w), n, true, c.dv(c.rowpart), c.dv(c.colpart), c.dv(c.r), c.dv(c.u2), s),
             "ap_step");
-#else
-    HIP_TRY(ap_step(X, c.dv(c.u), c.dv(c.w), n, c.dv(c.r), c.dv(c.u2), s), "ap_step");
-#endif
     std::swap(c.u.p, c.u2.p);
     std::swap(c.u.cap, c.u2.cap);
     return RTHX_OK;
   };
   TRY(ap_loop(c, max_iters, nz_over_N, step, delta_of, st));
-#ifndef RTHX_AP_FULL
-  HIP_TRY(recover_sym(X, c.dv(c.r), n, s), "recover");
-#else
-  HIP_TRY(recover(X, c.dv(c.r), n, s), "recover");
-#endif
+  HIP_TRY(recover_sym(X, ld, c.dv(c.r), n, F, s), "recover");
   return RTHX_OK;
 }
 
@@ -433,7 +425,7 @@ RTHX_EXPORT int rthx_smooth_F(const int64_t* row_ptr, const int32_t* cols, const
     const size_t bytes = (size_t)m * (size_t)m * 8;
     DevBuf A, Xb, P;
     DTRY(A.reserve(bytes), "hipMalloc dense F");
-    DTRY(Xb.reserve(bytes), "hipMalloc dense X");
+    DTRY(Xb.reserve((size_t)m * (size_t)ap_dense_ld(m) * 8), "hipMalloc dense X");  // also Xbar (n x n)
     // dense F_raw (truncated to m x m): the CSR rows < m, columns < m
     {
       DevBuf drp, dci, dv;
@@ -492,8 +484,8 @@ RTHX_EXPORT int rthx_smooth_F(const int64_t* row_ptr, const int32_t* cols, const
     RTRY(ap_dense(c, F, X, args->max_iters, nz_over_N, st));
     DTRY(hipStreamSynchronize(s), "AP");
     t_ap = now_ms() - t2;
-    std::swap(res->F.p, Xb.p);
-    std::swap(res->F.cap, Xb.cap);
+    std::swap(res->F.p, A.p);  // ap_dense leaves F_smooth in the F buffer
+    std::swap(res->F.cap, A.cap);
     res->dense = true;
     res->nnz = m * m;
   } else {

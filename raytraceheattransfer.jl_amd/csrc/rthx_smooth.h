@@ -36,20 +36,22 @@ hipError_t dual_setup(const double* w2, int64_t n, double* rowsum, double* dinv,
 hipError_t rmul(const double* w2, const double* rowsum, const double* p, int64_t n, double* out, hipStream_t s);
 hipError_t ap_step(double* X, const double* u, const double* w, int64_t n, double* r, double* u_next, hipStream_t s);
 hipError_t hunger(const double* X, const double* w, int64_t n, double* r, double* u, hipStream_t s);
-hipError_t delta_rows(const double* X, const double* u, const double* w2, int64_t n, double* part, hipStream_t s);
+hipError_t delta_rows(const double* X, int64_t ld, const double* u, const double* w2, int64_t n, double* part,
+                      hipStream_t s);
 hipError_t recover(double* X, const double* r, int64_t n, hipStream_t s);
-// Dense AP on the upper triangle (symmetric X): one scale! + hunger! step
-// (scale = false: hunger! alone); partial buffers of ap_sym_col_tiles(n) * n
-// (rowpart) and ap_sym_row_tiles(n) * n (colpart) doubles.
+// Dense AP on the upper triangle of a symmetric X with an even leading
+// dimension ld >= n: one scale! + hunger! step (scale = false: hunger!
+// alone); partial buffers of ap_sym_col_tiles(n) * n (rowpart) and
+// ap_sym_row_tiles(n) * n (colpart) doubles.  recover_sym writes F (n x n).
 int64_t ap_sym_row_tiles(int64_t n);
 int64_t ap_sym_col_tiles(int64_t n);
-hipError_t ap_sym(double* X, const double* u, const double* w, int64_t n, bool scale, double* rowpart,
+hipError_t ap_sym(double* X, int64_t ld, const double* u, const double* w, int64_t n, bool scale, double* rowpart,
                   double* colpart, double* r, double* u_next, hipStream_t s);
-hipError_t recover_sym(double* X, const double* r, int64_t n, hipStream_t s);
+hipError_t recover_sym(const double* X, int64_t ld, const double* r, int64_t n, double* F, hipStream_t s);
 hipError_t renorm(double* F, int64_t n, hipStream_t s);
 hipError_t op_dykstra(const double* Xbar, const double* lam, const double* w2, const double* inv_w, int64_t n,
                       double* P, bool keep_p, double* Fs, hipStream_t s);
-hipError_t build_x(const double* F, const double* w, int64_t n, double* X, hipStream_t s);
+hipError_t build_x(const double* F, const double* w, int64_t n, int64_t ld, double* X, hipStream_t s);
 hipError_t xbar(const double* F, const double* inv_w, const double* w2, int64_t n, double* Xbar, hipStream_t s);
 hipError_t dot(const double* a, const double* b, int64_t n, double* out, hipStream_t s);
 hipError_t pcg_xr(double* x, double* r, const double* p, const double* Ap, double alpha, int64_t n, hipStream_t s);

@@ -106,15 +106,9 @@ __global__ __launch_bounds__(kRow) void k_ap_step(double* __restrict__ X, const 
 //   colpart[it][j]: sum over tile row block it of X_ij, i < j
 // recover_F then writes both triangles of F from the upper X.
 // ---------------------------------------------------------------------------
-#ifndef RTHX_SYM_ROWS
-#define RTHX_SYM_ROWS 128
-#endif
-#ifndef RTHX_SYM_BATCH
-#define RTHX_SYM_BATCH 8
-#endif
-constexpr int kSymRows = RTHX_SYM_ROWS;    // rows per AP tile
-constexpr int kSymCols = 256;              // columns per AP tile (one per lane)
-constexpr int kSymBatch = RTHX_SYM_BATCH;  // rows loaded before any is stored (loads in flight), multiple of 8
+constexpr int kSymRows = 64;    // rows per AP tile
+constexpr int kSymCols = 512;   // columns per AP tile (two adjacent per lane, one 16-byte access)
+constexpr int kSymBatch = 8;    // rows loaded before any is stored (loads in flight)
 
 __host__ __device__ inline int64_t sym_jt0(int64_t it) { return it * kSymRows / kSymCols; }
 
@@ -144,62 +138,79 @@ __device__ __forceinline__ double wave_sum8(const double* v, int lane) {
   return t;
 }
 
+typedef double d2 __attribute__((ext_vector_type(2)));
+
 // Tile (it, jt) of the upper triangle; SCALE = false is hunger! (row sums
-// only).  EDGE: the tile crosses the diagonal or the matrix edge (per-entry
-// masks); interior tiles run unmasked.
+// only).  Lane owns columns j, j + 1 (j even; ld even, so one aligned 16-byte
+// access per row).  EDGE: the tile crosses the diagonal or the matrix edge
+// (per-entry masks); interior tiles run unmasked.
 template <bool SCALE, bool EDGE>
-__device__ __forceinline__ void ap_sym_tile(double* __restrict__ X, const double* __restrict__ u, int64_t n,
-                                            int64_t i0, int64_t j, double (*rs)[kSymCols / 64],
-                                            double& col) {
+__device__ __forceinline__ void ap_sym_tile(double* __restrict__ X, int64_t ld, const double* __restrict__ u,
+                                            int64_t n, int64_t i0, int64_t j, double (*rs)[kSymCols / 128],
+                                            double& col0, double& col1) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const bool jok = !EDGE || j < n;
-  const double uj = jok ? u[j] : 0.0;
+  const double uj0 = (!EDGE || j < n) ? u[j] : 0.0, uj1 = (!EDGE || j + 1 < n) ? u[j + 1] : 0.0;
   for (int y0 = 0; y0 < kSymRows; y0 += kSymBatch) {
-    double v[kSymBatch];
+    d2 v[kSymBatch];
 #pragma unroll
     for (int b = 0; b < kSymBatch; ++b) {
       const int64_t i = i0 + y0 + b;
-      v[b] = (!EDGE || (jok && i < n && j >= i)) ? X[i * n + j] : 0.0;
+      // j + 1 <= ld - 1 always (ld even, j even): the pair never leaves the row
+      v[b] = (!EDGE || (i < n && j + 1 >= i && j < n)) ? *(const d2*)&X[i * ld + j] : d2{0.0, 0.0};
+      if (EDGE) {
+        if (!(j >= i && j < n)) v[b].x = 0.0;
+        if (!(j + 1 >= i && j + 1 < n)) v[b].y = 0.0;
+      }
     }
+    double rsum[kSymBatch];
 #pragma unroll
     for (int b = 0; b < kSymBatch; ++b) {
       const int64_t i = i0 + y0 + b;
       if (SCALE) {
-        v[b] *= 0.5 * (u[!EDGE || i < n ? i : 0] + uj);
-        if (!EDGE || (jok && i < n && j >= i)) X[i * n + j] = v[b];
+        const double ui = u[!EDGE || i < n ? i : 0];
+        v[b].x *= 0.5 * (ui + uj0);
+        v[b].y *= 0.5 * (ui + uj1);
+        if (!EDGE || (i < n && j + 1 >= i && j < n)) {
+          if (!EDGE || j >= i)
+            *(d2*)&X[i * ld + j] = v[b];
+          else
+            X[i * ld + j + 1] = v[b].y;  // j = i - 1: only (i, i + 1) is in the upper triangle
+        }
       }
-      if (!EDGE || j > i) col += v[b];
+      if (!EDGE || j > i) col0 += v[b].x;
+      if (!EDGE || j + 1 > i) col1 += v[b].y;
+      rsum[b] = v[b].x + v[b].y;
     }
-#pragma unroll
-    for (int h = 0; h < kSymBatch; h += 8) {
-      const double t = wave_sum8(v + h, lane);
-      if ((lane & 7) == 0) rs[y0 + h + (lane >> 3)][wave] = t;
-    }
+    const double t = wave_sum8(rsum, lane);
+    if ((lane & 7) == 0) rs[y0 + (lane >> 3)][wave] = t;
   }
 }
 
 template <bool SCALE>
-__global__ __launch_bounds__(kSymCols) void k_ap_sym(double* __restrict__ X, const double* __restrict__ u, int64_t n,
-                                                     int64_t n_it, int64_t n_jt, double* __restrict__ rowpart,
-                                                     double* __restrict__ colpart) {
-  __shared__ double rs[kSymRows][kSymCols / 64];
+__global__ __launch_bounds__(kSymCols / 2) void k_ap_sym(double* __restrict__ X, int64_t ld,
+                                                         const double* __restrict__ u, int64_t n, int64_t n_it,
+                                                         int64_t n_jt, double* __restrict__ rowpart,
+                                                         double* __restrict__ colpart) {
+  __shared__ double rs[kSymRows][kSymCols / 128];
   // blockIdx.y = it, blockIdx.x = jt - sym_jt0(it); tiles past n_jt return
   const int64_t it = blockIdx.y;
   const int64_t jt = sym_jt0(it) + blockIdx.x;
   if (jt >= n_jt) return;
-  const int64_t i0 = it * kSymRows, j0 = jt * kSymCols, j = j0 + threadIdx.x;
+  const int64_t i0 = it * kSymRows, j0 = jt * kSymCols, j = j0 + 2 * threadIdx.x;
   const bool edge = j0 < i0 + kSymRows || i0 + kSymRows > n || j0 + kSymCols > n;  // uniform
-  double col = 0.0;
+  double col0 = 0.0, col1 = 0.0;
   if (edge)
-    ap_sym_tile<SCALE, true>(X, u, n, i0, j, rs, col);
+    ap_sym_tile<SCALE, true>(X, ld, u, n, i0, j, rs, col0, col1);
   else
-    ap_sym_tile<SCALE, false>(X, u, n, i0, j, rs, col);
-  if (j < n) colpart[it * n + j] = col;
+    ap_sym_tile<SCALE, false>(X, ld, u, n, i0, j, rs, col0, col1);
+  if (j < n) colpart[it * n + j] = col0;
+  if (j + 1 < n) colpart[it * n + j + 1] = col1;
   __syncthreads();
-  for (int y = threadIdx.x; y < kSymRows; y += kSymCols) {
+  if (threadIdx.x < kSymRows) {
+    const int y = threadIdx.x;
     const int64_t i = i0 + y;
     double t = 0.0;
-    for (int w = 0; w < kSymCols / 64; ++w) t += rs[y][w];
+    for (int w = 0; w < kSymCols / 128; ++w) t += rs[y][w];
     if (i < n) rowpart[jt * n + i] = t;
   }
 }
@@ -236,11 +247,12 @@ __global__ __launch_bounds__(64 * kRedSlices) void k_ap_sym_reduce(const double*
   }
 }
 
-// recover_F (:548) from the upper triangle: F_ij = X_ij / r_i for j >= i and
-// F_ij = X_ji / r_i for j < i.  Workgroup (bi, bj), bi <= bj, owns the tile
-// pair (bi, bj) / (bj, bi): it reads the upper tile, then writes both.
-__global__ __launch_bounds__(kTile * 8) void k_recover_sym(double* __restrict__ X, const double* __restrict__ r,
-                                                            int64_t n) {
+// recover_F (:548) from the upper triangle of X (leading dimension ld) into
+// F (n x n): F_ij = X_ij / r_i for j >= i and F_ij = X_ji / r_i for j < i.
+// Workgroup (bi, bj), bi <= bj, reads the upper tile and writes both.
+__global__ __launch_bounds__(kTile * 8) void k_recover_sym(const double* __restrict__ X, int64_t ld,
+                                                            const double* __restrict__ r, int64_t n,
+                                                            double* __restrict__ F) {
   __shared__ double t[kTile][kTile + 1];
   const int64_t tbi = blockIdx.y, tbj = blockIdx.x;
   if (tbj < tbi) return;
@@ -248,23 +260,23 @@ __global__ __launch_bounds__(kTile * 8) void k_recover_sym(double* __restrict__ 
   const int tx = threadIdx.x, ty = threadIdx.y;
   for (int y = ty; y < kTile; y += 8) {
     const int64_t i = bi + y, j = bj + tx;
-    t[y][tx] = (i < n && j < n) ? X[i * n + j] : 0.0;
+    t[y][tx] = (i < n && j < n && j >= i) ? X[i * ld + j] : 0.0;
   }
   __syncthreads();
   if (tbi == tbj) {
     for (int y = ty; y < kTile; y += 8) {
       const int64_t i = bi + y, j = bj + tx;
-      if (i < n && j < n) X[i * n + j] = (tx >= y ? t[y][tx] : t[tx][y]) / r[i];
+      if (i < n && j < n) F[i * n + j] = (tx >= y ? t[y][tx] : t[tx][y]) / r[i];
     }
     return;
   }
   for (int y = ty; y < kTile; y += 8) {
     const int64_t i = bi + y, j = bj + tx;
-    if (i < n && j < n) X[i * n + j] = t[y][tx] / r[i];
+    if (i < n && j < n) F[i * n + j] = t[y][tx] / r[i];
   }
   for (int y = ty; y < kTile; y += 8) {
     const int64_t i = bj + y, j = bi + tx;  // lower tile: F_ij = X_ji / r_i
-    if (i < n && j < n) X[i * n + j] = t[tx][y] / r[i];
+    if (i < n && j < n) F[i * n + j] = t[tx][y] / r[i];
   }
 }
 
@@ -284,12 +296,12 @@ __global__ __launch_bounds__(kRow) void k_hunger(const double* __restrict__ X, c
 }
 
 // delta_R_X_dense (:98-115) per row: sum_{j>i} (X_ij (u_i - u_j))^2 / (w_i^2 + w_j^2).
-__global__ __launch_bounds__(kRow) void k_delta_rows(const double* __restrict__ X, const double* __restrict__ u,
-                                                     const double* __restrict__ w2, int64_t n,
-                                                     double* __restrict__ part) {
+__global__ __launch_bounds__(kRow) void k_delta_rows(const double* __restrict__ X, int64_t ld,
+                                                     const double* __restrict__ u, const double* __restrict__ w2,
+                                                     int64_t n, double* __restrict__ part) {
   __shared__ double sh[kRow / 64];
   const int64_t i = blockIdx.x;
-  const double* x = X + i * n;
+  const double* x = X + i * ld;
   const double ui = u[i], a2 = w2[i];
   double s = 0.0;
   for (int64_t j = i + 1 + threadIdx.x; j < n; j += kRow) {
@@ -348,7 +360,7 @@ __global__ __launch_bounds__(kRow) void k_op_dykstra(const double* Xbar, const d
 template <bool XBAR>
 __global__ __launch_bounds__(kTile * 8) void k_pair(const double* __restrict__ F, const double* __restrict__ w,
                                                     const double* __restrict__ inv_w, const double* __restrict__ w2,
-                                                    int64_t n, double* __restrict__ out) {
+                                                    int64_t n, int64_t ld_out, double* __restrict__ out) {
   __shared__ double t[kTile][kTile + 1];  // F_ji block, transposed on read
   const int64_t bi = (int64_t)blockIdx.y * kTile, bj = (int64_t)blockIdx.x * kTile;
   const int tx = threadIdx.x, ty = threadIdx.y;
@@ -366,7 +378,7 @@ __global__ __launch_bounds__(kTile * 8) void k_pair(const double* __restrict__ F
         v = Y(w2[i], w2[j]) * (inv_w[i] * fij + fji * inv_w[j]);
       else
         v = 0.5 * (w[i] * fij + w[j] * fji);
-      out[i * n + j] = v;
+      out[i * ld_out + j] = v;
     }
   }
 }
@@ -511,8 +523,9 @@ hipError_t hunger(const double* X, const double* w, int64_t n, double* r, double
   hipLaunchKernelGGL(k_hunger, dim3((unsigned)n), dim3(kRow), 0, s, X, w, n, r, u);
   return hipGetLastError();
 }
-hipError_t delta_rows(const double* X, const double* u, const double* w2, int64_t n, double* part, hipStream_t s) {
-  hipLaunchKernelGGL(k_delta_rows, dim3((unsigned)n), dim3(kRow), 0, s, X, u, w2, n, part);
+hipError_t delta_rows(const double* X, int64_t ld, const double* u, const double* w2, int64_t n, double* part,
+                      hipStream_t s) {
+  hipLaunchKernelGGL(k_delta_rows, dim3((unsigned)n), dim3(kRow), 0, s, X, ld, u, w2, n, part);
   return hipGetLastError();
 }
 hipError_t recover(double* X, const double* r, int64_t n, hipStream_t s) {
@@ -521,23 +534,24 @@ hipError_t recover(double* X, const double* r, int64_t n, hipStream_t s) {
 }
 int64_t ap_sym_row_tiles(int64_t n) { return (n + kSymRows - 1) / kSymRows; }
 int64_t ap_sym_col_tiles(int64_t n) { return (n + kSymCols - 1) / kSymCols; }
-hipError_t ap_sym(double* X, const double* u, const double* w, int64_t n, bool scale, double* rowpart,
+hipError_t ap_sym(double* X, int64_t ld, const double* u, const double* w, int64_t n, bool scale, double* rowpart,
                   double* colpart, double* r, double* u_next, hipStream_t s) {
+  if (ld % 2 != 0 || ld < n) return hipErrorInvalidValue;
   const int64_t n_it = ap_sym_row_tiles(n), n_jt = ap_sym_col_tiles(n);
   dim3 g((unsigned)n_jt, (unsigned)n_it);  // blockIdx.x = jt - jt0(it); tiles past n_jt return at once
   if (scale)
-    hipLaunchKernelGGL(k_ap_sym<true>, g, dim3(kSymCols), 0, s, X, u, n, n_it, n_jt, rowpart, colpart);
+    hipLaunchKernelGGL(k_ap_sym<true>, g, dim3(kSymCols / 2), 0, s, X, ld, u, n, n_it, n_jt, rowpart, colpart);
   else
-    hipLaunchKernelGGL(k_ap_sym<false>, g, dim3(kSymCols), 0, s, X, u, n, n_it, n_jt, rowpart, colpart);
+    hipLaunchKernelGGL(k_ap_sym<false>, g, dim3(kSymCols / 2), 0, s, X, ld, u, n, n_it, n_jt, rowpart, colpart);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_ap_sym_reduce, dim3(grid1(n, 64)), dim3(64 * kRedSlices), 0, s, rowpart, colpart, w, n, n_it,
                      n_jt, r, u_next);
   return hipGetLastError();
 }
-hipError_t recover_sym(double* X, const double* r, int64_t n, hipStream_t s) {
+hipError_t recover_sym(const double* X, int64_t ld, const double* r, int64_t n, double* F, hipStream_t s) {
   dim3 g(grid1(n, kTile), grid1(n, kTile));
-  hipLaunchKernelGGL(k_recover_sym, g, dim3(kTile, 8), 0, s, X, r, n);
+  hipLaunchKernelGGL(k_recover_sym, g, dim3(kTile, 8), 0, s, X, ld, r, n, F);
   return hipGetLastError();
 }
 hipError_t renorm(double* F, int64_t n, hipStream_t s) {
@@ -550,14 +564,14 @@ hipError_t op_dykstra(const double* Xbar, const double* lam, const double* w2, c
                      Fs);
   return hipGetLastError();
 }
-hipError_t build_x(const double* F, const double* w, int64_t n, double* X, hipStream_t s) {
+hipError_t build_x(const double* F, const double* w, int64_t n, int64_t ld, double* X, hipStream_t s) {
   dim3 g(grid1(n, kTile), grid1(n, kTile));
-  hipLaunchKernelGGL(k_pair<false>, g, dim3(kTile, 8), 0, s, F, w, nullptr, nullptr, n, X);
+  hipLaunchKernelGGL(k_pair<false>, g, dim3(kTile, 8), 0, s, F, w, nullptr, nullptr, n, ld, X);
   return hipGetLastError();
 }
 hipError_t xbar(const double* F, const double* inv_w, const double* w2, int64_t n, double* Xbar, hipStream_t s) {
   dim3 g(grid1(n, kTile), grid1(n, kTile));
-  hipLaunchKernelGGL(k_pair<true>, g, dim3(kTile, 8), 0, s, F, nullptr, inv_w, w2, n, Xbar);
+  hipLaunchKernelGGL(k_pair<true>, g, dim3(kTile, 8), 0, s, F, nullptr, inv_w, w2, n, n, Xbar);
   return hipGetLastError();
 }
 hipError_t dot(const double* a, const double* b, int64_t n, double* out, hipStream_t s) {
