@@ -101,8 +101,14 @@ int check_grid(const rthx_grid_desc& g, int32_t count, const char* what) {
 }
 
 // Row splitting: target number of workgroups per launch (>> 256 CUs x ~5
-// resident workgroups) and the fewest rays a split workgroup traces.
-constexpr int64_t kSplitTargetBlocks = 8192;
+// resident workgroups) and the fewest rays a split workgroup traces.  4096
+// measured faster than 8192 for every multi-GPU shard of C2 (W = 2: 66.6 ->
+// 77.0 Grays/s per GPU; the dense merge of split rows costs more than the
+// tail of ~4 waves of workgroups), W = 1 unchanged (tools/split_ab.sh).
+#ifndef RTHX_SPLIT_TARGET
+#define RTHX_SPLIT_TARGET 4096
+#endif
+constexpr int64_t kSplitTargetBlocks = RTHX_SPLIT_TARGET;
 constexpr int64_t kSplitMinRays = 2048;
 
 // Device point-location grids: rthx_grid.cpp.  Cells per mean polygon extent

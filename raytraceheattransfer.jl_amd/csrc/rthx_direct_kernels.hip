@@ -48,8 +48,17 @@ __device__ __forceinline__ void philox_block(uint32_t w[4], uint32_t r0, uint32_
   philox4x32_10(w, k0, k1);
 }
 
+#ifndef RTHX_DIRECT_WAVES
+#define RTHX_DIRECT_WAVES 0  // > 0: amdgpu_waves_per_eu floor (register budget) for variants
+#endif
+#if RTHX_DIRECT_WAVES > 0
+#define RTHX_DIRECT_ATTR __attribute__((amdgpu_waves_per_eu(RTHX_DIRECT_WAVES)))
+#else
+#define RTHX_DIRECT_ATTR
+#endif
+
 template <bool UNIFORM, bool FAITHFUL, bool SINGLE, bool AXIS>
-__global__ __launch_bounds__(FAITHFUL ? kDirectThreads : kDirectMaxThreads) void trace_direct_kernel(const DevDomain* __restrict__ Dp,
+__global__ __launch_bounds__(FAITHFUL ? kDirectThreads : kDirectMaxThreads) RTHX_DIRECT_ATTR void trace_direct_kernel(const DevDomain* __restrict__ Dp,
                                                                       DirectParams Q) {
   // Q.hist: Q.hist copies of the [3][n_elem] counters; wave v adds into copy
   // v % Q.hist (fewer lanes contend for one LDS address on small domains)
