@@ -78,6 +78,21 @@ def test_dense_op_ap_matches_restatement(hip, ndim):
     check_props(Fg, w)
 
 
+def test_dense_ap_interior_tiles(hip):
+    """N = 1085 (odd, padded leading dimension): the upper-triangle AP runs
+    interior tiles (no masks) beside diagonal and edge tiles, and the
+    fixed-order partial sums span many tiles per row."""
+    dom = H.square_domain(31)
+    F = traced_F(dom, 3_000_000, seed=11)
+    from rthx.smoothing import get_w
+
+    w = get_w(dom)
+    assert F.shape[0] == 1085 and F.nnz / F.shape[0] ** 2 > 0.25
+    Fg, info, _ = compare(F, w, dom.num_surfaces)
+    assert info["dense"] == 1
+    check_props(Fg, w)
+
+
 @pytest.mark.parametrize("k", [0, 6])
 def test_prescribed_dykstra_rounds(hip, k):
     dom = H.square_domain(11)
