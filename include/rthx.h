@@ -383,6 +383,15 @@ typedef struct rthx_scene3d rthx_scene3d;
 
 int rthx_scene3d_create(const double* xyz, const int32_t* nv, const double* normal, int64_t n, int32_t device,
                         rthx_scene3d** out);
+/* As rthx_scene3d_create, with coplanar groups: group[k] >= 0 names the
+ * group of polygon k (NULL: every polygon its own group).  A ray is never
+ * absorbed by a polygon of its emitter's group -- the sub-faces of one planar
+ * face cannot be hit by a ray leaving that face at a positive angle, so this
+ * only removes round-off hits at t ~ 0 and lets the walk skip the emitter's
+ * face.  Each group's polygons must be one contiguous run of indices
+ * (face-major sub-face order), else RTHX_EINVAL. */
+int rthx_scene3d_create_grouped(const double* xyz, const int32_t* nv, const double* normal, const int32_t* group,
+                                int64_t n, int32_t device, rthx_scene3d** out);
 void rthx_scene3d_destroy(rthx_scene3d* scene);
 /* Acceleration-structure statistics of a scene (any pointer may be NULL):
  * Moeller-Trumbore triangles, BVH inner nodes, inner-node depth (the walk

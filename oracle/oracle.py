@@ -61,6 +61,9 @@ def load() -> C.CDLL:
     lib.oracle_view_factors_3d.argtypes = [dp, C.POINTER(C.c_int32), C.c_int64, C.c_int, dp, dp]
     lib.oracle_trace_exchange_3d.argtypes = [dp, C.POINTER(C.c_int32), dp, C.c_int64, C.POINTER(abi.TraceArgs), C.c_int,
                                              C.POINTER(C.c_uint32), C.POINTER(C.c_int64)]
+    lib.oracle_trace_exchange_3d_grouped.argtypes = [dp, C.POINTER(C.c_int32), dp, C.POINTER(C.c_int32), C.c_int64,
+                                                     C.POINTER(abi.TraceArgs), C.c_int, C.POINTER(C.c_uint32),
+                                                     C.POINTER(C.c_int64)]
     lib.oracle_last_error.restype = C.c_char_p
     _lib = lib
     return lib
@@ -168,8 +171,10 @@ def view_factors_3d(xyz, nv, nthreads: int = 0, with_F: bool = True):
     return F, area
 
 
-def trace_exchange_3d(xyz, nv, normals, R, seed=1, begin=0, end=None, stride=1, nthreads: int = 0):
-    """The 3D tracer restated on the CPU: dense counts[rows, n] and lost rays."""
+def trace_exchange_3d(xyz, nv, normals, R, seed=1, begin=0, end=None, stride=1, nthreads: int = 0, groups=None):
+    """The 3D tracer restated on the CPU: dense counts[rows, n] and lost rays.
+    ``groups``: coplanar group per polygon (rays skip their emitter's group),
+    None = every polygon its own group."""
     x = np.ascontiguousarray(xyz, dtype=np.float64).reshape(-1, 12)
     k = np.ascontiguousarray(nv, dtype=np.int32)
     nrm = np.ascontiguousarray(normals, dtype=np.float64).reshape(-1, 3)
@@ -179,8 +184,11 @@ def trace_exchange_3d(xyz, nv, normals, R, seed=1, begin=0, end=None, stride=1, 
     args, _keep = make_args(0, R, 0.0, seed, begin, end, stride)
     counts = np.zeros((max(rows, 1), n), dtype=np.uint32)
     lost = C.c_int64(0)
-    rc = load().oracle_trace_exchange_3d(abi.ptr(x, C.c_double), abi.ptr(k, C.c_int32), abi.ptr(nrm, C.c_double), n,
-                                         C.byref(args), nthreads, abi.ptr(counts, C.c_uint32), C.byref(lost))
+    g = None if groups is None else np.ascontiguousarray(groups, dtype=np.int32)
+    rc = load().oracle_trace_exchange_3d_grouped(abi.ptr(x, C.c_double), abi.ptr(k, C.c_int32),
+                                                 abi.ptr(nrm, C.c_double), None if g is None else abi.ptr(g, C.c_int32),
+                                                 n, C.byref(args), nthreads, abi.ptr(counts, C.c_uint32),
+                                                 C.byref(lost))
     assert rc == 0
     return counts[:rows], lost.value
 

@@ -1352,6 +1352,7 @@ static double t3_mt(const t3_tri* T, const double* o, const double* d) {
 typedef struct {
   const t3_poly* polys;
   const t3_tri* tris;
+  const int32_t* group; /* per polygon: rays are not absorbed by their emitter's group */
   int64_t n_tri, n, R, k0, k1, begin, stride;
   uint64_t seed;
   uint32_t* counts; /* dense [rows][n] */
@@ -1382,7 +1383,7 @@ static void* t3_worker(void* arg) {
       double best_t = INFINITY;
       int64_t best = -1;
       for (int64_t t = 0; t < W->n_tri; ++t) { /* index order: ties keep the lower index */
-        if (W->tris[t].poly == g) continue;
+        if (W->group[W->tris[t].poly] == W->group[g]) continue;
         double th = t3_mt(&W->tris[t], o, d);
         if (th > 0.0 && th < best_t) { best_t = th; best = t; }
       }
@@ -1395,8 +1396,9 @@ static void* t3_worker(void* arg) {
 
 /* Dense counts[n_rows][n] of emitters g = emitter_begin + k * stride; returns
  * the lost-ray total in *lost.  Polygons as rthx_scene3d_create. */
-ORACLE_API int oracle_trace_exchange_3d(const double* xyz, const int32_t* nv, const double* normal, int64_t n,
-                                        const rthx_trace_args* a, int nthreads, uint32_t* counts, int64_t* lost) {
+ORACLE_API int oracle_trace_exchange_3d_grouped(const double* xyz, const int32_t* nv, const double* normal,
+                                                const int32_t* group, int64_t n, const rthx_trace_args* a,
+                                                int nthreads, uint32_t* counts, int64_t* lost) {
   if (!xyz || !nv || !normal || !a || !counts || n < 2) return RTHX_EINVAL;
   t3_poly* P = (t3_poly*)calloc((size_t)n, sizeof(t3_poly));
   t3_tri* T = (t3_tri*)calloc(2 * (size_t)n, sizeof(t3_tri));
@@ -1433,6 +1435,8 @@ ORACLE_API int oracle_trace_exchange_3d(const double* xyz, const int32_t* nv, co
       t->poly = (int)k;
     }
   }
+  int32_t* G = (int32_t*)malloc((size_t)n * sizeof(int32_t));
+  for (int64_t k = 0; k < n; ++k) G[k] = group ? group[k] : (int32_t)k;
   int64_t end = a->emitter_end < n ? a->emitter_end : n;
   int64_t rows = end > a->emitter_begin ? (end - a->emitter_begin + a->emitter_stride - 1) / a->emitter_stride : 0;
   if (nthreads <= 0) nthreads = (int)sysconf(_SC_NPROCESSORS_ONLN);
@@ -1442,7 +1446,7 @@ ORACLE_API int oracle_trace_exchange_3d(const double* xyz, const int32_t* nv, co
   int64_t per = rows / nthreads, rem = rows % nthreads, start = 0;
   for (int t = 0; t < nthreads; ++t) {
     int64_t sz = per + (t < rem ? 1 : 0);
-    W[t].polys = P; W[t].tris = T; W[t].n_tri = nt; W[t].n = n; W[t].R = a->rays_per_emitter;
+    W[t].polys = P; W[t].tris = T; W[t].group = G; W[t].n_tri = nt; W[t].n = n; W[t].R = a->rays_per_emitter;
     W[t].begin = a->emitter_begin; W[t].stride = a->emitter_stride; W[t].seed = a->seed;
     W[t].k0 = start; W[t].k1 = start + sz; W[t].counts = counts;
     start += sz;
@@ -1453,6 +1457,12 @@ ORACLE_API int oracle_trace_exchange_3d(const double* xyz, const int32_t* nv, co
   int64_t lost_total = 0;
   for (int t = 0; t < nthreads; ++t) lost_total += W[t].lost;
   if (lost) *lost = lost_total;
-  free(th); free(W); free(P); free(T);
+  free(th); free(W); free(P); free(T); free(G);
   return RTHX_OK;
+}
+
+/* Every polygon its own group (rthx_scene3d_create). */
+ORACLE_API int oracle_trace_exchange_3d(const double* xyz, const int32_t* nv, const double* normal, int64_t n,
+                                        const rthx_trace_args* a, int nthreads, uint32_t* counts, int64_t* lost) {
+  return oracle_trace_exchange_3d_grouped(xyz, nv, normal, NULL, n, a, nthreads, counts, lost);
 }

@@ -19,6 +19,7 @@
 #include <cstring>
 #include <numeric>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/rthx.h"
@@ -69,6 +70,7 @@ constexpr int64_t kSplitMinRays = 1024;
 
 struct BuildTri {
   double lo[3], hi[3], c[3];
+  int group;
 };
 
 struct Box {
@@ -112,13 +114,22 @@ struct Bvh2Builder {
   bool median;
   int depth = 0;
 
-  void set_child(int idx, int slot, int32_t ref, const Box& bx) {
+  void set_child(int idx, int slot, int32_t ref, const Box& bx, int group) {
     rthx::Bvh2Node& nd = nodes[idx];
     nd.child[slot] = ref;
+    nd.group[slot] = group;
     for (int k = 0; k < 3; ++k) {
       nd.lo[slot][k] = down32(bx.lo[k] - pad);
       nd.hi[slot][k] = up32(bx.hi[k] + pad);
     }
+  }
+
+  // group of the range order[b, e): the common group of its triangles, or -1
+  int range_group(int b, int e) const {
+    const int g = b < e ? bt[order[b]].group : -1;
+    for (int i = b + 1; i < e; ++i)
+      if (bt[order[i]].group != g) return -1;
+    return g;
   }
 
   int32_t build(int b, int e, int level, Box& out) {
@@ -200,8 +211,8 @@ struct Bvh2Builder {
     Box lb, rb;
     const int32_t l = build(b, mid, level + 1, lb);
     const int32_t r = build(mid, e, level + 1, rb);
-    set_child(idx, 0, l, lb);
-    set_child(idx, 1, r, rb);
+    set_child(idx, 0, l, lb, range_group(b, mid));
+    set_child(idx, 1, r, rb, range_group(mid, e));
     return idx;
   }
 };
@@ -219,8 +230,8 @@ int build_bvh2(std::vector<rthx::Bvh2Node>& nodes, std::vector<int>& order, cons
     nodes.push_back(rthx::Bvh2Node{});
     Box bx, empty;
     for (int i = 0; i < n; ++i) bx.grow(bt[i].lo, bt[i].hi);
-    B.set_child(0, 0, leaf_ref(0, n), bx);
-    B.set_child(0, 1, leaf_ref(0, 0), empty);
+    B.set_child(0, 0, leaf_ref(0, n), bx, B.range_group(0, n));
+    B.set_child(0, 1, leaf_ref(0, 0), empty, -1);
     return 1;
   }
   Box root;
@@ -285,10 +296,32 @@ void layout_nodes(std::vector<rthx::Bvh2Node>& nodes) {
 
 RTHX_EXPORT int rthx_scene3d_create(const double* xyz, const int32_t* nv, const double* normal, int64_t n,
                                     int32_t device, rthx_scene3d** out) {
+  return rthx_scene3d_create_grouped(xyz, nv, normal, nullptr, n, device, out);
+}
+
+RTHX_EXPORT int rthx_scene3d_create_grouped(const double* xyz, const int32_t* nv, const double* normal,
+                                            const int32_t* group, int64_t n, int32_t device, rthx_scene3d** out) {
   if (!out) return fail(RTHX_EINVAL, "null out");
   *out = nullptr;
   if (!xyz || !nv || !normal || n < 2) return fail(RTHX_EINVAL, "null argument or fewer than 2 polygons");
   if (n >= (int64_t(1) << 30)) return fail(RTHX_ERANGE, "too many polygons");
+  // groups: each a contiguous run of polygon indices ([glo, ghi) per polygon)
+  std::vector<int32_t> glo(n), ghi(n);
+  {
+    std::unordered_map<int32_t, int64_t> seen;
+    int64_t run = 0;
+    for (int64_t k = 0; k < n; ++k) {
+      if (group && group[k] < 0) return fail(RTHX_EINVAL, "group ids must be >= 0");
+      if (k > 0 && (!group || group[k] != group[k - 1])) run = k;
+      const int32_t gk = group ? group[k] : (int32_t)k;
+      auto it = seen.find(gk);
+      if (it != seen.end() && it->second != run) return fail(RTHX_EINVAL, "a group's polygons must be contiguous");
+      seen[gk] = run;
+      glo[k] = (int32_t)run;
+    }
+    for (int64_t k = n - 1; k >= 0; --k)
+      ghi[k] = (k == n - 1 || glo[k + 1] != glo[k]) ? (int32_t)(k + 1) : ghi[k + 1];
+  }
   std::vector<rthx::Emit3> polys(n);
   std::vector<rthx::Tri3> tris;
   std::vector<BuildTri> bt;
@@ -336,7 +369,9 @@ RTHX_EXPORT int rthx_scene3d_create(const double* xyz, const int32_t* nv, const 
     E.t2[0] = t2.x; E.t2[1] = t2.y; E.t2[2] = t2.z;
     E.tri_frac = m == 4 ? a1 / (a1 + a2) : 1.0;
     E.nv = m;
-    E.reserved = 0;
+    E.group = group ? group[k] : (int32_t)k;
+    E.glo = glo[k];
+    E.ghi = ghi[k];
     const int corners[2][3] = {{0, 1, 2}, {2, 3, 0}};
     for (int h = 0; h < (m == 4 ? 2 : 1); ++h) {
       const V a = v[corners[h][0]], b = v[corners[h][1]], c = v[corners[h][2]];
@@ -356,6 +391,7 @@ RTHX_EXPORT int rthx_scene3d_create(const double* xyz, const int32_t* nv, const 
         B.hi[d] = std::max({x[0], x[1], x[2]});
         B.c[d] = (x[0] + x[1] + x[2]) / 3.0;
       }
+      B.group = E.group;
       bt.push_back(B);
     }
   }

@@ -17,7 +17,8 @@ struct alignas(16) Emit3 {
   double t2[3];       // n x t1
   double tri_frac;    // area(v0 v1 v2) / area (quads; 1 for triangles)
   int32_t nv;
-  int32_t reserved;
+  int32_t group;      // coplanar group (rthx_scene3d_create_grouped): rays never hit their own group
+  int32_t glo, ghi;   // the group's polygons are [glo, ghi) (one contiguous run)
 };
 
 // Triangle for the Moeller-Trumbore test: v0, e1 = v1 - v0, e2 = v2 - v0.
@@ -36,7 +37,7 @@ struct alignas(16) Tri3 {
 struct alignas(16) Bvh2Node {
   float lo[2][3], hi[2][3];
   int32_t child[2];
-  int32_t pad[2];
+  int32_t group[2];  // the group every triangle under child c belongs to, or -1 (mixed)
 };
 static_assert(sizeof(Bvh2Node) == 64, "Bvh2Node is one 64-byte record");
 

@@ -118,12 +118,12 @@ struct Walk {
     pending = 0;
   }
 
-  __device__ __forceinline__ void leaf(const DevScene3D& S, int skip, int ref) {
+  __device__ __forceinline__ void leaf(const DevScene3D& S, int glo, int glen, int ref) {
     ref = ~ref;
     const int first = ref >> kLeafBits, last = first + (ref & ((1 << kLeafBits) - 1));
     for (int k = first; k < last; ++k) {
       const Tri3 T = S.tris[k];
-      if (T.poly == skip) continue;
+      if ((unsigned)(T.poly - glo) < (unsigned)glen) continue;  // the emitter's group
       const double t = moller_trumbore(T, o, d);
       if (t > 0.0 && (t < best_t || (t == best_t && T.id < best_id))) {
         best_t = t;
@@ -137,8 +137,8 @@ struct Walk {
   // One round of the walk: descend (speculatively) until every live lane of
   // the wave holds a leaf, then test the leaves; false once this lane's walk
   // is over.
-  __device__ __forceinline__ bool step(const DevScene3D& S, const Bvh2Node RTHX_LDS* top, int n_top, int skip,
-                                       int RTHX_LDS* stk) {
+  __device__ __forceinline__ bool step(const DevScene3D& S, const Bvh2Node RTHX_LDS* top, int n_top, int group,
+                                       int glo, int glen, int RTHX_LDS* stk) {
     while (node >= 0) {
       Bvh2Node nd;
       if (node < n_top) {
@@ -159,7 +159,8 @@ struct Walk {
         tn[c] = fmaxf(fmaxf(fminf(a0, b0), fminf(a1, b1)), fmaxf(fminf(a2, b2), 0.0f));
         tf[c] = fminf(fminf(fmaxf(a0, b0), fmaxf(a1, b1)), fminf(fmaxf(a2, b2), best_tf));
       }
-      const bool h0 = tn[0] <= tf[0], h1 = tn[1] <= tf[1];
+      // a child whose triangles all belong to the emitter's group is never entered
+      const bool h0 = tn[0] <= tf[0] && nd.group[0] != group, h1 = tn[1] <= tf[1] && nd.group[1] != group;
       if (h0 && h1) {
         const bool near0 = tn[0] <= tn[1];
         stk[sp * kThreads] = near0 ? nd.child[1] : nd.child[0];
@@ -177,7 +178,7 @@ struct Walk {
       if (__ballot(pending == 0) == 0ull) break;
     }
     while (pending < 0) {
-      leaf(S, skip, pending);
+      leaf(S, glo, glen, pending);
       pending = 0;
       if (node < 0 && node != kWalkDone) {
         pending = node;
@@ -270,6 +271,8 @@ __global__ __launch_bounds__(kThreads) RTHX_T3_ATTR void trace_exchange_3d_kerne
   }
   __syncthreads();
   uint32_t tallied = 0;
+  // the emitter's coplanar group: its triangles are skipped, its subtrees pruned
+  const int grp = s_emit.group, glo = s_emit.glo, glen = s_emit.ghi - s_emit.glo;
   int RTHX_LDS* stk = (int RTHX_LDS*)(hist + trace3d_stack_offset(words)) + tid;
   auto tally = [&](int a) {
     if (a >= 0) {
@@ -302,7 +305,7 @@ __global__ __launch_bounds__(kThreads) RTHX_T3_ATTR void trace_exchange_3d_kerne
       }
     }
     if (__ballot(live) == 0ull) break;
-    if (live && !w.step(S, topo, n_top, (int)g, stk)) {
+    if (live && !w.step(S, topo, n_top, grp, glo, glen, stk)) {
       tally(w.best_poly);
       live = false;
     }
@@ -315,7 +318,7 @@ __global__ __launch_bounds__(kThreads) RTHX_T3_ATTR void trace_exchange_3d_kerne
                        P.key1, o, d);
     Walk w;
     w.init(o, d);
-    while (w.step(S, topo, n_top, (int)g, stk)) {
+    while (w.step(S, topo, n_top, grp, glo, glen, stk)) {
     }
     tally(w.best_poly);
   }

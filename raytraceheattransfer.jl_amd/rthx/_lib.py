@@ -79,6 +79,9 @@ def load(path: Optional[str] = None) -> C.CDLL:
                                       C.POINTER(C.c_uint64), C.POINTER(abi.DirectInfo)]
     lib.rthx_debug_alias.argtypes = [dp, C.c_int64, C.POINTER(C.c_uint64)]
     lib.rthx_scene3d_create.argtypes = [dp, C.POINTER(C.c_int32), dp, C.c_int64, C.c_int32, C.POINTER(C.c_void_p)]
+    if hasattr(lib, "rthx_scene3d_create_grouped"):  # (older A/B variant libraries lack it)
+        lib.rthx_scene3d_create_grouped.argtypes = [dp, C.POINTER(C.c_int32), dp, C.POINTER(C.c_int32), C.c_int64,
+                                                    C.c_int32, C.POINTER(C.c_void_p)]
     lib.rthx_scene3d_destroy.argtypes = [C.c_void_p]
     lib.rthx_scene3d_destroy.restype = None
     if hasattr(lib, "rthx_scene3d_stats"):  # (older A/B variant libraries lack it)

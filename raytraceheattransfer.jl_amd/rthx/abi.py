@@ -240,6 +240,7 @@ EXPORTED_SYMBOLS = (
     "rthx_trace_direct",
     "rthx_view_factors_3d",
     "rthx_scene3d_create",
+    "rthx_scene3d_create_grouped",
     "rthx_scene3d_destroy",
     "rthx_scene3d_stats",
     "rthx_trace_exchange_3d",

@@ -23,7 +23,7 @@ from . import abi
 class Scene3D:
     """An uploaded 3D polygon scene (rthx_scene3d*)."""
 
-    def __init__(self, xyz, nv, normals, device: int = 0):
+    def __init__(self, xyz, nv, normals, device: int = 0, groups=None):
         from ._lib import check, load
 
         self._lib = load()
@@ -33,8 +33,14 @@ class Scene3D:
         nrm = np.ascontiguousarray(normals, dtype=np.float64).reshape(-1, 3)
         self.n = len(k)
         h = C.c_void_p()
-        check(self._lib.rthx_scene3d_create(abi.ptr(x, C.c_double), abi.ptr(k, C.c_int32), abi.ptr(nrm, C.c_double),
-                                            self.n, device, C.byref(h)))
+        if groups is None:
+            check(self._lib.rthx_scene3d_create(abi.ptr(x, C.c_double), abi.ptr(k, C.c_int32),
+                                                abi.ptr(nrm, C.c_double), self.n, device, C.byref(h)))
+        else:  # coplanar groups: rays are never absorbed by their emitter's group
+            g = np.ascontiguousarray(groups, dtype=np.int32)
+            check(self._lib.rthx_scene3d_create_grouped(abi.ptr(x, C.c_double), abi.ptr(k, C.c_int32),
+                                                        abi.ptr(nrm, C.c_double), abi.ptr(g, C.c_int32), self.n,
+                                                        device, C.byref(h)))
         self.handle = h
 
     def trace(self, rays_per_emitter: int, seed: int = 1, faithful: bool = False, emitter_begin: int = 0,

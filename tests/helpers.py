@@ -315,3 +315,13 @@ def cube_icosphere_scene(ndim=10, level=3, radius=0.3):
         normals.append(tri.mean(axis=0) - centre)
     nv = np.array([4] * n_cube + [3] * (len(polys) - n_cube), dtype=np.int32)
     return np.array(polys), nv, np.array(normals), n_cube
+
+
+def cube_icosphere_groups(ndim=10, level=3):
+    """Coplanar groups of cube_icosphere_scene: the ndim x ndim sub-faces of
+    each cube face form one group (face-major, contiguous); every sphere
+    triangle is its own group."""
+    n_cube = 6 * ndim * ndim
+    n_sph = 20 * 4 ** level
+    return np.concatenate([np.arange(n_cube) // (ndim * ndim), 6 + np.arange(n_sph)]).astype(np.int32)
+

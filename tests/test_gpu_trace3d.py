@@ -19,10 +19,10 @@ from oracle import oracle
 pytestmark = pytest.mark.gpu
 
 
-def gpu_dense(xyz, nv, nrm, R, seed=1, begin=0, end=None, stride=1, faithful=False):
+def gpu_dense(xyz, nv, nrm, R, seed=1, begin=0, end=None, stride=1, faithful=False, groups=None):
     from rthx.trace3d import Scene3D
 
-    s = Scene3D(xyz, nv, nrm)
+    s = Scene3D(xyz, nv, nrm, groups=groups)
     try:
         rp, cols, cnt, info = s.trace(R, seed=seed, faithful=faithful, emitter_begin=begin, emitter_end=end,
                                       emitter_stride=stride)
@@ -152,3 +152,37 @@ def test_u32_counters_and_stats(hip):
         row = np.zeros(n, dtype=np.uint32)
         row[cols[rp[g]:rp[g + 1]]] = cnt[rp[g]:rp[g + 1]]
         assert np.array_equal(row, D[g]), g
+
+
+@pytest.mark.parametrize("ndim,level", [(3, 1), (6, 2)])
+def test_coplanar_groups_exact(hip, ndim, level):
+    """rthx_scene3d_create_grouped: the sub-faces of each cube face form one
+    group; rays are never absorbed by their emitter's group, and the walk
+    prunes subtrees whose triangles all belong to it.  Exact against the
+    restatement with the same groups; no same-face exchange."""
+    xyz, nv, nrm, nc = H.cube_icosphere_scene(ndim=ndim, level=level)
+    g = H.cube_icosphere_groups(ndim, level)
+    assert len(g) == len(nv)
+    D, info = gpu_dense(xyz, nv, nrm, 6000, seed=12, groups=g)
+    C, lost = oracle.trace_exchange_3d(xyz, nv, nrm, 6000, seed=12, nthreads=16, groups=g)
+    assert np.array_equal(D, C) and info["lost_total"] == lost
+    same = g[:, None] == g[None, :]
+    assert np.all(D[same] == 0)
+
+
+def test_group_validation(hip):
+    """Groups must be non-negative and contiguous runs of polygon indices."""
+    from rthx._lib import RthxError
+    from rthx.trace3d import Scene3D
+
+    xyz, nv, nrm, nc = H.cube_icosphere_scene(ndim=2, level=0)
+    g = H.cube_icosphere_groups(2, 0)
+    bad = g.copy()
+    bad[0], bad[5] = bad[5], bad[0]  # face 0 and face 1 interleaved
+    with pytest.raises(RthxError):
+        Scene3D(xyz, nv, nrm, groups=bad)
+    neg = g.copy()
+    neg[3] = -1
+    with pytest.raises(RthxError):
+        Scene3D(xyz, nv, nrm, groups=neg)
+

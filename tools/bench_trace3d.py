@@ -30,12 +30,14 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--cpu-rows", type=int, default=8)
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-groups", action="store_true", help="every polygon its own group (no coplanar faces)")
     args = ap.parse_args()
     xyz, nv, nrm, nc = H.cube_icosphere_scene(args.ndim, args.level, args.radius)
     n = len(nv)
     R = int(args.rays) // n
     t = time.perf_counter()
-    scene = Scene3D(xyz, nv, nrm)
+    groups = None if args.no_groups else H.cube_icosphere_groups(args.ndim, args.level)
+    scene = Scene3D(xyz, nv, nrm, groups=groups)
     t_build = time.perf_counter() - t
     scene.trace(R, device_only=True)
     ks, cs = [], []
@@ -52,7 +54,7 @@ def main():
     c = float(np.median(cs)) * 1e3
     rays = n * R
     line = (f"config4 cube {args.ndim}x{args.ndim}/face + icosphere L{args.level} (n={n}, {n - nc} triangles, "
-            f"{int(np.sum(np.where(nv == 4, 2, 1)))} MT triangles)  R={R} rays={rays:.3e}  scene build {t_build * 1e3:.0f} ms  "
+            f"{int(np.sum(np.where(nv == 4, 2, 1)))} MT triangles, {'polygon' if args.no_groups else 'face'} groups)  R={R} rays={rays:.3e}  scene build {t_build * 1e3:.0f} ms  "
             f"BVH {stats}  kernel {k:.2f} ms ({rays / k / 1e6:.2f} Grays/s)  call {c:.2f} ms  lost {info['lost_total']}  nnz {info['nnz']}")
     if args.cpu_rows > 0:
         from oracle import oracle
@@ -62,7 +64,7 @@ def main():
         Rc = 20_000
         t = time.perf_counter()
         oracle.trace_exchange_3d(xyz, nv, nrm, Rc, begin=0, end=rows * stride, stride=stride,
-                                 nthreads=args.cpu_threads)
+                                 nthreads=args.cpu_threads, groups=groups)
         dt = time.perf_counter() - t
         line += f"  | CPU restatement (brute force) {args.cpu_threads} thr: {rows * Rc / dt / 1e6:.3f} Mrays/s"
     print(line, flush=True)

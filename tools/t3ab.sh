@@ -11,4 +11,5 @@ for cfg in "--ndim 10 --level 3" "--ndim 20 --level 4"; do
     RTHX_LIB=$CS/$v/librthx.so timeout -k 10 200 python tools/bench_trace3d.py $cfg --cpu-rows 0 2>&1 | grep config4 | sed "s|^|$v |" || exit 1
   done
   timeout -k 10 200 python tools/bench_trace3d.py $cfg --cpu-rows 0 2>&1 | grep config4 | sed 's/^/build /' || exit 1
+  timeout -k 10 200 python tools/bench_trace3d.py $cfg --cpu-rows 0 --no-groups 2>&1 | grep config4 | sed 's/^/build /' || exit 1
 done
