@@ -466,7 +466,9 @@ end
 Monte Carlo counterpart of enclosureViewFactors3D for enclosures with
 obstructions (BASELINE config 4: a sphere inside a cube), where the analytic
 pair view factors (which assume every pair sees each other) do not hold.
-Sub-faces in the same face-major order; each leaves along its inwardNormal.
+Sub-faces in the same face-major order; each leaves along its inwardNormal,
+and the sub-faces of one super face form a coplanar group (a ray is never
+absorbed by its own face).
 `rays_tot` rays in total, div(rays_tot, n) per sub-face as the 2D tracer
 (parallelRayTracing.jl:6).  F_raw = counts / R, row-normalised like the 2D
 path (row_normalize!), then the reference's smooth_F with
@@ -475,6 +477,8 @@ smooth_surfaces_only = true (enclosureViewFactors3D.jl:88-91).
 function enclosureViewFactorsMC3D(superFaces, rays_tot::Integer; max_iters::Int = 1000, verbose::Bool = false)
     RTHT = parentmodule(@__MODULE__).RayTraceHeatTransfer
     subs = [sf for f in superFaces for sf in f.subFaces]
+    # the sub-faces of one super face are coplanar: one group (contiguous, face-major)
+    grp = Int32[i - 1 for (i, f) in enumerate(superFaces) for _ in f.subFaces]
     n = length(subs)
     xyz = zeros(Float64, 12n); nv = zeros(Int32, n); nrm = zeros(Float64, 3n)
     for (k, sf) in enumerate(subs)
@@ -488,9 +492,9 @@ function enclosureViewFactorsMC3D(superFaces, rays_tot::Integer; max_iters::Int 
     end
     R = div(rays_tot, n)
     scene = Ref{Ptr{Cvoid}}(C_NULL)
-    check(ccall((:rthx_scene3d_create, LIB[]), Cint,
-                (Ptr{Float64}, Ptr{Int32}, Ptr{Float64}, Int64, Int32, Ptr{Ptr{Cvoid}}),
-                xyz, nv, nrm, n, DEVICE[], scene))
+    check(ccall((:rthx_scene3d_create_grouped, LIB[]), Cint,
+                (Ptr{Float64}, Ptr{Int32}, Ptr{Float64}, Ptr{Int32}, Int64, Int32, Ptr{Ptr{Cvoid}}),
+                xyz, nv, nrm, grp, n, DEVICE[], scene))
     res = Ref{Ptr{Cvoid}}(C_NULL)
     try
         check(ccall((:rthx_result_create, LIB[]), Cint, (Ptr{Ptr{Cvoid}},), res))
