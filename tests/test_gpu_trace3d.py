@@ -186,3 +186,31 @@ def test_group_validation(hip):
     with pytest.raises(RthxError):
         Scene3D(xyz, nv, nrm, groups=neg)
 
+
+
+def test_config4_full_size_sampled_rows(hip):
+    """BASELINE config 4 at full size (cube 10x10 per face + icosphere L3,
+    1e8 rays, face groups): every ray is absorbed (closed enclosure), and
+    sampled rows equal the CPU restatement exactly at full R."""
+    from rthx.trace3d import Scene3D
+
+    xyz, nv, nrm, nc = H.cube_icosphere_scene(ndim=10, level=3)
+    g = H.cube_icosphere_groups(10, 3)
+    n = len(nv)
+    R = 100_000_000 // n
+    s = Scene3D(xyz, nv, nrm, groups=g)
+    try:
+        rp, cols, cnt, info = s.trace(R, seed=21)
+    finally:
+        s.close()
+    assert info["rays_traced"] == n * R and info["lost_total"] == 0
+    assert int(cnt.sum()) == n * R
+    stride = n // 4  # rows 0, 470 (cube faces), 940, 1410 (sphere triangles)
+    C, lost = oracle.trace_exchange_3d(xyz, nv, nrm, R, seed=21, begin=0, end=4 * stride, stride=stride,
+                                       nthreads=4, groups=g)
+    assert lost == 0
+    for k in range(4):
+        g0 = k * stride
+        row = np.zeros(n, dtype=np.uint32)
+        row[cols[rp[g0]:rp[g0 + 1]]] = cnt[rp[g0]:rp[g0 + 1]]
+        assert np.array_equal(row, C[k]), g0
