@@ -524,7 +524,24 @@ RTHX_EXPORT int rthx_trace_exchange(rthx_domain* dom, const rthx_trace_args* a, 
   T.row_tallied = res->row_tallied.as<uint32_t>();
   T.dense = split > 1 ? res->dense.as<uint32_t>() : nullptr;
 
+  // Unsplit launches write rows straight into the final CSR (decoupled
+  // look-back); RTHX_NO_LOOKBACK=1 keeps the staging + scan + pack sequence.
+  const char* nolb = getenv("RTHX_NO_LOOKBACK");
+  const bool lookback = split == 1 && n_rows > 0 && !(nolb && nolb[0] == '1');
+  if (lookback) {
+    HIP_TRY(res->lb_status.reserve((size_t)n_rows * 8), "hipMalloc look-back words");
+    T.lb_status = res->lb_status.as<unsigned long long>();
+    T.out_cols = res->cols.as<uint32_t>();
+    T.out_cnt = res->cnt.as<uint32_t>();
+    T.row_off = res->row_off.as<int64_t>();
+    T.totals = res->totals.as<unsigned long long>();
+    T.R = R;
+  }
   hipStream_t st = dom->stream;
+  if (lookback) {
+    HIP_TRY(hipMemsetAsync(T.lb_status, 0, (size_t)n_rows * 8, st), "hipMemset look-back words");
+    HIP_TRY(hipMemsetAsync(T.totals, 0, 32, st), "hipMemset totals");
+  }
   if (split > 1 && n_rows > 0) {
     HIP_TRY(hipMemsetAsync(T.dense, 0, (size_t)n_rows * N * 4, st), "hipMemset dense rows");
     HIP_TRY(hipMemsetAsync(T.row_tallied, 0, (size_t)n_rows * 4, st), "hipMemset row_tallied");
@@ -547,7 +564,7 @@ RTHX_EXPORT int rthx_trace_exchange(rthx_domain* dom, const rthx_trace_args* a, 
     HIP_TRY(rthx::launch_trace(L), "trace_exchange_kernel launch");
   }
   HIP_TRY(hipEventRecord(dom->ev[1], st), "hipEventRecord");
-  if (n_rows > 0) {
+  if (n_rows > 0 && !lookback) {
     if (split > 1) HIP_TRY(rthx::launch_compact(T, st), "row_compact_kernel launch");
     HIP_TRY(rthx::launch_scan(res->row_nnz.as<uint32_t>(), res->row_tallied.as<uint32_t>(), n_rows, R,
                               res->row_off.as<int64_t>(), res->totals.as<int64_t>(), st),
@@ -555,14 +572,14 @@ RTHX_EXPORT int rthx_trace_exchange(rthx_domain* dom, const rthx_trace_args* a, 
     HIP_TRY(rthx::launch_pack(res->stage_cols.as<uint32_t>(), res->stage_cnt.as<uint32_t>(), row_cap,
                               res->row_off.as<int64_t>(), n_rows, res->cols.as<uint32_t>(), res->cnt.as<uint32_t>(), st),
             "csr_pack_kernel launch");
-  } else {
+  } else if (n_rows == 0) {
     HIP_TRY(hipMemsetAsync(res->row_off.p, 0, 8, st), "hipMemset");
     HIP_TRY(hipMemsetAsync(res->totals.p, 0, 32, st), "hipMemset");
   }
   HIP_TRY(hipEventRecord(dom->ev[2], st), "hipEventRecord");
 
-  int64_t totals[3] = {0, 0, 0};
-  HIP_TRY(hipMemcpyAsync(totals, res->totals.p, 24, hipMemcpyDeviceToHost, st), "hipMemcpy totals");
+  int64_t totals[4] = {0, 0, 0, 0};
+  HIP_TRY(hipMemcpyAsync(totals, res->totals.p, 32, hipMemcpyDeviceToHost, st), "hipMemcpy totals");
   const bool device_only = (a->flags & RTHX_FLAG_DEVICE_ONLY) != 0;
   res->h_row_off.resize(n_rows + 1);
   res->host_row_off = !device_only;
@@ -574,6 +591,7 @@ RTHX_EXPORT int rthx_trace_exchange(rthx_domain* dom, const rthx_trace_args* a, 
   HIP_TRY(hipEventElapsedTime(&ms_trace, dom->ev[0], dom->ev[1]), "hipEventElapsedTime");
   HIP_TRY(hipEventElapsedTime(&ms_pack, dom->ev[1], dom->ev[2]), "hipEventElapsedTime");
 
+  if (lookback && totals[3] != 0) return fail(RTHX_EDEVICE, "direct-CSR look-back stalled (rows not dispatched in order)");
   res->info.nnz = totals[0];
   res->info.lost_total = totals[1];
   res->info.lost_max_row = totals[2];

@@ -48,6 +48,7 @@ struct rthx_result {
   int device = -1;
   rthx::DevBuf stage_cols, stage_cnt, row_nnz, row_tallied, row_off, totals, cols, cnt, dense;
   rthx::DevBuf rec_ids, rec_ok, rec_orig, rec_end;
+  rthx::DevBuf lb_status;  // direct-CSR look-back words (unsplit launches)
   bool valid = false;
   bool host_csr = false;
   bool host_row_off = false;
@@ -62,7 +63,7 @@ struct rthx_result {
   ~rthx_result() {
     if (device >= 0) (void)hipSetDevice(device);
     rthx::DevBuf* all[] = {&stage_cols, &stage_cnt, &row_nnz,  &row_tallied, &row_off,  &totals, &cols,
-                     &cnt,        &dense,     &rec_ids,  &rec_ok,      &rec_orig, &rec_end};
+                     &cnt,        &dense,     &rec_ids,  &rec_ok,      &rec_orig, &rec_end, &lb_status};
     for (rthx::DevBuf* b : all) b->release();
     h_cols.release();
     h_cnt.release();

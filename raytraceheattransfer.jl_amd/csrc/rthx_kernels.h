@@ -38,6 +38,15 @@ struct TallyParams {
   uint32_t* row_nnz;
   uint32_t* row_tallied;
   uint32_t* dense;      // split only: [n_rows][N]
+  // Unsplit 2D launches: rows go straight into the final CSR (cols / cnt at
+  // the row's offset, found by a decoupled look-back over lb_status, one
+  // zeroed u64 per row); nullptr = staging + row_scan_kernel + csr_pack_kernel.
+  unsigned long long* lb_status;
+  uint32_t* out_cols;
+  uint32_t* out_cnt;
+  int64_t* row_off;              // [n_rows + 1]
+  unsigned long long* totals;    // nnz, lost rays, max lost per row (zeroed; lost via atomics)
+  int64_t R;
 };
 
 struct LaunchCfg {

@@ -28,6 +28,43 @@ namespace rthx {
 #endif
 #define RTHX_TRACE_WAVES __attribute__((amdgpu_waves_per_eu(SINGLE ? RTHX_TRACE_WAVES_PER_EU : RTHX_TRACE_WAVES_PER_EU - 1)))
 
+// Decoupled look-back (Merrill & Garland 2016) over the rows of one launch:
+// row `slot` publishes its nnz as an aggregate (flag 1), walks back over its
+// predecessors' words adding aggregates until it meets an inclusive prefix
+// (flag 2), then publishes its own inclusive prefix.  Workgroups are
+// dispatched in row order, so every predecessor is resident or finished and
+// the walk ends.  One u64 per row: flag in bits 62-63, value below.
+// Agent-scope atomics (coherent across the XCDs' L2s).
+// Termination does not rest on the dispatch order alone: a wait longer than
+// ~2^20 polls (about a second; far beyond any row's trace) raises *stalled and gives up (the
+// host then fails the call loudly instead of returning a wrong CSR).
+__device__ __forceinline__ uint64_t lookback_offset(unsigned long long* status, int64_t slot, uint32_t nnz,
+                                                    unsigned long long* stalled) {
+  constexpr unsigned long long kAgg = 1ull << 62, kInc = 2ull << 62, kVal = (1ull << 62) - 1;
+  if (slot == 0) {
+    __hip_atomic_store(&status[0], kInc | nnz, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return 0;
+  }
+  __hip_atomic_store(&status[slot], kAgg | nnz, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  unsigned long long excl = 0;
+  uint32_t polls = 0;
+  for (int64_t j = slot - 1;; --j) {
+    unsigned long long v;
+    while (((v = __hip_atomic_load(&status[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 62) == 0) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++polls >= (1u << 20)) {
+        atomicAdd(stalled, 1ull);
+        v = kInc;  // give up: end the walk (the call fails on the host)
+        break;
+      }
+    }
+    excl += v & kVal;
+    if ((v >> 62) == 2) break;
+  }
+  __hip_atomic_store(&status[slot], kInc | (excl + nnz), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return excl;
+}
+
 // Workgroup-wide compaction of one row's counts, ascending absorber order
 // (the reference's sparse() sorts columns, parallelRayTracing.jl:154).
 // count2(w, lo, hi) gives the counts of absorbers 2w and 2w+1 (PAIRS) or of w
@@ -36,9 +73,11 @@ namespace rthx {
 // barrier to combine the four wave totals, then a writing pass whose lanes
 // store consecutive entries (coalesced).  Returns the row's nnz (valid in
 // every lane).
-template <bool PAIRS, class F>
-__device__ __forceinline__ uint32_t compact_row(int64_t n_words, F count2, uint32_t* __restrict__ out_c,
-                                                uint32_t* __restrict__ out_n, uint32_t* wave_sum) {
+// base_of(row nnz), called by every lane after the counting pass, gives the
+// row's output offset (0 for staging slots; the look-back for the direct CSR).
+template <bool PAIRS, class F, class B>
+__device__ __forceinline__ uint32_t compact_row(int64_t n_words, F count2, uint32_t* __restrict__ out_c_,
+                                                uint32_t* __restrict__ out_n_, uint32_t* wave_sum, B base_of) {
   const int kWaves = (int)(blockDim.x >> 6);
   const uint32_t lane = lane_id();
   const int wave = threadIdx.x >> 6;
@@ -61,6 +100,9 @@ __device__ __forceinline__ uint32_t compact_row(int64_t n_words, F count2, uint3
     base += i < wave ? ws : 0u;
     total += ws;
   }
+  const uint64_t gbase = base_of(total);
+  uint32_t* __restrict__ out_c = out_c_ + gbase;
+  uint32_t* __restrict__ out_n = out_n_ + gbase;
   for (int64_t w0 = wb; w0 < we; w0 += 64) {
     const int64_t w = w0 + lane;
     uint32_t lo = 0u, hi = 0u;
@@ -74,6 +116,12 @@ __device__ __forceinline__ uint32_t compact_row(int64_t n_words, F count2, uint3
   }
   __syncthreads();  // wave_sum may be reused by the caller
   return total;
+}
+
+template <bool PAIRS, class F>
+__device__ __forceinline__ uint32_t compact_row(int64_t n_words, F count2, uint32_t* __restrict__ out_c,
+                                                uint32_t* __restrict__ out_n, uint32_t* wave_sum) {
+  return compact_row<PAIRS>(n_words, count2, out_c, out_n, wave_sum, [](uint32_t) { return (uint64_t)0; });
 }
 
 template <bool UNIFORM, bool PACK16, bool FAITHFUL, bool SINGLE, bool REC, bool SPLIT, bool AXIS, bool CLDS>
@@ -243,14 +291,37 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
     if (tid == 0) atomicAdd(&T.row_tallied[slot], s_tallied);
     return;
   }
-  uint32_t nnz = compact_row<PACK16>(
-      n_words,
-      [&](int64_t w, uint32_t& lo, uint32_t& hi) {
-        uint32_t v = hist[w];
-        lo = PACK16 ? (v & 0xFFFFu) : v;
-        hi = PACK16 ? (v >> 16) : 0u;
-      },
-      T.stage_cols + slot * T.row_cap, T.stage_cnt + slot * T.row_cap, wave_sum);
+  auto count2 = [&](int64_t w, uint32_t& lo, uint32_t& hi) {
+    uint32_t v = hist[w];
+    lo = PACK16 ? (v & 0xFFFFu) : v;
+    hi = PACK16 ? (v >> 16) : 0u;
+  };
+  if (T.lb_status) {
+    // direct CSR: the row's offset is the sum of the earlier rows' nnz
+    __shared__ unsigned long long s_base;
+    auto base_of = [&](uint32_t nnz) -> uint64_t {
+      if (tid == 0) s_base = lookback_offset(T.lb_status, slot, nnz, &T.totals[3]);
+      __syncthreads();
+      return s_base;
+    };
+    const uint32_t nnz = compact_row<PACK16>(n_words, count2, T.out_cols, T.out_cnt, wave_sum, base_of);
+    if (tid == 0) {
+      const unsigned long long b = s_base;
+      T.row_off[slot] = (int64_t)b;
+      const unsigned long long lost = (unsigned long long)(T.R - (int64_t)s_tallied);
+      if (lost) {
+        atomicAdd(&T.totals[1], lost);
+        atomicMax(&T.totals[2], lost);
+      }
+      if (slot == T.n_rows - 1) {
+        T.row_off[T.n_rows] = (int64_t)(b + nnz);
+        T.totals[0] = b + nnz;
+      }
+    }
+    return;
+  }
+  uint32_t nnz = compact_row<PACK16>(n_words, count2, T.stage_cols + slot * T.row_cap, T.stage_cnt + slot * T.row_cap,
+                                     wave_sum);
   if (tid == 0) {
     T.row_nnz[slot] = nnz;
     T.row_tallied[slot] = s_tallied;
