@@ -524,10 +524,14 @@ RTHX_EXPORT int rthx_trace_exchange(rthx_domain* dom, const rthx_trace_args* a, 
   T.row_tallied = res->row_tallied.as<uint32_t>();
   T.dense = split > 1 ? res->dense.as<uint32_t>() : nullptr;
 
-  // Unsplit launches write rows straight into the final CSR (decoupled
-  // look-back); RTHX_NO_LOOKBACK=1 keeps the staging + scan + pack sequence.
+  // Unsplit launches on single-polygon domains write rows straight into the
+  // final CSR (decoupled look-back); RTHX_NO_LOOKBACK=1 keeps the staging +
+  // scan + pack sequence.  Multi-polygon domains keep it too: their rows
+  // finish at widely different times (rays cross different numbers of
+  // layers), and a row waiting on a slower predecessor idles its CU slot
+  // (C5 greenhouse: 15.2 -> 17.6 ms per band with the look-back).
   const char* nolb = getenv("RTHX_NO_LOOKBACK");
-  const bool lookback = split == 1 && n_rows > 0 && !(nolb && nolb[0] == '1');
+  const bool lookback = split == 1 && n_rows > 0 && dom->single_convex && !(nolb && nolb[0] == '1');
   if (lookback) {
     HIP_TRY(res->lb_status.reserve((size_t)n_rows * 8), "hipMalloc look-back words");
     T.lb_status = res->lb_status.as<unsigned long long>();

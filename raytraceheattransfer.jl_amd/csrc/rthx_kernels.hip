@@ -296,7 +296,7 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
     lo = PACK16 ? (v & 0xFFFFu) : v;
     hi = PACK16 ? (v >> 16) : 0u;
   };
-  if (T.lb_status) {
+  if (SINGLE && T.lb_status) {  // (host: single-polygon domains only; keeps the other kernels lean)
     // direct CSR: the row's offset is the sum of the earlier rows' nnz
     __shared__ unsigned long long s_base;
     auto base_of = [&](uint32_t nnz) -> uint64_t {
