@@ -140,8 +140,10 @@ typedef struct rthx_result_info {
   int64_t lost_total;      /* rays that were not tallied */
   int64_t lost_max_row;    /* max lost rays of one emitter (row_normalize! print) */
   int64_t n_recorded;      /* recorded (origin, endpoint) pairs */
-  double trace_ms;         /* device time of the trace kernel (hipEvents) */
-  double pack_ms;          /* device time of scan + CSR pack kernels */
+  double trace_ms;         /* device time of the trace kernel (hipEvents); on single-polygon
+                              domains it also writes the final CSR (direct look-back) */
+  double pack_ms;          /* device time of the merge / scan / CSR pack kernels that follow
+                              (about 0 when the trace kernel wrote the CSR itself) */
   double total_ms;         /* host wall time of the whole call */
 } rthx_result_info;
 
