@@ -82,6 +82,25 @@ def test_axis_rect_kernels_match_general_polygon_kernels(hip, ndim, monkeypatch)
     assert_same(a, oracle.trace_exchange(flat, args, 16))
 
 
+@pytest.mark.parametrize("ndim,rays", [(11, 600_000), (101, 20_000_000)])  # both unsplit (R < 4096 at C1)
+def test_direct_csr_lookback_matches_staging(hip, ndim, rays, monkeypatch):
+    """Unsplit single-polygon launches write the final CSR from the trace
+    kernel (decoupled look-back over the rows); RTHX_NO_LOOKBACK=1 keeps the
+    staging + row_scan + csr_pack sequence.  Row pointers, columns, counts and
+    lost-ray totals are identical, and equal the oracle on C1."""
+    dom = H.square_domain(ndim)
+    flat = dom.flat()
+    args, _k = _args(hip, flat, rays // flat.n_emitters)
+    a = gpu_trace(hip, flat, args)
+    assert a[3]["pack_ms"] < 0.05  # no pack kernels after the trace
+    monkeypatch.setenv("RTHX_NO_LOOKBACK", "1")
+    b = gpu_trace(hip, flat, args)
+    assert_same(a, b)
+    assert a[3]["lost_max_row"] == b[3]["lost_max_row"] and a[3]["nnz"] == b[3]["nnz"]
+    if ndim == 11:
+        assert_same(a, oracle.trace_exchange(flat, args, 16))
+
+
 def test_c1_matches_committed_golden(hip):
     g = np.load(H.os.path.join(H.GOLDEN, "oracle_c1_seed1.npz"))
     dom = H.square_domain(11)
