@@ -26,6 +26,9 @@ namespace rthx {
 #ifndef RTHX_TRACE_WAVES_PER_EU
 #define RTHX_TRACE_WAVES_PER_EU 5
 #endif
+#ifndef RTHX_REFILL
+#define RTHX_REFILL 16  // ray regeneration batch of the multi-polygon kernels (lanes)
+#endif
 #define RTHX_TRACE_WAVES __attribute__((amdgpu_waves_per_eu(SINGLE ? RTHX_TRACE_WAVES_PER_EU : RTHX_TRACE_WAVES_PER_EU - 1)))
 
 // Decoupled look-back (Merrill & Garland 2016) over the rows of one launch:
@@ -223,7 +226,7 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
     // counter, so waves do not idle until their longest ray ends.  Refills
     // are batched (a wave emits once at least kRefill of its lanes are idle)
     // so the emission code runs for many lanes at a time.
-    constexpr int kRefill = 16;
+    constexpr int kRefill = RTHX_REFILL;
     double px = 0.0, py = 0.0, dx = 0.0, dy = 0.0, S = 0.0, acc = 0.0, ox = 0.0, oy = 0.0;
     int c = 0, it = 0;
     uint32_t r = 0;
