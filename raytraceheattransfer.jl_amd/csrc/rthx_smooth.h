@@ -34,11 +34,8 @@ namespace sm {
 hipError_t rowsum(const double* A, int64_t n, double* out, hipStream_t s);
 hipError_t dual_setup(const double* w2, int64_t n, double* rowsum, double* dinv, hipStream_t s);
 hipError_t rmul(const double* w2, const double* rowsum, const double* p, int64_t n, double* out, hipStream_t s);
-hipError_t ap_step(double* X, const double* u, const double* w, int64_t n, double* r, double* u_next, hipStream_t s);
-hipError_t hunger(const double* X, const double* w, int64_t n, double* r, double* u, hipStream_t s);
 hipError_t delta_rows(const double* X, int64_t ld, const double* u, const double* w2, int64_t n, double* part,
                       hipStream_t s);
-hipError_t recover(double* X, const double* r, int64_t n, hipStream_t s);
 // Dense AP on the upper triangle of a symmetric X with an even leading
 // dimension ld >= n: one scale! + hunger! step (scale = false: hunger!
 // alone); partial buffers of ap_sym_col_tiles(n) * n (rowpart) and

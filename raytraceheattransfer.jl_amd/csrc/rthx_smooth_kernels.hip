@@ -7,7 +7,8 @@
 // fly instead of being stored (N^2 doubles saved, one division per entry).
 // Row kernels use one 256-lane workgroup per row and a fixed reduction order,
 // so every result is deterministic run to run.  Dense matrices are row-major
-// with leading dimension n.
+// with leading dimension n, except AP's symmetric X (even leading dimension,
+// upper triangle only: k_ap_sym).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -72,28 +73,6 @@ __global__ __launch_bounds__(kRow) void k_rmul(const double* __restrict__ w2, co
   for (int64_t j = threadIdx.x; j < n; j += kRow) s += Y(a2, w2[j]) * p[j];
   s = block_sum(s, sh);
   if (threadIdx.x == 0) out[i] = s + rowsum[i] * p[i];
-}
-
-// One AP step (:512-520 scale! then :492-496 hunger!): X_ij *= (u_i + u_j)/2
-// with the current u, then r_i = sum_j X_ij and u_next_i = w_i / r_i.
-__global__ __launch_bounds__(kRow) void k_ap_step(double* __restrict__ X, const double* __restrict__ u,
-                                                  const double* __restrict__ w, int64_t n, double* __restrict__ r,
-                                                  double* __restrict__ u_next) {
-  __shared__ double sh[kRow / 64];
-  const int64_t i = blockIdx.x;
-  double* x = X + i * n;
-  const double ui = u[i];
-  double s = 0.0;
-  for (int64_t j = threadIdx.x; j < n; j += kRow) {
-    const double v = x[j] * (0.5 * (ui + u[j]));
-    x[j] = v;
-    s += v;
-  }
-  s = block_sum(s, sh);
-  if (threadIdx.x == 0) {
-    r[i] = s;
-    u_next[i] = w[i] / s;
-  }
 }
 
 // ---------------------------------------------------------------------------
@@ -280,21 +259,6 @@ __global__ __launch_bounds__(kTile * 8) void k_recover_sym(const double* __restr
   }
 }
 
-// hunger! alone (the first (X_0, u_0)).
-__global__ __launch_bounds__(kRow) void k_hunger(const double* __restrict__ X, const double* __restrict__ w, int64_t n,
-                                                 double* __restrict__ r, double* __restrict__ u) {
-  __shared__ double sh[kRow / 64];
-  const int64_t i = blockIdx.x;
-  const double* x = X + i * n;
-  double s = 0.0;
-  for (int64_t j = threadIdx.x; j < n; j += kRow) s += x[j];
-  s = block_sum(s, sh);
-  if (threadIdx.x == 0) {
-    r[i] = s;
-    u[i] = w[i] / s;
-  }
-}
-
 // delta_R_X_dense (:98-115) per row: sum_{j>i} (X_ij (u_i - u_j))^2 / (w_i^2 + w_j^2).
 __global__ __launch_bounds__(kRow) void k_delta_rows(const double* __restrict__ X, int64_t ld,
                                                      const double* __restrict__ u, const double* __restrict__ w2,
@@ -310,14 +274,6 @@ __global__ __launch_bounds__(kRow) void k_delta_rows(const double* __restrict__ 
   }
   s = block_sum(s, sh);
   if (threadIdx.x == 0) part[i] = s;
-}
-
-// recover_F (:548): F_ij = X_ij / r_i, in place.
-__global__ __launch_bounds__(kRow) void k_recover(double* __restrict__ X, const double* __restrict__ r, int64_t n) {
-  const int64_t i = blockIdx.x;
-  double* x = X + i * n;
-  const double ri = r[i];
-  for (int64_t j = threadIdx.x; j < n; j += kRow) x[j] = x[j] / ri;
 }
 
 // F ./= sum(F, dims = 2) (:316), in place.
@@ -515,21 +471,9 @@ hipError_t rmul(const double* w2, const double* rowsum, const double* p, int64_t
   hipLaunchKernelGGL(k_rmul, dim3((unsigned)n), dim3(kRow), 0, s, w2, rowsum, p, n, out);
   return hipGetLastError();
 }
-hipError_t ap_step(double* X, const double* u, const double* w, int64_t n, double* r, double* u_next, hipStream_t s) {
-  hipLaunchKernelGGL(k_ap_step, dim3((unsigned)n), dim3(kRow), 0, s, X, u, w, n, r, u_next);
-  return hipGetLastError();
-}
-hipError_t hunger(const double* X, const double* w, int64_t n, double* r, double* u, hipStream_t s) {
-  hipLaunchKernelGGL(k_hunger, dim3((unsigned)n), dim3(kRow), 0, s, X, w, n, r, u);
-  return hipGetLastError();
-}
 hipError_t delta_rows(const double* X, int64_t ld, const double* u, const double* w2, int64_t n, double* part,
                       hipStream_t s) {
   hipLaunchKernelGGL(k_delta_rows, dim3((unsigned)n), dim3(kRow), 0, s, X, ld, u, w2, n, part);
-  return hipGetLastError();
-}
-hipError_t recover(double* X, const double* r, int64_t n, hipStream_t s) {
-  hipLaunchKernelGGL(k_recover, dim3((unsigned)n), dim3(kRow), 0, s, X, r, n);
   return hipGetLastError();
 }
 int64_t ap_sym_row_tiles(int64_t n) { return (n + kSymRows - 1) / kSymRows; }
