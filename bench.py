@@ -38,6 +38,18 @@ FP64_VECTOR_PEAK_TFLOPS = 78.6  # MI355X fp64 vector (AMD spec, SURVEY.md §8(d)
 TRACE_KERNEL = "trace_exchange_kernel"
 
 
+def profile_file(name):
+    """The newest committed copy of a profile summary (profiles/roundN/name)."""
+    base = os.path.join(ROOT, "profiles")
+    rounds = sorted((d for d in os.listdir(base) if d.startswith("round")), key=lambda d: int(d[5:] or 0),
+                    reverse=True) if os.path.isdir(base) else []
+    for d in rounds:
+        p = os.path.join(base, d, name)
+        if os.path.exists(p):
+            return p
+    return None
+
+
 def build_domain(ndim=NDIM):
     from rthx import PolyVolume2D, RayTracingDomain2D
 
@@ -48,63 +60,108 @@ def build_domain(ndim=NDIM):
     return RayTracingDomain2D([face], [(ndim, ndim)])
 
 
-def cpu_baseline(dom, R, nudge, seed, budget_s=12.0, threads=16):
+def host_cpu_share():
+    """(threads to use, description): the CPUs this process may run on
+    (sched_getaffinity), capped by a cgroup CPU quota when there is one (a GPU
+    box's share of a larger host), with the physical cores behind them."""
+    aff = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else list(range(os.cpu_count() or 1))
+    quota = None
+    for path in ("/sys/fs/cgroup/cpu.max", "/sys/fs/cgroup/cpu/cpu.cfs_quota_us"):
+        try:
+            with open(path) as fh:
+                parts = fh.read().split()
+            if path.endswith("cpu.max"):
+                if parts[0] != "max":
+                    quota = float(parts[0]) / float(parts[1])
+            else:
+                q = float(parts[0])
+                if q > 0:
+                    with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as fh:
+                        quota = q / float(fh.read().split()[0])
+            break
+        except (OSError, ValueError, IndexError):
+            continue
+    cores = set()
+    try:
+        cur = {}
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if not line.strip():
+                    if cur.get("processor") in aff:
+                        cores.add((cur.get("physical id"), cur.get("core id")))
+                    cur = {}
+                    continue
+                k, _, v = line.partition(":")
+                k, v = k.strip(), v.strip()
+                cur[k] = int(v) if k == "processor" else v
+    except OSError:
+        pass
+    env_cap = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    t = len(aff)
+    if quota is not None:
+        t = min(t, max(1, int(quota)))
+    if env_cap > 0:
+        t = min(t, env_cap)
+    desc = {"affinity_logical_cpus": len(aff), "physical_cores_in_affinity": len(cores) or None,
+            "cgroup_cpu_quota": round(quota, 2) if quota is not None else None,
+            "omp_num_threads": env_cap or None, "host_logical_cpus": os.cpu_count()}
+    return max(1, t), desc
+
+
+def cpu_baseline(dom, R, nudge, seed, budget_s=12.0):
     """Time the CPU restatement (oracle, test infrastructure) on a bounded
-    strided sample of the same emitters with the same R."""
+    strided sample of the same emitters with the same R, in the reference's
+    faithful sampling mode (acos/sin/cos emission), at
+    T = the CPUs this process may use (affinity, capped by the cgroup quota
+    and OMP_NUM_THREADS) and at T = 1."""
     from oracle import oracle
     from rthx import _lib
+    from rthx import abi
 
     flat = dom.flat()
     N = flat.n_emitters
-    threads = max(1, min(threads, os.cpu_count() or 1))
+    threads, share = host_cpu_share()
+    flags = abi.RTHX_FLAG_FAITHFUL_SAMPLING
+
+    def timed(stride, nthr):
+        args, _k = _lib.make_args(0, R, nudge, seed, 0, N, stride, flags=flags)
+        t = time.perf_counter()
+        _rp, _c, _n, info, _ = oracle.trace_exchange(flat, args, nthr)
+        return info, time.perf_counter() - t
+
     # probe on 1/256 of the rows, then size the sample to the budget
-    stride = 256
-    args, _k = _lib.make_args(0, R, nudge, seed, 0, N, stride)
-    t = time.perf_counter()
-    oracle.trace_exchange(flat, args, threads)
-    dt = time.perf_counter() - t
-    rows_probe = len(range(0, N, stride))
-    rate_rows = rows_probe / max(dt, 1e-6)
-    want_rows = max(rows_probe, int(rate_rows * budget_s))
+    info, dt = timed(256, threads)
+    want_rows = max(info["rows_traced"], int(info["rows_traced"] / max(dt, 1e-6) * budget_s))
     stride = max(1, N // want_rows)
-    args, _k = _lib.make_args(0, R, nudge, seed, 0, N, stride)
-    t = time.perf_counter()
-    _rp, _c, _n, info, _ = oracle.trace_exchange(flat, args, threads)
-    dt = time.perf_counter() - t
-    rays = info["rays_traced"]
-    # single thread (SURVEY.md §8(d): T = nproc and T = 1), ~budget/3 s
-    stride1 = 256
-    args1, _k1 = _lib.make_args(0, R, nudge, seed, 0, N, stride1)
-    t = time.perf_counter()
-    oracle.trace_exchange(flat, args1, 1)
-    dt1 = time.perf_counter() - t
-    rows1 = len(range(0, N, stride1))
+    info, dt = timed(stride, threads)
+    info1, dt1 = timed(256, 1)
+    rows1 = info1["rows_traced"]
     stride1 = max(1, N // max(rows1, int(rows1 / max(dt1, 1e-6) * budget_s / 3)))
-    args1, _k1 = _lib.make_args(0, R, nudge, seed, 0, N, stride1)
-    t = time.perf_counter()
-    _rp, _c, _n, info1, _ = oracle.trace_exchange(flat, args1, 1)
-    dt1 = time.perf_counter() - t
+    info1, dt1 = timed(stride1, 1)
     return {
-        "value": rays / dt / 1e6,
+        "value": info["rays_traced"] / dt / 1e6,
         "unit": "Mrays/s",
         "cores": threads,
         "kind": "port",
         "value_1_thread": info1["rays_traced"] / dt1 / 1e6,
-        "host_logical_cpus": os.cpu_count(),
+        "sampling": "faithful (acos/sin/cos emission as emitVolumeRay2D.jl:26-31)",
+        **share,
         "sample": (f"CPU restatement of the reference algorithm (oracle/rthx_oracle.c: pthreads, static emitter "
-                   f"partition, per-thread hash tallies, COO->CSR) on every {stride}-th emitter row of the same "
-                   f"101x101 workload: {info['rows_traced']} rows x R={R} = {rays} rays in {dt:.2f} s, "
-                   f"{threads} threads (the GPU box's CPU share; os.cpu_count() reports the whole host's logical "
-                   f"CPUs); single thread: every {stride1}-th row, {info1['rays_traced']} rays in {dt1:.2f} s"),
+                   f"partition as parallelRayTracing.jl:81-91, per-thread hash tallies, COO->CSR), faithful "
+                   f"sampling, on every {stride}-th emitter row of the same 101x101 workload: "
+                   f"{info['rows_traced']} rows x R={R} = {info['rays_traced']} rays in {dt:.2f} s on {threads} "
+                   f"threads (= the CPUs this process may use: affinity {share['affinity_logical_cpus']}, cgroup "
+                   f"quota {share['cgroup_cpu_quota']}, OMP_NUM_THREADS {share['omp_num_threads']}); single "
+                   f"thread: every {stride1}-th row, {info1['rays_traced']} rays in {dt1:.2f} s"),
     }
 
 
 def read_pmc_traffic():
     """HBM bytes per trace launch from the committed rocprofv3 --pmc summary
-    (profiles/round1/pmc_traffic.json, written by tools/pmc_summary.py from
+    (profiles/roundN/pmc_traffic.json, newest round, written by tools/pmc_summary.py from
     separate FETCH_SIZE / WRITE_SIZE passes of this bench), or None."""
-    p = os.path.join(ROOT, "profiles", "round1", "pmc_traffic.json")
-    if not os.path.exists(p):
+    p = profile_file("pmc_traffic.json")
+    if p is None:
         return None
     try:
         with open(p) as fh:
@@ -115,11 +172,11 @@ def read_pmc_traffic():
 
 def read_fp64_flops_per_ray():
     """fp64 FLOP per traced ray of the trace kernel from the committed SQ
-    counter summary (profiles/round1/pmc_sq.json, tools/gpu_sq.sh):
+    counter summary (profiles/roundN/pmc_sq.json, tools/gpu_sq.sh):
     (ADD + MUL + 2 FMA + TRANS) fp64 instructions per wave-ray -- one
     instruction per wave covers the 64 rays of its lanes."""
-    p = os.path.join(ROOT, "profiles", "round1", "pmc_sq.json")
-    if not os.path.exists(p):
+    p = profile_file("pmc_sq.json")
+    if p is None:
         return None
     try:
         with open(p) as fh:
@@ -137,17 +194,17 @@ def read_fp64_flops_per_ray():
 
 def read_valu_issue_per_ray():
     """VALU issue time floor per traced ray of the trace kernel (seconds of
-    whole-chip issue): the committed SQ counters (profiles/round1/pmc_sq.json)
+    whole-chip issue): the committed SQ counters (profiles/roundN/pmc_sq.json)
     split into full-rate fp64 (ADD/MUL/FMA), fp64 transcendentals and every
     other VALU instruction, each priced at the chip-wide issue rate that
     tools/probe/valu_probe.hip measured for v_fma_f64, v_rcp_f64 and
-    v_fma_f32 (profiles/round1/valu_probe.json).  Instructions are per wave,
+    v_fma_f32 (profiles/roundN/valu_probe.json).  Instructions are per wave,
     so one covers the 64 rays of its lanes.  Returns (seconds per ray,
     fp64-FMA-equivalent wave-instructions per ray, peak fp64-FMA wave-instr/s)
     or None."""
-    pq = os.path.join(ROOT, "profiles", "round1", "pmc_sq.json")
-    pp = os.path.join(ROOT, "profiles", "round1", "valu_probe.json")
-    if not (os.path.exists(pq) and os.path.exists(pp)):
+    pq = profile_file("pmc_sq.json")
+    pp = profile_file("valu_probe.json")
+    if pq is None or pp is None:
         return None
     try:
         with open(pq) as fh:
@@ -167,6 +224,23 @@ def read_valu_issue_per_ray():
         return None
 
 
+def _spawn_ranks(n):
+    """`python bench.py --gpus N` started as a plain process: launch the N
+    ranks with torch.distributed.run as a child (before this process touches
+    any GPU) and exit with its status."""
+    import socket
+    import subprocess
+
+    sock = socket.socket()
+    sock.bind(("127.0.0.1", 0))
+    port = sock.getsockname()[1]
+    sock.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -179,22 +253,33 @@ def main():
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--mode", choices=("ranks", "threads"), default="ranks",
+                    help="ranks: one process per GPU (torch.distributed.run; a plain `--gpus N` start spawns them); "
+                         "threads: this one process drives N devices through rthx_multi_trace_exchange")
     ap.add_argument("--emulate-world", type=int, default=0,
                     help="diagnostic: run rank 0's shard of a W-GPU job on this one GPU (no value claim)")
     args = ap.parse_args()
 
+    if args.mode == "ranks" and args.gpus > 1 and "WORLD_SIZE" not in os.environ and args.emulate_world <= 1:
+        sys.exit(_spawn_ranks(args.gpus))
+
     rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", str(args.gpus)))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.mode == "threads":
+        world = 1
     if args.emulate_world > 1:
         world = args.emulate_world
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and "WORLD_SIZE" in os.environ:
+    if args.mode == "ranks" and world != args.gpus and "WORLD_SIZE" in os.environ:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
     dist = None
     if world > 1 and args.emulate_world <= 1:
         import torch.distributed as dist  # noqa: F811
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        # The trace has no data-path exchange (disjoint emitter rows): the
+        # group only brackets the timed region (barrier) and max-reduces
+        # the elapsed time, so it stays on the host (gloo).
         dist.init_process_group("gloo", rank=rank, world_size=world)
 
     from rthx import _lib
@@ -204,20 +289,33 @@ def main():
     dom = build_domain()
     flat = dom.flat()
     N = flat.n_emitters
-    total_rays = args.rays_per_gpu * world
-    R = total_rays // N
-    # one process per GPU: rank r drives device LOCAL_RANK (more ranks than
-    # devices, e.g. a 2-rank rehearsal on a 1-GPU box, share devices round robin)
     ndev = _lib.device_count()
-    device = local_rank % max(ndev, 1)
-    dd = _lib.DeviceDomain(flat, device)
-    targs, _keep = _lib.make_args(0, R, nudge, args.seed, rank, N, world, device=device,
-                                  flags=abi.RTHX_FLAG_DEVICE_ONLY)
+    n_units = args.gpus if args.mode == "threads" else world  # GPUs doing the work
+    total_rays = args.rays_per_gpu * n_units
+    R = total_rays // N
+    if args.mode == "threads":
+        devices = [d % max(ndev, 1) for d in range(args.gpus)]
+        device = devices[0]
+        dd = _lib.MultiDeviceDomain(flat, devices) if args.gpus > 1 else _lib.DeviceDomain(flat, device)
+        targs, _keep = _lib.make_args(0, R, nudge, args.seed, 0, N, 1, device=device,
+                                      flags=abi.RTHX_FLAG_DEVICE_ONLY)
+    else:
+        # one process per GPU: rank r drives device LOCAL_RANK (more ranks than
+        # devices, e.g. a 2-rank rehearsal on a 1-GPU box, share devices round robin)
+        devices = None
+        device = local_rank % max(ndev, 1)
+        dd = _lib.DeviceDomain(flat, device)
+        targs, _keep = _lib.make_args(0, R, nudge, args.seed, rank, N, world, device=device,
+                                      flags=abi.RTHX_FLAG_DEVICE_ONLY)
     res = _lib.DeviceResult()
 
     def barrier():
         if dist is not None:
             dist.barrier()
+
+    def sync_all():
+        for d in (sorted(set(devices)) if devices else [device]):
+            _lib.synchronize(d)
 
     t_pre = time.perf_counter()
     prewarm_steps = 0
@@ -226,9 +324,9 @@ def main():
         prewarm_steps += 1
     for _ in range(args.warmup):
         res.trace(dd, targs)
-    _lib.synchronize(device)
+    sync_all()
     barrier()
-    _lib.synchronize(device)
+    sync_all()
     t0 = time.perf_counter()
     trace_ms = []
     pack_ms = []
@@ -238,7 +336,7 @@ def main():
         info = res.info()
         trace_ms.append(info["trace_ms"])
         pack_ms.append(info["pack_ms"])
-    _lib.synchronize(device)
+    sync_all()
     elapsed = time.perf_counter() - t0
     barrier()
 
@@ -256,27 +354,45 @@ def main():
     else:
         rays_all, nnz_all = rays_rank, nnz_rank
 
-    # PCIe-inclusive end-to-end pass (CSR copied to the host), reported aside
-    e2e = None
+    # PCIe-inclusive end-to-end passes, reported aside (never `value`): the
+    # trace plus the CSR of counts DMA'd into page-locked caller arrays that a
+    # caller reuses across traces (rthx_host_register), and the same with F_raw
+    # (counts normalised on the device, rthx_result_copy_F) instead of counts.
+    e2e = e2e_F = None
     if rank == 0:
-        args_h, _kh = _lib.make_args(0, R, nudge, args.seed, rank, N, world, device=device)
-        t = time.perf_counter()
+        pin = _lib.PinnedArrays()
+        args_h, _kh = _lib.make_args(0, R, nudge, args.seed, targs.emitter_begin, N, targs.emitter_stride,
+                                     device=device)
         res.trace(dd, args_h)
-        res.csr()
-        e2e_s = time.perf_counter() - t
-        e2e = rays_rank / e2e_s / 1e6
+        res.csr(pin)
+        res.F(pin)  # page-lock the destination arrays once
+        reps = 3
+        t = time.perf_counter()
+        for _ in range(reps):
+            res.trace(dd, args_h)
+            res.csr(pin)
+        e2e = reps * info["rays_traced"] / (time.perf_counter() - t) / 1e6
+        t = time.perf_counter()
+        for _ in range(reps):
+            res.trace(dd, args_h)
+            res.F(pin)
+        e2e_F = reps * info["rays_traced"] / (time.perf_counter() - t) / 1e6
+        pin.close()
 
     out = None
     if rank == 0:
         ms_per_step = elapsed / args.steps * 1e3
         value = rays_all * args.steps / elapsed / 1e6
         avg_trace_ms = float(np.mean(trace_ms))
-        # B_alg = 8 B/ray + 12 B x nnz/(N R)
+        # B_alg = 8 B/ray + 12 B x nnz/(N R), per GPU (in
+        # threads mode one result covers every device: per-device share)
+        per = n_units if args.mode == "threads" else 1
+        rays_rank, nnz_rank = rays_rank / per, nnz_rank / per
         b_alg = 8.0 * rays_rank + 12.0 * nnz_rank
         achieved = b_alg / (avg_trace_ms * 1e-3) / 1e9
         # the committed PMC traffic was measured on the 1-GPU launch; other
         # shard shapes (row-split launches) are not covered by it
-        traffic = read_pmc_traffic() if world == 1 else None
+        traffic = read_pmc_traffic() if n_units == 1 else None
         fpr = read_fp64_flops_per_ray()
         fp64_roof = None
         if fpr is not None:
@@ -284,7 +400,7 @@ def main():
             fp64_roof = {"bound": "fp64-valu", "achieved": round(tf, 3), "peak": FP64_VECTOR_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(tf / FP64_VECTOR_PEAK_TFLOPS, 4),
                          "flop_per_ray": round(fpr, 1),
-                         "note": "fp64 VALU instructions per ray from profiles/round1/pmc_sq.json (SQ counters)"}
+                         "note": f"fp64 VALU instructions per ray from {os.path.relpath(profile_file('pmc_sq.json'), ROOT)} (SQ counters)"}
         vi = read_valu_issue_per_ray()
         valu_roof = None
         if vi is not None:
@@ -294,14 +410,15 @@ def main():
             valu_roof = {"bound": "valu-issue", "achieved": round(ach / 1e9, 2), "peak": round(peak_rate / 1e9, 2),
                          "unit": "G wave-instr/s (v_fma_f64-equivalent)", "frac": round(floor_ms / avg_trace_ms, 4),
                          "issue_floor_ms": round(floor_ms, 4),
-                         "note": ("SQ instruction counts (profiles/round1/pmc_sq.json) priced at the issue rates "
-                                  "tools/probe/valu_probe.hip measured (profiles/round1/valu_probe.json): the "
-                                  "binding roofline of this kernel")}
+                         "note": (f"SQ instruction counts ({os.path.relpath(profile_file('pmc_sq.json'), ROOT)}) "
+                                  "priced at the issue rates tools/probe/valu_probe.hip measured "
+                                  f"({os.path.relpath(profile_file('valu_probe.json'), ROOT)}): the binding "
+                                  "roofline of this kernel")}
         out = {
             "metric": METRIC,
             "value": round(value, 3),
             "unit": "Mrays/s",
-            "n_gpus": world,
+            "n_gpus": n_units,
             "steps": args.steps,
             "warmup": args.warmup,
             "prewarm_steps": prewarm_steps,
@@ -313,12 +430,14 @@ def main():
             "data": "synthetic",
             "config": {
                 "workload": (f"101x101 grey kappa=1 sigma_s=0 unit-square enclosure (BASELINE configs[1]); "
-                             f"{args.rays_per_gpu:.0e} rays per GPU, emitter rows sharded over {world} rank(s)"),
+                             f"{args.rays_per_gpu:.0e} rays per GPU, emitter rows sharded over {n_units} GPU(s)"),
                 "n_emitters": N,
                 "rays_per_emitter": R,
                 "rays_per_step": rays_all,
                 "nnz_per_step": nnz_all,
-                "parallelism": f"emitter-rows x{world}",
+                "parallelism": (f"emitter-rows x{n_units} (" + ("one process, rthx_multi_trace_exchange)"
+                                if args.mode == "threads" else "one process per GPU)")),
+                "devices_visible": ndev,
                 "seed": args.seed,
             },
             "roofline": {
@@ -337,12 +456,13 @@ def main():
             "roofline_fp64": fp64_roof,
             "roofline_valu": valu_roof,
             "e2e_with_d2h_mrays_s": round(e2e, 3) if e2e else None,
+            "e2e_F_with_d2h_mrays_s": round(e2e_F, 3) if e2e_F else None,
         }
         if args.emulate_world > 1:
             out["emulated_rank0_of"] = world
             out["value"] = None  # one rank's shard only: not a whole-job measurement
             out["rank0_mrays_s"] = round(rays_rank * args.steps / elapsed / 1e6, 3)
-        if world == 1 and not args.no_cpu:
+        if n_units == 1 and not args.no_cpu:
             out["cpu_baseline"] = cpu_baseline(dom, R, nudge, args.seed, args.cpu_budget)
         else:
             out["cpu_baseline"] = None

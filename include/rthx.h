@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define RTHX_ABI_VERSION 1
+#define RTHX_ABI_VERSION 2
 
 /* status codes */
 #define RTHX_OK 0
@@ -145,6 +145,9 @@ typedef struct rthx_result_info {
   double pack_ms;          /* device time of the merge / scan / CSR pack kernels that follow
                               (about 0 when the trace kernel wrote the CSR itself) */
   double total_ms;         /* host wall time of the whole call */
+  int32_t n_devices;       /* devices that traced rows (rthx_multi_trace_exchange: > 1) */
+  int32_t lookback_fallbacks; /* launches whose direct-CSR look-back gave up waiting on a
+                              predecessor row and were re-traced on the staging path */
 } rthx_result_info;
 
 typedef struct rthx_domain rthx_domain;
@@ -177,9 +180,25 @@ int rthx_result_get_info(const rthx_result* res, rthx_result_info* info);
 
 /* Copy the count matrix as CSR over all N rows (rows that were not traced are
  * empty): row_ptr[N+1], cols[nnz], counts[nnz].  F_raw(i,j) of the reference
- * is counts / R followed by row normalisation. */
+ * is counts / R followed by row normalisation.  Any pointer may be NULL.
+ * cols and counts are DMA'd from the device straight into the caller's
+ * arrays; pinning them once with rthx_host_register makes that a single
+ * host-link transfer per call (otherwise the HIP runtime stages pageable
+ * memory through its own pinned buffers). */
 int rthx_result_copy_csr(const rthx_result* res, int64_t* row_ptr,
                          int32_t* cols, uint32_t* counts);
+
+/* F_raw of the reference (parallelRayTracing.jl:145, :154-158): counts / R
+ * with every row divided by its sum (row_normalize!, :161-169), computed on
+ * the device as count / (rays the row tallied) -- the exact quotient -- and
+ * copied as CSR over all N rows: row_ptr[N+1], cols[nnz], vals[nnz] (rows
+ * with no tallied ray are empty).  Any pointer may be NULL. */
+int rthx_result_copy_F(const rthx_result* res, int64_t* row_ptr, int32_t* cols, double* vals);
+
+/* Pin (page-lock) caller memory for direct device DMA, e.g. the cols/counts
+ * arrays a caller reuses across traces; unregister before freeing it. */
+int rthx_host_register(void* ptr, size_t bytes);
+int rthx_host_unregister(void* ptr);
 
 /* Copy the recorded rays (RayRecorder origins / endpoints,
  * parallelRayTracing.jl:120-123,135-138): xy pairs, plus the emitter of each
@@ -187,6 +206,28 @@ int rthx_result_copy_csr(const rthx_result* res, int64_t* row_ptr,
 int rthx_result_copy_rays(const rthx_result* res, double* origins_xy,
                           double* endpoints_xy, int64_t* emitter, int64_t cap,
                           int64_t* n_out);
+
+/* ------------------------------------------------------------------------
+ * Several devices: the GPU counterpart of the reference's
+ * static emitter partition over threads (parallelRayTracing.jl:81-102).  The
+ * domain is uploaded to every listed device; rthx_multi_trace_exchange splits
+ * the selected rows into one block per device, traces the blocks
+ * concurrently (one host thread and HIP stream per device) and fills one
+ * rthx_result whose info / copy calls cover all rows, exactly as a
+ * one-device trace of the same arguments would (every row is a pure
+ * function of (seed, bin, emitter, ray), so the counts are bit-identical for
+ * any device count).  Single-polygon domains get contiguous row blocks, which
+ * rthx_result_copy_csr DMAs from each device straight into the caller's
+ * arrays; multi-polygon domains (uneven row costs) get interleaved rows
+ * g = d, d + n, ... per device, reassembled on the host.  args.device is
+ * ignored.
+ * ------------------------------------------------------------------------ */
+typedef struct rthx_multi rthx_multi;
+
+int rthx_multi_create(const rthx_domain_desc* desc, const int32_t* devices, int32_t n_devices,
+                      rthx_multi** out);
+void rthx_multi_destroy(rthx_multi* m);
+int rthx_multi_trace_exchange(rthx_multi* m, const rthx_trace_args* args, rthx_result* res);
 
 /* ------------------------------------------------------------------------
  * Exchange-factor smoothing: smooth_F of
@@ -234,6 +275,13 @@ typedef struct rthx_smooth_result rthx_smooth_result;
 int rthx_smooth_F(const int64_t* row_ptr, const int32_t* cols, const double* vals, int64_t n,
                   const double* w, int64_t n_w, int32_t num_surfaces,
                   const rthx_smooth_args* args, rthx_smooth_result** out);
+/* The same smoothing of a trace result that is still on its device: F_raw is
+ * counts / R, row-normalised (parallelRayTracing.jl:145, :161-169), restricted
+ * to its leading n x n block (n = N, or Ns for surfaces_only,
+ * exchangeRayTracing.jl:9-11); the counts never cross the host link.
+ * args->device must be the result's device (a single-device result). */
+int rthx_smooth_F_result(const rthx_result* counts, int64_t n, const double* w, int64_t n_w,
+                         int32_t num_surfaces, const rthx_smooth_args* args, rthx_smooth_result** out);
 int rthx_smooth_get_info(const rthx_smooth_result* res, rthx_smooth_info* info);
 /* Dense result: out[n*n], row-major. */
 int rthx_smooth_copy_dense(const rthx_smooth_result* res, double* out);

@@ -17,6 +17,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/rthx.h"
@@ -405,86 +406,243 @@ RTHX_EXPORT int rthx_result_create(rthx_result** out) {
 
 RTHX_EXPORT void rthx_result_destroy(rthx_result* res) { delete res; }
 
-RTHX_EXPORT int rthx_trace_exchange(rthx_domain* dom, const rthx_trace_args* a, rthx_result* res) {
-  const double t0 = now_ms();
-  if (!dom || !a || !res) return fail(RTHX_EINVAL, "null argument");
+namespace rthx {
+
+// Staged rows -> final CSR, after the trace launch on `st`: merge split rows
+// into the staging slots, scan the per-row nnz (row_off, totals), read the
+// totals back, size cols / counts to nnz and pack the slots.  totals[0..3] =
+// nnz, lost rays, max lost per row, look-back stalls (0 here).
+int finish_staged(rthx_result* res, const TallyParams& T, bool split, hipStream_t st, hipEvent_t ev_end,
+                  int64_t totals[4]) {
+  if (T.n_rows > 0) {
+    if (split) HIP_TRY(launch_compact(T, st), "row_compact_kernel launch");
+    HIP_TRY(launch_scan(T.row_nnz, T.row_tallied, T.n_rows, T.R, res->row_off.as<int64_t>(),
+                        res->totals.as<int64_t>(), st),
+            "row_scan_kernel launch");
+  } else {
+    HIP_TRY(hipMemsetAsync(res->row_off.p, 0, 8, st), "hipMemset");
+  }
+  HIP_TRY(hipMemcpyAsync(totals, res->totals.p, 32, hipMemcpyDeviceToHost, st), "hipMemcpy totals");
+  HIP_TRY(hipStreamSynchronize(st), "row scan");
+  const size_t nnz = (size_t)std::max<int64_t>(totals[0], 1);
+  HIP_TRY(res->cols.reserve(nnz * 4), "hipMalloc cols");
+  HIP_TRY(res->cnt.reserve(nnz * 4), "hipMalloc cnt");
+  if (T.n_rows > 0)
+    HIP_TRY(launch_pack(T.stage_cols, T.stage_cnt, T.row_cap, res->row_off.as<int64_t>(), T.n_rows,
+                        res->cols.as<uint32_t>(), res->cnt.as<uint32_t>(), st),
+            "csr_pack_kernel launch");
+  HIP_TRY(hipEventRecord(ev_end, st), "hipEventRecord");
+  HIP_TRY(hipStreamSynchronize(st), "CSR pack");
+  return RTHX_OK;
+}
+
+}  // namespace rthx
+
+namespace {
+
+// Default bound on one look-back wait (100 MHz s_memrealtime ticks): a row
+// waits for its predecessors' nnz, which are published within about one row
+// time (~0.1-1 ms); a quarter second means the wait has gone wrong.
+// RTHX_LB_WAIT_US overrides it (tests force the fallback with 0).
+constexpr uint64_t kLookbackWaitTicks = 25'000'000;
+
+uint64_t lookback_wait_ticks() {
+  const char* e = getenv("RTHX_LB_WAIT_US");
+  if (e && *e) return (uint64_t)std::strtoull(e, nullptr, 10) * 100;  // 100 ticks per microsecond
+  return kLookbackWaitTicks;
+}
+
+bool env_flag(const char* name) {
+  const char* e = getenv(name);
+  return e && e[0] == '1';
+}
+
+// Launch geometry of one trace call (rows, split, LDS histogram layout).
+struct TracePlan {
+  int64_t N = 0, R = 0, end = 0, n_rows = 0, split = 1, row_cap = 1;
+  bool pack16 = true, clds = false, recording = false, uniform = true;
+  size_t lds_bytes = 0, cl_offset = 0;
+};
+
+int plan_trace(const rthx_domain* dom, const rthx_trace_args* a, TracePlan& p) {
   if (a->bin < 0 || a->bin >= dom->n_bins) return fail(RTHX_EINVAL, "bin out of range");
   if (a->rays_per_emitter < 0 || a->rays_per_emitter > 0xFFFFFFFFll)
     return fail(RTHX_ERANGE, "rays_per_emitter must be in [0, 2^32)");
   if (a->emitter_stride < 1 || a->emitter_begin < 0) return fail(RTHX_EINVAL, "bad emitter range");
   if (!std::isfinite(a->nudge)) return fail(RTHX_EINVAL, "non-finite nudge");
-  if (a->device != dom->device) return fail(RTHX_EINVAL, "args.device differs from the domain's device");
   if (a->n_record < 0 || (a->n_record > 0 && !a->record_ids)) return fail(RTHX_EINVAL, "bad record ids");
-  HIP_TRY(hipSetDevice(dom->device), "hipSetDevice");
-  if (res->device >= 0 && res->device != dom->device) return fail(RTHX_EINVAL, "result bound to another device");
-  res->device = dom->device;
-
-  const int64_t N = dom->n_emitters;
-  const int64_t R = a->rays_per_emitter;
-  const int64_t end = std::min<int64_t>(a->emitter_end, N);
-  const int64_t n_rows = end > a->emitter_begin ? (end - a->emitter_begin + a->emitter_stride - 1) / a->emitter_stride : 0;
-  if (n_rows >= (1ll << 31)) return fail(RTHX_ERANGE, "too many rows in one call");
+  p.N = dom->n_emitters;
+  p.R = a->rays_per_emitter;
+  p.end = std::min<int64_t>(a->emitter_end, p.N);
+  p.n_rows = p.end > a->emitter_begin ? (p.end - a->emitter_begin + a->emitter_stride - 1) / a->emitter_stride : 0;
+  if (p.n_rows >= (1ll << 31)) return fail(RTHX_ERANGE, "too many rows in one call");
+  const int64_t N = p.N, R = p.R;
   // Rows are split over several workgroups when there are too few rows to
   // fill the chip (or a row's rays would overflow the packed 16-bit LDS
   // counters of a large row); each workgroup then traces R/split rays.
-  const bool recording = a->n_record > 0 && a->record_bin == a->bin;
-  int64_t split = 1;
-  if (!recording && n_rows > 0 && n_rows < kSplitTargetBlocks && R >= 2 * kSplitMinRays)
-    split = std::min<int64_t>((kSplitTargetBlocks + n_rows - 1) / n_rows, R / kSplitMinRays);
-  if (!recording && R >= 65536 && ((N + 1) / 2) * 4 + rthx::kStaticLdsBytes <= (int64_t)rthx::kMaxLdsBytes &&
+  p.recording = a->n_record > 0 && a->record_bin == a->bin;
+  p.split = 1;
+  if (!p.recording && p.n_rows > 0 && p.n_rows < kSplitTargetBlocks && R >= 2 * kSplitMinRays)
+    p.split = std::min<int64_t>((kSplitTargetBlocks + p.n_rows - 1) / p.n_rows, R / kSplitMinRays);
+  if (!p.recording && R >= 65536 && ((N + 1) / 2) * 4 + rthx::kStaticLdsBytes <= (int64_t)rthx::kMaxLdsBytes &&
       N * 4 + rthx::kStaticLdsBytes > (int64_t)rthx::kMaxLdsBytes)
-    split = std::max<int64_t>(split, (R + 65534) / 65535);
-  const int64_t rays_per_block = split > 1 ? (R + split - 1) / split : R;
-  const bool pack16 = rays_per_block < 65536;
-  const int64_t words = pack16 ? (N + 1) / 2 : N;
-  size_t lds_bytes = (size_t)words * 4;
-  if (lds_bytes + rthx::kStaticLdsBytes > rthx::kMaxLdsBytes)
+    p.split = std::max<int64_t>(p.split, (R + 65534) / 65535);
+  const int64_t rays_per_block = p.split > 1 ? (R + p.split - 1) / p.split : R;
+  p.pack16 = rays_per_block < 65536;
+  const int64_t words = p.pack16 ? (N + 1) / 2 : N;
+  p.lds_bytes = (size_t)words * 4;
+  if (p.lds_bytes + rthx::kStaticLdsBytes > rthx::kMaxLdsBytes)
     return fail(RTHX_ERANGE, "N too large for the LDS row histogram of this build (N <= 76800)");
   // multi-polygon domains: the coarse mesh goes behind the histogram in LDS
   // when it fits (CLDS kernels, rthx_device.h segment_cl)
-  const size_t cl_offset = (lds_bytes + 15) & ~(size_t)15;
-  const bool clds = !dom->single_convex && dom->D.cl.bytes > 0 &&
-                    cl_offset + (size_t)dom->D.cl.bytes + rthx::kStaticLdsBytes <= rthx::kMaxLdsBytes &&
-                    !(getenv("RTHX_NO_CLDS") && getenv("RTHX_NO_CLDS")[0] == '1');
-  if (clds) lds_bytes = cl_offset + (size_t)dom->D.cl.bytes;
-  const int64_t row_cap = std::max<int64_t>(1, std::min<int64_t>(N, R));
+  p.cl_offset = (p.lds_bytes + 15) & ~(size_t)15;
+  p.clds = !dom->single_convex && dom->D.cl.bytes > 0 &&
+           p.cl_offset + (size_t)dom->D.cl.bytes + rthx::kStaticLdsBytes <= rthx::kMaxLdsBytes &&
+           !env_flag("RTHX_NO_CLDS");
+  if (p.clds) p.lds_bytes = p.cl_offset + (size_t)dom->D.cl.bytes;
+  p.row_cap = std::max<int64_t>(1, std::min<int64_t>(N, R));
+  p.uniform = dom->uniform_beta[a->bin] > -0.1;  // traceRay.jl:4
+  return RTHX_OK;
+}
+
+// One launch sequence of a planned trace.  lookback: the trace kernel writes
+// the final CSR itself (decoupled look-back over the rows); otherwise rows go
+// to staging slots, then row_scan + csr_pack.  Fills totals (see
+// finish_staged; totals[3] > 0: a look-back wait gave up).
+int run_trace(rthx_domain* dom, const rthx_trace_args* a, const TracePlan& p, rthx_result* res, bool lookback,
+              const rthx::RecordParams& rec, int64_t totals[4], float* ms_trace, float* ms_pack) {
+  const int64_t n_rows = p.n_rows, N = p.N, R = p.R;
+  hipStream_t st = dom->stream;
+  HIP_TRY(res->row_nnz.reserve((size_t)n_rows * 4), "hipMalloc row_nnz");
+  HIP_TRY(res->row_tallied.reserve((size_t)n_rows * 4), "hipMalloc row_tallied");
+  HIP_TRY(res->row_off.reserve((size_t)(n_rows + 1) * 8), "hipMalloc row_off");
+  HIP_TRY(res->totals.reserve(4 * 8), "hipMalloc totals");
+  // Staging slots only when the rows are staged; the direct CSR writes
+  // cols / counts in place, sized to the worst case n_rows x min(N, R).
+  if (lookback) {
+    res->stage_cols.release();
+    res->stage_cnt.release();
+    HIP_TRY(res->cols.reserve((size_t)n_rows * p.row_cap * 4), "hipMalloc cols");
+    HIP_TRY(res->cnt.reserve((size_t)n_rows * p.row_cap * 4), "hipMalloc cnt");
+    HIP_TRY(res->lb_status.reserve((size_t)n_rows * 8), "hipMalloc look-back words");
+  } else {
+    res->lb_status.release();
+    HIP_TRY(res->stage_cols.reserve((size_t)n_rows * p.row_cap * 4), "hipMalloc stage_cols");
+    HIP_TRY(res->stage_cnt.reserve((size_t)n_rows * p.row_cap * 4), "hipMalloc stage_cnt");
+  }
+  if (p.split > 1) HIP_TRY(res->dense.reserve((size_t)n_rows * N * 4), "hipMalloc dense rows");
+  else res->dense.release();
+
+  rthx::TraceParams P{};
+  P.R = R;
+  P.g_begin = a->emitter_begin;
+  P.g_stride = a->emitter_stride;
+  P.eta = a->nudge;
+  P.key0 = (uint32_t)a->seed;
+  P.key1 = (uint32_t)(a->seed >> 32);
+  P.bin = a->bin;
+  P.beta_uniform = dom->beta_first[a->bin];
+  P.inv_beta_uniform = P.beta_uniform > 0 ? 1.0 / P.beta_uniform : 0.0;
+
+  rthx::TallyParams T{};
+  T.n_emitters = N;
+  T.n_rows = n_rows;
+  T.row_cap = p.row_cap;
+  T.split = (int32_t)p.split;
+  T.cl_offset = p.clds ? (int32_t)p.cl_offset : 0;
+  T.stage_cols = res->stage_cols.as<uint32_t>();
+  T.stage_cnt = res->stage_cnt.as<uint32_t>();
+  T.row_nnz = res->row_nnz.as<uint32_t>();
+  T.row_tallied = res->row_tallied.as<uint32_t>();
+  T.dense = p.split > 1 ? res->dense.as<uint32_t>() : nullptr;
+  T.R = R;
+  if (lookback) {
+    T.lb_status = res->lb_status.as<unsigned long long>();
+    T.lb_wait_ticks = lookback_wait_ticks();
+    T.out_cols = res->cols.as<uint32_t>();
+    T.out_cnt = res->cnt.as<uint32_t>();
+    T.row_off = res->row_off.as<int64_t>();
+    T.totals = res->totals.as<unsigned long long>();
+    HIP_TRY(hipMemsetAsync(T.lb_status, 0, (size_t)n_rows * 8, st), "hipMemset look-back words");
+  }
+  HIP_TRY(hipMemsetAsync(res->totals.p, 0, 32, st), "hipMemset totals");
+  if (p.split > 1 && n_rows > 0) {
+    HIP_TRY(hipMemsetAsync(T.dense, 0, (size_t)n_rows * N * 4, st), "hipMemset dense rows");
+    HIP_TRY(hipMemsetAsync(T.row_tallied, 0, (size_t)n_rows * 4, st), "hipMemset row_tallied");
+  }
+  HIP_TRY(hipEventRecord(dom->ev[0], st), "hipEventRecord");
+  if (n_rows > 0) {
+    rthx::LaunchCfg L{};
+    L.D = dom->d_dom;
+    L.P = P;
+    L.T = T;
+    L.rec = rec;
+    L.lds_bytes = p.lds_bytes;
+    L.stream = st;
+    L.uniform = p.uniform;
+    L.pack16 = p.pack16;
+    L.faithful = (a->flags & RTHX_FLAG_FAITHFUL_SAMPLING) != 0;
+    L.single = dom->single_convex;
+    L.clds = p.clds;
+    L.axis = dom->axis_rect && !env_flag("RTHX_NO_AXIS");
+    HIP_TRY(rthx::launch_trace(L), "trace_exchange_kernel launch");
+  }
+  HIP_TRY(hipEventRecord(dom->ev[1], st), "hipEventRecord");
+  if (lookback) {
+    HIP_TRY(hipEventRecord(dom->ev[2], st), "hipEventRecord");
+    HIP_TRY(hipMemcpyAsync(totals, res->totals.p, 32, hipMemcpyDeviceToHost, st), "hipMemcpy totals");
+    HIP_TRY(hipStreamSynchronize(st), "trace kernel");
+  } else {
+    int rc = rthx::finish_staged(res, T, p.split > 1, st, dom->ev[2], totals);
+    if (rc) return rc;
+  }
+  HIP_TRY(hipEventElapsedTime(ms_trace, dom->ev[0], dom->ev[1]), "hipEventElapsedTime");
+  HIP_TRY(hipEventElapsedTime(ms_pack, dom->ev[1], dom->ev[2]), "hipEventElapsedTime");
+  return RTHX_OK;
+}
+
+// The whole of one device's trace (validated arguments, any device state).
+int trace_exchange_one(rthx_domain* dom, const rthx_trace_args* a, rthx_result* res) {
+  const double t0 = now_ms();
+  TracePlan p;
+  int rc = plan_trace(dom, a, p);
+  if (rc) return rc;
+  HIP_TRY(hipSetDevice(dom->device), "hipSetDevice");
+  if (res->device >= 0 && res->device != dom->device) return fail(RTHX_EINVAL, "result bound to another device");
+  for (rthx_result* q : res->parts) delete q;
+  res->parts.clear();
+  res->interleaved = false;
+  res->device = dom->device;
+  const int64_t R = p.R, n_rows = p.n_rows;
 
   res->valid = false;
-  res->host_csr = false;
   res->host_rec = false;
-  res->N = N;
+  res->host_row_off = false;
+  res->N = p.N;
   res->R = R;
   res->n_rows = n_rows;
   res->begin = a->emitter_begin;
   res->stride = a->emitter_stride;
+  res->split = p.split;
   res->info = rthx_result_info{};
-  res->info.n_emitters = N;
+  res->info.n_emitters = p.N;
   res->info.rows_traced = n_rows;
   res->info.rays_per_emitter = R;
   res->info.rays_traced = n_rows * R;
-  res->split = split;
+  res->info.n_devices = 1;
 
   // recorded emitters traced by this call (ascending, unique)
   res->rec_g.clear();
-  if (a->n_record > 0 && a->record_bin == a->bin) {
+  if (p.recording) {
     for (int i = 0; i < a->n_record; ++i) {
-      int64_t g = a->record_ids[i];
-      if (g >= a->emitter_begin && g < end && (g - a->emitter_begin) % a->emitter_stride == 0) res->rec_g.push_back(g);
+      const int64_t g = a->record_ids[i];
+      if (g >= a->emitter_begin && g < p.end && (g - a->emitter_begin) % a->emitter_stride == 0)
+        res->rec_g.push_back(g);
     }
     std::sort(res->rec_g.begin(), res->rec_g.end());
     res->rec_g.erase(std::unique(res->rec_g.begin(), res->rec_g.end()), res->rec_g.end());
   }
   const size_t n_rec = res->rec_g.size();
-
-  HIP_TRY(res->stage_cols.reserve((size_t)n_rows * row_cap * 4), "hipMalloc stage_cols");
-  HIP_TRY(res->stage_cnt.reserve((size_t)n_rows * row_cap * 4), "hipMalloc stage_cnt");
-  HIP_TRY(res->row_nnz.reserve((size_t)n_rows * 4), "hipMalloc row_nnz");
-  HIP_TRY(res->row_tallied.reserve((size_t)n_rows * 4), "hipMalloc row_tallied");
-  HIP_TRY(res->row_off.reserve((size_t)(n_rows + 1) * 8), "hipMalloc row_off");
-  HIP_TRY(res->totals.reserve(4 * 8), "hipMalloc totals");
-  HIP_TRY(res->cols.reserve((size_t)n_rows * row_cap * 4), "hipMalloc cols");
-  HIP_TRY(res->cnt.reserve((size_t)n_rows * row_cap * 4), "hipMalloc cnt");
-  if (split > 1) HIP_TRY(res->dense.reserve((size_t)n_rows * N * 4), "hipMalloc dense rows");
   rthx::RecordParams rec{};
   if (n_rec > 0) {
     HIP_TRY(res->rec_ids.reserve(n_rec * 8), "hipMalloc rec_ids");
@@ -500,139 +658,100 @@ RTHX_EXPORT int rthx_trace_exchange(rthx_domain* dom, const rthx_trace_args* a, 
     rec.end = res->rec_end.as<double>();
   }
 
-  rthx::TraceParams P{};
-  P.R = R;
-  P.g_begin = a->emitter_begin;
-  P.g_stride = a->emitter_stride;
-  P.eta = a->nudge;
-  P.key0 = (uint32_t)a->seed;
-  P.key1 = (uint32_t)(a->seed >> 32);
-  P.bin = a->bin;
-  P.beta_uniform = dom->beta_first[a->bin];
-  P.inv_beta_uniform = P.beta_uniform > 0 ? 1.0 / P.beta_uniform : 0.0;
-  const bool uniform = dom->uniform_beta[a->bin] > -0.1;  // traceRay.jl:4
-
-  rthx::TallyParams T{};
-  T.n_emitters = N;
-  T.n_rows = n_rows;
-  T.row_cap = row_cap;
-  T.split = (int32_t)split;
-  T.cl_offset = clds ? (int32_t)cl_offset : 0;
-  T.stage_cols = res->stage_cols.as<uint32_t>();
-  T.stage_cnt = res->stage_cnt.as<uint32_t>();
-  T.row_nnz = res->row_nnz.as<uint32_t>();
-  T.row_tallied = res->row_tallied.as<uint32_t>();
-  T.dense = split > 1 ? res->dense.as<uint32_t>() : nullptr;
-
   // Unsplit launches on single-polygon domains write rows straight into the
   // final CSR (decoupled look-back); RTHX_NO_LOOKBACK=1 keeps the staging +
   // scan + pack sequence.  Multi-polygon domains keep it too: their rows
   // finish at widely different times (rays cross different numbers of
   // layers), and a row waiting on a slower predecessor idles its CU slot
-  // (C5 greenhouse: 15.2 -> 17.6 ms per band with the look-back).
-  const char* nolb = getenv("RTHX_NO_LOOKBACK");
-  const bool lookback = split == 1 && n_rows > 0 && dom->single_convex && !(nolb && nolb[0] == '1');
-  if (lookback) {
-    HIP_TRY(res->lb_status.reserve((size_t)n_rows * 8), "hipMalloc look-back words");
-    T.lb_status = res->lb_status.as<unsigned long long>();
-    T.out_cols = res->cols.as<uint32_t>();
-    T.out_cnt = res->cnt.as<uint32_t>();
-    T.row_off = res->row_off.as<int64_t>();
-    T.totals = res->totals.as<unsigned long long>();
-    T.R = R;
-  }
-  hipStream_t st = dom->stream;
-  if (lookback) {
-    HIP_TRY(hipMemsetAsync(T.lb_status, 0, (size_t)n_rows * 8, st), "hipMemset look-back words");
-    HIP_TRY(hipMemsetAsync(T.totals, 0, 32, st), "hipMemset totals");
-  }
-  if (split > 1 && n_rows > 0) {
-    HIP_TRY(hipMemsetAsync(T.dense, 0, (size_t)n_rows * N * 4, st), "hipMemset dense rows");
-    HIP_TRY(hipMemsetAsync(T.row_tallied, 0, (size_t)n_rows * 4, st), "hipMemset row_tallied");
-  }
-  HIP_TRY(hipEventRecord(dom->ev[0], st), "hipEventRecord");
-  if (n_rows > 0) {
-    rthx::LaunchCfg L{};
-    L.D = dom->d_dom;
-    L.P = P;
-    L.T = T;
-    L.rec = rec;
-    L.lds_bytes = lds_bytes;
-    L.stream = st;
-    L.uniform = uniform;
-    L.pack16 = pack16;
-    L.faithful = (a->flags & RTHX_FLAG_FAITHFUL_SAMPLING) != 0;
-    L.single = dom->single_convex;
-    L.clds = clds;
-    L.axis = dom->axis_rect && !(getenv("RTHX_NO_AXIS") && getenv("RTHX_NO_AXIS")[0] == '1');
-    HIP_TRY(rthx::launch_trace(L), "trace_exchange_kernel launch");
-  }
-  HIP_TRY(hipEventRecord(dom->ev[1], st), "hipEventRecord");
-  if (n_rows > 0 && !lookback) {
-    if (split > 1) HIP_TRY(rthx::launch_compact(T, st), "row_compact_kernel launch");
-    HIP_TRY(rthx::launch_scan(res->row_nnz.as<uint32_t>(), res->row_tallied.as<uint32_t>(), n_rows, R,
-                              res->row_off.as<int64_t>(), res->totals.as<int64_t>(), st),
-            "row_scan_kernel launch");
-    HIP_TRY(rthx::launch_pack(res->stage_cols.as<uint32_t>(), res->stage_cnt.as<uint32_t>(), row_cap,
-                              res->row_off.as<int64_t>(), n_rows, res->cols.as<uint32_t>(), res->cnt.as<uint32_t>(), st),
-            "csr_pack_kernel launch");
-  } else if (n_rows == 0) {
-    HIP_TRY(hipMemsetAsync(res->row_off.p, 0, 8, st), "hipMemset");
-    HIP_TRY(hipMemsetAsync(res->totals.p, 0, 32, st), "hipMemset");
-  }
-  HIP_TRY(hipEventRecord(dom->ev[2], st), "hipEventRecord");
-
+  // (C5 greenhouse: 15.2 -> 17.6 ms per band with the look-back).  The
+  // recorder's kernels stage.
+  const bool lookback = p.split == 1 && n_rows > 0 && dom->single_convex && !p.recording && !env_flag("RTHX_NO_LOOKBACK");
   int64_t totals[4] = {0, 0, 0, 0};
-  HIP_TRY(hipMemcpyAsync(totals, res->totals.p, 32, hipMemcpyDeviceToHost, st), "hipMemcpy totals");
-  const bool device_only = (a->flags & RTHX_FLAG_DEVICE_ONLY) != 0;
-  res->h_row_off.resize(n_rows + 1);
-  res->host_row_off = !device_only;
-  if (!device_only)
-    HIP_TRY(hipMemcpyAsync(res->h_row_off.data(), res->row_off.p, (n_rows + 1) * 8, hipMemcpyDeviceToHost, st),
-            "hipMemcpy row_off");
-  HIP_TRY(hipStreamSynchronize(st), "trace kernels");
   float ms_trace = 0.f, ms_pack = 0.f;
-  HIP_TRY(hipEventElapsedTime(&ms_trace, dom->ev[0], dom->ev[1]), "hipEventElapsedTime");
-  HIP_TRY(hipEventElapsedTime(&ms_pack, dom->ev[1], dom->ev[2]), "hipEventElapsedTime");
-
-  if (lookback && totals[3] != 0) return fail(RTHX_EDEVICE, "direct-CSR look-back stalled (rows not dispatched in order)");
+  rc = run_trace(dom, a, p, res, lookback, rec, totals, &ms_trace, &ms_pack);
+  if (rc) return rc;
+  if (lookback && totals[3] != 0) {
+    // A look-back wait gave up (a predecessor row did not publish its nnz in
+    // time): the direct CSR may be misplaced, so the same launch -- same
+    // draws, same counts -- is traced again on the staging path.
+    res->info.lookback_fallbacks = 1;
+    float ms2 = 0.f, mp2 = 0.f;
+    rc = run_trace(dom, a, p, res, false, rec, totals, &ms2, &mp2);
+    if (rc) return rc;
+    ms_trace += ms2;
+    ms_pack += mp2;
+  }
   res->info.nnz = totals[0];
   res->info.lost_total = totals[1];
   res->info.lost_max_row = totals[2];
   res->info.trace_ms = ms_trace;
   res->info.pack_ms = ms_pack;
-  res->valid = true;
 
-  if (!device_only) {
-    const size_t nnz = (size_t)totals[0];
-    HIP_TRY(res->h_cols.reserve(nnz * 4), "hipHostMalloc cols");
-    HIP_TRY(res->h_cnt.reserve(nnz * 4), "hipHostMalloc counts");
-    if (nnz) {
-      HIP_TRY(hipMemcpy(res->h_cols.p, res->cols.p, nnz * 4, hipMemcpyDeviceToHost), "hipMemcpy cols");
-      HIP_TRY(hipMemcpy(res->h_cnt.p, res->cnt.p, nnz * 4, hipMemcpyDeviceToHost), "hipMemcpy counts");
-    }
-    res->host_csr = true;
-    if (n_rec > 0) {
-      res->h_ok.resize(n_rec * (size_t)R);
-      res->h_orig.resize(n_rec * (size_t)R * 2);
-      res->h_end.resize(n_rec * (size_t)R * 2);
-      HIP_TRY(hipMemcpy(res->h_ok.data(), res->rec_ok.p, n_rec * (size_t)R, hipMemcpyDeviceToHost), "hipMemcpy rec");
-      HIP_TRY(hipMemcpy(res->h_orig.data(), res->rec_orig.p, n_rec * (size_t)R * 16, hipMemcpyDeviceToHost), "hipMemcpy rec");
-      HIP_TRY(hipMemcpy(res->h_end.data(), res->rec_end.p, n_rec * (size_t)R * 16, hipMemcpyDeviceToHost), "hipMemcpy rec");
-      res->host_rec = true;
-    }
+  if (!(a->flags & RTHX_FLAG_DEVICE_ONLY)) {
+    res->h_row_off.resize(n_rows + 1);
+    HIP_TRY(hipMemcpy(res->h_row_off.data(), res->row_off.p, (n_rows + 1) * 8, hipMemcpyDeviceToHost),
+            "hipMemcpy row_off");
+    res->host_row_off = true;
   }
   int64_t nrec = 0;
   if (n_rec > 0) {
-    if (!res->host_rec) {
-      res->h_ok.resize(n_rec * (size_t)R);
-      HIP_TRY(hipMemcpy(res->h_ok.data(), res->rec_ok.p, n_rec * (size_t)R, hipMemcpyDeviceToHost), "hipMemcpy rec");
-    }
+    res->h_ok.resize(n_rec * (size_t)R);
+    HIP_TRY(hipMemcpy(res->h_ok.data(), res->rec_ok.p, n_rec * (size_t)R, hipMemcpyDeviceToHost), "hipMemcpy rec");
     for (uint8_t v : res->h_ok) nrec += v;
   }
   res->info.n_recorded = nrec;
+  res->valid = true;
   res->info.total_ms = now_ms() - t0;
   return RTHX_OK;
+}
+
+int fetch_row_off(rthx_result* res) {
+  if (res->host_row_off) return RTHX_OK;
+  HIP_TRY(hipSetDevice(res->device), "hipSetDevice");
+  res->h_row_off.resize(res->n_rows + 1);
+  HIP_TRY(hipMemcpy(res->h_row_off.data(), res->row_off.p, (res->n_rows + 1) * 8, hipMemcpyDeviceToHost),
+          "hipMemcpy row_off");
+  res->host_row_off = true;
+  return RTHX_OK;
+}
+
+int fetch_rays(rthx_result* res) {
+  const size_t n_rec = res->rec_g.size(), R = (size_t)res->R;
+  if (n_rec == 0 || res->host_rec) return RTHX_OK;
+  HIP_TRY(hipSetDevice(res->device), "hipSetDevice");
+  res->h_orig.resize(n_rec * R * 2);
+  res->h_end.resize(n_rec * R * 2);
+  HIP_TRY(hipMemcpy(res->h_orig.data(), res->rec_orig.p, n_rec * R * 16, hipMemcpyDeviceToHost), "hipMemcpy rec");
+  HIP_TRY(hipMemcpy(res->h_end.data(), res->rec_end.p, n_rec * R * 16, hipMemcpyDeviceToHost), "hipMemcpy rec");
+  res->host_rec = true;
+  return RTHX_OK;
+}
+
+// Run f(d) for every device part on its own host thread; the first error
+// (with its thread-local message) is returned on the calling thread.
+template <class F>
+int for_each_part(size_t n, F f) {
+  std::vector<int> rc(n, RTHX_OK);
+  std::vector<std::string> msg(n);
+  std::vector<std::thread> th;
+  th.reserve(n);
+  for (size_t d = 0; d < n; ++d)
+    th.emplace_back([&, d] {
+      rc[d] = f(d);
+      if (rc[d]) msg[d] = rthx::g_last_error;
+    });
+  for (auto& t : th) t.join();
+  for (size_t d = 0; d < n; ++d)
+    if (rc[d]) return fail(rc[d], msg[d]);
+  return RTHX_OK;
+}
+
+}  // namespace
+
+RTHX_EXPORT int rthx_trace_exchange(rthx_domain* dom, const rthx_trace_args* a, rthx_result* res) {
+  if (!dom || !a || !res) return fail(RTHX_EINVAL, "null argument");
+  if (a->device != dom->device) return fail(RTHX_EINVAL, "args.device differs from the domain's device");
+  return trace_exchange_one(dom, a, res);
 }
 
 RTHX_EXPORT int rthx_result_get_info(const rthx_result* res, rthx_result_info* info) {
@@ -642,43 +761,134 @@ RTHX_EXPORT int rthx_result_get_info(const rthx_result* res, rthx_result_info* i
   return RTHX_OK;
 }
 
+RTHX_EXPORT int rthx_host_register(void* ptr, size_t bytes) {
+  if (!ptr || bytes == 0) return fail(RTHX_EINVAL, "null or empty host range");
+  HIP_TRY(hipHostRegister(ptr, bytes, hipHostRegisterPortable), "hipHostRegister");
+  return RTHX_OK;
+}
+
+RTHX_EXPORT int rthx_host_unregister(void* ptr) {
+  if (!ptr) return fail(RTHX_EINVAL, "null pointer");
+  HIP_TRY(hipHostUnregister(ptr), "hipHostUnregister");
+  return RTHX_OK;
+}
+
+namespace {
+
+// Global CSR row pointers over all N rows of a single-device result: rows
+// g = begin + k * stride hold slot k, every other row is empty.
+void expand_row_ptr(const rthx_result* res, int64_t* row_ptr) {
+  row_ptr[0] = 0;
+  int64_t k = 0;
+  for (int64_t g = 0; g < res->N; ++g) {
+    int64_t n = 0;
+    if (k < res->n_rows && g == res->begin + k * res->stride) {
+      n = res->h_row_off[k + 1] - res->h_row_off[k];
+      ++k;
+    }
+    row_ptr[g + 1] = row_ptr[g] + n;
+  }
+}
+
+// D2H of one single-device result's cols / counts / F values (nnz entries
+// each) to the given host arrays (any may be null).  F values are formed on
+// the device first (counts_to_F_kernel).
+int copy_part_csr(rthx_result* res, int32_t* cols, uint32_t* counts, double* vals) {
+  const size_t nnz = (size_t)res->info.nnz;
+  if (nnz == 0) return RTHX_OK;
+  HIP_TRY(hipSetDevice(res->device), "hipSetDevice");
+  if (vals) {
+    HIP_TRY(res->fvals.reserve(nnz * 8), "hipMalloc F values");
+    HIP_TRY(rthx::launch_counts_to_F(res->row_off.as<int64_t>(), res->cnt.as<uint32_t>(), res->n_rows,
+                                     res->fvals.as<double>(), nullptr),
+            "counts_to_F_kernel launch");
+    HIP_TRY(hipMemcpy(vals, res->fvals.p, nnz * 8, hipMemcpyDeviceToHost), "hipMemcpy F values");
+  }
+  if (cols) HIP_TRY(hipMemcpy(cols, res->cols.p, nnz * 4, hipMemcpyDeviceToHost), "hipMemcpy cols");
+  if (counts) HIP_TRY(hipMemcpy(counts, res->cnt.p, nnz * 4, hipMemcpyDeviceToHost), "hipMemcpy counts");
+  return RTHX_OK;
+}
+
+// rthx_result_copy_csr / rthx_result_copy_F: row pointers over all N rows,
+// then per device its entries -- straight into place for contiguous row
+// blocks, through pinned bounce buffers and a row scatter for interleaved ones.
+int copy_result(rthx_result* res, int64_t* row_ptr, int32_t* cols, uint32_t* counts, double* vals) {
+  if (res->parts.empty()) {
+    int rc = copy_part_csr(res, cols, counts, vals);
+    if (rc) return rc;
+    if (row_ptr) {
+      if ((rc = fetch_row_off(res))) return rc;
+      expand_row_ptr(res, row_ptr);
+    }
+    return RTHX_OK;
+  }
+  const size_t nd = res->parts.size();
+  int rc = for_each_part(nd, [&](size_t d) { return fetch_row_off(res->parts[d]); });
+  if (rc) return rc;
+  // global row pointers: part d's slot k is row g = begin_d + k * stride_d
+  std::vector<int64_t> len(res->N, 0);
+  for (rthx_result* q : res->parts)
+    for (int64_t k = 0; k < q->n_rows; ++k) len[q->begin + k * q->stride] = q->h_row_off[k + 1] - q->h_row_off[k];
+  std::vector<int64_t> rp_local;
+  int64_t* rp = row_ptr;
+  if (!rp) {
+    rp_local.resize(res->N + 1);
+    rp = rp_local.data();
+  }
+  rp[0] = 0;
+  for (int64_t g = 0; g < res->N; ++g) rp[g + 1] = rp[g] + len[g];
+  if (!cols && !counts && !vals) return RTHX_OK;
+  if (!res->interleaved) {
+    return for_each_part(nd, [&](size_t d) {
+      rthx_result* q = res->parts[d];
+      const int64_t off = q->n_rows > 0 ? rp[q->begin] : 0;
+      return copy_part_csr(q, cols ? cols + off : nullptr, counts ? counts + off : nullptr, vals ? vals + off : nullptr);
+    });
+  }
+  return for_each_part(nd, [&](size_t d) {
+    rthx_result* q = res->parts[d];
+    const size_t nnz = (size_t)q->info.nnz;
+    if (nnz == 0) return (int)RTHX_OK;
+    HIP_TRY(hipSetDevice(q->device), "hipSetDevice");
+    int32_t* bc = nullptr;
+    uint32_t* bn = nullptr;
+    double* bv = nullptr;
+    if (cols) {
+      HIP_TRY(q->h_cols.reserve(nnz * 4), "hipHostMalloc cols");
+      bc = static_cast<int32_t*>(q->h_cols.p);
+    }
+    if (counts) {
+      HIP_TRY(q->h_cnt.reserve(nnz * 4), "hipHostMalloc counts");
+      bn = static_cast<uint32_t*>(q->h_cnt.p);
+    }
+    if (vals) {
+      HIP_TRY(q->h_vals.reserve(nnz * 8), "hipHostMalloc F values");
+      bv = static_cast<double*>(q->h_vals.p);
+    }
+    int r2 = copy_part_csr(q, bc, bn, bv);
+    if (r2) return r2;
+    for (int64_t k = 0; k < q->n_rows; ++k) {
+      const int64_t g = q->begin + k * q->stride, a0 = q->h_row_off[k], n = q->h_row_off[k + 1] - a0;
+      if (cols) std::memcpy(cols + rp[g], bc + a0, n * 4);
+      if (counts) std::memcpy(counts + rp[g], bn + a0, n * 4);
+      if (vals) std::memcpy(vals + rp[g], bv + a0, n * 8);
+    }
+    return (int)RTHX_OK;
+  });
+}
+
+}  // namespace
+
 RTHX_EXPORT int rthx_result_copy_csr(const rthx_result* cres, int64_t* row_ptr, int32_t* cols, uint32_t* counts) {
   if (!cres) return fail(RTHX_EINVAL, "null result");
   if (!cres->valid) return fail(RTHX_ESTATE, "result holds no trace");
-  rthx_result* res = const_cast<rthx_result*>(cres);
-  const size_t nnz = (size_t)res->info.nnz;
-  if (!res->host_csr) {
-    HIP_TRY(hipSetDevice(res->device), "hipSetDevice");
-    HIP_TRY(res->h_cols.reserve(nnz * 4), "hipHostMalloc cols");
-    HIP_TRY(res->h_cnt.reserve(nnz * 4), "hipHostMalloc counts");
-    if (nnz) {
-      HIP_TRY(hipMemcpy(res->h_cols.p, res->cols.p, nnz * 4, hipMemcpyDeviceToHost), "hipMemcpy cols");
-      HIP_TRY(hipMemcpy(res->h_cnt.p, res->cnt.p, nnz * 4, hipMemcpyDeviceToHost), "hipMemcpy counts");
-    }
-    res->host_csr = true;
-  }
-  if (row_ptr && !res->host_row_off) {
-    HIP_TRY(hipSetDevice(res->device), "hipSetDevice");
-    HIP_TRY(hipMemcpy(res->h_row_off.data(), res->row_off.p, (res->n_rows + 1) * 8, hipMemcpyDeviceToHost),
-            "hipMemcpy row_off");
-    res->host_row_off = true;
-  }
-  if (row_ptr) {
-    // rows g = begin + k*stride hold slot k; all other rows are empty
-    row_ptr[0] = 0;
-    int64_t k = 0;
-    for (int64_t g = 0; g < res->N; ++g) {
-      int64_t n = 0;
-      if (k < res->n_rows && g == res->begin + k * res->stride) {
-        n = res->h_row_off[k + 1] - res->h_row_off[k];
-        ++k;
-      }
-      row_ptr[g + 1] = row_ptr[g] + n;
-    }
-  }
-  if (cols && nnz) std::memcpy(cols, res->h_cols.p, nnz * 4);
-  if (counts && nnz) std::memcpy(counts, res->h_cnt.p, nnz * 4);
-  return RTHX_OK;
+  return copy_result(const_cast<rthx_result*>(cres), row_ptr, cols, counts, nullptr);
+}
+
+RTHX_EXPORT int rthx_result_copy_F(const rthx_result* cres, int64_t* row_ptr, int32_t* cols, double* vals) {
+  if (!cres) return fail(RTHX_EINVAL, "null result");
+  if (!cres->valid) return fail(RTHX_ESTATE, "result holds no trace");
+  return copy_result(const_cast<rthx_result*>(cres), row_ptr, cols, nullptr, vals);
 }
 
 RTHX_EXPORT int rthx_result_copy_rays(const rthx_result* cres, double* origins_xy, double* endpoints_xy,
@@ -686,29 +896,137 @@ RTHX_EXPORT int rthx_result_copy_rays(const rthx_result* cres, double* origins_x
   if (!cres) return fail(RTHX_EINVAL, "null result");
   if (!cres->valid) return fail(RTHX_ESTATE, "result holds no trace");
   rthx_result* res = const_cast<rthx_result*>(cres);
-  const size_t n_rec = res->rec_g.size();
-  const size_t R = (size_t)res->R;
-  if (n_rec > 0 && !res->host_rec) {
-    HIP_TRY(hipSetDevice(res->device), "hipSetDevice");
-    res->h_ok.resize(n_rec * R);
-    res->h_orig.resize(n_rec * R * 2);
-    res->h_end.resize(n_rec * R * 2);
-    HIP_TRY(hipMemcpy(res->h_ok.data(), res->rec_ok.p, n_rec * R, hipMemcpyDeviceToHost), "hipMemcpy rec");
-    HIP_TRY(hipMemcpy(res->h_orig.data(), res->rec_orig.p, n_rec * R * 16, hipMemcpyDeviceToHost), "hipMemcpy rec");
-    HIP_TRY(hipMemcpy(res->h_end.data(), res->rec_end.p, n_rec * R * 16, hipMemcpyDeviceToHost), "hipMemcpy rec");
-    res->host_rec = true;
+  // (emitter, part, index in part) of every recorded emitter, ascending emitter
+  std::vector<rthx_result*> srcs = res->parts.empty() ? std::vector<rthx_result*>{res} : res->parts;
+  std::vector<std::pair<int64_t, std::pair<size_t, size_t>>> order;
+  for (size_t d = 0; d < srcs.size(); ++d) {
+    int rc = fetch_rays(srcs[d]);
+    if (rc) return rc;
+    for (size_t i = 0; i < srcs[d]->rec_g.size(); ++i) order.push_back({srcs[d]->rec_g[i], {d, i}});
   }
+  std::sort(order.begin(), order.end());
+  const size_t R = (size_t)res->R;
   int64_t n = 0;
-  for (size_t i = 0; i < n_rec; ++i)
+  for (const auto& o : order) {
+    const rthx_result* q = srcs[o.second.first];
+    const size_t i = o.second.second;
     for (size_t r = 0; r < R; ++r) {
-      size_t k = i * R + r;
-      if (!res->h_ok[k]) continue;
+      const size_t k = i * R + r;
+      if (!q->h_ok[k]) continue;
       if (n >= cap) break;
-      if (origins_xy) { origins_xy[2 * n] = res->h_orig[2 * k]; origins_xy[2 * n + 1] = res->h_orig[2 * k + 1]; }
-      if (endpoints_xy) { endpoints_xy[2 * n] = res->h_end[2 * k]; endpoints_xy[2 * n + 1] = res->h_end[2 * k + 1]; }
-      if (emitter) emitter[n] = res->rec_g[i];
+      if (origins_xy) { origins_xy[2 * n] = q->h_orig[2 * k]; origins_xy[2 * n + 1] = q->h_orig[2 * k + 1]; }
+      if (endpoints_xy) { endpoints_xy[2 * n] = q->h_end[2 * k]; endpoints_xy[2 * n + 1] = q->h_end[2 * k + 1]; }
+      if (emitter) emitter[n] = o.first;
       ++n;
     }
+  }
   if (n_out) *n_out = n;
+  return RTHX_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Several devices
+// ---------------------------------------------------------------------------
+struct rthx_multi {
+  std::vector<rthx_domain*> doms;
+  ~rthx_multi() {
+    for (rthx_domain* d : doms) rthx_domain_destroy(d);
+  }
+};
+
+RTHX_EXPORT int rthx_multi_create(const rthx_domain_desc* desc, const int32_t* devices, int32_t n_devices,
+                                  rthx_multi** out) {
+  if (!out) return fail(RTHX_EINVAL, "null out");
+  *out = nullptr;
+  if (!devices || n_devices < 1) return fail(RTHX_EINVAL, "empty device list");
+  // (a device may be listed more than once: its blocks then run on
+  // concurrent streams of that device)
+  rthx_multi* m = new (std::nothrow) rthx_multi();
+  if (!m) return fail(RTHX_ENOMEM, "host allocation failed");
+  m->doms.assign(n_devices, nullptr);
+  const int rc = for_each_part((size_t)n_devices, [&](size_t d) { return rthx_domain_create(desc, devices[d], &m->doms[d]); });
+  if (rc) {
+    delete m;
+    return rc;
+  }
+  *out = m;
+  return RTHX_OK;
+}
+
+RTHX_EXPORT void rthx_multi_destroy(rthx_multi* m) { delete m; }
+
+RTHX_EXPORT int rthx_multi_trace_exchange(rthx_multi* m, const rthx_trace_args* a, rthx_result* res) {
+  const double t0 = now_ms();
+  if (!m || !a || !res) return fail(RTHX_EINVAL, "null argument");
+  const size_t nd = m->doms.size();
+  TracePlan p;
+  int rc = plan_trace(m->doms[0], a, p);  // argument checks
+  if (rc) return rc;
+  // a result that held a single-device trace gives up its device buffers
+  if (res->device >= 0) {
+    (void)hipSetDevice(res->device);
+    rthx::DevBuf* all[] = {&res->stage_cols, &res->stage_cnt, &res->row_nnz, &res->row_tallied, &res->row_off,
+                           &res->totals,     &res->cols,      &res->cnt,     &res->dense,       &res->rec_ids,
+                           &res->rec_ok,     &res->rec_orig,  &res->rec_end, &res->lb_status};
+    for (rthx::DevBuf* b : all) b->release();
+    res->device = -1;
+  }
+  while (res->parts.size() < nd) res->parts.push_back(new rthx_result());
+  while (res->parts.size() > nd) {
+    delete res->parts.back();
+    res->parts.pop_back();
+  }
+  for (size_t d = 0; d < nd; ++d)
+    if (res->parts[d]->device >= 0 && res->parts[d]->device != m->doms[d]->device) {
+      delete res->parts[d];
+      res->parts[d] = new rthx_result();
+    }
+  // Row blocks: contiguous slots [n_rows d / nd, n_rows (d+1) / nd) on
+  // single-polygon domains (every row costs about the same), interleaved
+  // slots d, d + nd, ... on multi-polygon domains.
+  const bool interleave = !m->doms[0]->single_convex;
+  std::vector<rthx_trace_args> pa(nd, *a);
+  for (size_t d = 0; d < nd; ++d) {
+    pa[d].device = m->doms[d]->device;
+    if (interleave) {
+      pa[d].emitter_begin = a->emitter_begin + (int64_t)d * a->emitter_stride;
+      pa[d].emitter_stride = a->emitter_stride * (int64_t)nd;
+      pa[d].emitter_end = p.end;
+    } else {
+      const int64_t s0 = p.n_rows * (int64_t)d / (int64_t)nd, s1 = p.n_rows * (int64_t)(d + 1) / (int64_t)nd;
+      pa[d].emitter_begin = a->emitter_begin + s0 * a->emitter_stride;
+      pa[d].emitter_end = std::min<int64_t>(a->emitter_begin + s1 * a->emitter_stride, p.end);
+      if (s1 <= s0) pa[d].emitter_end = pa[d].emitter_begin;
+    }
+  }
+  res->valid = false;
+  rc = for_each_part(nd, [&](size_t d) { return trace_exchange_one(m->doms[d], &pa[d], res->parts[d]); });
+  if (rc) return rc;
+  res->interleaved = interleave;
+  res->N = p.N;
+  res->R = p.R;
+  res->n_rows = p.n_rows;
+  res->begin = a->emitter_begin;
+  res->stride = a->emitter_stride;
+  res->split = 1;
+  rthx_result_info& I = res->info;
+  I = rthx_result_info{};
+  I.n_emitters = p.N;
+  I.rays_per_emitter = p.R;
+  I.n_devices = (int32_t)nd;
+  for (rthx_result* q : res->parts) {
+    const rthx_result_info& J = q->info;
+    I.rows_traced += J.rows_traced;
+    I.rays_traced += J.rays_traced;
+    I.nnz += J.nnz;
+    I.lost_total += J.lost_total;
+    I.lost_max_row = std::max(I.lost_max_row, J.lost_max_row);
+    I.n_recorded += J.n_recorded;
+    I.trace_ms = std::max(I.trace_ms, J.trace_ms);
+    I.pack_ms = std::max(I.pack_ms, J.pack_ms);
+    I.lookback_fallbacks += J.lookback_fallbacks;
+  }
+  res->valid = true;
+  I.total_ms = now_ms() - t0;
   return RTHX_OK;
 }

@@ -46,26 +46,42 @@ struct rthx_domain {
 
 struct rthx_result {
   int device = -1;
+  // rthx_multi_trace_exchange: one sub-result per device (their rows
+  // contiguous blocks, or interleaved g = d, d + n, ...); the fields below
+  // then describe the whole trace and the device buffers stay empty.
+  std::vector<rthx_result*> parts;
+  bool interleaved = false;
   rthx::DevBuf stage_cols, stage_cnt, row_nnz, row_tallied, row_off, totals, cols, cnt, dense;
   rthx::DevBuf rec_ids, rec_ok, rec_orig, rec_end;
   rthx::DevBuf lb_status;  // direct-CSR look-back words (unsplit launches)
+  rthx::DevBuf fvals;      // F_raw values (rthx_result_copy_F)
   bool valid = false;
-  bool host_csr = false;
   bool host_row_off = false;
   int64_t N = 0, R = 0, n_rows = 0, begin = 0, stride = 1, split = 1;
   std::vector<int64_t> h_row_off;
-  rthx::HostBuf h_cols, h_cnt;  // pinned
+  rthx::HostBuf h_cols, h_cnt, h_vals;  // pinned bounce buffers (interleaved multi-device reassembly)
   std::vector<int64_t> rec_g;  // recorded emitters (ascending)
   std::vector<uint8_t> h_ok;
   std::vector<double> h_orig, h_end;
   bool host_rec = false;
   rthx_result_info info{};
   ~rthx_result() {
+    for (rthx_result* p : parts) delete p;
     if (device >= 0) (void)hipSetDevice(device);
     rthx::DevBuf* all[] = {&stage_cols, &stage_cnt, &row_nnz,  &row_tallied, &row_off,  &totals, &cols,
-                     &cnt,        &dense,     &rec_ids,  &rec_ok,      &rec_orig, &rec_end, &lb_status};
+                     &cnt,        &dense,     &rec_ids,  &rec_ok,      &rec_orig, &rec_end, &lb_status, &fvals};
     for (rthx::DevBuf* b : all) b->release();
     h_cols.release();
     h_cnt.release();
+    h_vals.release();
   }
 };
+
+namespace rthx {
+struct TallyParams;
+// rthx_api.cpp: staged rows -> final CSR after a trace launch on `st` (split
+// merge, row scan, totals read back, cols / counts sized to nnz, pack; ev_end
+// recorded after the pack).  Shared by the 2D and 3D tracers.
+int finish_staged(rthx_result* res, const TallyParams& T, bool split, hipStream_t st, hipEvent_t ev_end,
+                  int64_t totals[4]);
+}  // namespace rthx

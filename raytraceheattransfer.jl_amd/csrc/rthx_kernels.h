@@ -45,8 +45,9 @@ struct TallyParams {
   uint32_t* out_cols;
   uint32_t* out_cnt;
   int64_t* row_off;              // [n_rows + 1]
-  unsigned long long* totals;    // nnz, lost rays, max lost per row (zeroed; lost via atomics)
+  unsigned long long* totals;    // nnz, lost rays, max lost per row, look-back stalls (zeroed)
   int64_t R;
+  uint64_t lb_wait_ticks;        // longest look-back wait (s_memrealtime ticks, 100 MHz) before giving up
 };
 
 struct LaunchCfg {
@@ -60,6 +61,10 @@ struct LaunchCfg {
 };
 
 hipError_t launch_trace(const LaunchCfg& L);
+// F_raw values of a CSR of counts: vals[k] = cnt[k] / (sum of the row's counts)
+// (row_normalize! of counts / R, parallelRayTracing.jl:145, :161-169).
+hipError_t launch_counts_to_F(const int64_t* row_off, const uint32_t* cnt, int64_t n_rows, double* vals,
+                              hipStream_t stream);
 hipError_t launch_compact(const TallyParams& T, hipStream_t stream);
 hipError_t launch_scan(const uint32_t* row_nnz, const uint32_t* row_tallied, int64_t n_rows, int64_t R,
                        int64_t* row_off, int64_t* totals, hipStream_t stream);

@@ -34,15 +34,21 @@ namespace rthx {
 // Decoupled look-back (Merrill & Garland 2016) over the rows of one launch:
 // row `slot` publishes its nnz as an aggregate (flag 1), walks back over its
 // predecessors' words adding aggregates until it meets an inclusive prefix
-// (flag 2), then publishes its own inclusive prefix.  Workgroups are
-// dispatched in row order, so every predecessor is resident or finished and
-// the walk ends.  One u64 per row: flag in bits 62-63, value below.
-// Agent-scope atomics (coherent across the XCDs' L2s).
-// Termination does not rest on the dispatch order alone: a wait longer than
-// ~2^20 polls (about a second; far beyond any row's trace) raises *stalled and gives up (the
-// host then fails the call loudly instead of returning a wrong CSR).
+// (flag 2), then publishes its own inclusive prefix.  One u64 per row: flag
+// in bits 62-63, value below.  Agent-scope atomics (coherent across the
+// XCDs' L2s).
+// Progress: workgroups are dispatched in order within each XCD (not across
+// the chip), so the lowest unfinished row m is always resident or next in
+// line: every row ahead of it in its XCD's queue has a smaller index and has
+// finished.  m waits only on finished rows, so it completes, and by
+// induction every row does.
+// The wait is still bounded by time (wait_ticks of the 100 MHz
+// s_memrealtime clock): past it the row raises *stalled and ends its walk
+// with a partial prefix.  Partial prefixes are never larger than the true
+// ones, so the misplaced rows stay inside cols / counts, and the host then
+// traces the launch again on the staging path (rthx_api.cpp run_trace).
 __device__ __forceinline__ uint64_t lookback_offset(unsigned long long* status, int64_t slot, uint32_t nnz,
-                                                    unsigned long long* stalled) {
+                                                    unsigned long long* stalled, uint64_t wait_ticks) {
   constexpr unsigned long long kAgg = 1ull << 62, kInc = 2ull << 62, kVal = (1ull << 62) - 1;
   if (slot == 0) {
     __hip_atomic_store(&status[0], kInc | nnz, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -50,14 +56,16 @@ __device__ __forceinline__ uint64_t lookback_offset(unsigned long long* status, 
   }
   __hip_atomic_store(&status[slot], kAgg | nnz, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   unsigned long long excl = 0;
-  uint32_t polls = 0;
-  for (int64_t j = slot - 1;; --j) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  bool gave_up = false;
+  for (int64_t j = slot - 1; !gave_up; --j) {
     unsigned long long v;
     while (((v = __hip_atomic_load(&status[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 62) == 0) {
       __builtin_amdgcn_s_sleep(1);
-      if (++polls >= (1u << 20)) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > wait_ticks) {
         atomicAdd(stalled, 1ull);
-        v = kInc;  // give up: end the walk (the call fails on the host)
+        gave_up = true;
+        v = kInc;  // end the walk (the host re-traces the launch)
         break;
       }
     }
@@ -303,7 +311,7 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
     // direct CSR: the row's offset is the sum of the earlier rows' nnz
     __shared__ unsigned long long s_base;
     auto base_of = [&](uint32_t nnz) -> uint64_t {
-      if (tid == 0) s_base = lookback_offset(T.lb_status, slot, nnz, &T.totals[3]);
+      if (tid == 0) s_base = lookback_offset(T.lb_status, slot, nnz, &T.totals[3], T.lb_wait_ticks);
       __syncthreads();
       return s_base;
     };
@@ -490,6 +498,31 @@ hipError_t launch_trace(const LaunchCfg& L) {
   }
   if (L.uniform) return L.pack16 ? launch_trace_u<true, true, false>(L) : launch_trace_u<true, false, false>(L);
   return L.pack16 ? launch_trace_u<false, true, false>(L) : launch_trace_u<false, false, false>(L);
+}
+
+// One wave per row: the row's tallied rays (exact integer sum of its counts),
+// then every entry's share count / tallied -- the exact quotient of the
+// reference's (count / R) / (row sum of count / R).
+__global__ __launch_bounds__(256) void counts_to_F_kernel(const int64_t* __restrict__ row_off,
+                                                          const uint32_t* __restrict__ cnt, int64_t n_rows,
+                                                          double* __restrict__ vals) {
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= n_rows) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t b = row_off[row], e = row_off[row + 1];
+  uint64_t t = 0;
+  for (int64_t k = b + lane; k < e; k += 64) t += cnt[k];
+  for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off);
+  const double td = (double)t;
+  for (int64_t k = b + lane; k < e; k += 64) vals[k] = (double)cnt[k] / td;
+}
+
+hipError_t launch_counts_to_F(const int64_t* row_off, const uint32_t* cnt, int64_t n_rows, double* vals,
+                              hipStream_t stream) {
+  if (n_rows <= 0) return hipSuccess;
+  hipLaunchKernelGGL(counts_to_F_kernel, dim3((unsigned)((n_rows + 3) / 4)), dim3(256), 0, stream, row_off, cnt,
+                     n_rows, vals);
+  return hipGetLastError();
 }
 
 hipError_t launch_compact(const TallyParams& T, hipStream_t stream) {

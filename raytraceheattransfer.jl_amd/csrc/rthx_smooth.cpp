@@ -6,6 +6,8 @@
 // dense/sparse switch, Dykstra-round choice, the defect schedule of AP with
 // its contraction estimate and floor acceptance -- follows the reference
 // line by line; the numerical passes differ from it only in summation order.
+// host-only translation unit: device pointers are plain pointers here
+#define RTHX_HOST_ONLY_TU 1
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -16,6 +18,7 @@
 #include <vector>
 
 #include "rthx_common.h"
+#include "rthx_domain.h"
 #include "rthx_smooth.h"
 
 using rthx::DevBuf;
@@ -282,63 +285,31 @@ int ap_sparse(Ctx& c, rthx_smooth_result* res, int max_iters, double nz_over_N, 
 
 }  // namespace
 
-RTHX_EXPORT int rthx_smooth_F(const int64_t* row_ptr, const int32_t* cols, const double* vals, int64_t n,
-                              const double* w_in, int64_t n_w, int32_t num_surfaces, const rthx_smooth_args* args,
-                              rthx_smooth_result** out) {
-  const double t0 = now_ms();
-  if (!out) return fail(RTHX_EINVAL, "null out");
-  *out = nullptr;
-  if (!row_ptr || !w_in || !args || n < 1 || n_w < n) return fail(RTHX_EINVAL, "bad smoothing arguments");
-  if (n >= (1ll << 31)) return fail(RTHX_ERANGE, "matrix too large");
-  if (row_ptr[0] != 0) return fail(RTHX_EINVAL, "row_ptr[0] != 0");
-  const int64_t nnz = row_ptr[n];
-  if (nnz > 0 && (!cols || !vals)) return fail(RTHX_EINVAL, "null CSR arrays");
-  for (int64_t i = 0; i < n_w; ++i)
-    if (!(w_in[i] > 0) || !std::isfinite(w_in[i])) return fail(RTHX_EINVAL, "weights must be positive and finite");
-  if (num_surfaces < 0 || num_surfaces > n_w) return fail(RTHX_EINVAL, "num_surfaces out of range");
-  int ndev = 0;
-  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) return fail(RTHX_EDEVICE, "no HIP device visible");
-  if (args->device < 0 || args->device >= ndev) return fail(RTHX_EINVAL, "device ordinal out of range");
-  HIP_TRY(hipSetDevice(args->device), "hipSetDevice");
+namespace {
 
-  // One pass over F_raw: validation, row order, and the surface-gas coupling
-  // sum of cross_coupling_chi (:212-241).  Rows must be sorted by column for
-  // the sparse build; unsorted input is sorted into a copy.
-  double chi_acc = 0.0;
-  bool sorted = true;
-  for (int64_t i = 0; i < n; ++i) {
-    if (row_ptr[i + 1] < row_ptr[i] || row_ptr[i + 1] > nnz) return fail(RTHX_EINVAL, "row_ptr not monotone");
-    const bool si = i < num_surfaces;
-    for (int64_t k = row_ptr[i]; k < row_ptr[i + 1]; ++k) {
-      const int32_t c = cols[k];
-      if (c < 0 || c >= n || !std::isfinite(vals[k])) return fail(RTHX_EINVAL, "bad CSR entry");
-      if (k > row_ptr[i] && !(cols[k - 1] < c)) sorted = false;
-      if (si != (c < num_surfaces)) chi_acc += vals[k];
-    }
-  }
-  std::vector<int32_t> ci_sorted;
-  std::vector<double> v_sorted;
-  const int64_t* rp = row_ptr;
-  const int32_t* ci = cols;
-  const double* v = vals;
-  if (!sorted) {
-    ci_sorted.assign(cols, cols + nnz);
-    v_sorted.assign(vals, vals + nnz);
-    for (int64_t i = 0; i < n; ++i) {
-      std::vector<std::pair<int32_t, double>> row;
-      for (int64_t k = rp[i]; k < rp[i + 1]; ++k) row.emplace_back(cols[k], vals[k]);
-      std::sort(row.begin(), row.end(), [](auto& x, auto& y) { return x.first < y.first; });
-      for (size_t q = 1; q < row.size(); ++q)
-        if (row[q].first == row[q - 1].first) return fail(RTHX_EINVAL, "duplicate CSR entry");
-      for (size_t q = 0; q < row.size(); ++q) {
-        ci_sorted[rp[i] + q] = row[q].first;
-        v_sorted[rp[i] + q] = row[q].second;
-      }
-    }
-    ci = ci_sorted.data();
-    v = v_sorted.data();
-  }
+// F_raw as the smoothing sees it: a host CSR with sorted rows, or (counts !=
+// nullptr) a single-device trace result whose count CSR is still on the
+// device, normalised on the fly (value = count / tallied[row]).
+struct SmoothInput {
+  int64_t n = 0, nnz = 0;  // leading n x n block and its stored entries
+  double chi_acc = 0.0;    // sum of surface-volume coupling entries of the block
+  const int64_t* rp = nullptr;
+  const int32_t* ci = nullptr;
+  const double* v = nullptr;
+  const rthx_result* counts = nullptr;
+  const double* tallied = nullptr;  // device [n]: rays each row tallied
+};
 
+int smooth_core(const SmoothInput& in, const double* w_in, int64_t n_w, int32_t num_surfaces,
+                const rthx_smooth_args* args, rthx_smooth_result** out, double t0) {
+  const int64_t n = in.n, nnz = in.nnz;
+  const double chi_acc = in.chi_acc;
+  const int64_t* rp = in.rp;
+  const int32_t* ci = in.ci;
+  const double* v = in.v;
+  std::vector<int64_t> h_rp;
+  std::vector<int32_t> h_ci;
+  std::vector<double> h_v;
   const bool verbose = args->verbose != 0;
   const int64_t N = n_w;  // length(w)
   double chi = 0.0, nz_over_N;
@@ -427,7 +398,13 @@ RTHX_EXPORT int rthx_smooth_F(const int64_t* row_ptr, const int32_t* cols, const
     DTRY(A.reserve(bytes), "hipMalloc dense F");
     DTRY(Xb.reserve((size_t)m * (size_t)ap_dense_ld(m) * 8), "hipMalloc dense X");  // also Xbar (n x n)
     // dense F_raw (truncated to m x m): the CSR rows < m, columns < m
-    {
+    if (in.counts) {
+      DTRY(hipMemsetAsync(A.p, 0, bytes, s), "hipMemset");
+      DTRY(rthx::sm::scatter_counts(in.counts->row_off.as<int64_t>(), in.counts->cols.as<uint32_t>(),
+                                    in.counts->cnt.as<uint32_t>(), m, in.tallied, A.as<double>(), s),
+           "scatter_counts");
+      DTRY(hipStreamSynchronize(s), "scatter");
+    } else {
       DevBuf drp, dci, dv;
       const int64_t mnnz = rp[m];
       DTRY(drp.reserve((m + 1) * 8), "hipMalloc");
@@ -490,6 +467,36 @@ RTHX_EXPORT int rthx_smooth_F(const int64_t* row_ptr, const int32_t* cols, const
     res->nnz = m * m;
   } else {
     const double t2 = now_ms();
+    if (in.counts) {
+      // the sparse X pattern is built on the host: bring the block's
+      // normalised F_raw over once (rows < m, columns < m)
+      const rthx_result* cr = in.counts;
+      std::vector<int64_t> ro(m + 1);
+      std::vector<uint32_t> cc, cn;
+      std::vector<double> rs(m);
+      DTRY(hipMemcpy(ro.data(), cr->row_off.p, (m + 1) * 8, hipMemcpyDeviceToHost), "hipMemcpy row_off");
+      cc.resize(std::max<int64_t>(ro[m], 1));
+      cn.resize(std::max<int64_t>(ro[m], 1));
+      if (ro[m]) {
+        DTRY(hipMemcpy(cc.data(), cr->cols.p, ro[m] * 4, hipMemcpyDeviceToHost), "hipMemcpy cols");
+        DTRY(hipMemcpy(cn.data(), cr->cnt.p, ro[m] * 4, hipMemcpyDeviceToHost), "hipMemcpy counts");
+      }
+      DTRY(hipMemcpy(rs.data(), in.tallied, m * 8, hipMemcpyDeviceToHost), "hipMemcpy tallied");
+      h_rp.assign(m + 1, 0);
+      h_ci.reserve(nnz);
+      h_v.reserve(nnz);
+      for (int64_t i = 0; i < m; ++i) {
+        for (int64_t k = ro[i]; k < ro[i + 1]; ++k)
+          if ((int64_t)cc[k] < m) {
+            h_ci.push_back((int32_t)cc[k]);
+            h_v.push_back((double)cn[k] / rs[i]);
+          }
+        h_rp[i + 1] = (int64_t)h_ci.size();
+      }
+      rp = h_rp.data();
+      ci = h_ci.data();
+      v = h_v.data();
+    }
     std::vector<int64_t> xrp;
     std::vector<int32_t> xci;
     std::vector<double> xv;
@@ -530,6 +537,118 @@ RTHX_EXPORT int rthx_smooth_F(const int64_t* row_ptr, const int32_t* cols, const
   I.ms_total = now_ms() - t0;
   *out = res;
   return RTHX_OK;
+}
+
+}  // namespace
+
+RTHX_EXPORT int rthx_smooth_F(const int64_t* row_ptr, const int32_t* cols, const double* vals, int64_t n,
+                              const double* w_in, int64_t n_w, int32_t num_surfaces, const rthx_smooth_args* args,
+                              rthx_smooth_result** out) {
+  const double t0 = now_ms();
+  if (!out) return fail(RTHX_EINVAL, "null out");
+  *out = nullptr;
+  if (!row_ptr || !w_in || !args || n < 1 || n_w < n) return fail(RTHX_EINVAL, "bad smoothing arguments");
+  if (n >= (1ll << 31)) return fail(RTHX_ERANGE, "matrix too large");
+  if (row_ptr[0] != 0) return fail(RTHX_EINVAL, "row_ptr[0] != 0");
+  const int64_t nnz = row_ptr[n];
+  if (nnz > 0 && (!cols || !vals)) return fail(RTHX_EINVAL, "null CSR arrays");
+  for (int64_t i = 0; i < n_w; ++i)
+    if (!(w_in[i] > 0) || !std::isfinite(w_in[i])) return fail(RTHX_EINVAL, "weights must be positive and finite");
+  if (num_surfaces < 0 || num_surfaces > n_w) return fail(RTHX_EINVAL, "num_surfaces out of range");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) return fail(RTHX_EDEVICE, "no HIP device visible");
+  if (args->device < 0 || args->device >= ndev) return fail(RTHX_EINVAL, "device ordinal out of range");
+  HIP_TRY(hipSetDevice(args->device), "hipSetDevice");
+
+  // One pass over F_raw: validation, row order, and the surface-gas coupling
+  // sum of cross_coupling_chi (:212-241).  Rows must be sorted by column for
+  // the sparse build; unsorted input is sorted into a copy.
+  double chi_acc = 0.0;
+  bool sorted = true;
+  for (int64_t i = 0; i < n; ++i) {
+    if (row_ptr[i + 1] < row_ptr[i] || row_ptr[i + 1] > nnz) return fail(RTHX_EINVAL, "row_ptr not monotone");
+    const bool si = i < num_surfaces;
+    for (int64_t k = row_ptr[i]; k < row_ptr[i + 1]; ++k) {
+      const int32_t c = cols[k];
+      if (c < 0 || c >= n || !std::isfinite(vals[k])) return fail(RTHX_EINVAL, "bad CSR entry");
+      if (k > row_ptr[i] && !(cols[k - 1] < c)) sorted = false;
+      if (si != (c < num_surfaces)) chi_acc += vals[k];
+    }
+  }
+  std::vector<int32_t> ci_sorted;
+  std::vector<double> v_sorted;
+  const int64_t* rp = row_ptr;
+  const int32_t* ci = cols;
+  const double* v = vals;
+  if (!sorted) {
+    ci_sorted.assign(cols, cols + nnz);
+    v_sorted.assign(vals, vals + nnz);
+    for (int64_t i = 0; i < n; ++i) {
+      std::vector<std::pair<int32_t, double>> row;
+      for (int64_t k = rp[i]; k < rp[i + 1]; ++k) row.emplace_back(cols[k], vals[k]);
+      std::sort(row.begin(), row.end(), [](auto& x, auto& y) { return x.first < y.first; });
+      for (size_t q = 1; q < row.size(); ++q)
+        if (row[q].first == row[q - 1].first) return fail(RTHX_EINVAL, "duplicate CSR entry");
+      for (size_t q = 0; q < row.size(); ++q) {
+        ci_sorted[rp[i] + q] = row[q].first;
+        v_sorted[rp[i] + q] = row[q].second;
+      }
+    }
+    ci = ci_sorted.data();
+    v = v_sorted.data();
+  }
+
+  SmoothInput in;
+  in.n = n;
+  in.nnz = nnz;
+  in.chi_acc = chi_acc;
+  in.rp = rp;
+  in.ci = ci;
+  in.v = v;
+  return smooth_core(in, w_in, n_w, num_surfaces, args, out, t0);
+}
+
+RTHX_EXPORT int rthx_smooth_F_result(const rthx_result* cr, int64_t n, const double* w_in, int64_t n_w,
+                                     int32_t num_surfaces, const rthx_smooth_args* args, rthx_smooth_result** out) {
+  const double t0 = now_ms();
+  if (!out) return fail(RTHX_EINVAL, "null out");
+  *out = nullptr;
+  if (!cr || !w_in || !args) return fail(RTHX_EINVAL, "bad smoothing arguments");
+  if (!cr->valid) return fail(RTHX_ESTATE, "result holds no trace");
+  if (!cr->parts.empty() || cr->device < 0)
+    return fail(RTHX_EINVAL, "rthx_smooth_F_result needs a single-device result (gather a multi-device CSR first)");
+  if (cr->begin != 0 || cr->stride != 1 || cr->n_rows != cr->N)
+    return fail(RTHX_EINVAL, "rthx_smooth_F_result needs a trace of every emitter row");
+  if (n < 1 || n > cr->N || n_w < n) return fail(RTHX_EINVAL, "bad block size");
+  if (n >= (1ll << 31)) return fail(RTHX_ERANGE, "matrix too large");
+  if (args->device != cr->device) return fail(RTHX_EINVAL, "args.device differs from the result's device");
+  for (int64_t i = 0; i < n_w; ++i)
+    if (!(w_in[i] > 0) || !std::isfinite(w_in[i])) return fail(RTHX_EINVAL, "weights must be positive and finite");
+  if (num_surfaces < 0 || num_surfaces > n_w) return fail(RTHX_EINVAL, "num_surfaces out of range");
+  if (cr->R < 1) return fail(RTHX_EINVAL, "a trace with R = 0 rays per emitter has no F_raw");
+  HIP_TRY(hipSetDevice(cr->device), "hipSetDevice");
+  // tallied rays per row, block nnz and the cross-coupling sum on the device
+  DevBuf tallied, chi_part, nnz_part;
+  HIP_TRY(tallied.reserve(n * 8), "hipMalloc");
+  HIP_TRY(chi_part.reserve(n * 8), "hipMalloc");
+  HIP_TRY(nnz_part.reserve(n * 8), "hipMalloc");
+  HIP_TRY(rthx::sm::count_rowstats(cr->row_off.as<int64_t>(), cr->cols.as<uint32_t>(), cr->cnt.as<uint32_t>(), n,
+                                   num_surfaces, tallied.as<double>(), chi_part.as<double>(), nnz_part.as<int64_t>(),
+                                   nullptr),
+          "count_rowstats");
+  std::vector<double> chi_h(n);
+  std::vector<int64_t> nnz_h(n);
+  HIP_TRY(hipMemcpy(chi_h.data(), chi_part.p, n * 8, hipMemcpyDeviceToHost), "hipMemcpy");
+  HIP_TRY(hipMemcpy(nnz_h.data(), nnz_part.p, n * 8, hipMemcpyDeviceToHost), "hipMemcpy");
+  SmoothInput in;
+  in.n = n;
+  for (int64_t i = 0; i < n; ++i) {
+    in.nnz += nnz_h[i];
+    in.chi_acc += chi_h[i];
+  }
+  in.counts = cr;
+  in.tallied = tallied.as<double>();
+  return smooth_core(in, w_in, n_w, num_surfaces, args, out, t0);
 }
 
 RTHX_EXPORT int rthx_smooth_get_info(const rthx_smooth_result* res, rthx_smooth_info* info) {

@@ -61,6 +61,13 @@ hipError_t sp_delta_rows(const int64_t* rp, const int32_t* ci, const double* v, 
                          int64_t n, double* part, hipStream_t s);
 hipError_t scatter(const int64_t* rp, const int32_t* ci, const double* v, int64_t n, double* A, hipStream_t s);
 hipError_t sp_recover(const int64_t* rp, double* v, const double* r, int64_t n, hipStream_t s);
+// F_raw from a trace result's device CSR (counts): per-row tallied rays,
+// block nnz and cross-coupling partials, and the dense scatter of the
+// normalised block (count / tallied).
+hipError_t count_rowstats(const int64_t* ro, const uint32_t* ci, const uint32_t* cnt, int64_t n, int32_t ns,
+                          double* tallied, double* chi_part, int64_t* nnz_block, hipStream_t s);
+hipError_t scatter_counts(const int64_t* ro, const uint32_t* ci, const uint32_t* cnt, int64_t n, const double* tallied,
+                          double* A, hipStream_t s);
 
 }  // namespace sm
 }  // namespace rthx

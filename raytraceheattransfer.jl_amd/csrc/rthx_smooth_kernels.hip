@@ -454,6 +454,58 @@ __global__ __launch_bounds__(kRow) void k_scatter(const int64_t* __restrict__ rp
   }
 }
 
+// F_raw straight from a trace result's device CSR (u32 columns and counts,
+// i64 row offsets; rthx_smooth_F_result), normalised as rthx_result_copy_F:
+// value = count / tallied, tallied = the row's count sum (row_normalize! of
+// count / R, parallelRayTracing.jl:145, :161-169, applied before the
+// surfaces_only truncation of exchangeRayTracing.jl:9-11).  One wave per row
+// i < n: tallied[i], nnz_block[i] = entries with column < n, chi_part[i] =
+// the block's normalised entries that couple a surface with a volume
+// (cross_coupling_chi, smoothExchangeFactors.jl:212-241).
+__global__ __launch_bounds__(kRow) void k_count_rowstats(const int64_t* __restrict__ ro, const uint32_t* __restrict__ ci,
+                                                         const uint32_t* __restrict__ cnt, int64_t n, int32_t ns,
+                                                         double* __restrict__ tallied, double* __restrict__ chi_part,
+                                                         int64_t* __restrict__ nnz_block) {
+  const int64_t i = (int64_t)blockIdx.x * (kRow / 64) + (threadIdx.x >> 6);
+  if (i >= n) return;
+  const int lane = threadIdx.x & 63;
+  uint64_t t = 0;
+  for (int64_t k = ro[i] + lane; k < ro[i + 1]; k += 64) t += cnt[k];
+  for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off);
+  const double td = (double)t;
+  const bool si = i < ns;
+  double chi = 0.0;
+  int64_t nb = 0;
+  for (int64_t k = ro[i] + lane; k < ro[i + 1]; k += 64) {
+    const int64_t c = ci[k];
+    if (c >= n) continue;
+    ++nb;
+    if (si != (c < ns)) chi += (double)cnt[k] / td;
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    chi += __shfl_xor(chi, off);
+    nb += __shfl_xor(nb, off);
+  }
+  if (lane == 0) {
+    tallied[i] = td;
+    chi_part[i] = chi;
+    nnz_block[i] = nb;
+  }
+}
+
+// A[i][c] = count / tallied[i] for the block's entries (A zeroed).
+__global__ __launch_bounds__(kRow) void k_scatter_counts(const int64_t* __restrict__ ro, const uint32_t* __restrict__ ci,
+                                                         const uint32_t* __restrict__ cnt, int64_t n,
+                                                         const double* __restrict__ tallied, double* __restrict__ A) {
+  const int64_t i = (int64_t)blockIdx.x * (kRow / 64) + (threadIdx.x >> 6);
+  if (i >= n) return;
+  const double td = tallied[i];
+  for (int64_t k = ro[i] + (threadIdx.x & 63); k < ro[i + 1]; k += 64) {
+    const int64_t c = ci[k];
+    if (c < n) A[i * n + c] = (double)cnt[k] / td;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
@@ -551,6 +603,17 @@ hipError_t sp_delta_rows(const int64_t* rp, const int32_t* ci, const double* v, 
 }
 hipError_t scatter(const int64_t* rp, const int32_t* ci, const double* v, int64_t n, double* A, hipStream_t s) {
   hipLaunchKernelGGL(k_scatter, dim3(grid1(n, kRow / 64)), dim3(kRow), 0, s, rp, ci, v, n, A);
+  return hipGetLastError();
+}
+hipError_t count_rowstats(const int64_t* ro, const uint32_t* ci, const uint32_t* cnt, int64_t n, int32_t ns,
+                          double* tallied, double* chi_part, int64_t* nnz_block, hipStream_t s) {
+  hipLaunchKernelGGL(k_count_rowstats, dim3(grid1(n, kRow / 64)), dim3(kRow), 0, s, ro, ci, cnt, n, ns, tallied,
+                     chi_part, nnz_block);
+  return hipGetLastError();
+}
+hipError_t scatter_counts(const int64_t* ro, const uint32_t* ci, const uint32_t* cnt, int64_t n, const double* tallied,
+                          double* A, hipStream_t s) {
+  hipLaunchKernelGGL(k_scatter_counts, dim3(grid1(n, kRow / 64)), dim3(kRow), 0, s, ro, ci, cnt, n, tallied, A);
   return hipGetLastError();
 }
 hipError_t sp_recover(const int64_t* rp, double* v, const double* r, int64_t n, hipStream_t s) {

@@ -485,8 +485,11 @@ RTHX_EXPORT int rthx_trace_exchange_3d(rthx_scene3d* sc, const rthx_trace_args* 
     return fail(RTHX_ERANGE, "N too large for the LDS row histogram and walk stacks of the 3D tracer");
   if (n_rows * split >= (int64_t(1) << 31)) return fail(RTHX_ERANGE, "too many rows in one call");
   const int64_t row_cap = std::max<int64_t>(1, std::min<int64_t>(N, R));
+  for (rthx_result* q : res->parts) delete q;
+  res->parts.clear();
+  res->interleaved = false;
   res->valid = false;
-  res->host_csr = false;
+  res->host_row_off = false;
   res->host_rec = false;
   res->rec_g.clear();
   res->N = N;
@@ -500,14 +503,14 @@ RTHX_EXPORT int rthx_trace_exchange_3d(rthx_scene3d* sc, const rthx_trace_args* 
   res->info.rows_traced = n_rows;
   res->info.rays_per_emitter = R;
   res->info.rays_traced = n_rows * R;
+  res->info.n_devices = 1;
+  res->lb_status.release();
   HIP_TRY(res->stage_cols.reserve((size_t)n_rows * row_cap * 4), "hipMalloc stage_cols");
   HIP_TRY(res->stage_cnt.reserve((size_t)n_rows * row_cap * 4), "hipMalloc stage_cnt");
   HIP_TRY(res->row_nnz.reserve((size_t)n_rows * 4), "hipMalloc row_nnz");
   HIP_TRY(res->row_tallied.reserve((size_t)n_rows * 4), "hipMalloc row_tallied");
   HIP_TRY(res->row_off.reserve((size_t)(n_rows + 1) * 8), "hipMalloc row_off");
   HIP_TRY(res->totals.reserve(4 * 8), "hipMalloc totals");
-  HIP_TRY(res->cols.reserve((size_t)n_rows * row_cap * 4), "hipMalloc cols");
-  HIP_TRY(res->cnt.reserve((size_t)n_rows * row_cap * 4), "hipMalloc cnt");
   HIP_TRY(res->dense.reserve((size_t)n_rows * N * 4), "hipMalloc dense rows");
 
   rthx::TallyParams T{};
@@ -520,6 +523,7 @@ RTHX_EXPORT int rthx_trace_exchange_3d(rthx_scene3d* sc, const rthx_trace_args* 
   T.row_nnz = res->row_nnz.as<uint32_t>();
   T.row_tallied = res->row_tallied.as<uint32_t>();
   T.dense = res->dense.as<uint32_t>();
+  T.R = R;
   rthx::TraceParams P{};
   P.R = R;
   P.g_begin = a->emitter_begin;
@@ -527,6 +531,7 @@ RTHX_EXPORT int rthx_trace_exchange_3d(rthx_scene3d* sc, const rthx_trace_args* 
   P.key0 = (uint32_t)a->seed;
   P.key1 = (uint32_t)(a->seed >> 32);
   hipStream_t st = sc->stream;
+  HIP_TRY(hipMemsetAsync(res->totals.p, 0, 32, st), "hipMemset totals");
   if (n_rows > 0) {
     HIP_TRY(hipMemsetAsync(T.dense, 0, (size_t)n_rows * N * 4, st), "hipMemset dense rows");
     HIP_TRY(hipMemsetAsync(T.row_tallied, 0, (size_t)n_rows * 4, st), "hipMemset row_tallied");
@@ -545,47 +550,26 @@ RTHX_EXPORT int rthx_trace_exchange_3d(rthx_scene3d* sc, const rthx_trace_args* 
     HIP_TRY(rthx::launch_trace3d(L), "trace_exchange_3d_kernel launch");
   }
   HIP_TRY(hipEventRecord(sc->ev[1], st), "hipEventRecord");
-  if (n_rows > 0) {
-    HIP_TRY(rthx::launch_compact(T, st), "row_compact_kernel launch");
-    HIP_TRY(rthx::launch_scan(T.row_nnz, T.row_tallied, n_rows, R, res->row_off.as<int64_t>(), res->totals.as<int64_t>(),
-                              st),
-            "row_scan_kernel launch");
-    HIP_TRY(rthx::launch_pack(T.stage_cols, T.stage_cnt, row_cap, res->row_off.as<int64_t>(), n_rows,
-                              res->cols.as<uint32_t>(), res->cnt.as<uint32_t>(), st),
-            "csr_pack_kernel launch");
-  } else {
-    HIP_TRY(hipMemsetAsync(res->row_off.p, 0, 8, st), "hipMemset");
-    HIP_TRY(hipMemsetAsync(res->totals.p, 0, 32, st), "hipMemset");
+  int64_t totals[4] = {0, 0, 0, 0};
+  {
+    int rc = rthx::finish_staged(res, T, true, st, sc->ev[2], totals);
+    if (rc) return rc;
   }
-  HIP_TRY(hipEventRecord(sc->ev[2], st), "hipEventRecord");
-  int64_t totals[3] = {0, 0, 0};
-  HIP_TRY(hipMemcpyAsync(totals, res->totals.p, 24, hipMemcpyDeviceToHost, st), "hipMemcpy totals");
-  res->h_row_off.resize(n_rows + 1);
-  const bool device_only = (a->flags & RTHX_FLAG_DEVICE_ONLY) != 0;
-  res->host_row_off = !device_only;
-  if (!device_only)
-    HIP_TRY(hipMemcpyAsync(res->h_row_off.data(), res->row_off.p, (n_rows + 1) * 8, hipMemcpyDeviceToHost, st),
-            "hipMemcpy row_off");
-  HIP_TRY(hipStreamSynchronize(st), "3D trace kernels");
   float ms_trace = 0.f, ms_pack = 0.f;
   HIP_TRY(hipEventElapsedTime(&ms_trace, sc->ev[0], sc->ev[1]), "hipEventElapsedTime");
   HIP_TRY(hipEventElapsedTime(&ms_pack, sc->ev[1], sc->ev[2]), "hipEventElapsedTime");
+  if (!(a->flags & RTHX_FLAG_DEVICE_ONLY)) {
+    res->h_row_off.resize(n_rows + 1);
+    HIP_TRY(hipMemcpy(res->h_row_off.data(), res->row_off.p, (n_rows + 1) * 8, hipMemcpyDeviceToHost),
+            "hipMemcpy row_off");
+    res->host_row_off = true;
+  }
   res->info.nnz = totals[0];
   res->info.lost_total = totals[1];
   res->info.lost_max_row = totals[2];
   res->info.trace_ms = ms_trace;
   res->info.pack_ms = ms_pack;
   res->valid = true;
-  if (!device_only) {
-    const size_t nnz = (size_t)totals[0];
-    HIP_TRY(res->h_cols.reserve(nnz * 4), "hipHostMalloc cols");
-    HIP_TRY(res->h_cnt.reserve(nnz * 4), "hipHostMalloc counts");
-    if (nnz) {
-      HIP_TRY(hipMemcpy(res->h_cols.p, res->cols.p, nnz * 4, hipMemcpyDeviceToHost), "hipMemcpy cols");
-      HIP_TRY(hipMemcpy(res->h_cnt.p, res->cnt.p, nnz * 4, hipMemcpyDeviceToHost), "hipMemcpy counts");
-    }
-    res->host_csr = true;
-  }
   res->info.total_ms = now_ms() - t0;
   return RTHX_OK;
 }

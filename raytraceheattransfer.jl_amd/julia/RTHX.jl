@@ -14,6 +14,7 @@ everything above it (bin grouping, surfaces-only truncation, `smooth_F`,
     include("raytraceheattransfer.jl_amd/julia/RTHX.jl")
     RTHX.enable!(; lib = "raytraceheattransfer.jl_amd/csrc/_build/librthx.so", device = 0, seed = 1)
     mesh(100_000_000; method = :exchange)      # traced on the GPU
+    RTHX.enable!(; lib = ..., devices = 0:7)   # rows split over 8 GPUs (rthx_multi_trace_exchange)
 
 Not executable in the build container (no Julia toolchain); kept in step
 with `include/rthx.h` by `tests/test_abi.py::test_julia_shim_mirrors_header`.
@@ -22,11 +23,12 @@ module RTHX
 
 using SparseArrays
 
-const RTHX_ABI_VERSION = Int32(1)
+const RTHX_ABI_VERSION = Int32(2)
 const RTHX_FLAG_FAITHFUL_SAMPLING = UInt32(0x1)
 
 const LIB = Ref{String}("")
-const DEVICE = Ref{Int32}(0)
+const DEVICE = Ref{Int32}(0)          # device of the single-device calls (first of DEVICES)
+const DEVICES = Ref{Vector{Int32}}(Int32[0])  # devices the exchange tracer splits its rows over
 const SEED = Ref{UInt64}(1)
 const FAITHFUL = Ref{Bool}(false)
 
@@ -95,6 +97,8 @@ struct ResultInfo
     trace_ms::Float64
     pack_ms::Float64
     total_ms::Float64
+    n_devices::Int32
+    lookback_fallbacks::Int32
 end
 
 struct SmoothArgs
@@ -246,8 +250,9 @@ function flatten(rtm)
     return Flat(keep, grids, Ref(desc))
 end
 
-# one uploaded domain per (rtm, device)
-const DOMAINS = IdDict{Any, Tuple{Flat, Ptr{Cvoid}}}()
+# one uploaded domain per rtm: an rthx_domain (one device) or an rthx_multi
+# (DEVICES, rows split over them)
+const DOMAINS = IdDict{Any, Tuple{Flat, Ptr{Cvoid}, Bool}}()
 
 function device_domain(rtm)
     haskey(DOMAINS, rtm) && return DOMAINS[rtm][2]
@@ -257,8 +262,38 @@ function device_domain(rtm)
         check(ccall((:rthx_domain_create, LIB[]), Cint, (Ptr{DomainDesc}, Int32, Ptr{Ptr{Cvoid}}),
                     flat.desc, DEVICE[], h))
     end
-    DOMAINS[rtm] = (flat, h[])
+    DOMAINS[rtm] = (flat, h[], false)
     return h[]
+end
+
+const MULTI = IdDict{Any, Tuple{Flat, Ptr{Cvoid}}}()
+
+function multi_domain(rtm)
+    haskey(MULTI, rtm) && return MULTI[rtm][2]
+    flat = flatten(rtm)
+    h = Ref{Ptr{Cvoid}}(C_NULL)
+    devs = DEVICES[]
+    GC.@preserve flat devs begin
+        check(ccall((:rthx_multi_create, LIB[]), Cint, (Ptr{DomainDesc}, Ptr{Int32}, Int32, Ptr{Ptr{Cvoid}}),
+                    flat.desc, devs, Int32(length(devs)), h))
+    end
+    MULTI[rtm] = (flat, h[])
+    return h[]
+end
+
+# Page-locked cols / counts buffers reused across traces (rthx_host_register):
+# the library DMAs the device CSR straight into them.
+const PINNED = Dict{Symbol, Any}()
+
+function pinned(name::Symbol, ::Type{T}, n::Integer) where T
+    a = get(PINNED, name, nothing)
+    if a === nothing || length(a) < n
+        a === nothing || check(ccall((:rthx_host_unregister, LIB[]), Cint, (Ptr{Cvoid},), a))
+        a = zeros(T, max(cld(5n, 4), 1024))
+        check(ccall((:rthx_host_register, LIB[]), Cint, (Ptr{Cvoid}, Csize_t), a, sizeof(a)))
+        PINNED[name] = a
+    end
+    return a::Vector{T}
 end
 
 """
@@ -271,7 +306,8 @@ then `sparse` + `row_normalize!` exactly as the reference (:154-158).
 function computeExchangeFactorsBin(rtm, rays_per_emitter::Integer, nudge, spectral_bin::Integer,
                                    surface_mapping, volume_mapping, num_surfaces, num_volumes, num_emitters,
                                    verbose, rec)
-    dom = device_domain(rtm)
+    multi = length(DEVICES[]) > 1
+    dom = multi ? multi_domain(rtm) : device_domain(rtm)
     ids = rec === nothing ? Int64[] : Int64[i - 1 for i in rec.ids]
     rbin = rec === nothing ? Int32(0) : Int32(rec.bin - 1)
     args = Ref(TraceArgs(Int32(spectral_bin - 1), FAITHFUL[] ? RTHX_FLAG_FAITHFUL_SAMPLING : UInt32(0),
@@ -281,18 +317,19 @@ function computeExchangeFactorsBin(rtm, rays_per_emitter::Integer, nudge, spectr
     check(ccall((:rthx_result_create, LIB[]), Cint, (Ptr{Ptr{Cvoid}},), res))
     try
         GC.@preserve ids begin
-            check(ccall((:rthx_trace_exchange, LIB[]), Cint, (Ptr{Cvoid}, Ptr{TraceArgs}, Ptr{Cvoid}),
-                        dom, args, res[]))
+            check(ccall((multi ? :rthx_multi_trace_exchange : :rthx_trace_exchange, LIB[]), Cint,
+                        (Ptr{Cvoid}, Ptr{TraceArgs}, Ptr{Cvoid}), dom, args, res[]))
         end
         info = Ref{ResultInfo}()
         check(ccall((:rthx_result_get_info, LIB[]), Cint, (Ptr{Cvoid}, Ptr{ResultInfo}), res[], info))
         N, nnz = info[].n_emitters, info[].nnz
         rowptr = Vector{Int64}(undef, N + 1)
-        cols = Vector{Int32}(undef, max(nnz, 1))
-        counts = Vector{UInt32}(undef, max(nnz, 1))
+        cols = pinned(:cols, Int32, max(nnz, 1))
+        counts = pinned(:counts, UInt32, max(nnz, 1))
         check(ccall((:rthx_result_copy_csr, LIB[]), Cint, (Ptr{Cvoid}, Ptr{Int64}, Ptr{Int32}, Ptr{UInt32}),
                     res[], rowptr, cols, counts))
-        verbose && println("  rthx: $(info[].rays_traced) rays, nnz $nnz, trace $(round(info[].trace_ms; digits=3)) ms")
+        verbose && println("  rthx: $(info[].rays_traced) rays on $(info[].n_devices) device(s), nnz $nnz, ",
+                           "trace $(round(info[].trace_ms; digits=3)) ms")
         if rec !== nothing && info[].n_recorded > 0
             n = info[].n_recorded
             o = Vector{Float64}(undef, 2n); e = Vector{Float64}(undef, 2n); g = Vector{Int64}(undef, n)
@@ -534,16 +571,21 @@ function enclosureViewFactorsMC3D(superFaces, rays_tot::Integer; max_iters::Int 
 end
 
 """
-    enable!(; lib, device=0, seed=1, faithful=false)
+    enable!(; lib, device=0, devices=[device], seed=1, faithful=false)
 
 Redirect RayTraceHeatTransfer's `computeExchangeFactorsBin` (and, with
 `direct = true`, `directRayTracingSingleBin!`; with `viewfactors3d = true`,
-`enclosureViewFactors3D`) to the GPU.
+`enclosureViewFactors3D`) to the GPU.  With several `devices` the exchange
+tracer splits each bin's emitter rows over them (rthx_multi_trace_exchange:
+one host thread and stream per GPU, the counts identical to one device's);
+the other calls run on the first.
 """
-function enable!(; lib::AbstractString, device::Integer = 0, seed::Integer = 1, faithful::Bool = false,
-                 smoothing::Bool = false, direct::Bool = true, viewfactors3d::Bool = true)
+function enable!(; lib::AbstractString, device::Integer = 0, devices = [device], seed::Integer = 1,
+                 faithful::Bool = false, smoothing::Bool = false, direct::Bool = true, viewfactors3d::Bool = true)
     LIB[] = lib
-    DEVICE[] = Int32(device)
+    DEVICES[] = Int32[d for d in devices]
+    isempty(DEVICES[]) && error("enable!: empty device list")
+    DEVICE[] = DEVICES[][1]
     SEED[] = UInt64(seed)
     FAITHFUL[] = faithful
     v = ccall((:rthx_abi_version, LIB[]), Cint, ())

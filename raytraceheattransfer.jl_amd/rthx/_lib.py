@@ -59,8 +59,19 @@ def load(path: Optional[str] = None) -> C.CDLL:
     lib.rthx_result_get_info.argtypes = [C.c_void_p, C.POINTER(abi.ResultInfo)]
     lib.rthx_result_copy_csr.argtypes = [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int32),
                                          C.POINTER(C.c_uint32)]
+    lib.rthx_result_copy_F.argtypes = [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int32),
+                                       C.POINTER(C.c_double)]
     lib.rthx_result_copy_rays.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double),
                                           C.POINTER(C.c_int64), C.c_int64, C.POINTER(C.c_int64)]
+    lib.rthx_host_register.argtypes = [C.c_void_p, C.c_size_t]
+    lib.rthx_host_unregister.argtypes = [C.c_void_p]
+    lib.rthx_multi_create.argtypes = [C.POINTER(abi.DomainDesc), C.POINTER(C.c_int32), C.c_int32,
+                                      C.POINTER(C.c_void_p)]
+    lib.rthx_multi_destroy.argtypes = [C.c_void_p]
+    lib.rthx_multi_destroy.restype = None
+    lib.rthx_multi_trace_exchange.argtypes = [C.c_void_p, C.POINTER(abi.TraceArgs), C.c_void_p]
+    lib.rthx_smooth_F_result.argtypes = [C.c_void_p, C.c_int64, C.POINTER(C.c_double), C.c_int64, C.c_int32,
+                                         C.POINTER(abi.SmoothArgs), C.POINTER(C.c_void_p)]
     lib.rthx_smooth_F.argtypes = [C.POINTER(C.c_int64), C.POINTER(C.c_int32), C.POINTER(C.c_double), C.c_int64,
                                   C.POINTER(C.c_double), C.c_int64, C.c_int32, C.POINTER(abi.SmoothArgs),
                                   C.POINTER(C.c_void_p)]
@@ -172,6 +183,61 @@ class DeviceDomain:
             pass
 
 
+class MultiDeviceDomain:
+    """A domain uploaded to several devices (``rthx_multi*``): traces split
+    their rows over the devices, one host thread and stream each."""
+
+    def __init__(self, flat, devices: Sequence[int]):
+        self._lib = load()
+        self.devices = [int(d) for d in devices]
+        self.n_emitters = flat.n_emitters
+        devs = (C.c_int32 * len(self.devices))(*self.devices)
+        h = C.c_void_p()
+        check(self._lib.rthx_multi_create(C.byref(flat.desc), devs, len(self.devices), C.byref(h)))
+        self.handle = h
+
+    def close(self) -> None:
+        if getattr(self, "handle", None):
+            self._lib.rthx_multi_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class PinnedArrays:
+    """numpy arrays page-locked with ``rthx_host_register`` (direct DMA
+    targets that a caller reuses across traces); grow-only."""
+
+    def __init__(self):
+        self._arrays = {}
+
+    def get(self, name: str, n: int, dtype) -> np.ndarray:
+        a = self._arrays.get(name)
+        if a is None or a.size < n or a.dtype != np.dtype(dtype):
+            if a is not None:
+                check(load().rthx_host_unregister(a.ctypes.data))
+            a = np.empty(max(int(n * 1.25), 1024), dtype=dtype)
+            a.fill(0)  # fault the pages in before pinning
+            check(load().rthx_host_register(a.ctypes.data, a.nbytes))
+            self._arrays[name] = a
+        return a[:n]
+
+    def close(self) -> None:
+        for a in self._arrays.values():
+            load().rthx_host_unregister(a.ctypes.data)
+        self._arrays.clear()
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class DeviceResult:
     """A reusable ``rthx_result*``."""
 
@@ -181,8 +247,11 @@ class DeviceResult:
         check(self._lib.rthx_result_create(C.byref(h)))
         self.handle = h
 
-    def trace(self, dom: DeviceDomain, args) -> "DeviceResult":
-        check(self._lib.rthx_trace_exchange(dom.handle, C.byref(args), self.handle))
+    def trace(self, dom, args) -> "DeviceResult":
+        if isinstance(dom, MultiDeviceDomain):
+            check(self._lib.rthx_multi_trace_exchange(dom.handle, C.byref(args), self.handle))
+        else:
+            check(self._lib.rthx_trace_exchange(dom.handle, C.byref(args), self.handle))
         return self
 
     def info(self) -> dict:
@@ -190,16 +259,41 @@ class DeviceResult:
         check(self._lib.rthx_result_get_info(self.handle, C.byref(inf)))
         return inf.as_dict()
 
-    def csr(self):
+    def csr(self, pinned: Optional[PinnedArrays] = None):
+        """(row_ptr, cols, counts) on the host.  With `pinned`, cols and
+        counts land in its page-locked arrays (views, valid until the next
+        csr() into the same PinnedArrays)."""
         inf = self.info()
         n = inf["n_emitters"]
         nnz = inf["nnz"]
         row_ptr = np.empty(n + 1, dtype=np.int64)
-        cols = np.empty(max(nnz, 1), dtype=np.int32)
-        counts = np.empty(max(nnz, 1), dtype=np.uint32)
+        if pinned is not None:
+            cols = pinned.get("cols", max(nnz, 1), np.int32)
+            counts = pinned.get("counts", max(nnz, 1), np.uint32)
+        else:
+            cols = np.empty(max(nnz, 1), dtype=np.int32)
+            counts = np.empty(max(nnz, 1), dtype=np.uint32)
         check(self._lib.rthx_result_copy_csr(self.handle, abi.ptr(row_ptr, C.c_int64),
                                              abi.ptr(cols, C.c_int32), abi.ptr(counts, C.c_uint32)))
         return row_ptr, cols[:nnz], counts[:nnz]
+
+    def F(self, pinned: Optional[PinnedArrays] = None):
+        """F_raw as CSR (row_ptr, cols, vals): counts / R, row-normalised on
+        the device (rthx_result_copy_F).  With `pinned`, cols and vals land in
+        its page-locked arrays (views valid until its next use)."""
+        inf = self.info()
+        n = inf["n_emitters"]
+        nnz = inf["nnz"]
+        row_ptr = np.empty(n + 1, dtype=np.int64)
+        if pinned is not None:
+            cols = pinned.get("cols", max(nnz, 1), np.int32)
+            vals = pinned.get("vals", max(nnz, 1), np.float64)
+        else:
+            cols = np.empty(max(nnz, 1), dtype=np.int32)
+            vals = np.empty(max(nnz, 1), dtype=np.float64)
+        check(self._lib.rthx_result_copy_F(self.handle, abi.ptr(row_ptr, C.c_int64), abi.ptr(cols, C.c_int32),
+                                           abi.ptr(vals, C.c_double)))
+        return row_ptr, cols[:nnz], vals[:nnz]
 
     def rays(self):
         inf = self.info()
@@ -226,15 +320,58 @@ class DeviceResult:
 
 
 class HipBackend:
-    """The product backend: trace one bin on an MI355X through librthx."""
+    """The product backend: trace one bin on an MI355X through librthx.
+
+    ``devices``: trace on several devices (rthx_multi_trace_exchange, rows
+    split over them); default one device, the call's ``device``."""
 
     name = "hip"
+
+    def __init__(self, devices: Optional[Sequence[int]] = None):
+        self.devices = [int(d) for d in devices] if devices else None
+
+    def _domain(self, dom, device: int):
+        if self.devices and len(self.devices) > 1:
+            key = ("multi",) + tuple(self.devices)
+            dd = dom._device_domains.get(key)
+            if dd is None:
+                dd = MultiDeviceDomain(dom.flat(), self.devices)
+                dom._device_domains[key] = dd
+            return dd, self.devices[0]
+        dev = self.devices[0] if self.devices else device
+        return device_domain(dom, dev), dev
+
+    def trace_F(self, dom, bin0: int, rays_per_emitter: int, nudge: float, seed: int, device: int,
+                faithful: bool, record_ids=None, record_bin0: int = 0):
+        """One traced bin with F_raw formed on the device: returns (F_raw as
+        scipy CSR, info, recorded rays, the DeviceResult -- its counts stay
+        on the device for rthx_smooth_F_result)."""
+        import scipy.sparse as sp
+
+        flat = dom.flat()
+        dd, dev = self._domain(dom, device)
+        flags = abi.RTHX_FLAG_FAITHFUL_SAMPLING if faithful else 0
+        args, keep = make_args(bin0, rays_per_emitter, nudge, seed, 0, flat.n_emitters, 1, dev, flags,
+                               record_ids, record_bin0)
+        res = DeviceResult()
+        try:
+            res.trace(dd, args)
+            row_ptr, cols, vals = res.F()
+            info = res.info()
+            rays = res.rays() if info["n_recorded"] > 0 else None
+        except Exception:
+            res.close()
+            raise
+        del keep
+        n = flat.n_emitters
+        F = sp.csr_matrix((vals, cols, row_ptr), shape=(n, n))
+        return F, info, rays, res
 
     def trace(self, dom, bin0: int, rays_per_emitter: int, nudge: float, seed: int, device: int,
               faithful: bool, record_ids=None, record_bin0: int = 0, emitter_begin: int = 0,
               emitter_end: Optional[int] = None, emitter_stride: int = 1):
         flat = dom.flat()
-        dd = device_domain(dom, device)
+        dd, device = self._domain(dom, device)
         end = flat.n_emitters if emitter_end is None else emitter_end
         flags = abi.RTHX_FLAG_FAITHFUL_SAMPLING if faithful else 0
         args, keep = make_args(bin0, rays_per_emitter, nudge, seed, emitter_begin, end, emitter_stride,

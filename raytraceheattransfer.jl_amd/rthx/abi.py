@@ -6,7 +6,7 @@ from __future__ import annotations
 
 import ctypes as C
 
-RTHX_ABI_VERSION = 1
+RTHX_ABI_VERSION = 2
 
 RTHX_OK = 0
 RTHX_EINVAL = -1
@@ -95,6 +95,8 @@ class ResultInfo(C.Structure):
         ("trace_ms", C.c_double),
         ("pack_ms", C.c_double),
         ("total_ms", C.c_double),
+        ("n_devices", C.c_int32),
+        ("lookback_fallbacks", C.c_int32),
     ]
 
     def as_dict(self) -> dict:
@@ -230,7 +232,14 @@ EXPORTED_SYMBOLS = (
     "rthx_result_get_info",
     "rthx_result_copy_csr",
     "rthx_result_copy_rays",
+    "rthx_result_copy_F",
+    "rthx_host_register",
+    "rthx_host_unregister",
+    "rthx_multi_create",
+    "rthx_multi_destroy",
+    "rthx_multi_trace_exchange",
     "rthx_smooth_F",
+    "rthx_smooth_F_result",
     "rthx_smooth_get_info",
     "rthx_smooth_copy_dense",
     "rthx_smooth_copy_csr",

@@ -7,8 +7,10 @@ traced it.  One process per GPU traces the strided row set
 g = rank, rank + W, rank + 2W, ... (strided rather than contiguous so that
 surface and volume rows are spread evenly); assembling F is a gather of
 disjoint CSR row blocks — there is no reduction, hence no data-path
-collective.  ``gather_csr`` uses torch.distributed (gloo on the host) only to
-bring the row blocks to rank 0 for the host-side SparseMatrixCSC build.
+collective.  ``gather_csr`` brings the row blocks to one rank (or all) when
+the caller wants the whole F: tensor all-reduce / all-gather, over RCCL and
+xGMI on an NCCL group, over gloo on the host otherwise.  Inside one process,
+rthx_multi_trace_exchange splits rows over several devices instead.
 """
 from __future__ import annotations
 
@@ -54,16 +56,63 @@ def merge_csr(pieces: Sequence[Tuple[np.ndarray, np.ndarray, np.ndarray]], n: in
     return row_ptr, cols, counts
 
 
-def gather_csr(row_ptr, cols, counts, n: int, group=None):
-    """All ranks send their CSR block to rank 0 (torch.distributed object gather).
-    Returns the merged CSR on rank 0 and None elsewhere."""
+def _place(pieces_rows, pieces, lens_global, row_ptr, nnz):
+    """Scatter CSR pieces (each: its rows ascending, their entries in row
+    order) into the global arrays."""
+    cols = np.zeros(nnz, dtype=np.int32)
+    counts = np.zeros(nnz, dtype=np.uint32)
+    for rows, (c, v) in zip(pieces_rows, pieces):
+        lens = lens_global[rows]
+        tot = int(lens.sum())
+        if tot == 0:
+            continue
+        src_start = np.concatenate(([0], np.cumsum(lens)[:-1]))
+        dst = np.repeat(row_ptr[rows] - src_start, lens) + np.arange(tot)
+        cols[dst] = c[:tot]
+        counts[dst] = v[:tot]
+    return cols, counts
+
+
+def gather_csr(row_ptr, cols, counts, n: int, group=None, dst: int = 0):
+    """Bring every rank's CSR block (disjoint row sets, each over all n rows)
+    to rank `dst` (dst = -1: to every rank) with tensor collectives: one
+    all-reduce of the row lengths and owners, one all-gather of the padded
+    (col, count) pairs.  On an NCCL (= RCCL on ROCm) group the tensors travel
+    over xGMI from device memory; on gloo through the host.  Returns the
+    merged CSR (row_ptr, cols, counts) where requested, else None."""
+    import torch
     import torch.distributed as dist
 
     rank = dist.get_rank(group)
     world = dist.get_world_size(group)
-    payload = (np.asarray(row_ptr), np.asarray(cols), np.asarray(counts))
-    out: List = [None] * world if rank == 0 else None
-    dist.gather_object(payload, out, dst=0, group=group)
-    if rank != 0:
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else torch.device("cpu")
+    rp = np.asarray(row_ptr, dtype=np.int64)
+    lens = np.diff(rp)
+    nnz_local = int(rp[-1])
+    mine = np.zeros(n, dtype=np.int64)
+    mine[lens > 0] = rank + 1
+    meta = torch.from_numpy(np.concatenate([lens, mine, [nnz_local]])).to(dev)
+    # lengths and owners (disjoint rows: the sums are the values), and the
+    # largest block for the padding
+    sizes = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
+    dist.all_gather(sizes, meta[-1:].clone(), group=group)
+    meta = meta[:-1]
+    dist.all_reduce(meta, group=group)
+    meta = meta.cpu().numpy()
+    lens_g, owner = meta[:n], meta[n:]
+    nnz_k = [int(x.item()) for x in sizes]
+    cap = max(max(nnz_k), 1)
+    buf = np.zeros((2, cap), dtype=np.int64)
+    buf[0, :nnz_local] = np.asarray(cols, dtype=np.int64)[:nnz_local]
+    buf[1, :nnz_local] = np.asarray(counts, dtype=np.int64)[:nnz_local]
+    t = torch.from_numpy(buf).to(dev)
+    out = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(out, t, group=group)
+    if dst >= 0 and rank != dst:
         return None
-    return merge_csr(out, n)
+    g_rp = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(lens_g, out=g_rp[1:])
+    pieces = [(o[0].cpu().numpy(), o[1].cpu().numpy()) for o in out]
+    rows = [np.nonzero(owner == k + 1)[0] for k in range(world)]
+    c, v = _place(rows, pieces, lens_g, g_rp, int(g_rp[-1]))
+    return g_rp, c, v

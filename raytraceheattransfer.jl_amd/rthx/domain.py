@@ -328,13 +328,44 @@ class RayTracingDomain2D:
 
         self.wavelength_band_limits = None  # DomainStructs.jl:105 (set by the user for spectral runs)
         self.F_raw = None
-        self.F_smooth = None
+        self._F_smooth = None
+        self._F_smooth_handle = None  # device-resident F_smooth (SmoothHandle) not yet copied to the host
         self.rays_per_emitter = None
         self.last_trace_info: List[dict] = []
         self._flat: Optional[FlatDomain] = None
         self._device_domains: Dict[int, object] = {}
 
     # ------------------------------------------------------------------
+    @property
+    def F_smooth(self):
+        """exchangeRayTracing.jl:74.  When the smoothing ran on the device
+        from the traced counts, F_smooth stays there (the GERT solve reads it
+        in place) and is copied to the host on first access."""
+        h = self._F_smooth_handle
+        if h is not None:
+            self._F_smooth = h.host()
+            self._F_smooth_handle = None
+            self._F_smooth_device = (self._F_smooth, h)
+        return self._F_smooth
+
+    @F_smooth.setter
+    def F_smooth(self, value):
+        self._F_smooth = value
+        self._F_smooth_handle = None
+
+    def _set_F_smooth_device(self, handle) -> None:
+        old = getattr(self, "_F_smooth_device", None)
+        if old is not None and old[1] is not handle:
+            old[1].close()
+        self._F_smooth = None
+        self._F_smooth_handle = handle
+        self._F_smooth_device = (None, handle)
+
+    def F_smooth_device(self):
+        """The device-resident dense F_smooth handle, or None."""
+        dev = getattr(self, "_F_smooth_device", None)
+        return dev[1] if dev is not None and dev[1].dense else None
+
     @property
     def num_surfaces(self) -> int:
         return len(self.surface_mapping)
@@ -356,6 +387,9 @@ class RayTracingDomain2D:
     def invalidate(self) -> None:
         """Drop cached flat/device copies after mutating geometry or extinction."""
         self._flat = None
+        from .exchange import release_device_results
+
+        release_device_results(self)
         for h in self._device_domains.values():
             h.close()
         self._device_domains.clear()
@@ -379,8 +413,10 @@ class RayTracingDomain2D:
             F_raw = exchange_ray_tracing(self, int(rays_tot), trace_nudge, verbose, rec,
                                          seed=seed, device=device, faithful=faithful)
             if smooth:
-                self.F_smooth = smooth_exchange_factors(self, F_raw, max_iters=max_iters, k_dykstra=k_dykstra,
-                                                        verbose=verbose, device=device)
+                Fs = smooth_exchange_factors(self, F_raw, max_iters=max_iters, k_dykstra=k_dykstra,
+                                             verbose=verbose, device=device)
+                if Fs is not None:  # (None: F_smooth stays on the device until read)
+                    self.F_smooth = Fs
             return F_raw
         if method == "direct":
             from .direct import direct_ray_tracing

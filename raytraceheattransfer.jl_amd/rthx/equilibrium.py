@@ -124,7 +124,14 @@ def equilibrium_grey(dom, F, spectral_bin: int = 1, device: int = 0, verbose: bo
     Fm = F
     handle = None
     dev = getattr(dom, "_F_smooth_device", None)
-    if dev is not None and dev[0] is F and dev[1].dense:
+    if F is None:  # dom.F_smooth: read in place on the device when it lives there
+        if dom.F_smooth_device() is not None:
+            handle = dom.F_smooth_device()
+        else:
+            F = Fm = dom.F_smooth
+    if handle is not None:
+        pass
+    elif dev is not None and dev[0] is F and dev[1].dense:
         handle = dev[1]
     elif sp.issparse(F):
         Fm = F.tocsr()[:n, :n]
@@ -200,7 +207,7 @@ def solve_equilibrium(dom, F=None, device: int = 0, verbose: bool = False):
         raise NotImplementedError("spectral GERT solves (equilibriumSpectral2D!, ...Spectral3D!) are out of scope")
     if isinstance(dom, ViewFactorDomain3D):  # solveEquilibrium.jl:13-22
         return equilibrium_surfaces_grey_3d(dom, dom.F_smooth if F is None else F, device=device, verbose=verbose)
-    return equilibrium_grey(dom, dom.F_smooth if F is None else F, device=device, verbose=verbose)
+    return equilibrium_grey(dom, F, device=device, verbose=verbose)
 
 
 def equilibrium_surfaces_grey_3d(domain, F, spectral_bin: int = 1, device: int = 0, verbose: bool = False,

@@ -85,6 +85,23 @@ def counts_to_F(row_ptr, cols, counts, n: int, rays_per_emitter: int) -> sp.csr_
     return sp.csr_matrix((data, cols.astype(np.int64), row_ptr.astype(np.int64)), shape=(n, n))
 
 
+def _keep_device_result(dom, spectral_bin: int, res) -> None:
+    """Keep a traced bin's device result (its counts) for the smoothing."""
+    held = getattr(dom, "_trace_results", None)
+    if held is None:
+        held = dom._trace_results = {}
+    old = held.pop(spectral_bin, None)
+    if old is not None:
+        old.close()
+    held[spectral_bin] = res
+
+
+def release_device_results(dom) -> None:
+    for r in getattr(dom, "_trace_results", {}).values():
+        r.close()
+    dom._trace_results = {}
+
+
 def _default_backend():
     from ._lib import HipBackend
 
@@ -105,6 +122,26 @@ def compute_exchange_factors_bin(dom, rays_per_emitter: int, nudge: float, spect
     if rec is not None and rec.bin == spectral_bin:
         rec_ids = [i - 1 for i in rec.ids]
         rec_bin0 = rec.bin - 1
+    if hasattr(backend, "trace_F"):
+        # F_raw formed on the device (count / tallied, the exact quotient of
+        # :145 + row_normalize!); the counts stay there for the smoothing
+        F, info, rays, res = backend.trace_F(dom, spectral_bin - 1, rays_per_emitter, nudge, seed, device,
+                                             faithful, record_ids=rec_ids, record_bin0=rec_bin0)
+        _keep_device_result(dom, spectral_bin, res)
+        info = dict(info)
+        info["bin"] = spectral_bin
+        info["backend"] = getattr(backend, "name", type(backend).__name__)
+        dom.last_trace_info.append(info)
+        if verbose:
+            print(f"  bin {spectral_bin}: {info['rays_traced']} rays, nnz {info['nnz']}, "
+                  f"trace {info['trace_ms']:.3f} ms")
+            print(f"Maximum ray tracing ray loss per emitter: {info['lost_max_row']}/{rays_per_emitter}")
+        if rec is not None and rays is not None:
+            o, e, _g = rays
+            rec.origins.append(o)
+            rec.endpoints.append(e)
+            rec.emitters.append(_g + 1)
+        return F
     row_ptr, cols, counts, info, rays = backend.trace(
         dom, spectral_bin - 1, rays_per_emitter, nudge, seed, device, faithful,
         record_ids=rec_ids, record_bin0=rec_bin0)
@@ -131,6 +168,7 @@ def parallel_ray_tracing(dom, rays_total: int, nudge: float, verbose: bool, rec=
     rays_per_emitter = rays_total // num_emitters
     n_bins = dom.n_spectral_bins
     dom.last_trace_info = []
+    release_device_results(dom)
     kw = dict(seed=seed, device=device, faithful=faithful, backend=backend)
     if dom.spectral_mode == "spectral_variable":
         F_vec: List[Optional[sp.csr_matrix]] = [None] * n_bins

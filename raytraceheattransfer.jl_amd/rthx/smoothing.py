@@ -34,8 +34,17 @@ def get_w(dom, spectral_bin: int = 1) -> np.ndarray:
 class SmoothHandle:
     """A device-resident rthx_smooth_result (kept for rthx_solve_grey_smoothed)."""
 
-    def __init__(self, lib, h, device: int, dense: bool):
+    def __init__(self, lib, h, device: int, dense: bool, inf=None):
         self._lib, self.handle, self.device, self.dense = lib, h, device, dense
+        self._inf = inf
+
+    def host(self):
+        """Copy F_smooth to the host (dense ndarray or CSR matrix)."""
+        inf = self._inf
+        if inf is None:
+            inf = abi.SmoothInfo()
+            check(self._lib.rthx_smooth_get_info(self.handle, C.byref(inf)))
+        return _fetch(self._lib, self.handle, inf)
 
     def close(self) -> None:
         if getattr(self, "handle", None):
@@ -47,6 +56,55 @@ class SmoothHandle:
             self.close()
         except Exception:
             pass
+
+
+def _smooth_args(device, max_iters, k_dykstra, smooth_surfaces_only, renorm, verbose, input_dense):
+    a = abi.SmoothArgs()
+    a.device = device
+    a.max_iters = max_iters
+    a.k_dykstra = -1 if k_dykstra is None else int(k_dykstra)
+    a.smooth_surfaces_only = 1 if smooth_surfaces_only else 0
+    a.renorm = 1 if renorm else 0
+    a.verbose = 1 if verbose else 0
+    a.input_dense = 1 if input_dense else 0
+    return a
+
+
+def _fetch(lib, h, inf):
+    """Host copy of a smoothing result: dense ndarray or CSR matrix."""
+    m = inf.n
+    if inf.dense:
+        out = np.empty((m, m))
+        check(lib.rthx_smooth_copy_dense(h, abi.ptr(out, C.c_double)))
+        return out
+    orp = np.empty(m + 1, dtype=np.int64)
+    oci = np.empty(max(inf.nnz, 1), dtype=np.int32)
+    ov = np.empty(max(inf.nnz, 1))
+    check(lib.rthx_smooth_copy_csr(h, abi.ptr(orp, C.c_int64), abi.ptr(oci, C.c_int32), abi.ptr(ov, C.c_double)))
+    return sp.csr_matrix((ov[:inf.nnz], oci[:inf.nnz], orp), shape=(m, m))
+
+
+def smooth_F_device(result, n: int, w, num_surfaces: int, max_iters: int = 1000,
+                    smooth_surfaces_only: bool = False, k_dykstra: Optional[int] = None, verbose: bool = True,
+                    renorm: bool = True, device: int = 0, info: Optional[dict] = None) -> SmoothHandle:
+    """smooth_F of a traced bin whose counts are still on the device
+    (rthx_smooth_F_result): F_raw = count / tallied over the leading n x n
+    block.  Returns the device-resident SmoothHandle (``.host()`` copies it)."""
+    lib = load()
+    ww = np.ascontiguousarray(w, dtype=np.float64)
+    a = _smooth_args(device, max_iters, k_dykstra, smooth_surfaces_only, renorm, verbose, False)
+    h = C.c_void_p()
+    check(lib.rthx_smooth_F_result(result.handle, int(n), abi.ptr(ww, C.c_double), len(ww), int(num_surfaces),
+                                   C.byref(a), C.byref(h)))
+    inf = abi.SmoothInfo()
+    try:
+        check(lib.rthx_smooth_get_info(h, C.byref(inf)))
+    except Exception:
+        lib.rthx_smooth_destroy(h)
+        raise
+    if info is not None:
+        info.update(inf.as_dict())
+    return SmoothHandle(lib, h, device, bool(inf.dense), inf)
 
 
 def smooth_F(F_raw, w, num_surfaces: int, max_iters: int = 1000, smooth_surfaces_only: bool = False,
@@ -67,31 +125,14 @@ def smooth_F(F_raw, w, num_surfaces: int, max_iters: int = 1000, smooth_surfaces
     ci = np.ascontiguousarray(F.indices, dtype=np.int32)
     vv = np.ascontiguousarray(F.data, dtype=np.float64)
     ww = np.ascontiguousarray(w, dtype=np.float64)
-    a = abi.SmoothArgs()
-    a.device = device
-    a.max_iters = max_iters
-    a.k_dykstra = -1 if k_dykstra is None else int(k_dykstra)
-    a.smooth_surfaces_only = 1 if smooth_surfaces_only else 0
-    a.renorm = 1 if renorm else 0
-    a.verbose = 1 if verbose else 0
-    a.input_dense = 0 if sp.issparse(F_raw) else 1
+    a = _smooth_args(device, max_iters, k_dykstra, smooth_surfaces_only, renorm, verbose, not sp.issparse(F_raw))
     h = C.c_void_p()
     check(lib.rthx_smooth_F(abi.ptr(rp, C.c_int64), abi.ptr(ci, C.c_int32), abi.ptr(vv, C.c_double), n,
                             abi.ptr(ww, C.c_double), len(ww), int(num_surfaces), C.byref(a), C.byref(h)))
     try:
         inf = abi.SmoothInfo()
         check(lib.rthx_smooth_get_info(h, C.byref(inf)))
-        m = inf.n
-        if inf.dense:
-            out = np.empty((m, m))
-            check(lib.rthx_smooth_copy_dense(h, abi.ptr(out, C.c_double)))
-        else:
-            orp = np.empty(m + 1, dtype=np.int64)
-            oci = np.empty(max(inf.nnz, 1), dtype=np.int32)
-            ov = np.empty(max(inf.nnz, 1))
-            check(lib.rthx_smooth_copy_csr(h, abi.ptr(orp, C.c_int64), abi.ptr(oci, C.c_int32),
-                                           abi.ptr(ov, C.c_double)))
-            out = sp.csr_matrix((ov[:inf.nnz], oci[:inf.nnz], orp), shape=(m, m))
+        out = _fetch(lib, h, inf)
         if info is not None:
             info.update(inf.as_dict())
     except Exception:
@@ -113,14 +154,36 @@ def smooth_exchange_factors(dom, F_raw, max_iters: int = 1000, k_dykstra: Option
     ns = len(dom.surface_mapping)
     kw = dict(max_iters=max_iters, k_dykstra=k_dykstra, verbose=verbose,
               smooth_surfaces_only=dom.surfaces_only, device=device)
+    held = getattr(dom, "_trace_results", {})
+    res = held.get(1)
+    if (dom.spectral_mode != "spectral_variable" and res is not None and res.info()["n_devices"] == 1
+            and not isinstance(F_raw, list)):
+        # the traced counts are still on the device: smooth them there and
+        # keep F_smooth there for the solve; the host copy of F_smooth is made
+        # on first access (dom.F_smooth)
+        info = {}
+        handle = smooth_F_device(res, F_raw.shape[0], get_w(dom), ns, info=info, **kw)
+        dom._set_F_smooth_device(handle)
+        return None
     if dom.spectral_mode == "spectral_variable":
         out = [None] * dom.n_spectral_bins
         groups, _reps, nonuniform = group_uniform_bins(dom.uniform_across_bin)
+
+        def smooth_bin(b):
+            r = held.get(b)
+            if r is not None and r.info()["n_devices"] == 1:  # counts still on the device
+                h = smooth_F_device(r, F_raw[b - 1].shape[0], get_w(dom, b), ns, **kw)
+                try:
+                    return h.host()
+                finally:
+                    h.close()
+            return smooth_F(F_raw[b - 1], get_w(dom, b), ns, **kw)
+
         for b in nonuniform:
-            out[b - 1] = smooth_F(F_raw[b - 1], get_w(dom, b), ns, **kw)
+            out[b - 1] = smooth_bin(b)
         for idx_group in groups:
             rep = idx_group[0]
-            Fs = smooth_F(F_raw[rep - 1], get_w(dom, rep), ns, **kw)
+            Fs = smooth_bin(rep)
             for j in idx_group:
                 out[j - 1] = Fs
         return out

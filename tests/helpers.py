@@ -172,6 +172,18 @@ def reciprocity_weights(dom, bin0=0):
 # --------------------------------------------------------------------------
 # statistical / analytic checks
 # --------------------------------------------------------------------------
+def csr_rows_subset(row_ptr, cols, counts, n, rows):
+    """The CSR (row_ptr[n+1], cols, counts) restricted to `rows` (ascending):
+    every other row empty, as a strided shard of the same trace returns it."""
+    rows = np.asarray(rows, dtype=np.int64)
+    lens = np.zeros(n, dtype=np.int64)
+    lens[rows] = row_ptr[rows + 1] - row_ptr[rows]
+    rp = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(lens, out=rp[1:])
+    idx = np.concatenate([np.arange(row_ptr[r], row_ptr[r + 1]) for r in rows]) if len(rows) else np.zeros(0, np.int64)
+    return rp, cols[idx], counts[idx]
+
+
 def counts_matrix(row_ptr, cols, counts, n):
     return sp.csr_matrix((counts.astype(np.float64), cols.astype(np.int64), row_ptr.astype(np.int64)), shape=(n, n))
 

@@ -1,0 +1,273 @@
+"""The C-ABI boundary beyond one plain trace, on the GPU: the multi-device
+trace (rthx_multi_trace_exchange), F_raw formed on the device
+(rthx_result_copy_F), DMA into page-locked caller memory, the look-back's
+fallback to the staging path, and trace -> smooth -> solve without F_raw
+leaving the device.
+
+Counts are compared exactly (every row is a pure function of (seed, bin,
+emitter, ray)); F values to 1e-15 relative (one division each); smoothing
+results to 1e-12 (iterative fp64 with different reduction orders).
+"""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+import helpers as H
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _args(hip, flat, R, seed=1, bin0=0, begin=0, end=None, stride=1, rec=None, flags=0):
+    return hip.make_args(bin0, R, H.NUDGE, seed, begin, flat.n_emitters if end is None else end, stride,
+                         flags=flags, record_ids=rec)
+
+
+def _trace(hip, dd, args, pinned=None):
+    res = hip.DeviceResult()
+    try:
+        res.trace(dd, args)
+        info = res.info()
+        rp, cols, cnt = res.csr(pinned)
+        out = (rp.copy(), cols.copy(), cnt.copy(), info)
+    finally:
+        res.close()
+    return out
+
+
+@pytest.mark.parametrize("case", ["square", "greenhouse", "wedges"])
+@pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0]])
+def test_multi_device_equals_one_device(hip, case, devices):
+    """Rows split over several device slots (contiguous blocks on the
+    single-polygon square, interleaved rows on the multi-polygon greenhouse
+    and wedges) give the one-device counts bit for bit.  On a one-GPU box the
+    slots are concurrent streams of device 0."""
+    dom = {"square": lambda: H.square_domain(31), "greenhouse": lambda: H.greenhouse_domain(12, 21, 3, 8),
+           "wedges": lambda: H.wedge_domain(16, 4)}[case]()
+    flat = dom.flat()
+    for bin0 in ((0, 5) if case == "greenhouse" else (0,)):
+        args, _k = _args(hip, flat, 3000, seed=21, bin0=bin0)
+        dd = hip.DeviceDomain(flat, 0)
+        one = _trace(hip, dd, args)
+        dd.close()
+        md = hip.MultiDeviceDomain(flat, devices)
+        multi = _trace(hip, md, args)
+        md.close()
+        assert multi[3]["n_devices"] == len(devices)
+        for a, b in zip(one[:3], multi[:3]):
+            assert np.array_equal(a, b)
+        for k in ("nnz", "lost_total", "lost_max_row", "rays_traced", "rows_traced"):
+            assert one[3][k] == multi[3][k], k
+
+
+def test_multi_device_shard_and_recorder(hip):
+    """A strided row subset and recorded emitters through the multi-device
+    trace equal the oracle (recorded rays in emitter order)."""
+    dom = H.wedge_domain(8, 3)
+    flat = dom.flat()
+    ids = [0, 5, 17, flat.n_emitters - 1]
+    args, _k = _args(hip, flat, 700, seed=7, rec=ids)
+    md = hip.MultiDeviceDomain(flat, [0, 0, 0])
+    res = hip.DeviceResult()
+    try:
+        res.trace(md, args)
+        rp, cols, cnt = res.csr()
+        o, e, g = res.rays()
+    finally:
+        res.close()
+        md.close()
+    orp, ocols, ocnt, oinfo, (oo, oe, og) = oracle.trace_exchange(flat, args, 16)
+    assert np.array_equal(rp, orp) and np.array_equal(cols, ocols) and np.array_equal(cnt, ocnt)
+    order = np.lexsort((np.arange(len(og)), og))
+    assert np.array_equal(g, og[order])
+    assert np.allclose(o, oo[order], rtol=0, atol=1e-12)
+    args, _k = _args(hip, flat, 900, seed=8, begin=2, stride=5)
+    md = hip.MultiDeviceDomain(flat, [0, 0])
+    got = _trace(hip, md, args)
+    md.close()
+    ref = oracle.trace_exchange(flat, args, 16)
+    assert np.array_equal(got[0], ref[0]) and np.array_equal(got[1], ref[1]) and np.array_equal(got[2], ref[2])
+
+
+def test_recorder_on_single_polygon_domain(hip):
+    """Recording on a one-polygon domain runs the staging kernels (never the
+    direct-CSR look-back): counts and rays equal the oracle."""
+    dom = H.square_domain(9)
+    flat = dom.flat()
+    ids = [0, 3, flat.n_emitters - 1]
+    args, _k = _args(hip, flat, 1500, seed=4, rec=ids)
+    dd = hip.DeviceDomain(flat, 0)
+    res = hip.DeviceResult()
+    try:
+        res.trace(dd, args)
+        rp, cols, cnt = res.csr()
+        o, e, g = res.rays()
+    finally:
+        res.close()
+        dd.close()
+    orp, ocols, ocnt, oinfo, (oo, oe, og) = oracle.trace_exchange(flat, args, 16)
+    assert np.array_equal(rp, orp) and np.array_equal(cols, ocols) and np.array_equal(cnt, ocnt)
+    order = np.lexsort((np.arange(len(og)), og))
+    assert np.array_equal(g, og[order])
+    assert np.allclose(e, oe[order], rtol=0, atol=1e-9)
+
+
+def test_copy_F_is_normalised_counts(hip):
+    """rthx_result_copy_F: F_raw = count / tallied per row (the reference's
+    count / R followed by row_normalize!), same pattern as the counts; rows
+    sum to 1; also through the multi-device result and into pinned arrays."""
+    dom = H.wedge_domain(8, 3)  # open spokes: some rays lost, so tallied < R in places
+    flat = dom.flat()
+    args, _k = _args(hip, flat, 2500, seed=9)
+    for kind in ("one", "multi"):
+        dd = hip.DeviceDomain(flat, 0) if kind == "one" else hip.MultiDeviceDomain(flat, [0, 0])
+        pin = hip.PinnedArrays()
+        res = hip.DeviceResult()
+        try:
+            res.trace(dd, args)
+            rp, cols, cnt = [x.copy() for x in res.csr()]
+            frp, fcols, vals = [x.copy() for x in res.F(pin)]
+        finally:
+            res.close()
+            dd.close()
+            pin.close()
+        assert np.array_equal(rp, frp) and np.array_equal(cols, fcols)
+        tallied = np.add.reduceat(cnt.astype(np.int64), rp[:-1][np.diff(rp) > 0])
+        want = cnt / np.repeat(tallied, np.diff(rp)[np.diff(rp) > 0])
+        np.testing.assert_allclose(vals, want, rtol=1e-15, atol=0)
+        F = sp.csr_matrix((vals, fcols, frp), shape=(flat.n_emitters,) * 2)
+        rs = np.asarray(F.sum(axis=1)).ravel()
+        assert np.allclose(rs[np.diff(rp) > 0], 1.0, rtol=0, atol=1e-12)
+
+
+def test_pinned_copy_equals_pageable_copy(hip):
+    dom = H.square_domain(41)
+    flat = dom.flat()
+    args, _k = _args(hip, flat, 5000, seed=3)
+    dd = hip.DeviceDomain(flat, 0)
+    pin = hip.PinnedArrays()
+    try:
+        a = _trace(hip, dd, args)
+        b = _trace(hip, dd, args, pinned=pin)
+    finally:
+        dd.close()
+        pin.close()
+    for x, y in zip(a[:3], b[:3]):
+        assert np.array_equal(x, y)
+
+
+def test_lookback_stall_falls_back_to_staging(hip, monkeypatch):
+    """RTHX_LB_WAIT_US=0: a row gives up its look-back wait as soon as a
+    predecessor has not yet published; the call then re-traces the launch on
+    the staging path.  The returned CSR must equal the staging path's (and
+    the oracle's), never a misplaced direct write."""
+    dom = H.square_domain(31)
+    flat = dom.flat()
+    args, _k = _args(hip, flat, 3000, seed=5)
+    monkeypatch.setenv("RTHX_NO_LOOKBACK", "1")
+    dd = hip.DeviceDomain(flat, 0)
+    ref = _trace(hip, dd, args)
+    monkeypatch.delenv("RTHX_NO_LOOKBACK")
+    assert ref[3]["lookback_fallbacks"] == 0
+    monkeypatch.setenv("RTHX_LB_WAIT_US", "0")
+    fallbacks = 0
+    for _ in range(3):
+        got = _trace(hip, dd, args)
+        fallbacks += got[3]["lookback_fallbacks"]
+        for x, y in zip(ref[:3], got[:3]):
+            assert np.array_equal(x, y)
+        assert got[3]["nnz"] == ref[3]["nnz"] and got[3]["lost_max_row"] == ref[3]["lost_max_row"]
+    assert fallbacks >= 1, "a zero wait bound never stalled"
+    monkeypatch.delenv("RTHX_LB_WAIT_US")
+    got = _trace(hip, dd, args)  # default bound: the direct write, no fallback
+    dd.close()
+    assert got[3]["lookback_fallbacks"] == 0 and got[3]["pack_ms"] < 0.05
+    assert np.array_equal(got[1], ref[1]) and np.array_equal(got[2], ref[2])
+    small = oracle.trace_exchange(flat, args, 16)
+    assert np.array_equal(ref[2], small[2])
+
+
+@pytest.mark.parametrize("case", ["grey11", "transparent", "scatter"])
+def test_smooth_from_device_result_equals_host_csr_smoothing(hip, case):
+    """rthx_smooth_F_result (counts never leave the device) equals
+    rthx_smooth_F on the host CSR of the same F_raw, to 1e-12: dense OP+AP
+    (grey 11x11), the surfaces-only block (kappa = 0, n = Ns), and sparse AP."""
+    from rthx.smoothing import get_w, smooth_F, smooth_F_device
+
+    dom = {"grey11": lambda: H.square_domain(11), "transparent": lambda: H.square_domain(6, kappa=0.0),
+           "scatter": lambda: H.square_domain(25, sigma_s=5.0)}[case]()
+    flat = dom.flat()
+    R = {"grey11": 6000, "transparent": 4000, "scatter": 150}[case]
+    args, _k = _args(hip, flat, R, seed=2)
+    dd = hip.DeviceDomain(flat, 0)
+    res = hip.DeviceResult()
+    try:
+        res.trace(dd, args)
+        rp, cols, vals = res.F()
+        n = dom.num_surfaces if dom.surfaces_only else flat.n_emitters
+        F = sp.csr_matrix((vals, cols, rp), shape=(flat.n_emitters,) * 2)[:n, :n].tocsr()
+        w = get_w(dom)
+        kw = dict(smooth_surfaces_only=dom.surfaces_only, verbose=False)
+        i_host, i_dev = {}, {}
+        A = smooth_F(F, w, dom.num_surfaces, info=i_host, **kw)
+        h = smooth_F_device(res, n, w, dom.num_surfaces, info=i_dev, **kw)
+        B = h.host()
+        h.close()
+    finally:
+        res.close()
+        dd.close()
+    assert i_host["dense"] == i_dev["dense"] and i_host["k_dykstra"] == i_dev["k_dykstra"]
+    assert abs(i_host["ap_iters"] - i_dev["ap_iters"]) <= 2
+    assert abs(i_host["chi"] - i_dev["chi"]) <= 1e-12
+    if case == "scatter":
+        assert not i_dev["dense"]
+    A = A.toarray() if sp.issparse(A) else A
+    B = B.toarray() if sp.issparse(B) else B
+    assert np.max(np.abs(A - B)) <= 1e-12
+
+
+def test_mesh_keeps_F_on_device_until_read(hip):
+    """mesh(): trace -> smoothing of the device counts -> GERT solve on the
+    device-resident F_smooth; F_smooth crosses to the host only when read,
+    and then equals the host-CSR smoothing of the returned F_raw."""
+    from rthx.equilibrium import equilibrium_grey
+    from rthx.smoothing import get_w, smooth_F
+
+    dom = H.square_domain(11)
+    F_raw = dom(1_000_000, seed=11, verbose=False)
+    assert dom._F_smooth_handle is not None and dom._F_smooth is None
+    T, j, Abs, r = equilibrium_grey(dom, None)
+    assert dom._F_smooth_handle is not None  # the solve read F_smooth in place
+    assert abs(dom.energy_error) < 1e-4
+    Fs = dom.F_smooth
+    assert dom._F_smooth_handle is None and isinstance(Fs, np.ndarray)
+    ref = smooth_F(F_raw, get_w(dom), dom.num_surfaces, verbose=False)
+    assert np.max(np.abs(Fs - ref)) <= 1e-12
+    T2, *_ = equilibrium_grey(dom, dom.F_smooth)  # the host copy is still recognised as device-resident
+    np.testing.assert_allclose(T2, T, rtol=1e-12)
+
+
+def _bench_line(argv, timeout=240):
+    import json
+    import subprocess
+    import sys
+
+    out = subprocess.run([sys.executable, H.os.path.join(H.ROOT, "bench.py")] + argv, capture_output=True, text=True,
+                         timeout=timeout, cwd=H.ROOT)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("mode", ["ranks", "threads"])
+def test_bench_two_gpus_as_a_plain_command(hip, mode):
+    """`python bench.py --gpus 2` started as a plain process spawns its two
+    ranks itself (torch.distributed.run, before any GPU call); `--mode
+    threads` drives two device slots from one process.  On a one-GPU box both
+    share device 0; the line is well-formed with n_gpus 2 and 2e7 rays per
+    GPU slot."""
+    d = _bench_line(["--gpus", "2", "--steps", "3", "--warmup", "1", "--prewarm-s", "0", "--no-cpu",
+                     "--rays-per-gpu", "20000000", "--mode", mode])
+    assert d["n_gpus"] == 2 and d["value"] > 0
+    assert d["config"]["rays_per_step"] == (40_000_000 // 10605) * 10605
