@@ -78,14 +78,18 @@ def philox(ctr, key):
     return list(o)
 
 
-DRAW_NAMES = ("R1", "R2", "path", "sel", "th", "ph", "l1", "l2")
+DRAW_NAMES = ("a0", "a1", "a2", "a3", "pw", "sw")
 
 
 def ray_draws(seed, bin0, g, r) -> dict:
-    """The eight uniforms of ray (g, r) (layout: rthx_oracle.c ray_draws)."""
+    """The six 32-bit uniforms of ray (g, r) of a volume quad emitter
+    (layout: rthx_oracle.c ray_words): a0..a3 (position, position, theta,
+    phi; a surface ray uses them as position, Lambert l1, l2, free path), pw
+    (volume free path, shared block of rays 4q..4q+3), sw (triangle
+    selection)."""
     out = (C.c_double * 8)()
     load().oracle_ray_draws(seed, bin0, g, r, out)
-    return dict(zip(DRAW_NAMES, list(out)))
+    return dict(zip(DRAW_NAMES, list(out)[:6]))
 
 
 def trace_ray(flat, args, g, r):

@@ -79,47 +79,70 @@ static inline double u52(uint32_t hi, uint32_t lo) {
 /* Uniform in [0, 1) with 32 random bits (exact in double). */
 static inline double u32(uint32_t w) { return (double)w * 0x1.0p-32; }
 
-/* The random draws of ray (g, r) in bin b: two Philox blocks, counters
- * (r, g, 0, b) -> a[0..3] and (r, g, 1, b) -> c[0..3], key (seed lo, seed hi).
- *   R1   = u52(a0, a1)  surface position / volume sqrt-weight
- *   R2   = u52(a2, a3)  volume second barycentric draw
- *   path = u52(c0, c1)  free path (-ln u)
- *   sel  = u32(c2)      quad triangle selection
- *   th   = u32(c3)      volume cos(theta) draw
- *   ph   = u32(a1[11:0] << 20 | a3[11:0] << 8 | c1[11:4])  volume phi draw
- *   l1   = u32(a2), l2 = u32(a3)   surface Lambert draws (rounded to Float32)
- * Draws that feed positions and free paths keep 52 bits like Julia's rand();
- * angle and selection draws use 32 bits (then rounded or compared). */
+/* The random words of one 2D emission (the device's RayWords,
+ * csrc/rthx_device.h):
+ *   surface emitter: pos = u32(a0), Lambert draws l1 = u32(a1), l2 = u32(a2)
+ *                    (rounded to Float32 as lambertSample2D.jl:2-5), free
+ *                    path u32(a3)
+ *   volume emitter:  u1 = u32(a0), u2 = u32(a1), theta draw u32(a2), phi
+ *                    draw u32(a3), free path u32(pw), quad triangle
+ *                    selection u32(sw)
+ * 32 random bits per draw.  Exchange ray (g, r) in bin b: a = Philox(r, g,
+ * 0, b), pw = word r & 3 of Philox(r >> 2, g, 1, b) (one block for four
+ * consecutive rays), sw = word 0 of Philox(r, g, 2, b), drawn only by quads
+ * that are not axis-aligned rectangles (and by every quad in faithful
+ * sampling). */
 typedef struct {
-  double R1, R2, path, sel, th, ph, l1, l2;
-} draws_t;
+  uint32_t a[4];
+  uint32_t pw, sw;
+} words_t;
 
-/* Draws from the counter pair (w0, w1, blk, w3), (w0, w1, blk + 1, w3). */
-static void draws_at(uint64_t seed, uint32_t w0, uint32_t w1, uint32_t blk, uint32_t w3, draws_t* d) {
+static void block_words(uint64_t seed, uint32_t w0, uint32_t w1, uint32_t blk, uint32_t w3, uint32_t out[4]) {
   uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
-  uint32_t ca[4] = {w0, w1, blk, w3}, cc[4] = {w0, w1, blk + 1u, w3};
+  uint32_t ctr[4] = {w0, w1, blk, w3};
+  oracle_philox4x32_10(ctr, key, out);
+}
+
+static void ray_words(uint64_t seed, uint32_t bin, uint32_t g, uint32_t r, int volume, int need_sel, words_t* w) {
+  block_words(seed, r, g, 0u, bin, w->a);
+  w->pw = w->sw = 0u;
+  if (volume) {
+    uint32_t b[4];
+    block_words(seed, r >> 2, g, 1u, bin, b);
+    w->pw = b[r & 3u];
+    if (need_sel) {
+      uint32_t c[4];
+      block_words(seed, r, g, 2u, bin, c);
+      w->sw = c[0];
+    }
+  }
+}
+
+/* Two-block draws of the 3D tracer (the device's RayDraws): counters
+ * (w0, w1, blk, w3) -> a and (w0, w1, blk + 1, w3) -> c;
+ *   R1 = u52(a0, a1), R2 = u52(a2, a3), path = u52(c0, c1), sel = u32(c2). */
+typedef struct {
+  double R1, R2, path, sel;
+} draws3_t;
+
+static void draws3_at(uint64_t seed, uint32_t w0, uint32_t w1, uint32_t blk, uint32_t w3, draws3_t* d) {
   uint32_t a[4], c[4];
-  oracle_philox4x32_10(ca, key, a);
-  oracle_philox4x32_10(cc, key, c);
+  block_words(seed, w0, w1, blk, w3, a);
+  block_words(seed, w0, w1, blk + 1u, w3, c);
   d->R1 = u52(a[0], a[1]);
   d->R2 = u52(a[2], a[3]);
   d->path = u52(c[0], c[1]);
   d->sel = u32(c[2]);
-  d->th = u32(c[3]);
-  d->ph = u32(((a[1] & 0xFFFu) << 20) | ((a[3] & 0xFFFu) << 8) | ((c[1] & 0xFFFu) >> 4));
-  d->l1 = u32(a[2]);
-  d->l2 = u32(a[3]);
 }
 
-static void ray_draws(uint64_t seed, uint32_t bin, uint32_t g, uint32_t r, draws_t* d) {
-  draws_at(seed, r, g, 0u, bin, d);
-}
-
+/* The words as doubles (tests): the eight draws u32(a0..a3), u32(pw), u32(sw). */
 ORACLE_API void oracle_ray_draws(uint64_t seed, uint32_t bin, uint32_t g, uint32_t r, double out[8]) {
-  draws_t d;
-  ray_draws(seed, bin, g, r, &d);
-  out[0] = d.R1; out[1] = d.R2; out[2] = d.path; out[3] = d.sel;
-  out[4] = d.th; out[5] = d.ph; out[6] = d.l1; out[7] = d.l2;
+  words_t w;
+  ray_words(seed, bin, g, r, 1, 1, &w);
+  for (int i = 0; i < 4; ++i) out[i] = u32(w.a[i]);
+  out[4] = u32(w.pw);
+  out[5] = u32(w.sw);
+  out[6] = out[7] = 0.0;
 }
 
 /* ------------------------------------------------------------------------ */
@@ -251,13 +274,13 @@ static void lambert_dir(double tx, double ty, double l1, double l2, int faithful
  * draws of lambertSample2D.  The direction is left un-normalised (its length
  * is the in-plane projection of a 3D unit vector). */
 static void emit_surface(const rthx_domain_desc* d, int f, int w, double eta, int faithful,
-                         const draws_t* rd, double* p, double* dir) {
+                         const words_t* rw, double* p, double* dir) {
   const double* xy = d->fine_xy + 8 * (size_t)f;
   int n = d->fine_nv[f];
   int w2 = (w + 1) % n;
   double p1x = xy[2 * w], p1y = xy[2 * w + 1];
   double p2x = xy[2 * w2], p2y = xy[2 * w2 + 1];
-  double R = rd->R1;
+  double R = u32(rw->a[0]);
   double px = p1x + (p2x - p1x) * R;
   double py = p1y + (p2y - p1y) * R;
   const double* m = d->fine_mid + 2 * (size_t)f;
@@ -267,24 +290,38 @@ static void emit_surface(const rthx_domain_desc* d, int f, int w, double eta, in
   /* xVecLocal = normalize(p2 - p1) */
   double ex = p2x - p1x, ey = p2y - p1y;
   double len = sqrt(ex * ex + ey * ey);
-  lambert_dir(ex / len, ey / len, rd->l1, rd->l2, faithful, dir);
+  lambert_dir(ex / len, ey / len, u32(rw->a[1]), u32(rw->a[2]), faithful, dir);
   p[0] = px;
   p[1] = py;
+}
+
+/* Axis-aligned rectangle in canonical order (v0 the min corner, CCW): the
+ * cells meshQuad makes of rectangles (meshQuad.jl:139-179). */
+static int is_rect(const rthx_domain_desc* d, int f) {
+  const double* v = d->fine_xy + 8 * (size_t)f;
+  return d->fine_nv[f] == 4 && v[0] < v[2] && v[1] < v[5] && v[2] == v[4] && v[6] == v[0] && v[3] == v[1] &&
+         v[7] == v[5];
 }
 
 /* emitVolumeRay2D.jl:1-33: uniform point (quad = two triangles ABC / CDA
  * chosen by area, triangle formula (1-sqrt u1)A + sqrt u1 (1-u2) B +
  * sqrt u1 u2 C), nudged toward the midpoint, isotropic 3D direction
- * projected onto the plane: (sin(theta) cos(phi), cos(theta)). */
-static void emit_volume(const rthx_domain_desc* d, int f, double eta, int faithful, const draws_t* rd,
+ * projected onto the plane: (sin(theta) cos(phi), cos(theta)).  An
+ * axis-aligned rectangle takes its uniform point directly, (x0 + u1 (x1-x0),
+ * y0 + u2 (y1-y0)) -- the same distribution as the two triangles -- except
+ * in faithful sampling, which keeps the reference's construction. */
+static void emit_volume(const rthx_domain_desc* d, int f, double eta, int faithful, const words_t* rw,
                         double* p, double* dir) {
   const double* v = d->fine_xy + 8 * (size_t)f;
   int n = d->fine_nv[f];
   double px, py;
-  if (n == 4) {
+  double R1 = u32(rw->a[0]), R2 = u32(rw->a[1]);
+  if (!faithful && is_rect(d, f)) {
+    px = v[0] + (v[2] - v[0]) * R1;
+    py = v[1] + (v[5] - v[1]) * R2;
+  } else if (n == 4) {
     double Ax = v[0], Ay = v[1], Bx = v[2], By = v[3], Cx = v[4], Cy = v[5], Dx = v[6], Dy = v[7];
-    double R1 = rd->R1, R2 = rd->R2;
-    double sel = rd->sel;
+    double sel = u32(rw->sw);
     double a1 = 0.5 * (Ax * (By - Cy) + Bx * (Cy - Ay) + Cx * (Ay - By)) / d->fine_volume[f];
     double s1 = sqrt(R1);
     double wa = 1.0 - s1, wb = s1 * (1.0 - R2), wc = s1 * R2;
@@ -297,7 +334,6 @@ static void emit_volume(const rthx_domain_desc* d, int f, double eta, int faithf
     }
   } else {
     double Ax = v[0], Ay = v[1], Bx = v[2], By = v[3], Cx = v[4], Cy = v[5];
-    double R1 = rd->R1, R2 = rd->R2;
     double s1 = sqrt(R1);
     double wa = 1.0 - s1, wb = s1 * (1.0 - R2), wc = s1 * R2;
     px = wa * Ax + wb * Bx + wc * Cx;
@@ -307,7 +343,7 @@ static void emit_volume(const rthx_domain_desc* d, int f, double eta, int faithf
   px = px + (m[0] - px) * eta;
   py = py + (m[1] - py) * eta;
 
-  double u4 = rd->th, u5 = rd->ph;
+  double u4 = u32(rw->a[2]), u5 = u32(rw->a[3]);
   double st, ct;
   if (faithful) {
     double theta = acos(1.0 - 2.0 * u4);
@@ -435,25 +471,30 @@ static hit_t trace_one(const dom_t* D, const rthx_trace_args* a, int64_t g, int6
                        double* origin) {
   const rthx_domain_desc* d = D->d;
   int faithful = (a->flags & RTHX_FLAG_FAITHFUL_SAMPLING) != 0;
-  draws_t rd;
-  ray_draws(a->seed, (uint32_t)a->bin, (uint32_t)g, (uint32_t)r, &rd);
+  words_t rw;
   double p[2], dir[2];
   int f;
+  double u_path;
   if (g < d->n_surfaces) {
     f = D->surf_face[g];
-    emit_surface(d, f, D->surf_wall[g], a->nudge, faithful, &rd, p, dir);
+    ray_words(a->seed, (uint32_t)a->bin, (uint32_t)g, (uint32_t)r, 0, 0, &rw);
+    emit_surface(d, f, D->surf_wall[g], a->nudge, faithful, &rw, p, dir);
+    u_path = u32(rw.a[3]);
   } else {
     f = (int)(g - d->n_surfaces);
-    emit_volume(d, f, a->nudge, faithful, &rd, p, dir);
+    const int need_sel = d->fine_nv[f] == 4 && (faithful || !is_rect(d, f));
+    ray_words(a->seed, (uint32_t)a->bin, (uint32_t)g, (uint32_t)r, 1, need_sel, &rw);
+    emit_volume(d, f, a->nudge, faithful, &rw, p, dir);
+    u_path = u32(rw.pw);
   }
   origin[0] = p[0];
   origin[1] = p[1];
   int c = D->coarse_of[f];
   if (d->uniform_beta[a->bin] > -0.1) {
     double beta = d->beta[(size_t)a->bin * d->n_fine + 0];
-    return trace_uniform(D, p[0], p[1], dir[0], dir[1], beta, a->nudge, c, rd.path);
+    return trace_uniform(D, p[0], p[1], dir[0], dir[1], beta, a->nudge, c, u_path);
   }
-  return trace_variable(D, p[0], p[1], dir[0], dir[1], a->bin, a->nudge, c, rd.path);
+  return trace_variable(D, p[0], p[1], dir[0], dir[1], a->bin, a->nudge, c, u_path);
 }
 
 /* ------------------------------------------------------------------------ */
@@ -827,7 +868,7 @@ ORACLE_API int oracle_trace_ray(const rthx_domain_desc* d, const rthx_trace_args
 /* (DirectTracing2D/directRayTracing.jl:19-152) and traceSingleRay          */
 /* (traceSingleRay.jl:1-83), restated per ray with the Philox blocks the    */
 /* HIP kernel draws (csrc/rthx_direct_kernels.hip header):                  */
-/*   blk 0: emitter (alias table); blk 1, 2: emission draws (draws_at);     */
+/*   blk 0: emitter (alias table); blk 1, 2: emission words (words_t);      */
 /*   blk 2i+2: interaction of iteration i (choice, direction);              */
 /*   blk 2i+1 (i >= 2): roulette + free path of iteration i;                */
 /*   blk 3: roulette of iteration 1 when roulette_after == 0.               */
@@ -956,20 +997,30 @@ static void direct_ray(dworker_t* W, uint64_t ray) {
   uint32_t col = (uint32_t)(((uint64_t)w[0] * (uint64_t)n) >> 32);
   uint64_t at = W->alias[col];
   int64_t g = (w[1] < (uint32_t)at) ? (int64_t)col : (int64_t)(at >> 32);
-  draws_t rd;
-  draws_at(a->seed, r0, r1, 1u, tag, &rd);
+  /* emission words: a = block 1, free path / triangle selection = words 0,
+   * 1 of block 2 (the device's RayWords) */
+  words_t rw;
+  block_words(a->seed, r0, r1, 1u, tag, rw.a);
+  {
+    uint32_t c2[4];
+    block_words(a->seed, r0, r1, 2u, tag, c2);
+    rw.pw = c2[0];
+    rw.sw = c2[1];
+  }
   double p[2], dir[2];
   int f;
+  double u_path;
   if (g < ns) { /* :72-78 */
     f = D->surf_face[g];
-    emit_surface(d, f, D->surf_wall[g], a->nudge, faithful, &rd, p, dir);
+    emit_surface(d, f, D->surf_wall[g], a->nudge, faithful, &rw, p, dir);
+    u_path = u32(rw.a[3]);
   } else {       /* :79-87 */
     f = (int)(g - ns);
-    emit_volume(d, f, a->nudge, faithful, &rd, p, dir);
+    emit_volume(d, f, a->nudge, faithful, &rw, p, dir);
+    u_path = u32(rw.pw);
   }
   if (!W->reemit[g]) W->counts[g]++; /* temp_value >= 0.0 -> emitted count */
   int c = D->coarse_of[f];
-  double u_path = rd.path;
   size_t np = 0;  /* buffered (kind, element) entries */
   int64_t nev = 0; /* path events (a re-emission buffers two entries) */
   int it = 1;
@@ -1366,8 +1417,8 @@ static void* t3_worker(void* arg) {
     int64_t g = W->begin + k * W->stride;
     const t3_poly* E = W->polys + g;
     for (int64_t r = 0; r < W->R; ++r) {
-      draws_t rd;
-      draws_at(W->seed, (uint32_t)r, (uint32_t)g, 0u, 0x40000000u, &rd);
+      draws3_t rd;
+      draws3_at(W->seed, (uint32_t)r, (uint32_t)g, 0u, 0x40000000u, &rd);
       uint32_t cc[4] = {(uint32_t)r, (uint32_t)g, 1u, 0x40000000u}, c[4];
       oracle_philox4x32_10(cc, key, c);
       double s1 = sqrt(rd.R1);

@@ -68,6 +68,11 @@ void fill_tables(double* t) {
 
 namespace {
 
+bool env_flag(const char* name) {
+  const char* e = getenv(name);
+  return e && e[0] == '1';
+}
+
 template <class T>
 int upload(rthx_domain* d, const T* src, size_t n, const T** dst, const char* what) {
   if (n == 0) {
@@ -382,6 +387,80 @@ RTHX_EXPORT int rthx_domain_create(const rthx_domain_desc* desc, int32_t device,
     }
     D.cl = L;
   }
+  // Lattice of a single axis-aligned coarse rectangle (rthx_device.h
+  // LatticeLayout; LAT kernels): the fine cells must be exactly the nx x ny
+  // boxes between the sorted distinct x and y coordinates, and only boundary
+  // fine walls may be solid.
+  if (d->single_convex && d->axis_rect && !env_flag("RTHX_NO_LAT")) {
+    std::vector<double> xs, ys;
+    for (size_t f = 0; f < nf; ++f) {
+      xs.push_back(fpoly[f].x[0]);
+      xs.push_back(fpoly[f].x[1]);
+      ys.push_back(fpoly[f].y[0]);
+      ys.push_back(fpoly[f].y[2]);
+    }
+    std::sort(xs.begin(), xs.end());
+    xs.erase(std::unique(xs.begin(), xs.end()), xs.end());
+    std::sort(ys.begin(), ys.end());
+    ys.erase(std::unique(ys.begin(), ys.end()), ys.end());
+    const int64_t lnx = (int64_t)xs.size() - 1, lny = (int64_t)ys.size() - 1;
+    bool ok = lnx >= 1 && lny >= 1 && lnx * lny == (int64_t)nf && lnx <= 4096 && lny <= 4096;
+    std::vector<int32_t> map(ok ? (size_t)(lnx * lny) : 0, -1);
+    bool identity = ok;
+    for (size_t f = 0; f < nf && ok; ++f) {
+      const auto ix = std::lower_bound(xs.begin(), xs.end(), fpoly[f].x[0]) - xs.begin();
+      const auto iy = std::lower_bound(ys.begin(), ys.end(), fpoly[f].y[0]) - ys.begin();
+      ok = ix < lnx && iy < lny && xs[ix + 1] == fpoly[f].x[1] && ys[iy + 1] == fpoly[f].y[2] &&
+           map[iy * lnx + ix] < 0;
+      if (!ok) break;
+      map[iy * lnx + ix] = (int32_t)f;
+      identity = identity && (int64_t)f == iy * lnx + ix;
+      // interior fine walls must be open (boundary walls: w 0 bottom, 1 right, 2 top, 3 left)
+      const bool bnd[4] = {iy == 0, ix == lnx - 1, iy == lny - 1, ix == 0};
+      for (int w = 0; w < 4 && ok; ++w) ok = bnd[w] || s.fine_surface[4 * f + w] < 0;
+    }
+    if (ok) {
+      rthx::LatticeLayout L{};
+      L.nx = (int32_t)lnx;
+      L.ny = (int32_t)lny;
+      L.identity = identity ? 1 : 0;
+      auto a16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
+      size_t off = a16(8 * xs.size());
+      L.off_ys = (int32_t)off;
+      off = a16(off + 8 * ys.size());
+      L.off_bot = (int32_t)off;
+      off = a16(off + 4 * lnx);
+      L.off_right = (int32_t)off;
+      off = a16(off + 4 * lny);
+      L.off_top = (int32_t)off;
+      off = a16(off + 4 * lnx);
+      L.off_left = (int32_t)off;
+      off = a16(off + 4 * lny);
+      L.bytes = (int32_t)off;
+      L.inv_x = (double)lnx / (xs[lnx] - xs[0]);
+      L.inv_y = (double)lny / (ys[lny] - ys[0]);
+      std::vector<uint4> blob(off / 16);
+      char* b = reinterpret_cast<char*>(blob.data());
+      std::memset(b, 0, off);
+      std::memcpy(b, xs.data(), 8 * xs.size());
+      std::memcpy(b + L.off_ys, ys.data(), 8 * ys.size());
+      int32_t* bot = reinterpret_cast<int32_t*>(b + L.off_bot);
+      int32_t* right = reinterpret_cast<int32_t*>(b + L.off_right);
+      int32_t* top = reinterpret_cast<int32_t*>(b + L.off_top);
+      int32_t* left = reinterpret_cast<int32_t*>(b + L.off_left);
+      for (int64_t i = 0; i < lnx; ++i) {
+        bot[i] = s.fine_surface[4 * (size_t)map[i] + 0];
+        top[i] = s.fine_surface[4 * (size_t)map[(lny - 1) * lnx + i] + 2];
+      }
+      for (int64_t j = 0; j < lny; ++j) {
+        right[j] = s.fine_surface[4 * (size_t)map[j * lnx + lnx - 1] + 1];
+        left[j] = s.fine_surface[4 * (size_t)map[j * lnx] + 3];
+      }
+      UP(blob.data(), blob.size(), D.lat_blob);
+      if (!identity) UP(map.data(), map.size(), D.lat_map);
+      D.lat = L;
+    }
+  }
 #undef UP
   {
     int r3 = upload(d, &d->D, 1, &d->d_dom, "domain record");
@@ -452,11 +531,6 @@ uint64_t lookback_wait_ticks() {
   return kLookbackWaitTicks;
 }
 
-bool env_flag(const char* name) {
-  const char* e = getenv(name);
-  return e && e[0] == '1';
-}
-
 // Launch geometry of one trace call (rows, split, LDS histogram layout).
 struct TracePlan {
   int64_t N = 0, R = 0, end = 0, n_rows = 0, split = 1, row_cap = 1;
@@ -492,7 +566,7 @@ int plan_trace(const rthx_domain* dom, const rthx_trace_args* a, TracePlan& p) {
   const int64_t words = p.pack16 ? (N + 1) / 2 : N;
   p.lds_bytes = (size_t)words * 4;
   if (p.lds_bytes + rthx::kStaticLdsBytes > rthx::kMaxLdsBytes)
-    return fail(RTHX_ERANGE, "N too large for the LDS row histogram of this build (N <= 76800)");
+    return fail(RTHX_ERANGE, "N too large for the LDS row histogram of this build");
   // multi-polygon domains: the coarse mesh goes behind the histogram in LDS
   // when it fits (CLDS kernels, rthx_device.h segment_cl)
   p.cl_offset = (p.lds_bytes + 15) & ~(size_t)15;
@@ -500,6 +574,12 @@ int plan_trace(const rthx_domain* dom, const rthx_trace_args* a, TracePlan& p) {
            p.cl_offset + (size_t)dom->D.cl.bytes + rthx::kStaticLdsBytes <= rthx::kMaxLdsBytes &&
            !env_flag("RTHX_NO_CLDS");
   if (p.clds) p.lds_bytes = p.cl_offset + (size_t)dom->D.cl.bytes;
+  // single axis-aligned rectangles: the lattice behind the histogram (LAT kernels)
+  if (dom->single_convex && dom->D.lat.bytes > 0 && !p.recording &&
+      p.cl_offset + (size_t)dom->D.lat.bytes + rthx::kStaticLdsBytes <= rthx::kMaxLdsBytes) {
+    p.clds = true;
+    p.lds_bytes = p.cl_offset + (size_t)dom->D.lat.bytes;
+  }
   p.row_cap = std::max<int64_t>(1, std::min<int64_t>(N, R));
   p.uniform = dom->uniform_beta[a->bin] > -0.1;  // traceRay.jl:4
   return RTHX_OK;

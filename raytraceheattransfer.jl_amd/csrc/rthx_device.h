@@ -22,6 +22,10 @@
 #ifndef RTHX_ABLATE
 #define RTHX_ABLATE 0
 #endif
+// 1: keep the Philox key schedule out of loop-invariant SGPRs (A/B knob)
+#ifndef RTHX_PHILOX_OPAQUE_KEY
+#define RTHX_PHILOX_OPAQUE_KEY 1
+#endif
 
 namespace rthx {
 
@@ -74,6 +78,22 @@ struct CoarseLayout {
   int32_t off_fgrid, off_bbox, off_first, off_solid, off_cells, off_beta;
 };
 
+// Lattice form of a single axis-aligned coarse rectangle whose fine cells
+// are the nx x ny rectangles [xs[i], xs[i+1]) x [ys[j], ys[j+1]) (meshQuad
+// on a rectangle, meshQuad.jl:139-179).  LAT kernels stage the blob in LDS:
+// xs[nx+1], ys[ny+1] (f64), then the surface index of the boundary walls
+// bottom[nx], right[ny], top[nx], left[ny] (i32, -1 where not solid; every
+// interior fine wall is open).  Fine cell (i, j) is polygon j nx + i when
+// `identity`, else lat_map[j nx + i].  bytes == 0: not a lattice.
+struct LatticeLayout {
+  int32_t bytes;             // blob bytes (multiple of 16)
+  int32_t nx, ny;
+  int32_t identity;
+  int32_t off_ys, off_bot, off_right, off_top, off_left;
+  int32_t reserved;
+  double inv_x, inv_y;       // nx / (xs[nx] - xs[0]), ny / (ys[ny] - ys[0]): first guess of the cell
+};
+
 struct DevDomain {
   int32_t n_coarse, n_fine, n_surfaces, n_bins;
   // coarse polygons
@@ -108,6 +128,10 @@ struct DevDomain {
   const uint4 RTHX_GLOBAL* c_blob;     // [cl.blob_bytes / 16]
   const double RTHX_GLOBAL* c_beta;    // [n_bins][n_coarse]
   CoarseLayout cl;
+  // lattice of a single axis-aligned coarse rectangle (LatticeLayout)
+  const uint4 RTHX_GLOBAL* lat_blob;   // [lat.bytes / 16]
+  const int32_t RTHX_GLOBAL* lat_map;  // [nx ny] when !identity
+  LatticeLayout lat;
 };
 
 struct TraceParams {
@@ -130,6 +154,11 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
 }
 
 __device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
+#if RTHX_PHILOX_OPAQUE_KEY
+  // Opaque key: the 20 round keys are formed in each block (scalar adds)
+  // instead of being hoisted into 20 SGPRs held across the whole ray loop.
+  __asm__ volatile("" : "+s"(k0), "+s"(k1));
+#endif
 #pragma unroll
   for (int i = 0; i < ((RTHX_ABLATE & 1) ? 1 : 10); ++i) {
     // one 32x32->64 multiply per product (v_mad_u64_u32) instead of mul_lo + mul_hi
@@ -153,20 +182,12 @@ __device__ __forceinline__ double u52(uint32_t hi, uint32_t lo) {
 
 __device__ __forceinline__ double u32(uint32_t w) { return (double)w * 0x1.0p-32; }
 
-// The random draws of ray (g, r) in bin b: two Philox blocks, counters
-// (r, g, 0, b) -> a[0..3] and (r, g, 1, b) -> c[0..3] (same layout as the CPU
-// restatement, oracle/rthx_oracle.c ray_draws):
-//   R1 = u52(a0,a1)  R2 = u52(a2,a3)  path = u52(c0,c1)
-//   sel = u32(c2)    th = u32(c3)     ph = u32(a1[11:0]<<20 | a3[11:0]<<8 | c1[11:4])
-//   l1 = u32(a2)     l2 = u32(a3)     (surface Lambert draws, rounded to Float32)
-// Positions and free paths keep 52 bits like Julia's rand(); angles and the
-// triangle selection use 32 bits.  Two blocks per ray (not three).
+// Two-block draws (the 3D tracer, rthx_trace3d_kernels.hip): counters
+// (w0, w1, blk, w3) -> a and (w0, w1, blk + 1, w3) -> c;
+//   R1 = u52(a0,a1)  R2 = u52(a2,a3)  path = u52(c0,c1)  sel = u32(c2)
+//   th = u32(c3)     ph = u32(a1[11:0]<<20 | a3[11:0]<<8 | c1[11:4])
 struct RayDraws {
   uint32_t a[4], c[4];
-  __device__ __forceinline__ RayDraws(uint32_t r, uint32_t g, uint32_t bin, uint32_t k0, uint32_t k1)
-      : RayDraws(r, g, 0u, bin, k0, k1) {}
-  // Generic counters (w0, w1, blk, w3) -> a and (w0, w1, blk + 1, w3) -> c
-  // (the direct method's emission, rthx_direct_kernels.hip).
   __device__ __forceinline__ RayDraws(uint32_t w0, uint32_t w1, uint32_t blk, uint32_t w3, uint32_t k0, uint32_t k1) {
     a[0] = w0; a[1] = w1; a[2] = blk; a[3] = w3;
     c[0] = w0; c[1] = w1; c[2] = blk + 1u; c[3] = w3;
@@ -182,9 +203,31 @@ struct RayDraws {
     return ((a[1] & 0xFFFu) << 20) | ((a[3] & 0xFFFu) << 8) | ((c[1] & 0xFFFu) >> 4);
   }
   __device__ __forceinline__ double ph() const { return u32(ph_bits()); }
-  __device__ __forceinline__ double l1() const { return u32(a[2]); }
-  __device__ __forceinline__ double l2() const { return u32(a[3]); }
 };
+
+// The random words of one 2D emission (exchange tracer and the direct
+// method's emission; the CPU restatement's emit_words has the same layout):
+//   surface emitter: pos = u32(a0), Lambert draws l1 = u32(a1), l2 = u32(a2)
+//                    (rounded to Float32, lambertSample2D.jl:2-5), free path
+//                    u32(a3)
+//   volume emitter:  u1 = u32(a0), u2 = u32(a1), theta draw u32(a2), phi
+//                    word a3, free path u32(pw), triangle selection u32(sw)
+//                    (quads that are not axis-aligned rectangles, and
+//                    faithful sampling)
+// 32 random bits per draw.  The exchange tracer's words of ray (g, r) in bin
+// b: a = Philox(r, g, 0, b); pw = word r & 3 of Philox(r >> 2, g, 1, b) --
+// one block serves four consecutive rays, so a volume ray costs 1.25 Philox
+// blocks (2.25 with sw = word 0 of Philox(r, g, 2, b)) and a surface ray one.
+struct RayWords {
+  uint32_t a[4];
+  uint32_t pw, sw;
+};
+
+__device__ __forceinline__ void philox_words(uint32_t w0, uint32_t w1, uint32_t blk, uint32_t w3, uint32_t k0,
+                                             uint32_t k1, uint32_t out[4]) {
+  out[0] = w0; out[1] = w1; out[2] = blk; out[3] = w3;
+  philox4x32_10(out, k0, k1);
+}
 
 #define RTHX_TWO_PI 6.283185307179586
 
@@ -441,6 +484,8 @@ struct Emitter {
   int nv;
   int coarse;
   bool surface;
+  bool rect;          // axis-aligned rectangle, v0 the min corner (volume)
+  bool need_sel;      // quad emission draws the triangle selection (sw)
 };
 
 __device__ __forceinline__ Emitter load_emitter(const DevDomain& D, int64_t g) {
@@ -486,6 +531,10 @@ __device__ __forceinline__ Emitter load_emitter(const DevDomain& D, int64_t g) {
   e.tx = tx;
   e.ty = ty;
   e.surface = surface;
+  const bool rect = !surface && nv == 4 && v[0] < v[2] && v[1] < v[5] && v[2] == v[4] && v[6] == v[0] &&
+                    v[3] == v[1] && v[7] == v[5];
+  e.rect = rect;
+  e.need_sel = !surface && nv == 4 && !rect;
   return e;
 }
 
@@ -511,14 +560,14 @@ __device__ __forceinline__ void lambert_dir(double tx, double ty, double l1, dou
 }
 
 template <bool FAITHFUL>
-__device__ __forceinline__ void emit_surface(const Emitter& e, double eta, const RayDraws& rd, double& px,
+__device__ __forceinline__ void emit_surface(const Emitter& e, double eta, const RayWords& rw, double& px,
                                              double& py, double& dx, double& dy) {
-  double R = rd.R1();
+  double R = u32(rw.a[0]);
   px = e.v[0] + __dmul_rn(e.v[2] - e.v[0], R);
   py = e.v[1] + __dmul_rn(e.v[3] - e.v[1], R);
   px = px + __dmul_rn(e.mx - px, eta);
   py = py + __dmul_rn(e.my - py, eta);
-  lambert_dir<FAITHFUL>(e.tx, e.ty, rd.l1(), rd.l2(), dx, dy);
+  lambert_dir<FAITHFUL>(e.tx, e.ty, u32(rw.a[1]), u32(rw.a[2]), dx, dy);
 }
 
 // isotropicScatter2D.jl:1-4: theta = acos(2u - 1), phi = 2 pi v, direction
@@ -546,35 +595,44 @@ __device__ __forceinline__ void iso_dir(uint32_t w_th, uint32_t w_ph, const doub
 // emitVolumeRay2D.jl:1-33: uniform point (quad = triangles ABC / CDA chosen
 // by area), nudged toward the midpoint, isotropic 3D direction projected on
 // the plane (sin(theta) cos(phi), cos(theta)).  cos_tab: the kCosTable
-// (cos, sin) pairs in LDS (non-faithful sampling).
+// (cos, sin) pairs in LDS (non-faithful sampling).  An axis-aligned
+// rectangle (the cells of meshQuad on rectangles) takes its uniform point
+// directly, (x0 + u1 (x1 - x0), y0 + u2 (y1 - y0)): the same distribution as
+// the reference's two triangles without the square root and the selection
+// draw (faithful sampling keeps the reference's construction).
 template <bool FAITHFUL>
-__device__ __forceinline__ void emit_volume(const Emitter& e, double eta, const RayDraws& rd, const double* cos_tab,
+__device__ __forceinline__ void emit_volume(const Emitter& e, double eta, const RayWords& rw, const double* cos_tab,
                                             double& px, double& py, double& dx, double& dy) {
-  double R1 = rd.R1(), R2 = rd.R2();
-  double s1 = FAITHFUL ? sqrt(R1) : sqrt_unit(R1);
-  double wa = 1.0 - s1, wb = __dmul_rn(s1, 1.0 - R2), wc = __dmul_rn(s1, R2);
-  double Ax = e.v[0], Ay = e.v[1], Bx = e.v[2], By = e.v[3], Cx = e.v[4], Cy = e.v[5];
-  if (e.nv == 4) {
-    double sel = rd.sel();
-    if (!(sel < e.tri_frac)) {  // (C, D, A)
-      Ax = e.v[4]; Ay = e.v[5]; Bx = e.v[6]; By = e.v[7]; Cx = e.v[0]; Cy = e.v[1];
+  const double R1 = u32(rw.a[0]), R2 = u32(rw.a[1]);
+  if (!FAITHFUL && e.rect) {
+    px = e.v[0] + __dmul_rn(e.v[2] - e.v[0], R1);
+    py = e.v[1] + __dmul_rn(e.v[5] - e.v[1], R2);
+  } else {
+    double s1 = FAITHFUL ? sqrt(R1) : sqrt_unit(R1);
+    double wa = 1.0 - s1, wb = __dmul_rn(s1, 1.0 - R2), wc = __dmul_rn(s1, R2);
+    double Ax = e.v[0], Ay = e.v[1], Bx = e.v[2], By = e.v[3], Cx = e.v[4], Cy = e.v[5];
+    if (e.nv == 4) {
+      double sel = u32(rw.sw);
+      if (!(sel < e.tri_frac)) {  // (C, D, A)
+        Ax = e.v[4]; Ay = e.v[5]; Bx = e.v[6]; By = e.v[7]; Cx = e.v[0]; Cy = e.v[1];
+      }
     }
+    px = __dmul_rn(wa, Ax) + __dmul_rn(wb, Bx) + __dmul_rn(wc, Cx);
+    py = __dmul_rn(wa, Ay) + __dmul_rn(wb, By) + __dmul_rn(wc, Cy);
   }
-  px = __dmul_rn(wa, Ax) + __dmul_rn(wb, Bx) + __dmul_rn(wc, Cx);
-  py = __dmul_rn(wa, Ay) + __dmul_rn(wb, By) + __dmul_rn(wc, Cy);
   px = px + __dmul_rn(e.mx - px, eta);
   py = py + __dmul_rn(e.my - py, eta);
-  double u4 = rd.th();
+  double u4 = u32(rw.a[2]);
   double st, ct, cphi;
   if (FAITHFUL) {
     double theta = acos(1.0 - 2.0 * u4);
     st = sin(theta);
     ct = cos(theta);
-    cphi = cos(RTHX_TWO_PI * rd.ph());
+    cphi = cos(RTHX_TWO_PI * u32(rw.a[3]));
   } else {
     ct = 1.0 - 2.0 * u4;                       // cos(acos(x)) = x
     st = 2.0 * sqrt_unit(__dmul_rn(u4, 1.0 - u4));  // sin(acos(x)) = sqrt((1-x)(1+x))
-    cphi = (RTHX_ABLATE & 4) ? (1.0 - 2.0 * rd.ph()) : cos_2pi_u32(rd.ph_bits(), cos_tab);
+    cphi = (RTHX_ABLATE & 4) ? (1.0 - 2.0 * u32(rw.a[3])) : cos_2pi_u32(rw.a[3], cos_tab);
   }
   dx = __dmul_rn(st, cphi);
   dy = ct;
@@ -653,6 +711,105 @@ __device__ __forceinline__ int segment(const DevDomain& D, const TraceParams& P,
   if (UNIFORM) S -= u; else acc += tau_b;
   c = locate_coarse(D, px, py);
   return c < 0 ? -1 : kRayContinue;
+}
+
+// ---------------------------------------------------------------------------
+// LAT kernels: one axis-aligned coarse rectangle meshed as a lattice
+// (LatticeLayout, staged in LDS).  findFace2D's answer for an axis-aligned
+// rectangle is the half-open box test x0 <= px < x1, y0 <= py < y1
+// (pointInPolygonFast2D, findFace2D.jl:84-99, on its two vertical edges; the
+// horizontal ones never cross), and the lattice's half-open boxes partition
+// [xs[0], xs[nx]) x [ys[0], ys[ny]), so the cell that contains p is the
+// reference's first hit in any candidate order -- found here by a guess
+// from the uniform spacing, corrected against the exact boundaries.
+// ---------------------------------------------------------------------------
+#ifndef RTHX_LDS
+#define RTHX_LDS __attribute__((address_space(3)))
+#endif
+
+// Index i with b[i] <= x < b[i+1], 0 <= i < n, or -1.  The guess from the
+// uniform spacing is exact except for x within rounding of a boundary; the
+// walk that corrects it runs only then (for every lane of a wave only when
+// one of them needs it).
+__device__ __forceinline__ int lattice_index(const double RTHX_LDS* b, int n, double inv, double x) {
+  double fi = floor(__dmul_rn(x - b[0], inv));
+  fi = fmin(fmax(fi, 0.0), (double)(n - 1));
+  int i = (int)fi;
+  if (b[i] <= x && x < b[i + 1]) return i;
+  while (i > 0 && x < b[i]) --i;
+  while (i < n - 1 && !(x < b[i + 1])) ++i;
+  return (b[i] <= x && x < b[i + 1]) ? i : -1;
+}
+
+struct LatticeLds {
+  const double RTHX_LDS* xs;
+  const double RTHX_LDS* ys;
+  const int32_t RTHX_LDS* bot;
+  const int32_t RTHX_LDS* right;
+  const int32_t RTHX_LDS* top;
+  const int32_t RTHX_LDS* left;
+};
+
+__device__ __forceinline__ LatticeLds lattice_lds_view(const char RTHX_LDS* base, const LatticeLayout& L) {
+  LatticeLds v;
+  v.xs = (const double RTHX_LDS*)base;
+  v.ys = (const double RTHX_LDS*)(base + L.off_ys);
+  v.bot = (const int32_t RTHX_LDS*)(base + L.off_bot);
+  v.right = (const int32_t RTHX_LDS*)(base + L.off_right);
+  v.top = (const int32_t RTHX_LDS*)(base + L.off_top);
+  v.left = (const int32_t RTHX_LDS*)(base + L.off_left);
+  return v;
+}
+
+// segment<UNIFORM, SINGLE = true, AXIS = true> with the lattice locate: the
+// gas / wall end point's cell, and for a wall hit the fine wall of that cell
+// (dist_to_rect on its lattice bounds: the same candidates and ties as on its
+// DevPoly) and the wall's surface index from the boundary arrays.
+template <bool UNIFORM>
+__device__ __forceinline__ int segment_lat(const DevDomain& D, const TraceParams& P, const SingleCoarse& sc,
+                                           const LatticeLds& L, const LatticeLayout& G, double& px, double& py,
+                                           double dx, double dy, double& S, double& acc) {
+  const double eta = P.eta;
+  int k;
+  const double u = dist_to_rect(px, py, dx, dy, sc.poly, k);
+  bool gas;
+  double beta = 0.0, tau_b = 0.0;
+  if (UNIFORM) {
+    gas = S < u;
+  } else {
+    const int i0 = lattice_index(L.xs, G.nx, G.inv_x, px), j0 = lattice_index(L.ys, G.ny, G.inv_y, py);
+    if (i0 < 0 || j0 < 0) return -1;
+    const int f0 = G.identity ? j0 * G.nx + i0 : D.lat_map[j0 * G.nx + i0];
+    beta = D.beta[(size_t)P.bin * D.n_fine + f0];
+    tau_b = __dmul_rn(beta, u);
+    gas = acc + tau_b >= S;
+  }
+  const bool wall = !gas && ((sc.solid >> k) & 1u);
+  if (!(gas || wall)) return -1;  // an open wall of the only polygon leads outside
+  const double t = gas ? (UNIFORM ? S : (S - acc) / beta) - eta : u - eta;
+  px = px + __dmul_rn(t, dx);
+  py = py + __dmul_rn(t, dy);
+  const int i = lattice_index(L.xs, G.nx, G.inv_x, px), j = lattice_index(L.ys, G.ny, G.inv_y, py);
+  if (i < 0 || j < 0) return -1;
+  if (gas) return D.n_surfaces + (G.identity ? j * G.nx + i : D.lat_map[j * G.nx + i]);
+  const double x0 = L.xs[i], x1 = L.xs[i + 1], y0 = L.ys[j], y1 = L.ys[j + 1];
+  const double num[4] = {py - y0, x1 - px, y1 - py, px - x0};
+  const double den[4] = {-dy, dx, dy, -dx};
+  double bn = 1.0, bd = 0.0;
+  int w = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const double an = fabs(num[q]), ad = fabs(den[q]);
+    const bool better = (ad >= 1e-10) && (__dmul_rn(num[q], den[q]) > 0.0) && (__dmul_rn(an, bd) < __dmul_rn(bn, ad));
+    bn = better ? an : bn;
+    bd = better ? ad : bd;
+    w = better ? q : w;
+  }
+  // (w = 0 when no wall qualifies, as dist_to_rect / distToSurface2D's findmin)
+  return w == 0 ? (j == 0 ? L.bot[i] : -1)
+       : w == 1 ? (i == G.nx - 1 ? L.right[j] : -1)
+       : w == 2 ? (j == G.ny - 1 ? L.top[i] : -1)
+                : (i == 0 ? L.left[j] : -1);
 }
 
 // ---------------------------------------------------------------------------
@@ -758,29 +915,69 @@ __device__ __forceinline__ double free_path(const TraceParams& P, const double* 
   return FAITHFUL ? -log(u) : neg_log_tab(u, tabs + kLogTableOffset);
 }
 
+// The words of ray (g, r) of emitter e (RayWords); pw: the free-path word
+// when the caller already holds the ray's word of block (r >> 2, g, 1, b)
+// (SINGLE kernels amortise that block over four consecutive rays).
+__device__ __forceinline__ RayWords ray_words(const TraceParams& P, const Emitter& e, uint32_t g, uint32_t r,
+                                              bool have_pw, uint32_t pw, bool faithful) {
+  RayWords rw;
+  philox_words(r, g, 0u, (uint32_t)P.bin, P.key0, P.key1, rw.a);
+  rw.pw = 0u;
+  rw.sw = 0u;
+  if (!e.surface) {
+    if (have_pw) {
+      rw.pw = pw;
+    } else {
+      uint32_t b[4];
+      philox_words(r >> 2, g, 1u, (uint32_t)P.bin, P.key0, P.key1, b);
+      const uint32_t j = r & 3u;
+      rw.pw = j == 0 ? b[0] : j == 1 ? b[1] : j == 2 ? b[2] : b[3];
+    }
+    if (e.need_sel || (faithful && e.nv == 4)) {
+      uint32_t c[4];
+      philox_words(r, g, 2u, (uint32_t)P.bin, P.key0, P.key1, c);
+      rw.sw = c[0];
+    }
+  }
+  return rw;
+}
+
 // Emission of ray (g, r): point, direction and free path / tau*.
+template <bool UNIFORM, bool FAITHFUL>
+__device__ __forceinline__ void start_ray_w(const TraceParams& P, const Emitter& e, const double* tabs,
+                                            const RayWords& rw, double& px, double& py, double& dx, double& dy,
+                                            double& S) {
+  if (e.surface)
+    emit_surface<FAITHFUL>(e, P.eta, rw, px, py, dx, dy);
+  else
+    emit_volume<FAITHFUL>(e, P.eta, rw, tabs, px, py, dx, dy);
+  // (opaque copies: a select between the two struct fields becomes a
+  // dynamically indexed scratch load)
+  uint32_t w_surf = rw.a[3], w_vol = rw.pw;
+  __asm__ volatile("" : "+v"(w_surf), "+v"(w_vol));
+  S = free_path<UNIFORM, FAITHFUL>(P, tabs, u32(e.surface ? w_surf : w_vol));
+}
+
 template <bool UNIFORM, bool FAITHFUL>
 __device__ __forceinline__ void start_ray(const TraceParams& P, const Emitter& e, const double* tabs, uint32_t g,
                                           uint32_t r, double& px, double& py, double& dx, double& dy, double& S) {
-  const RayDraws rd(r, g, (uint32_t)P.bin, P.key0, P.key1);
-  if (e.surface)
-    emit_surface<FAITHFUL>(e, P.eta, rd, px, py, dx, dy);
-  else
-    emit_volume<FAITHFUL>(e, P.eta, rd, tabs, px, py, dx, dy);
-  S = free_path<UNIFORM, FAITHFUL>(P, tabs, rd.path());
+  const RayWords rw = ray_words(P, e, g, r, false, 0u, FAITHFUL);
+  start_ray_w<UNIFORM, FAITHFUL>(P, e, tabs, rw, px, py, dx, dy, S);
 }
 
 // One ray (g, r) of emitter e traced to the end (SINGLE domains: one
-// segment).  Returns absorber (-1 = lost); (ox, oy) emission point, (px, py)
-// end point.
-template <bool UNIFORM, bool FAITHFUL, bool SINGLE, bool AXIS>
-__device__ __forceinline__ int trace_one(const DevDomain& D, const TraceParams& P, const Emitter& e,
-                                         const SingleCoarse& sc, const double* tabs, uint32_t g, uint32_t r,
-                                         double& ox, double& oy, double& px, double& py) {
+// segment), from its random words.  Returns absorber (-1 = lost); (ox, oy)
+// emission point, (px, py) end point.
+template <bool UNIFORM, bool FAITHFUL, bool SINGLE, bool AXIS, bool LAT = false>
+__device__ __forceinline__ int trace_one_w(const DevDomain& D, const TraceParams& P, const Emitter& e,
+                                           const SingleCoarse& sc, const double* tabs, const RayWords& rw,
+                                           double& ox, double& oy, double& px, double& py,
+                                           const char RTHX_LDS* lat_base = nullptr) {
   double dx, dy, S, acc = 0.0;
-  start_ray<UNIFORM, FAITHFUL>(P, e, tabs, g, r, px, py, dx, dy, S);
+  start_ray_w<UNIFORM, FAITHFUL>(P, e, tabs, rw, px, py, dx, dy, S);
   ox = px;
   oy = py;
+  if (LAT) return segment_lat<UNIFORM>(D, P, sc, lattice_lds_view(lat_base, D.lat), D.lat, px, py, dx, dy, S, acc);
   int c = e.coarse;
   for (int it = 0; it < (SINGLE ? 1 : 10000); ++it) {  // traceRay.jl:27 (10,000 steps, then lost)
     const int a = segment<UNIFORM, SINGLE, AXIS>(D, P, sc, c, px, py, dx, dy, S, acc);

@@ -12,7 +12,7 @@
 // Random numbers: ray r (64-bit) owns the Philox blocks with counter
 // (r lo, r hi, blk, bin | kDirectTag):
 //   blk 0            emitter draw: column = mulhi(w0, n), accept w1 < threshold (alias table)
-//   blk 1, 2         emission (the exchange tracer's RayDraws layout: point, direction, first free path)
+//   blk 1, 2         emission (RayWords: block 1 = a, words 0, 1 of block 2 = free path, triangle selection)
 //   blk 2i+2, i >= 1 interaction of iteration i: choice u52(w0,w1), direction draws w2, w3
 //   blk 2i+1, i >= 2 start of iteration i: roulette u52(w0,w1), free path u52(w2,w3)
 //   blk 3            roulette of iteration 1 (only when roulette_after == 0)
@@ -144,12 +144,17 @@ __global__ __launch_bounds__(FAITHFUL ? kDirectThreads : kDirectMaxThreads) RTHX
           const int g = (w[1] < (uint32_t)at) ? (int)col : (int)(at >> 32);
           const double* tab = (const double*)lds_opaque(&s_tab[0]);
           const Emitter e = load_emitter(D, g);
-          const RayDraws rd(r0, r1, 1u, tag, k0, k1);
-          if (e.surface)
-            emit_surface<FAITHFUL>(e, eta, rd, px, py, dx, dy);
-          else
-            emit_volume<FAITHFUL>(e, eta, rd, tab, px, py, dx, dy);
-          S = free_path<UNIFORM, FAITHFUL>(Q.P, tab, rd.path());
+          // emission words (RayWords): a = block 1; free path and triangle
+          // selection of volume emitters = words 0 and 1 of block 2
+          RayWords rw;
+          philox_block(rw.a, r0, r1, 1u, tag, k0, k1);
+          {
+            uint32_t c2[4];
+            philox_block(c2, r0, r1, 2u, tag, k0, k1);
+            rw.pw = c2[0];
+            rw.sw = c2[1];
+          }
+          start_ray_w<UNIFORM, FAITHFUL>(Q.P, e, tab, rw, px, py, dx, dy, S);
           acc = 0.0;
           c = e.coarse;
           seg = 0;

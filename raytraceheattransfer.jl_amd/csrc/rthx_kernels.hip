@@ -14,6 +14,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "rthx_device.h"
 #include "rthx_kernels.h"
 #include "rthx_wave.h"
@@ -26,10 +28,14 @@ namespace rthx {
 #ifndef RTHX_TRACE_WAVES_PER_EU
 #define RTHX_TRACE_WAVES_PER_EU 5
 #endif
+#ifndef RTHX_LAT_WAVES_PER_EU
+#define RTHX_LAT_WAVES_PER_EU 6  // LAT kernels (lattice locate): no cell records in registers
+#endif
 #ifndef RTHX_REFILL
 #define RTHX_REFILL 16  // ray regeneration batch of the multi-polygon kernels (lanes)
 #endif
-#define RTHX_TRACE_WAVES __attribute__((amdgpu_waves_per_eu(SINGLE ? RTHX_TRACE_WAVES_PER_EU : RTHX_TRACE_WAVES_PER_EU - 1)))
+#define RTHX_TRACE_WAVES \
+  __attribute__((amdgpu_waves_per_eu(SINGLE ? (CLDS ? RTHX_LAT_WAVES_PER_EU : RTHX_TRACE_WAVES_PER_EU) : RTHX_TRACE_WAVES_PER_EU - 1)))
 
 // Decoupled look-back (Merrill & Garland 2016) over the rows of one launch:
 // row `slot` publishes its nnz as an aggregate (flag 1), walks back over its
@@ -58,11 +64,14 @@ __device__ __forceinline__ uint64_t lookback_offset(unsigned long long* status, 
   unsigned long long excl = 0;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   bool gave_up = false;
+  uint32_t polls = 0;
   for (int64_t j = slot - 1; !gave_up; --j) {
     unsigned long long v;
     while (((v = __hip_atomic_load(&status[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 62) == 0) {
       __builtin_amdgcn_s_sleep(1);
-      if (__builtin_amdgcn_s_memrealtime() - t0 > wait_ticks) {
+      // the clock is read every 16th poll (a scalar-memory round trip each);
+      // a zero bound (tests) gives up at the first unpublished predecessor
+      if ((wait_ticks == 0 || (++polls & 15u) == 0) && __builtin_amdgcn_s_memrealtime() - t0 >= wait_ticks) {
         atomicAdd(stalled, 1ull);
         gave_up = true;
         v = kInc;  // end the walk (the host re-traces the launch)
@@ -167,7 +176,10 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
   // CLDS: the coarse mesh behind the histogram (T.cl_offset bytes in), and
   // this bin's coarse betas
   char RTHX_LDS* cl_base = (char RTHX_LDS*)hist + T.cl_offset;
-  if (CLDS) {
+  if (CLDS && SINGLE) {  // LAT: the lattice of the single coarse rectangle (LatticeLayout)
+    uint4* dst = (uint4*)cl_base;
+    for (int i = tid; i < D.lat.bytes / 16; i += nthr) dst[i] = D.lat_blob[i];
+  } else if (CLDS) {
     uint4* dst = (uint4*)cl_base;  // generic view (HIP vector assignment); stores stay ds_write
     for (int i = tid; i < D.cl.blob_bytes / 16; i += nthr) dst[i] = D.c_blob[i];
     double RTHX_LDS* cb = (double RTHX_LDS*)(cl_base + D.cl.off_beta);
@@ -214,18 +226,52 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
     }
   };
   if (SINGLE) {
-    // One segment per ray: every lane traces rays r = tid, tid + nthr, ...
-    for (uint32_t r = (uint32_t)r_begin + tid; r < (uint32_t)r_end; r += (uint32_t)nthr) {
+    // One segment per ray.  Rays go to lanes in groups of four consecutive
+    // indices: a lane traces rays 4q .. 4q+3 of groups q = q0 + tid,
+    // q0 + tid + nthr, ..., and one free-path Philox block (q, g, 1, bin)
+    // serves all four (RayWords).  The groups left over after the last full
+    // round over the lanes are traced one ray per lane, each drawing its
+    // own free-path block, so that no lane traces more than one ray beyond
+    // the row's average.
+    auto one_ray = [&](uint32_t r, bool have_pw, uint32_t pw) {
       double ox, oy, px, py;
       // Opaque LDS addresses: re-read the loop-invariant coarse record and cos
       // table at their point of use instead of hoisting ~40 values into VGPRs.
       const SingleCoarse RTHX_LDS* sc = lds_opaque(&s_single);
       const double RTHX_LDS* tab = lds_opaque(&s_tab[0]);
       const Emitter RTHX_LDS* em = lds_opaque(&s_emit);
-      int a = trace_one<UNIFORM, FAITHFUL, SINGLE, AXIS>(D, P, *(const Emitter*)em, *(const SingleCoarse*)sc,
-                                                         (const double*)tab, (uint32_t)g, r, ox, oy, px, py);
+      const Emitter& e = *(const Emitter*)em;
+      const RayWords rw = ray_words(P, e, (uint32_t)g, r, have_pw, pw, FAITHFUL);
+      int a = trace_one_w<UNIFORM, FAITHFUL, SINGLE, AXIS, CLDS && AXIS>(
+          D, P, e, *(const SingleCoarse*)sc, (const double*)tab, rw, ox, oy, px, py, lds_opaque(cl_base));
       tally(a);
       record(r, a, ox, oy, px, py);
+    };
+    const uint32_t rb = (uint32_t)r_begin, re = (uint32_t)r_end;
+    const uint32_t q0 = rb >> 2, q1 = (re + 3u) >> 2;
+    const uint32_t q_full = q0 + ((q1 - q0) / (uint32_t)nthr) * (uint32_t)nthr;
+    const bool volume = !lds_opaque(&s_emit)->surface;
+    // Every lane runs the same number of group rounds (q_full - q0 is a
+    // multiple of nthr), then the tail rays one per lane: the iteration
+    // count and the phase are uniform over the workgroup (scalar registers),
+    // and a lane's ray index is tid plus a uniform offset.  One code site for
+    // the block and for the ray keeps the loop body single.
+    const uint32_t n_grp = 4u * ((q_full - q0) / (uint32_t)nthr);
+    const uint32_t r_tail = 4u * q_full > rb ? 4u * q_full : rb;
+    const uint32_t n_it = n_grp + (re > r_tail ? (re - r_tail + (uint32_t)nthr - 1u) / (uint32_t)nthr : 0u);
+    uint32_t b0 = 0u, b1 = 0u, b2 = 0u, b3 = 0u;
+    for (uint32_t it = 0; it < n_it; ++it) {
+      const bool grp = it < n_grp;
+      const uint32_t r = grp ? 4u * (q0 + (it >> 2) * (uint32_t)nthr + (uint32_t)tid) + (it & 3u)
+                             : r_tail + (it - n_grp) * (uint32_t)nthr + (uint32_t)tid;
+      if (volume && (!grp || (it & 3u) == 0u)) {
+        uint32_t b[4];
+        philox_words(r >> 2, (uint32_t)g, 1u, (uint32_t)P.bin, P.key0, P.key1, b);
+        b0 = b[0]; b1 = b[1]; b2 = b[2]; b3 = b[3];
+      }
+      const uint32_t k = r & 3u;
+      const uint32_t pw = k == 0u ? b0 : k == 1u ? b1 : k == 2u ? b2 : b3;
+      if (r >= rb && r < re) one_ray(r, true, pw);
     }
   } else {
     // Several domains' rays cross many coarse polygons (the greenhouse's 67
@@ -448,35 +494,45 @@ __global__ __launch_bounds__(256) void csr_pack_kernel(const uint32_t* __restric
 template <bool UNIFORM, bool PACK16, bool FAITHFUL, bool SINGLE, bool REC, bool SPLIT, bool AXIS, bool CLDS = false>
 static hipError_t launch_trace_t(const LaunchCfg& L) {
   auto kern = trace_exchange_kernel<UNIFORM, PACK16, FAITHFUL, SINGLE, REC, SPLIT, AXIS, CLDS>;
-  if (L.lds_bytes > 64 * 1024) {
+  if (L.lds_bytes > 64 * 1024) {  // (occupancy queries above 64 KiB need the attribute first)
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)L.lds_bytes);
     if (e != hipSuccess) return e;
   }
   const int64_t blocks = L.T.n_rows * (SPLIT ? L.T.split : 1);
+  auto lds_for = [&](int) { return L.lds_bytes; };
   // Workgroup size: the one that keeps most waves resident per CU.  With a
   // large LDS row histogram (large N) only one or two workgroups fit a CU,
   // and 1024-lane workgroups keep 16 waves busy instead of 4.
   int threads = kTraceThreads, best_waves = 0;
   for (int t = kTraceThreads; t <= kMaxTraceThreads; t *= 2) {
+    if (lds_for(t) + (size_t)kStaticLdsBytes > kMaxLdsBytes) break;
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, t, L.lds_bytes) != hipSuccess)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, t, lds_for(t)) != hipSuccess)
       break;
     if (per_cu * (t / 64) > best_waves) {
       best_waves = per_cu * (t / 64);
       threads = t;
     }
   }
-  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(threads), L.lds_bytes, L.stream, L.D, L.P, L.T, L.rec);
+  const size_t lds = lds_for(threads);
+  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(threads), lds, L.stream, L.D, L.P, L.T, L.rec);
   return hipGetLastError();
 }
 
 template <bool UNIFORM, bool PACK16, bool FAITHFUL, bool AXIS>
 static hipError_t launch_trace_a(const LaunchCfg& L) {
+  // SINGLE kernels with CLDS = the lattice locate (LAT; axis-aligned only)
   if (L.T.split > 1) {
+    if constexpr (AXIS) {
+      if (L.single && L.clds) return launch_trace_t<UNIFORM, PACK16, FAITHFUL, true, false, true, AXIS, true>(L);
+    }
     if (L.single) return launch_trace_t<UNIFORM, PACK16, FAITHFUL, true, false, true, AXIS>(L);
     if (L.clds) return launch_trace_t<UNIFORM, PACK16, FAITHFUL, false, false, true, AXIS, true>(L);
     return launch_trace_t<UNIFORM, PACK16, FAITHFUL, false, false, true, AXIS>(L);
+  }
+  if constexpr (AXIS) {
+    if (L.single && L.clds) return launch_trace_t<UNIFORM, PACK16, FAITHFUL, true, false, false, AXIS, true>(L);
   }
   if (L.single) return launch_trace_t<UNIFORM, PACK16, FAITHFUL, true, false, false, AXIS>(L);
   if (L.clds) return launch_trace_t<UNIFORM, PACK16, FAITHFUL, false, false, false, AXIS, true>(L);

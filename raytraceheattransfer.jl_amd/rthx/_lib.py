@@ -342,10 +342,10 @@ class HipBackend:
         return device_domain(dom, dev), dev
 
     def trace_F(self, dom, bin0: int, rays_per_emitter: int, nudge: float, seed: int, device: int,
-                faithful: bool, record_ids=None, record_bin0: int = 0):
+                faithful: bool, record_ids=None, record_bin0: int = 0, host: bool = True):
         """One traced bin with F_raw formed on the device: returns (F_raw as
-        scipy CSR, info, recorded rays, the DeviceResult -- its counts stay
-        on the device for rthx_smooth_F_result)."""
+        scipy CSR -- None unless `host` --, info, recorded rays, the
+        DeviceResult: its counts stay on the device for rthx_smooth_F_result)."""
         import scipy.sparse as sp
 
         flat = dom.flat()
@@ -356,15 +356,17 @@ class HipBackend:
         res = DeviceResult()
         try:
             res.trace(dd, args)
-            row_ptr, cols, vals = res.F()
+            F = None
+            if host:
+                row_ptr, cols, vals = res.F()
+                n = flat.n_emitters
+                F = sp.csr_matrix((vals, cols, row_ptr), shape=(n, n))
             info = res.info()
             rays = res.rays() if info["n_recorded"] > 0 else None
         except Exception:
             res.close()
             raise
         del keep
-        n = flat.n_emitters
-        F = sp.csr_matrix((vals, cols, row_ptr), shape=(n, n))
         return F, info, rays, res
 
     def trace(self, dom, bin0: int, rays_per_emitter: int, nudge: float, seed: int, device: int,

@@ -327,7 +327,8 @@ class RayTracingDomain2D:
         self.fine_grids_opt = [build_uniform_grid(sub, bb) for sub, bb in zip(self.fine_mesh, self.fine_bboxes)]
 
         self.wavelength_band_limits = None  # DomainStructs.jl:105 (set by the user for spectral runs)
-        self.F_raw = None
+        self._F_raw = None
+        self._F_raw_lazy = None  # callable: host copy of a device-resident F_raw
         self._F_smooth = None
         self._F_smooth_handle = None  # device-resident F_smooth (SmoothHandle) not yet copied to the host
         self.rays_per_emitter = None
@@ -336,6 +337,25 @@ class RayTracingDomain2D:
         self._device_domains: Dict[int, object] = {}
 
     # ------------------------------------------------------------------
+    @property
+    def F_raw(self):
+        """exchangeRayTracing.jl:73.  After a device trace the counts stay on
+        the device; F_raw (count / tallied per row) is copied once, on first
+        read."""
+        if self._F_raw_lazy is not None:
+            self._F_raw = self._F_raw_lazy()
+            self._F_raw_lazy = None
+        return self._F_raw
+
+    @F_raw.setter
+    def F_raw(self, value):
+        self._F_raw = value
+        self._F_raw_lazy = None
+
+    def _set_F_raw_lazy(self, thunk) -> None:
+        self._F_raw = None
+        self._F_raw_lazy = thunk
+
     @property
     def F_smooth(self):
         """exchangeRayTracing.jl:74.  When the smoothing ran on the device
@@ -399,7 +419,9 @@ class RayTracingDomain2D:
                  rec=None, seed: int = 1, device: int = 0, faithful: bool = False, smooth: bool = True):
         """multiDispatchRayTrace2D.jl:1-18.  ``method="exchange"``: trace (F_raw)
         then smooth (F_smooth, exchangeRayTracing.jl:13-74) on the device;
-        ``smooth=False`` stops after tracing (F_smooth stays None).
+        ``smooth=False`` stops after tracing (F_smooth stays None).  The
+        results land in ``self.F_raw`` / ``self.F_smooth`` (copied from the
+        device on first read); returns None.
         ``method="direct"``: directRayTracing! (directRayTracing.jl:1-17) on
         the device; writes powers and temperatures into the fine faces.
         """
@@ -410,14 +432,17 @@ class RayTracingDomain2D:
             verbose = self.verbose
         trace_nudge = 10_000 * np.finfo(np.float64).eps if nudge is None else float(nudge)
         if method == "exchange":
-            F_raw = exchange_ray_tracing(self, int(rays_tot), trace_nudge, verbose, rec,
-                                         seed=seed, device=device, faithful=faithful)
+            # F_raw and F_smooth stay on the device (the counts are smoothed
+            # where they were traced, the GERT solve reads F_smooth in place);
+            # each is copied to the host once, when first read
+            exchange_ray_tracing(self, int(rays_tot), trace_nudge, verbose, rec, seed=seed, device=device,
+                                 faithful=faithful, lazy=True)
             if smooth:
-                Fs = smooth_exchange_factors(self, F_raw, max_iters=max_iters, k_dykstra=k_dykstra,
+                Fs = smooth_exchange_factors(self, None, max_iters=max_iters, k_dykstra=k_dykstra,
                                              verbose=verbose, device=device)
                 if Fs is not None:  # (None: F_smooth stays on the device until read)
                     self.F_smooth = Fs
-            return F_raw
+            return None
         if method == "direct":
             from .direct import direct_ray_tracing
 

@@ -85,6 +85,23 @@ def counts_to_F(row_ptr, cols, counts, n: int, rays_per_emitter: int) -> sp.csr_
     return sp.csr_matrix((data, cols.astype(np.int64), row_ptr.astype(np.int64)), shape=(n, n))
 
 
+class DeviceF:
+    """F_raw of one traced bin whose counts are still on the device
+    (lazy mode of exchange_ray_tracing): ``host()`` forms F_raw there
+    (count / tallied, rthx_result_copy_F) and copies it once."""
+
+    def __init__(self, res, n: int):
+        self.res, self.n = res, n
+
+    @property
+    def shape(self):
+        return (self.n, self.n)
+
+    def host(self) -> sp.csr_matrix:
+        row_ptr, cols, vals = self.res.F()
+        return sp.csr_matrix((vals, cols, row_ptr), shape=(self.n, self.n))
+
+
 def _keep_device_result(dom, spectral_bin: int, res) -> None:
     """Keep a traced bin's device result (its counts) for the smoothing."""
     held = getattr(dom, "_trace_results", None)
@@ -110,7 +127,7 @@ def _default_backend():
 
 def compute_exchange_factors_bin(dom, rays_per_emitter: int, nudge: float, spectral_bin: int,
                                  verbose: bool, rec: Optional[RayRecorder], seed: int = 1,
-                                 device: int = 0, faithful: bool = False, backend=None):
+                                 device: int = 0, faithful: bool = False, backend=None, lazy: bool = False):
     """computeExchangeFactorsBin, parallelRayTracing.jl:64-159 (``spectral_bin`` 1-based).
 
     The whole per-emitter loop (:69-152) is one device call; the host keeps
@@ -124,9 +141,13 @@ def compute_exchange_factors_bin(dom, rays_per_emitter: int, nudge: float, spect
         rec_bin0 = rec.bin - 1
     if hasattr(backend, "trace_F"):
         # F_raw formed on the device (count / tallied, the exact quotient of
-        # :145 + row_normalize!); the counts stay there for the smoothing
+        # :145 + row_normalize!); the counts stay there for the smoothing.
+        # lazy: F_raw is not copied here (DeviceF; the host copy is made when
+        # dom.F_raw is read)
         F, info, rays, res = backend.trace_F(dom, spectral_bin - 1, rays_per_emitter, nudge, seed, device,
-                                             faithful, record_ids=rec_ids, record_bin0=rec_bin0)
+                                             faithful, record_ids=rec_ids, record_bin0=rec_bin0, host=not lazy)
+        if lazy:
+            F = DeviceF(res, dom.num_emitters)
         _keep_device_result(dom, spectral_bin, res)
         info = dict(info)
         info["bin"] = spectral_bin
@@ -162,14 +183,14 @@ def compute_exchange_factors_bin(dom, rays_per_emitter: int, nudge: float, spect
 
 
 def parallel_ray_tracing(dom, rays_total: int, nudge: float, verbose: bool, rec=None, seed: int = 1,
-                         device: int = 0, faithful: bool = False, backend=None):
+                         device: int = 0, faithful: bool = False, backend=None, lazy: bool = False):
     """parallelRayTracing, parallelRayTracing.jl:1-62."""
     num_emitters = dom.num_emitters
     rays_per_emitter = rays_total // num_emitters
     n_bins = dom.n_spectral_bins
     dom.last_trace_info = []
     release_device_results(dom)
-    kw = dict(seed=seed, device=device, faithful=faithful, backend=backend)
+    kw = dict(seed=seed, device=device, faithful=faithful, backend=backend, lazy=lazy)
     if dom.spectral_mode == "spectral_variable":
         F_vec: List[Optional[sp.csr_matrix]] = [None] * n_bins
         groups, _reps, nonuniform = group_uniform_bins(dom.uniform_across_bin)
@@ -189,12 +210,35 @@ def parallel_ray_tracing(dom, rays_total: int, nudge: float, verbose: bool, rec=
     return F, rays_per_emitter
 
 
+def materialize_F_raw(F_raw, ns: int, surfaces_only: bool):
+    """Host copies of lazily traced bins (DeviceF), each once (grouped bins
+    share one matrix), truncated to the surface block for surfaces_only."""
+    seen = {}
+
+    def one(F):
+        if id(F) not in seen:
+            H = F.host() if isinstance(F, DeviceF) else F
+            seen[id(F)] = H[:ns, :ns].tocsr() if surfaces_only else H
+        return seen[id(F)]
+
+    return [one(F) for F in F_raw] if isinstance(F_raw, list) else one(F_raw)
+
+
 def exchange_ray_tracing(dom, rays_tot: int, nudge: float, verbose: bool, rec=None, seed: int = 1,
-                         device: int = 0, faithful: bool = False, backend=None):
-    """exchangeRayTracing!, exchangeRayTracing.jl:1-11 and :73 (tracing half)."""
+                         device: int = 0, faithful: bool = False, backend=None, lazy: bool = False):
+    """exchangeRayTracing!, exchangeRayTracing.jl:1-11 and :73 (tracing half).
+
+    lazy: F_raw stays on the device (dom.F_raw copies it on first read);
+    returns None.  Needs a backend that keeps its results (HipBackend)."""
+    backend = backend or _default_backend()
+    lazy = lazy and hasattr(backend, "trace_F")
     F_raw, rpe = parallel_ray_tracing(dom, rays_tot, nudge, verbose, rec, seed=seed, device=device,
-                                      faithful=faithful, backend=backend)
+                                      faithful=faithful, backend=backend, lazy=lazy)
     ns = dom.num_surfaces
+    dom.rays_per_emitter = rpe
+    if lazy:
+        dom._set_F_raw_lazy(lambda: materialize_F_raw(F_raw, ns, dom.surfaces_only))
+        return None
     if dom.surfaces_only:
         if isinstance(F_raw, list):
             seen = {}

@@ -20,14 +20,15 @@ from ._lib import check, load
 
 def get_w(dom, spectral_bin: int = 1) -> np.ndarray:
     """get_w, smoothExchangeFactors.jl:320-341: wall lengths for surfaces, then
-    max(1e-6, 4 beta V) for volumes (1-based ``spectral_bin``)."""
-    ns = len(dom.surface_mapping)
-    w = np.zeros(ns + len(dom.volume_mapping))
-    for (c, f, wall), s in dom.surface_mapping.items():
-        w[s - 1] = dom.fine_mesh[c - 1][f - 1].area[wall - 1]
-    for (c, f), v in dom.volume_mapping.items():
-        face = dom.fine_mesh[c - 1][f - 1]
-        w[ns + v - 1] = max(1e-6, 4.0 * face.beta(spectral_bin - 1) * face.volume)
+    max(1e-6, 4 beta V) for volumes (1-based ``spectral_bin``), from the
+    flattened domain (surface order = the surface index, volume v = fine
+    polygon v, beta = kappa + sigma_s of the bin)."""
+    flat = dom.flat()
+    ns = flat.n_surfaces
+    beta = flat.beta.reshape(flat.n_bins, flat.n_fine)[spectral_bin - 1]
+    w = np.empty(ns + flat.n_fine)
+    w[:ns] = dom.surface_areas
+    w[ns:] = np.maximum(1e-6, 4.0 * beta * flat.fine_volume)
     return w
 
 
@@ -156,15 +157,21 @@ def smooth_exchange_factors(dom, F_raw, max_iters: int = 1000, k_dykstra: Option
               smooth_surfaces_only=dom.surfaces_only, device=device)
     held = getattr(dom, "_trace_results", {})
     res = held.get(1)
-    if (dom.spectral_mode != "spectral_variable" and res is not None and res.info()["n_devices"] == 1
-            and not isinstance(F_raw, list)):
+    n_block = ns if dom.surfaces_only else dom.num_emitters  # exchangeRayTracing.jl:9-11
+    if dom.spectral_mode != "spectral_variable" and res is not None and res.info()["n_devices"] == 1:
         # the traced counts are still on the device: smooth them there and
         # keep F_smooth there for the solve; the host copy of F_smooth is made
         # on first access (dom.F_smooth)
         info = {}
-        handle = smooth_F_device(res, F_raw.shape[0], get_w(dom), ns, info=info, **kw)
+        handle = smooth_F_device(res, n_block, get_w(dom), ns, info=info, **kw)
         dom._set_F_smooth_device(handle)
+        dom.last_smooth_info = info
         return None
+
+    def host_F(b=None):  # host copy of F_raw (multi-device or host-side results)
+        F = dom.F_raw if F_raw is None else F_raw
+        return F if b is None else F[b - 1]
+
     if dom.spectral_mode == "spectral_variable":
         out = [None] * dom.n_spectral_bins
         groups, _reps, nonuniform = group_uniform_bins(dom.uniform_across_bin)
@@ -172,12 +179,12 @@ def smooth_exchange_factors(dom, F_raw, max_iters: int = 1000, k_dykstra: Option
         def smooth_bin(b):
             r = held.get(b)
             if r is not None and r.info()["n_devices"] == 1:  # counts still on the device
-                h = smooth_F_device(r, F_raw[b - 1].shape[0], get_w(dom, b), ns, **kw)
+                h = smooth_F_device(r, n_block, get_w(dom, b), ns, **kw)
                 try:
                     return h.host()
                 finally:
                     h.close()
-            return smooth_F(F_raw[b - 1], get_w(dom, b), ns, **kw)
+            return smooth_F(host_F(b), get_w(dom, b), ns, **kw)
 
         for b in nonuniform:
             out[b - 1] = smooth_bin(b)
@@ -187,7 +194,7 @@ def smooth_exchange_factors(dom, F_raw, max_iters: int = 1000, k_dykstra: Option
             for j in idx_group:
                 out[j - 1] = Fs
         return out
-    F_s, handle = smooth_F(F_raw, get_w(dom), ns, keep_device=True, **kw)
+    F_s, handle = smooth_F(host_F(), get_w(dom), ns, keep_device=True, **kw)
     old = getattr(dom, "_F_smooth_device", None)
     if old is not None:
         old[1].close()

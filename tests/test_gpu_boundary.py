@@ -234,13 +234,17 @@ def test_mesh_keeps_F_on_device_until_read(hip):
     from rthx.smoothing import get_w, smooth_F
 
     dom = H.square_domain(11)
-    F_raw = dom(1_000_000, seed=11, verbose=False)
+    assert dom(1_000_000, seed=11, verbose=False) is None
     assert dom._F_smooth_handle is not None and dom._F_smooth is None
+    assert dom._F_raw_lazy is not None and dom._F_raw is None
     T, j, Abs, r = equilibrium_grey(dom, None)
     assert dom._F_smooth_handle is not None  # the solve read F_smooth in place
     assert abs(dom.energy_error) < 1e-4
     Fs = dom.F_smooth
     assert dom._F_smooth_handle is None and isinstance(Fs, np.ndarray)
+    F_raw = dom.F_raw  # host copy on first read
+    assert dom._F_raw_lazy is None and F_raw.shape == (dom.num_emitters,) * 2
+    assert np.allclose(np.asarray(F_raw.sum(axis=1)).ravel(), 1.0, rtol=0, atol=1e-12)
     ref = smooth_F(F_raw, get_w(dom), dom.num_surfaces, verbose=False)
     assert np.max(np.abs(Fs - ref)) <= 1e-12
     T2, *_ = equilibrium_grey(dom, dom.F_smooth)  # the host copy is still recognised as device-resident

@@ -35,11 +35,17 @@ def main():
         t2 = time.perf_counter()
         _ = dom.F_smooth  # host copy on first access
         t3 = time.perf_counter()
+        _ = dom.F_raw  # host copy on first access
+        t4 = time.perf_counter()
+        sm = getattr(dom, "last_smooth_info", {})
         tr = dom.last_trace_info[0]
         print(f"ndim {a.ndim} rays {a.rays:.0e}: mesh() {1e3 * (t1 - t0):.0f} ms (trace kernel "
               f"{tr['trace_ms']:.2f} ms), solve {1e3 * (t2 - t1):.0f} ms (GMRES {info['iterations']} iterations, "
               f"library {info['ms_total']:.1f} ms, residual {info['residual']:.2e}), energy error "
-              f"{dom.energy_error:.2e}; F_smooth to the host {1e3 * (t3 - t2):.0f} ms", flush=True)
+              f"{dom.energy_error:.2e}; smoothing library {sm.get('ms_total', float('nan')):.1f} ms (OP "
+              f"{sm.get('ms_op', float('nan')):.1f}, AP {sm.get('ms_ap', float('nan')):.1f}, {sm.get('ap_iters')} "
+              f"iterations); on first read: F_smooth to the host {1e3 * (t3 - t2):.0f} ms, F_raw "
+              f"{1e3 * (t4 - t3):.0f} ms", flush=True)
 
 
 if __name__ == "__main__":
