@@ -57,6 +57,8 @@ def main():
     ap.add_argument("--rays", type=float, default=1e8)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--only", default="C2,C3,C5")
+    ap.add_argument("--bins", default="0,1,2,3,4,5,6,7", help="C5 bands (0-based)")
+    ap.add_argument("--no-ramp", action="store_true", help="skip the C2 clock ramp (counter passes)")
     args = ap.parse_args()
     only = args.only.split(",")
     rays = int(args.rays)
@@ -67,7 +69,7 @@ def main():
     res = _lib.DeviceResult()
     a, _k = _lib.make_args(0, 9429, H.NUDGE, 1, 0, flat.n_emitters, 1, flags=abi.RTHX_FLAG_DEVICE_ONLY)
     t = time.perf_counter()
-    while time.perf_counter() - t < 0.3:
+    while not args.no_ramp and time.perf_counter() - t < 0.3:
         res.trace(dd, a)
     res.close()
     dd.close()
@@ -76,7 +78,7 @@ def main():
     if "C3" in only:
         run("C3", H.square_domain(51, kappa=1.0, sigma_s=5.0), rays, args.steps)
     if "C5" in only:
-        run("C5", H.greenhouse_domain(), rays, max(1, args.steps // 4), bins=tuple(range(8)))
+        run("C5", H.greenhouse_domain(), rays, max(1, args.steps // 4), bins=tuple(int(b) for b in args.bins.split(",")))
 
 
 if __name__ == "__main__":
