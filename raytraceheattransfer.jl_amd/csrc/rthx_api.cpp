@@ -68,6 +68,13 @@ void fill_tables(double* t) {
 
 namespace {
 
+// Integer tuning knob from the environment, clamped to [lo, hi].
+int64_t env_int(const char* name, int64_t dflt, int64_t lo, int64_t hi) {
+  const char* e = getenv(name);
+  if (!e || !*e) return dflt;
+  return std::min<int64_t>(hi, std::max<int64_t>(lo, std::strtoll(e, nullptr, 10)));
+}
+
 bool env_flag(const char* name) {
   const char* e = getenv(name);
   return e && e[0] == '1';
@@ -491,10 +498,11 @@ namespace rthx {
 // into the staging slots, scan the per-row nnz (row_off, totals), read the
 // totals back, size cols / counts to nnz and pack the slots.  totals[0..3] =
 // nnz, lost rays, max lost per row, look-back stalls (0 here).
-int finish_staged(rthx_result* res, const TallyParams& T, bool split, hipStream_t st, hipEvent_t ev_end,
+int finish_staged(rthx_result* res, const TallyParams& T, int merge, hipStream_t st, hipEvent_t ev_end,
                   int64_t totals[4]) {
   if (T.n_rows > 0) {
-    if (split) HIP_TRY(launch_compact(T, st), "row_compact_kernel launch");
+    if (merge == kMergeDense) HIP_TRY(launch_compact(T, st), "row_compact_kernel launch");
+    if (merge == kMergeParts) HIP_TRY(launch_part_merge(T, st), "part_merge_kernel launch");
     HIP_TRY(launch_scan(T.row_nnz, T.row_tallied, T.n_rows, T.R, res->row_off.as<int64_t>(),
                         res->totals.as<int64_t>(), st),
             "row_scan_kernel launch");
@@ -533,10 +541,15 @@ uint64_t lookback_wait_ticks() {
 
 // Launch geometry of one trace call (rows, split, LDS histogram layout).
 struct TracePlan {
-  int64_t N = 0, R = 0, end = 0, n_rows = 0, split = 1, row_cap = 1;
-  bool pack16 = true, clds = false, recording = false, uniform = true;
+  int64_t N = 0, R = 0, end = 0, n_rows = 0, split = 1, row_cap = 1, hash_cap = 0, bm_words = 0;
+  int tally = rthx::kTallyU16;
+  bool clds = false, recording = false, uniform = true;
   size_t lds_bytes = 0, cl_offset = 0;
 };
+
+// Hash tallies (large N): the largest table the trace kernel's LDS holds
+// (keys + counts, 8 B per slot); a workgroup traces at most 3/4 as many rays.
+constexpr int64_t kMaxHashCap = 16384;
 
 int plan_trace(const rthx_domain* dom, const rthx_trace_args* a, TracePlan& p) {
   if (a->bin < 0 || a->bin >= dom->n_bins) return fail(RTHX_EINVAL, "bin out of range");
@@ -561,12 +574,38 @@ int plan_trace(const rthx_domain* dom, const rthx_trace_args* a, TracePlan& p) {
   if (!p.recording && R >= 65536 && ((N + 1) / 2) * 4 + rthx::kStaticLdsBytes <= (int64_t)rthx::kMaxLdsBytes &&
       N * 4 + rthx::kStaticLdsBytes > (int64_t)rthx::kMaxLdsBytes)
     p.split = std::max<int64_t>(p.split, (R + 65534) / 65535);
-  const int64_t rays_per_block = p.split > 1 ? (R + p.split - 1) / p.split : R;
-  p.pack16 = rays_per_block < 65536;
-  const int64_t words = p.pack16 ? (N + 1) / 2 : N;
+  int64_t rays_per_block = p.split > 1 ? (R + p.split - 1) / p.split : R;
+  p.tally = rays_per_block < 65536 ? rthx::kTallyU16 : rthx::kTallyU32;
+  const int64_t words = p.tally == rthx::kTallyU16 ? (N + 1) / 2 : N;
   p.lds_bytes = (size_t)words * 4;
-  if (p.lds_bytes + rthx::kStaticLdsBytes > rthx::kMaxLdsBytes)
-    return fail(RTHX_ERANGE, "N too large for the LDS row histogram of this build");
+  p.row_cap = std::max<int64_t>(1, std::min<int64_t>(N, R));
+  if (p.lds_bytes + rthx::kStaticLdsBytes > rthx::kMaxLdsBytes || env_flag("RTHX_FORCE_HASH")) {
+    // Large N: the row is an LDS hash table (rthx_kernels.hip hash_tally)
+    // filled at most to load_pct, so a workgroup traces at most 3/4 x
+    // kMaxHashCap rays by default; longer rows are split, and their sorted
+    // parts merged.
+    p.tally = rthx::kTallyHash;
+    const int64_t cap_max = env_int("RTHX_HASH_MAX", kMaxHashCap, 256, kMaxHashCap);
+    const int64_t load_pct = env_int("RTHX_HASH_LOAD_PCT", 75, 10, 90);  // most slots a workgroup fills (A/B: tools/hash_ab.sh)
+    const int64_t max_rays = cap_max * load_pct / 100;
+    if (rays_per_block > max_rays) {
+      if (p.recording) return fail(RTHX_ERANGE, "recording a large-N domain needs fewer rays_per_emitter");
+      p.split = (R + max_rays - 1) / max_rays;
+      rays_per_block = (R + p.split - 1) / p.split;
+    }
+    p.hash_cap = 256;
+    while (p.hash_cap * load_pct < 100 * rays_per_block) p.hash_cap *= 2;
+    p.lds_bytes = (size_t)p.hash_cap * 8;
+    // ascending output through an N-bit bitmap behind the table when it fits
+    // (and leaves room for the single rectangle's lattice); else LDS sort
+    const int64_t bm = (N + 31) / 32;
+    const size_t lat = dom->single_convex ? (size_t)dom->D.lat.bytes + 16 : 0;
+    if (p.lds_bytes + 4 * bm + lat + rthx::kStaticLdsBytes <= rthx::kMaxLdsBytes && !env_flag("RTHX_HASH_SORT")) {
+      p.bm_words = bm;
+      p.lds_bytes += 4 * (size_t)bm;
+    }
+    if (p.split > 1) p.row_cap = std::max<int64_t>(1, R);  // part lists at p * chunk
+  }
   // multi-polygon domains: the coarse mesh goes behind the histogram in LDS
   // when it fits (CLDS kernels, rthx_device.h segment_cl)
   p.cl_offset = (p.lds_bytes + 15) & ~(size_t)15;
@@ -580,7 +619,6 @@ int plan_trace(const rthx_domain* dom, const rthx_trace_args* a, TracePlan& p) {
     p.clds = true;
     p.lds_bytes = p.cl_offset + (size_t)dom->D.lat.bytes;
   }
-  p.row_cap = std::max<int64_t>(1, std::min<int64_t>(N, R));
   p.uniform = dom->uniform_beta[a->bin] > -0.1;  // traceRay.jl:4
   return RTHX_OK;
 }
@@ -610,7 +648,12 @@ int run_trace(rthx_domain* dom, const rthx_trace_args* a, const TracePlan& p, rt
     HIP_TRY(res->stage_cols.reserve((size_t)n_rows * p.row_cap * 4), "hipMalloc stage_cols");
     HIP_TRY(res->stage_cnt.reserve((size_t)n_rows * p.row_cap * 4), "hipMalloc stage_cnt");
   }
-  if (p.split > 1) HIP_TRY(res->dense.reserve((size_t)n_rows * N * 4), "hipMalloc dense rows");
+  const bool hash = p.tally == rthx::kTallyHash;
+  // split rows: the dense per-row counts, or (hash tallies) the part merge's
+  // scratch [2][n_rows][row_cap] followed by part_nnz [n_rows][split]
+  const size_t dense_bytes = hash ? (size_t)n_rows * p.row_cap * 8 + (size_t)n_rows * p.split * 4
+                                  : (size_t)n_rows * N * 4;
+  if (p.split > 1) HIP_TRY(res->dense.reserve(dense_bytes), "hipMalloc dense rows");
   else res->dense.release();
 
   rthx::TraceParams P{};
@@ -635,6 +678,12 @@ int run_trace(rthx_domain* dom, const rthx_trace_args* a, const TracePlan& p, rt
   T.row_nnz = res->row_nnz.as<uint32_t>();
   T.row_tallied = res->row_tallied.as<uint32_t>();
   T.dense = p.split > 1 ? res->dense.as<uint32_t>() : nullptr;
+  T.part_nnz = p.split > 1 && hash ? T.dense + 2 * (size_t)n_rows * p.row_cap : nullptr;
+  T.hash_cap = (int32_t)p.hash_cap;
+  int32_t shift = 32;
+  for (int64_t c = p.hash_cap; c > 1; c >>= 1) --shift;
+  T.hash_shift = shift;
+  T.bm_words = p.bm_words;
   T.R = R;
   if (lookback) {
     T.lb_status = res->lb_status.as<unsigned long long>();
@@ -647,7 +696,7 @@ int run_trace(rthx_domain* dom, const rthx_trace_args* a, const TracePlan& p, rt
   }
   HIP_TRY(hipMemsetAsync(res->totals.p, 0, 32, st), "hipMemset totals");
   if (p.split > 1 && n_rows > 0) {
-    HIP_TRY(hipMemsetAsync(T.dense, 0, (size_t)n_rows * N * 4, st), "hipMemset dense rows");
+    if (!hash) HIP_TRY(hipMemsetAsync(T.dense, 0, (size_t)n_rows * N * 4, st), "hipMemset dense rows");
     HIP_TRY(hipMemsetAsync(T.row_tallied, 0, (size_t)n_rows * 4, st), "hipMemset row_tallied");
   }
   HIP_TRY(hipEventRecord(dom->ev[0], st), "hipEventRecord");
@@ -660,7 +709,8 @@ int run_trace(rthx_domain* dom, const rthx_trace_args* a, const TracePlan& p, rt
     L.lds_bytes = p.lds_bytes;
     L.stream = st;
     L.uniform = p.uniform;
-    L.pack16 = p.pack16;
+    L.tally = p.tally;
+    L.threads = (int)env_int("RTHX_TRACE_THREADS", 0, 0, rthx::kMaxTraceThreads);
     L.faithful = (a->flags & RTHX_FLAG_FAITHFUL_SAMPLING) != 0;
     L.single = dom->single_convex;
     L.clds = p.clds;
@@ -673,7 +723,8 @@ int run_trace(rthx_domain* dom, const rthx_trace_args* a, const TracePlan& p, rt
     HIP_TRY(hipMemcpyAsync(totals, res->totals.p, 32, hipMemcpyDeviceToHost, st), "hipMemcpy totals");
     HIP_TRY(hipStreamSynchronize(st), "trace kernel");
   } else {
-    int rc = rthx::finish_staged(res, T, p.split > 1, st, dom->ev[2], totals);
+    const int merge = p.split == 1 ? rthx::kNoMerge : hash ? rthx::kMergeParts : rthx::kMergeDense;
+    int rc = rthx::finish_staged(res, T, merge, st, dom->ev[2], totals);
     if (rc) return rc;
   }
   HIP_TRY(hipEventElapsedTime(ms_trace, dom->ev[0], dom->ev[1]), "hipEventElapsedTime");

@@ -79,9 +79,11 @@ struct rthx_result {
 
 namespace rthx {
 struct TallyParams;
+// How split rows are joined before the row scan (finish_staged).
+enum SplitMerge : int { kNoMerge = 0, kMergeDense = 1, kMergeParts = 2 };
 // rthx_api.cpp: staged rows -> final CSR after a trace launch on `st` (split
 // merge, row scan, totals read back, cols / counts sized to nnz, pack; ev_end
 // recorded after the pack).  Shared by the 2D and 3D tracers.
-int finish_staged(rthx_result* res, const TallyParams& T, bool split, hipStream_t st, hipEvent_t ev_end,
+int finish_staged(rthx_result* res, const TallyParams& T, int merge, hipStream_t st, hipEvent_t ev_end,
                   int64_t totals[4]);
 }  // namespace rthx

@@ -23,21 +23,34 @@ struct RecordParams {
   double* end;          // [n*R*2]
 };
 
+// Row tally of the trace kernels: a dense LDS histogram of N u32 counters,
+// of N u16 counters packed two per word (< 65536 rays per workgroup), or --
+// when even the packed histogram does not fit LDS (large N) -- an LDS hash
+// table of (absorber, count) pairs with at most hash_cap/2 rays per workgroup.
+enum Tally : int { kTallyU32 = 0, kTallyU16 = 1, kTallyHash = 2 };
+
 // Where the counts go.  Unsplit: each workgroup compacts its row into
-// stage_*[slot*row_cap ..] and writes row_nnz / row_tallied.  Split: the
-// `split` workgroups of a row add into dense[slot*N ..] and row_tallied
-// (both zeroed first); row_compact_kernel then fills stage_* / row_nnz.
+// stage_*[slot*row_cap ..] and writes row_nnz / row_tallied.  Split, dense
+// tallies: the `split` workgroups of a row add into dense[slot*N ..] and
+// row_tallied (both zeroed first); row_compact_kernel then fills stage_* /
+// row_nnz.  Split, hash tallies: part p of a row writes its sorted list to
+// stage_*[slot*row_cap + p*chunk ..] (row_cap = R) and part_nnz[slot*split+p];
+// part_merge_kernel merges the parts (scratch: dense) back into the slot.
 struct TallyParams {
   int64_t n_emitters;   // N (histogram length)
   int64_t n_rows;
-  int64_t row_cap;      // min(N, R)
+  int64_t row_cap;      // min(N, R); R for split hash tallies
   int32_t split;        // workgroups per row (>= 1)
   int32_t cl_offset;    // CLDS kernels: byte offset of the coarse mesh in dynamic LDS
   uint32_t* stage_cols;
   uint32_t* stage_cnt;
   uint32_t* row_nnz;
   uint32_t* row_tallied;
-  uint32_t* dense;      // split only: [n_rows][N]
+  uint32_t* dense;      // split only: [n_rows][N] (dense tallies) or merge scratch [2][n_rows][row_cap] (hash)
+  uint32_t* part_nnz;   // split hash tallies: [n_rows][split]
+  int32_t hash_cap;     // hash tallies: table slots (power of two; keys then counts in dynamic LDS)
+  int32_t hash_shift;   // 32 - log2(hash_cap)
+  int64_t bm_words;     // hash tallies: N-bit absorber bitmap after the table (words), 0 = sort the table
   // Unsplit 2D launches: rows go straight into the final CSR (cols / cnt at
   // the row's offset, found by a decoupled look-back over lb_status, one
   // zeroed u64 per row); nullptr = staging + row_scan_kernel + csr_pack_kernel.
@@ -57,7 +70,9 @@ struct LaunchCfg {
   RecordParams rec;
   size_t lds_bytes;
   hipStream_t stream;
-  bool uniform, pack16, faithful, single, axis, clds;
+  int tally;    // Tally
+  int threads;  // workgroup size; 0 = the one with the most resident waves
+  bool uniform, faithful, single, axis, clds;
 };
 
 hipError_t launch_trace(const LaunchCfg& L);
@@ -66,6 +81,7 @@ hipError_t launch_trace(const LaunchCfg& L);
 hipError_t launch_counts_to_F(const int64_t* row_off, const uint32_t* cnt, int64_t n_rows, double* vals,
                               hipStream_t stream);
 hipError_t launch_compact(const TallyParams& T, hipStream_t stream);
+hipError_t launch_part_merge(const TallyParams& T, hipStream_t stream);
 hipError_t launch_scan(const uint32_t* row_nnz, const uint32_t* row_tallied, int64_t n_rows, int64_t R,
                        int64_t* row_off, int64_t* totals, hipStream_t stream);
 hipError_t launch_pack(const uint32_t* stage_cols, const uint32_t* stage_cnt, int64_t row_cap, const int64_t* row_off,

@@ -9,6 +9,9 @@
 //   order into a fixed-stride staging slot of min(N, R) entries (no global
 //   atomics, deterministic); split rows add their histogram into a dense
 //   per-row count buffer that row_compact_kernel compacts afterwards.
+//   Large N (the packed histogram does not fit LDS): the row is an LDS hash
+//   table of (absorber, count) -- the Dict itself -- sorted in LDS at the end
+//   of the row; split rows' sorted parts are merged by part_merge_kernel.
 // row_scan_kernel: exclusive scan of per-row nnz + lost-ray reductions.
 // csr_pack_kernel: copies every row's staging slot into the dense CSR arrays.
 #include <hip/hip_runtime.h>
@@ -144,7 +147,146 @@ __device__ __forceinline__ uint32_t compact_row(int64_t n_words, F count2, uint3
   return compact_row<PAIRS>(n_words, count2, out_c, out_n, wave_sum, [](uint32_t) { return (uint64_t)0; });
 }
 
-template <bool UNIFORM, bool PACK16, bool FAITHFUL, bool SINGLE, bool REC, bool SPLIT, bool AXIS, bool CLDS>
+// ---------------------------------------------------------------------------
+// Hash tallies (large N).  keys[hash_cap] then cnts[hash_cap] in dynamic LDS;
+// key 0 = empty slot, absorber a is stored as a + 1.  A workgroup traces at
+// most 3/4 x hash_cap rays (host: RTHX_HASH_LOAD_PCT), so a quarter of the
+// slots always stays empty and a linear probe always ends.  Fibonacci hashing of the key spreads the
+// neighbouring absorbers of a row over the table.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void hash_tally(uint32_t* keys, uint32_t* cnts, uint32_t mask, uint32_t shift,
+                                           uint32_t a) {
+  const uint32_t key = a + 1u;
+  uint32_t p = (key * 0x9E3779B1u) >> shift;
+  while (true) {
+    uint32_t k = keys[p];
+    if (k == 0u) {
+      k = atomicCAS(&keys[p], 0u, key);
+      if (k == 0u) k = key;  // claimed
+    }
+    if (k == key) break;
+    p = (p + 1u) & mask;
+  }
+  atomicAdd(&cnts[p], 1u);
+}
+
+// Sort a workgroup's hash table in place and return its nnz: keys[i] - 1 is
+// then the i-th absorber in ascending order (the reference's sparse() order,
+// parallelRayTracing.jl:154) and cnts[i] its count.  The occupied slots are
+// first compacted to the front, in slot order, one workgroup-wide chunk at a
+// time: every lane reads its slot before the barrier and no destination
+// passes its source.  The nnz entries are padded with ~0u keys to a power of
+// two P <= cap and bitonic-sorted by key (all keys differ).
+__device__ uint32_t hash_sort(uint32_t* keys, uint32_t* cnts, uint32_t cap, uint32_t* wave_sum) {
+  const uint32_t nthr = blockDim.x, tid = threadIdx.x, lane = lane_id();
+  const int n_waves = (int)(nthr >> 6), wave = (int)(tid >> 6);
+  const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  uint32_t run = 0;
+  for (uint32_t c0 = 0; c0 < cap; c0 += nthr) {
+    const uint32_t i = c0 + tid;
+    const uint32_t k = i < cap ? keys[i] : 0u;
+    const uint32_t n = k ? cnts[i] : 0u;
+    const uint64_t m = __ballot(k != 0u);
+    if (lane == 0) wave_sum[wave] = (uint32_t)__popcll(m);
+    __syncthreads();
+    uint32_t pos = run + (uint32_t)__popcll(m & lt_mask), tot = 0;
+    for (int w = 0; w < n_waves; ++w) {
+      const uint32_t ws = wave_sum[w];
+      pos += w < wave ? ws : 0u;
+      tot += ws;
+    }
+    if (k) {
+      keys[pos] = k;
+      cnts[pos] = n;
+    }
+    run += tot;
+    __syncthreads();
+  }
+  const uint32_t nnz = run;
+  uint32_t P = 1u;
+  while (P < nnz) P <<= 1;
+  for (uint32_t i = nnz + tid; i < P; i += nthr) keys[i] = ~0u;
+  __syncthreads();
+  for (uint32_t k = 2u; k <= P; k <<= 1)
+    for (uint32_t j = k >> 1; j > 0u; j >>= 1) {
+      for (uint32_t i = tid; i < P / 2u; i += nthr) {
+        const uint32_t lo = ((i & ~(j - 1u)) << 1) | (i & (j - 1u)), hi = lo + j;
+        const uint32_t a = keys[lo], b = keys[hi];
+        if ((a > b) == ((lo & k) == 0u)) {
+          keys[lo] = b;
+          keys[hi] = a;
+          const uint32_t t = cnts[lo];
+          cnts[lo] = cnts[hi];
+          cnts[hi] = t;
+        }
+      }
+      __syncthreads();
+    }
+  return nnz;
+}
+
+// Count of absorber a (a + 1 = key present) in a workgroup's hash table.
+__device__ __forceinline__ uint32_t hash_count(const uint32_t* keys, const uint32_t* cnts, uint32_t mask,
+                                               uint32_t shift, uint32_t a) {
+  const uint32_t key = a + 1u;
+  uint32_t p = (key * 0x9E3779B1u) >> shift;
+  while (keys[p] != key) p = (p + 1u) & mask;
+  return cnts[p];
+}
+
+// Ascending output of a hash-tallied row through an N-bit LDS bitmap (when
+// it fits next to the table): every occupied slot sets its absorber's bit;
+// each lane then owns a contiguous span of bitmap words, and one
+// workgroup-wide exclusive scan of the spans' popcounts gives every lane
+// the rank of its first absorber.  Four barriers per row instead of the
+// bitonic sort's O(log^2 nnz).  out(nnz) returns the output (cols, counts)
+// base pointers after every lane knows the row's nnz.
+template <class Out>
+__device__ __forceinline__ uint32_t hash_emit_bitmap(const uint32_t* keys, const uint32_t* cnts, uint32_t* bm,
+                                                     uint32_t cap, uint32_t shift, uint32_t n_bm_words,
+                                                     uint32_t* wave_sum, Out out) {
+  const uint32_t nthr = blockDim.x, tid = threadIdx.x, lane = lane_id();
+  const int n_waves = (int)(nthr >> 6), wave = (int)(tid >> 6);
+  for (uint32_t i = tid; i < cap; i += nthr) {
+    const uint32_t k = keys[i];
+    if (k) atomicOr(&bm[(k - 1u) >> 5], 1u << ((k - 1u) & 31u));
+  }
+  __syncthreads();
+  const uint32_t span = (n_bm_words + nthr - 1u) / nthr;
+  const uint32_t w0 = tid * span < n_bm_words ? tid * span : n_bm_words;
+  const uint32_t w1 = w0 + span < n_bm_words ? w0 + span : n_bm_words;
+  uint32_t c = 0;
+  for (uint32_t w = w0; w < w1; ++w) c += (uint32_t)__popc(bm[w]);
+  uint32_t incl = c;
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t v = __shfl_up(incl, off);
+    if ((int)lane >= off) incl += v;
+  }
+  if (lane == 63) wave_sum[wave] = incl;
+  __syncthreads();
+  uint32_t base = 0, total = 0;
+  for (int w = 0; w < n_waves; ++w) {
+    const uint32_t ws = wave_sum[w];
+    base += w < wave ? ws : 0u;
+    total += ws;
+  }
+  uint32_t *oc, *on;
+  out(total, oc, on);
+  uint32_t pos = base + incl - c;
+  for (uint32_t w = w0; w < w1; ++w) {
+    uint32_t bits = bm[w];
+    while (bits) {
+      const uint32_t a = 32u * w + (uint32_t)(__ffs(bits) - 1);
+      bits &= bits - 1u;
+      oc[pos] = a;
+      on[pos] = hash_count(keys, cnts, cap - 1u, shift, a);
+      ++pos;
+    }
+  }
+  return total;
+}
+
+template <bool UNIFORM, int TALLY, bool FAITHFUL, bool SINGLE, bool REC, bool SPLIT, bool AXIS, bool CLDS>
 __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_exchange_kernel(const DevDomain* __restrict__ Dp,
                                                                      TraceParams P, TallyParams T,
                                                                      RecordParams rec) {
@@ -169,7 +311,8 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
   const int64_t r_begin = part * chunk;
   const int64_t r_end = SPLIT ? (r_begin + chunk < P.R ? r_begin + chunk : P.R) : P.R;
   const int64_t g = P.g_begin + slot * P.g_stride;
-  const int64_t n_words = PACK16 ? (T.n_emitters + 1) / 2 : T.n_emitters;
+  constexpr bool PACK16 = TALLY == kTallyU16, HASH = TALLY == kTallyHash;
+  const int64_t n_words = HASH ? 2 * (int64_t)T.hash_cap + T.bm_words : PACK16 ? (T.n_emitters + 1) / 2 : T.n_emitters;
 
   const int nthr = (int)blockDim.x;  // 256, 512 or 1024 (launch_trace_t)
   for (int64_t w = tid; w < n_words; w += nthr) hist[w] = 0u;
@@ -210,7 +353,9 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
   uint32_t tallied = 0;
   auto tally = [&](int a) {
     if (a >= 0) {
-      if (PACK16)
+      if (HASH)
+        hash_tally(hist, hist + T.hash_cap, (uint32_t)T.hash_cap - 1u, (uint32_t)T.hash_shift, (uint32_t)a);
+      else if (PACK16)
         atomicAdd(&hist[a >> 1], 1u << ((uint32_t)(a & 1) << 4));
       else
         atomicAdd(&hist[a], 1u);
@@ -332,6 +477,71 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
   if (lane_id() == 0) atomicAdd(&s_tallied, tallied);
   __syncthreads();
 
+  // direct CSR (single-polygon domains, unsplit): the row's offset is the sum
+  // of the earlier rows' nnz; tid 0 then writes the row's bookkeeping
+  __shared__ unsigned long long s_base;
+  auto lb_finish = [&](uint32_t nnz) {
+    if (tid == 0) {
+      const unsigned long long b = s_base;
+      T.row_off[slot] = (int64_t)b;
+      const unsigned long long lost = (unsigned long long)(T.R - (int64_t)s_tallied);
+      if (lost) {
+        atomicAdd(&T.totals[1], lost);
+        atomicMax(&T.totals[2], lost);
+      }
+      if (slot == T.n_rows - 1) {
+        T.row_off[T.n_rows] = (int64_t)(b + nnz);
+        T.totals[0] = b + nnz;
+      }
+    }
+  };
+  if constexpr (HASH) {
+    const uint32_t cap = (uint32_t)T.hash_cap;
+    const uint32_t* keys = hist;
+    const uint32_t* cnts = hist + cap;
+    // output pointers of the row (or part); the look-back runs once every lane knows nnz
+    auto out = [&](uint32_t nnz, uint32_t*& oc, uint32_t*& on) {
+      if (SPLIT) {
+        const int64_t o = slot * T.row_cap + part * chunk;
+        oc = T.stage_cols + o;
+        on = T.stage_cnt + o;
+      } else if (SINGLE && T.lb_status) {
+        if (tid == 0) s_base = lookback_offset(T.lb_status, slot, nnz, &T.totals[3], T.lb_wait_ticks);
+        __syncthreads();
+        oc = T.out_cols + s_base;
+        on = T.out_cnt + s_base;
+      } else {
+        oc = T.stage_cols + slot * T.row_cap;
+        on = T.stage_cnt + slot * T.row_cap;
+      }
+    };
+    uint32_t nnz;
+    if (T.bm_words > 0) {
+      nnz = hash_emit_bitmap(keys, cnts, hist + 2 * cap, cap, (uint32_t)T.hash_shift, (uint32_t)T.bm_words, wave_sum,
+                             out);
+    } else {
+      nnz = hash_sort(hist, hist + cap, cap, wave_sum);
+      uint32_t *oc, *on;
+      out(nnz, oc, on);
+      for (uint32_t i = (uint32_t)tid; i < nnz; i += (uint32_t)nthr) {
+        oc[i] = keys[i] - 1u;
+        on[i] = cnts[i];
+      }
+    }
+    if (SPLIT) {
+      if (tid == 0) {
+        T.part_nnz[blockIdx.x] = nnz;
+        atomicAdd(&T.row_tallied[slot], s_tallied);
+      }
+    } else if (SINGLE && T.lb_status) {
+      lb_finish(nnz);
+    } else if (tid == 0) {
+      T.row_nnz[slot] = nnz;
+      T.row_tallied[slot] = s_tallied;
+    }
+    return;
+  }
+
   if (SPLIT) {
     // add this slice's nonzero counters into the row's dense buffer
     uint32_t* dense = T.dense + slot * T.n_emitters;
@@ -354,27 +564,12 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
     hi = PACK16 ? (v >> 16) : 0u;
   };
   if (SINGLE && T.lb_status) {  // (host: single-polygon domains only; keeps the other kernels lean)
-    // direct CSR: the row's offset is the sum of the earlier rows' nnz
-    __shared__ unsigned long long s_base;
     auto base_of = [&](uint32_t nnz) -> uint64_t {
       if (tid == 0) s_base = lookback_offset(T.lb_status, slot, nnz, &T.totals[3], T.lb_wait_ticks);
       __syncthreads();
       return s_base;
     };
-    const uint32_t nnz = compact_row<PACK16>(n_words, count2, T.out_cols, T.out_cnt, wave_sum, base_of);
-    if (tid == 0) {
-      const unsigned long long b = s_base;
-      T.row_off[slot] = (int64_t)b;
-      const unsigned long long lost = (unsigned long long)(T.R - (int64_t)s_tallied);
-      if (lost) {
-        atomicAdd(&T.totals[1], lost);
-        atomicMax(&T.totals[2], lost);
-      }
-      if (slot == T.n_rows - 1) {
-        T.row_off[T.n_rows] = (int64_t)(b + nnz);
-        T.totals[0] = b + nnz;
-      }
-    }
+    lb_finish(compact_row<PACK16>(n_words, count2, T.out_cols, T.out_cnt, wave_sum, base_of));
     return;
   }
   uint32_t nnz = compact_row<PACK16>(n_words, count2, T.stage_cols + slot * T.row_cap, T.stage_cnt + slot * T.row_cap,
@@ -422,6 +617,81 @@ __global__ __launch_bounds__(kTraceThreads) void row_compact_kernel(TallyParams 
   uint32_t nnz = compact_row_global(T.n_emitters, dense, T.stage_cols + slot * T.row_cap,
                                     T.stage_cnt + slot * T.row_cap, wave_sum, &s_running);
   if (threadIdx.x == 0) T.row_nnz[slot] = nnz;
+}
+
+// Split rows with hash tallies: merge the row's `split` sorted part lists
+// (stage_*[slot*row_cap + p*chunk ..], part_nnz) into one ascending list in
+// the row's staging slot.  Each entry goes to its rank in the merged order
+// (its index in its own list plus, by binary search, the entries of the
+// other lists that precede it: equal keys of earlier parts first), in the
+// row's scratch; equal keys (at most one per part) are then adjacent and the
+// run heads, with their summed counts, are compacted back into the slot.
+__global__ __launch_bounds__(kTraceThreads) void part_merge_kernel(TallyParams T) {
+  __shared__ uint32_t wave_sum[kTraceThreads / 64];
+  const int64_t slot = blockIdx.x, S = T.split;
+  const int64_t chunk = (T.R + S - 1) / S;
+  const uint32_t tid = threadIdx.x, lane = lane_id();
+  const int wave = (int)(tid >> 6);
+  const uint32_t* pn = T.part_nnz + slot * S;
+  uint32_t* sc = T.stage_cols + slot * T.row_cap;
+  uint32_t* sn = T.stage_cnt + slot * T.row_cap;
+  uint32_t* xk = T.dense + slot * T.row_cap;
+  uint32_t* xn = T.dense + (T.n_rows + slot) * T.row_cap;
+  uint32_t total = 0;
+  for (int64_t p = 0; p < S; ++p) {
+    const uint32_t n = pn[p];
+    total += n;
+    const uint32_t* lk = sc + p * chunk;
+    for (uint32_t i = tid; i < n; i += kTraceThreads) {
+      const uint32_t k = lk[i];
+      uint32_t rank = i;
+      for (int64_t q = 0; q < S; ++q) {
+        if (q == p) continue;
+        const uint32_t* qk = sc + q * chunk;
+        uint32_t lo = 0, hi = pn[q];
+        while (lo < hi) {
+          const uint32_t mid = (lo + hi) >> 1;
+          const uint32_t v = qk[mid];
+          if (q < p ? v <= k : v < k) lo = mid + 1;
+          else hi = mid;
+        }
+        rank += lo;
+      }
+      xk[rank] = k;
+      xn[rank] = sn[p * chunk + i];
+    }
+  }
+  __syncthreads();  // every part entry read and scattered before the slot is rewritten
+  const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  uint32_t run = 0;
+  for (uint32_t j0 = 0; j0 < total; j0 += kTraceThreads) {
+    const uint32_t j = j0 + tid;
+    bool head = false;
+    uint32_t k = 0, c = 0;
+    if (j < total) {
+      k = xk[j];
+      head = j == 0 || xk[j - 1] != k;
+      if (head) {
+        c = xn[j];
+        for (uint32_t t = j + 1; t < total && xk[t] == k; ++t) c += xn[t];
+      }
+    }
+    const uint64_t m = __ballot(head);
+    if (lane == 0) wave_sum[wave] = (uint32_t)__popcll(m);
+    __syncthreads();
+    uint32_t pos = run + (uint32_t)__popcll(m & lt_mask), tot = 0;
+    for (int w = 0; w < kTraceThreads / 64; ++w) {
+      pos += w < wave ? wave_sum[w] : 0u;
+      tot += wave_sum[w];
+    }
+    if (head) {
+      sc[pos] = k;
+      sn[pos] = c;
+    }
+    run += tot;
+    __syncthreads();
+  }
+  if (tid == 0) T.row_nnz[slot] = run;
 }
 
 // Exclusive scan of row_nnz -> row_off[n_rows+1]; totals of lost rays.
@@ -491,9 +761,9 @@ __global__ __launch_bounds__(256) void csr_pack_kernel(const uint32_t* __restric
 // ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
-template <bool UNIFORM, bool PACK16, bool FAITHFUL, bool SINGLE, bool REC, bool SPLIT, bool AXIS, bool CLDS = false>
+template <bool UNIFORM, int TALLY, bool FAITHFUL, bool SINGLE, bool REC, bool SPLIT, bool AXIS, bool CLDS = false>
 static hipError_t launch_trace_t(const LaunchCfg& L) {
-  auto kern = trace_exchange_kernel<UNIFORM, PACK16, FAITHFUL, SINGLE, REC, SPLIT, AXIS, CLDS>;
+  auto kern = trace_exchange_kernel<UNIFORM, TALLY, FAITHFUL, SINGLE, REC, SPLIT, AXIS, CLDS>;
   if (L.lds_bytes > 64 * 1024) {  // (occupancy queries above 64 KiB need the attribute first)
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)L.lds_bytes);
@@ -515,45 +785,51 @@ static hipError_t launch_trace_t(const LaunchCfg& L) {
       threads = t;
     }
   }
+  if (L.threads == 256 || L.threads == 512 || L.threads == 1024) threads = L.threads;
   const size_t lds = lds_for(threads);
   hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(threads), lds, L.stream, L.D, L.P, L.T, L.rec);
   return hipGetLastError();
 }
 
-template <bool UNIFORM, bool PACK16, bool FAITHFUL, bool AXIS>
+template <bool UNIFORM, int TALLY, bool FAITHFUL, bool AXIS>
 static hipError_t launch_trace_a(const LaunchCfg& L) {
   // SINGLE kernels with CLDS = the lattice locate (LAT; axis-aligned only)
   if (L.T.split > 1) {
     if constexpr (AXIS) {
-      if (L.single && L.clds) return launch_trace_t<UNIFORM, PACK16, FAITHFUL, true, false, true, AXIS, true>(L);
+      if (L.single && L.clds) return launch_trace_t<UNIFORM, TALLY, FAITHFUL, true, false, true, AXIS, true>(L);
     }
-    if (L.single) return launch_trace_t<UNIFORM, PACK16, FAITHFUL, true, false, true, AXIS>(L);
-    if (L.clds) return launch_trace_t<UNIFORM, PACK16, FAITHFUL, false, false, true, AXIS, true>(L);
-    return launch_trace_t<UNIFORM, PACK16, FAITHFUL, false, false, true, AXIS>(L);
+    if (L.single) return launch_trace_t<UNIFORM, TALLY, FAITHFUL, true, false, true, AXIS>(L);
+    if (L.clds) return launch_trace_t<UNIFORM, TALLY, FAITHFUL, false, false, true, AXIS, true>(L);
+    return launch_trace_t<UNIFORM, TALLY, FAITHFUL, false, false, true, AXIS>(L);
   }
   if constexpr (AXIS) {
-    if (L.single && L.clds) return launch_trace_t<UNIFORM, PACK16, FAITHFUL, true, false, false, AXIS, true>(L);
+    if (L.single && L.clds) return launch_trace_t<UNIFORM, TALLY, FAITHFUL, true, false, false, AXIS, true>(L);
   }
-  if (L.single) return launch_trace_t<UNIFORM, PACK16, FAITHFUL, true, false, false, AXIS>(L);
-  if (L.clds) return launch_trace_t<UNIFORM, PACK16, FAITHFUL, false, false, false, AXIS, true>(L);
-  return launch_trace_t<UNIFORM, PACK16, FAITHFUL, false, false, false, AXIS>(L);
+  if (L.single) return launch_trace_t<UNIFORM, TALLY, FAITHFUL, true, false, false, AXIS>(L);
+  if (L.clds) return launch_trace_t<UNIFORM, TALLY, FAITHFUL, false, false, false, AXIS, true>(L);
+  return launch_trace_t<UNIFORM, TALLY, FAITHFUL, false, false, false, AXIS>(L);
 }
 
-template <bool UNIFORM, bool PACK16, bool FAITHFUL>
+template <bool UNIFORM, int TALLY, bool FAITHFUL>
 static hipError_t launch_trace_u(const LaunchCfg& L) {
   // Recording is a plotting aid: generic (non-SINGLE, unsplit, general
   // polygon) instances carry it.
-  if (L.rec.n > 0) return launch_trace_t<UNIFORM, PACK16, FAITHFUL, false, true, false, false>(L);
-  return L.axis ? launch_trace_a<UNIFORM, PACK16, FAITHFUL, true>(L) : launch_trace_a<UNIFORM, PACK16, FAITHFUL, false>(L);
+  if (L.rec.n > 0) return launch_trace_t<UNIFORM, TALLY, FAITHFUL, false, true, false, false>(L);
+  return L.axis ? launch_trace_a<UNIFORM, TALLY, FAITHFUL, true>(L) : launch_trace_a<UNIFORM, TALLY, FAITHFUL, false>(L);
+}
+
+template <bool UNIFORM, bool FAITHFUL>
+static hipError_t launch_trace_f(const LaunchCfg& L) {
+  switch (L.tally) {
+    case kTallyU16: return launch_trace_u<UNIFORM, kTallyU16, FAITHFUL>(L);
+    case kTallyHash: return launch_trace_u<UNIFORM, kTallyHash, FAITHFUL>(L);
+    default: return launch_trace_u<UNIFORM, kTallyU32, FAITHFUL>(L);
+  }
 }
 
 hipError_t launch_trace(const LaunchCfg& L) {
-  if (L.faithful) {
-    if (L.uniform) return L.pack16 ? launch_trace_u<true, true, true>(L) : launch_trace_u<true, false, true>(L);
-    return L.pack16 ? launch_trace_u<false, true, true>(L) : launch_trace_u<false, false, true>(L);
-  }
-  if (L.uniform) return L.pack16 ? launch_trace_u<true, true, false>(L) : launch_trace_u<true, false, false>(L);
-  return L.pack16 ? launch_trace_u<false, true, false>(L) : launch_trace_u<false, false, false>(L);
+  if (L.faithful) return L.uniform ? launch_trace_f<true, true>(L) : launch_trace_f<false, true>(L);
+  return L.uniform ? launch_trace_f<true, false>(L) : launch_trace_f<false, false>(L);
 }
 
 // One wave per row: the row's tallied rays (exact integer sum of its counts),
@@ -583,6 +859,11 @@ hipError_t launch_counts_to_F(const int64_t* row_off, const uint32_t* cnt, int64
 
 hipError_t launch_compact(const TallyParams& T, hipStream_t stream) {
   hipLaunchKernelGGL(row_compact_kernel, dim3((unsigned)T.n_rows), dim3(kTraceThreads), 0, stream, T);
+  return hipGetLastError();
+}
+
+hipError_t launch_part_merge(const TallyParams& T, hipStream_t stream) {
+  hipLaunchKernelGGL(part_merge_kernel, dim3((unsigned)T.n_rows), dim3(kTraceThreads), 0, stream, T);
   return hipGetLastError();
 }
 

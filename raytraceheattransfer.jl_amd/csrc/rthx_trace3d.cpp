@@ -552,7 +552,7 @@ RTHX_EXPORT int rthx_trace_exchange_3d(rthx_scene3d* sc, const rthx_trace_args* 
   HIP_TRY(hipEventRecord(sc->ev[1], st), "hipEventRecord");
   int64_t totals[4] = {0, 0, 0, 0};
   {
-    int rc = rthx::finish_staged(res, T, true, st, sc->ev[2], totals);
+    int rc = rthx::finish_staged(res, T, rthx::kMergeDense, st, sc->ev[2], totals);
     if (rc) return rc;
   }
   float ms_trace = 0.f, ms_pack = 0.f;

@@ -260,8 +260,11 @@ def test_errors_do_not_crash(hip):
     dd.close()
 
 
-def test_lds_limit_reports_erange(hip):
-    """N above the LDS row-histogram limit is refused, not faulted."""
+def test_large_n_recording_limit_reports_erange(hip):
+    """N above the packed LDS histogram (hash tallies): the recorder's
+    kernels are unsplit, so recording with more rays per emitter than one
+    table holds (12,288) is refused, not faulted; without recording the same
+    call traces."""
     import ctypes as C
 
     from rthx import abi
@@ -270,8 +273,11 @@ def test_lds_limit_reports_erange(hip):
     flat = dom.flat()
     dd = hip.DeviceDomain(flat, 0)
     res = hip.DeviceResult()
-    a, _k = _args(hip, flat, 10, end=1)
+    a, _k = _args(hip, flat, 13_000, end=1, rec=[0])
     assert hip.load().rthx_trace_exchange(dd.handle, C.byref(a), res.handle) == abi.RTHX_ERANGE
+    a, _k = _args(hip, flat, 13_000, end=1)
+    assert hip.load().rthx_trace_exchange(dd.handle, C.byref(a), res.handle) == abi.RTHX_OK
+    assert res.info()["rays_traced"] == 13_000
     res.close()
     dd.close()
 

@@ -9,6 +9,7 @@ C3  51x51 kappa=1 sigma_s=5 (beta=6)            exchange path: no re-scatter
 C5  201x201 8-band greenhouse, 67 layers        every band spatially non-uniform;
                                                rays per band as the reference
                                                (parallelRayTracing.jl:6,22)
+L301 301x301 grey kappa=1 (N = 91805)          large N: LDS hash row tallies
 """
 import argparse
 import os
@@ -77,6 +78,8 @@ def main():
         run("C2", H.square_domain(101), rays, args.steps)
     if "C3" in only:
         run("C3", H.square_domain(51, kappa=1.0, sigma_s=5.0), rays, args.steps)
+    if "L301" in only:
+        run("L301", H.square_domain(301), rays, args.steps)
     if "C5" in only:
         run("C5", H.greenhouse_domain(), rays, max(1, args.steps // 4), bins=tuple(int(b) for b in args.bins.split(",")))
 
