@@ -379,20 +379,106 @@ RTHX_EXPORT int rthx_domain_create(const rthx_domain_desc* desc, int32_t device,
       std::memcpy(b + L.off_first, s.fine_offset, (nc + 1) * sizeof(int32_t));
       std::memcpy(b + L.off_solid, csolid.data(), nc * sizeof(uint32_t));
       std::memcpy(b + L.off_cells, gcells.data(), ncells * sizeof(rthx::CellRec));
-      std::vector<double> cbeta((size_t)s.n_bins * nc, -1.0);
-      for (int bn = 0; bn < s.n_bins; ++bn)
-        for (size_t c = 0; c < nc; ++c) {
-          const int f0 = s.fine_offset[c], f1 = s.fine_offset[c + 1];
-          if (f1 <= f0) continue;
-          const double* bb = s.beta + (size_t)bn * nf;
-          bool same = true;
-          for (int f = f0 + 1; f < f1 && same; ++f) same = bb[f] == bb[f0];
-          if (same) cbeta[(size_t)bn * nc + c] = bb[f0];
-        }
       UP(blob.data(), blob.size(), D.c_blob);
-      UP(cbeta.data(), cbeta.size(), D.c_beta);
     }
     D.cl = L;
+  }
+  if (nc >= 2) {
+    std::vector<double> cbeta((size_t)s.n_bins * nc, -1.0);
+    for (int bn = 0; bn < s.n_bins; ++bn)
+      for (size_t c = 0; c < nc; ++c) {
+        const int f0 = s.fine_offset[c], f1 = s.fine_offset[c + 1];
+        const double* bb = s.beta + (size_t)bn * nf;
+        bool same = true;
+        for (int f = f0 + 1; f < f1 && same; ++f) same = bb[f] == bb[f0];
+        if (same) cbeta[(size_t)bn * nc + c] = bb[f0];
+      }
+    UP(cbeta.data(), cbeta.size(), D.c_beta);
+  }
+  // Multi-polygon lattice (rthx_device.h MLatLayout; MLAT kernels): the
+  // coarse rectangles are the boxes of a coarse lattice, and the fine
+  // rectangles of each are, x fastest, the boxes of one global fine lattice
+  // inside it.
+  if (!d->single_convex && d->axis_rect && nc >= 2 && !env_flag("RTHX_NO_MLAT")) {
+    auto lines = [](const std::vector<rthx::DevPoly>& q, size_t n, bool xdir) {
+      std::vector<double> v;
+      for (size_t p = 0; p < n; ++p) {
+        v.push_back(xdir ? q[p].x[0] : q[p].y[0]);
+        v.push_back(xdir ? q[p].x[1] : q[p].y[2]);
+      }
+      std::sort(v.begin(), v.end());
+      v.erase(std::unique(v.begin(), v.end()), v.end());
+      return v;
+    };
+    const std::vector<double> xs = lines(fpoly, nf, true), ys = lines(fpoly, nf, false);
+    const std::vector<double> cxs = lines(cpoly, nc, true), cys = lines(cpoly, nc, false);
+    const int64_t nx = (int64_t)xs.size() - 1, ny = (int64_t)ys.size() - 1;
+    const int64_t ncx = (int64_t)cxs.size() - 1, ncy = (int64_t)cys.size() - 1;
+    auto index_of = [](const std::vector<double>& v, double x) -> int64_t {
+      const auto it = std::lower_bound(v.begin(), v.end(), x);
+      return (it != v.end() && *it == x) ? (int64_t)(it - v.begin()) : -1;
+    };
+    bool ok = ncx >= 1 && ncy >= 1 && ncx * ncy == (int64_t)nc && nx <= 65536 && ny <= 65536;
+    std::vector<int32_t> cmap(ok ? (size_t)(ncx * ncy) : 0, -1);
+    std::vector<rthx::MCoarse> info(nc);
+    for (size_t c = 0; c < nc && ok; ++c) {
+      const rthx::DevPoly& q = cpoly[c];
+      const int64_t ci = index_of(cxs, q.x[0]), cj = index_of(cys, q.y[0]);
+      ok = ci >= 0 && cj >= 0 && ci < ncx && cj < ncy && cxs[ci + 1] == q.x[1] && cys[cj + 1] == q.y[2] &&
+           cmap[cj * ncx + ci] < 0;
+      if (!ok) break;
+      cmap[cj * ncx + ci] = (int32_t)c;
+      const int64_t i0 = index_of(xs, q.x[0]), i1 = index_of(xs, q.x[1]);
+      const int64_t j0 = index_of(ys, q.y[0]), j1 = index_of(ys, q.y[2]);
+      const int f0 = s.fine_offset[c], f1 = s.fine_offset[c + 1];
+      ok = i0 >= 0 && i1 > i0 && j0 >= 0 && j1 > j0 && (i1 - i0) * (j1 - j0) == f1 - f0;
+      for (int f = f0; f < f1 && ok; ++f) {
+        const int64_t i = i0 + (f - f0) % (i1 - i0), j = j0 + (f - f0) / (i1 - i0);
+        ok = fpoly[f].x[0] == xs[i] && fpoly[f].x[1] == xs[i + 1] && fpoly[f].y[0] == ys[j] && fpoly[f].y[2] == ys[j + 1];
+      }
+      info[c] = rthx::MCoarse{f0, (int32_t)i0, (int32_t)j0, (int32_t)(i1 - i0), (int32_t)(j1 - j0), (int32_t)ci,
+                              (int32_t)cj, csolid[c]};
+    }
+    if (ok) {
+      auto a16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
+      rthx::MLatLayout G{};
+      G.nx = (int32_t)nx;
+      G.ny = (int32_t)ny;
+      G.ncx = (int32_t)ncx;
+      G.ncy = (int32_t)ncy;
+      size_t off = a16(8 * xs.size());
+      G.off_ys = (int32_t)off;
+      off = a16(off + 8 * ys.size());
+      G.off_cxs = (int32_t)off;
+      off = a16(off + 8 * cxs.size());
+      G.off_cys = (int32_t)off;
+      off = a16(off + 8 * cys.size());
+      G.off_cmap = (int32_t)off;
+      off = a16(off + 4 * cmap.size());
+      G.off_cinfo = (int32_t)off;
+      off = a16(off + sizeof(rthx::MCoarse) * nc);
+      G.off_beta = (int32_t)off;
+      G.blob_bytes = (int32_t)off;
+      off = a16(off + 8 * nc);
+      G.inv_x = (double)nx / (xs[nx] - xs[0]);
+      G.inv_y = (double)ny / (ys[ny] - ys[0]);
+      G.inv_cx = (double)ncx / (cxs[ncx] - cxs[0]);
+      G.inv_cy = (double)ncy / (cys[ncy] - cys[0]);
+      if (off <= rthx::kMaxCoarseLdsBytes) {
+        G.bytes = (int32_t)off;
+        std::vector<uint4> blob((size_t)G.blob_bytes / 16);
+        char* b = reinterpret_cast<char*>(blob.data());
+        std::memset(b, 0, (size_t)G.blob_bytes);
+        std::memcpy(b, xs.data(), 8 * xs.size());
+        std::memcpy(b + G.off_ys, ys.data(), 8 * ys.size());
+        std::memcpy(b + G.off_cxs, cxs.data(), 8 * cxs.size());
+        std::memcpy(b + G.off_cys, cys.data(), 8 * cys.size());
+        std::memcpy(b + G.off_cmap, cmap.data(), 4 * cmap.size());
+        std::memcpy(b + G.off_cinfo, info.data(), sizeof(rthx::MCoarse) * nc);
+        UP(blob.data(), blob.size(), D.ml_blob);
+        D.ml = G;
+      }
+    }
   }
   // Lattice of a single axis-aligned coarse rectangle (rthx_device.h
   // LatticeLayout; LAT kernels): the fine cells must be exactly the nx x ny
@@ -543,7 +629,8 @@ uint64_t lookback_wait_ticks() {
 struct TracePlan {
   int64_t N = 0, R = 0, end = 0, n_rows = 0, split = 1, row_cap = 1, hash_cap = 0, bm_words = 0;
   int tally = rthx::kTallyU16;
-  bool clds = false, recording = false, uniform = true;
+  int clds = 0;  // rthx_kernels.h LaunchCfg::clds
+  bool recording = false, uniform = true;
   size_t lds_bytes = 0, cl_offset = 0;
 };
 
@@ -609,14 +696,21 @@ int plan_trace(const rthx_domain* dom, const rthx_trace_args* a, TracePlan& p) {
   // multi-polygon domains: the coarse mesh goes behind the histogram in LDS
   // when it fits (CLDS kernels, rthx_device.h segment_cl)
   p.cl_offset = (p.lds_bytes + 15) & ~(size_t)15;
-  p.clds = !dom->single_convex && dom->D.cl.bytes > 0 &&
-           p.cl_offset + (size_t)dom->D.cl.bytes + rthx::kStaticLdsBytes <= rthx::kMaxLdsBytes &&
-           !env_flag("RTHX_NO_CLDS");
-  if (p.clds) p.lds_bytes = p.cl_offset + (size_t)dom->D.cl.bytes;
+  const bool axis = dom->axis_rect && !env_flag("RTHX_NO_AXIS");
+  const bool no_clds = env_flag("RTHX_NO_CLDS");  // (tests: the global-memory multi-polygon kernels)
+  if (!dom->single_convex && axis && dom->D.ml.bytes > 0 && !no_clds &&
+      p.cl_offset + (size_t)dom->D.ml.bytes + rthx::kStaticLdsBytes <= rthx::kMaxLdsBytes) {
+    p.clds = 2;  // multi-polygon lattice (MLAT kernels)
+    p.lds_bytes = p.cl_offset + (size_t)dom->D.ml.bytes;
+  } else if (!dom->single_convex && dom->D.cl.bytes > 0 &&
+             p.cl_offset + (size_t)dom->D.cl.bytes + rthx::kStaticLdsBytes <= rthx::kMaxLdsBytes && !no_clds) {
+    p.clds = 1;
+    p.lds_bytes = p.cl_offset + (size_t)dom->D.cl.bytes;
+  }
   // single axis-aligned rectangles: the lattice behind the histogram (LAT kernels)
   if (dom->single_convex && dom->D.lat.bytes > 0 && !p.recording &&
       p.cl_offset + (size_t)dom->D.lat.bytes + rthx::kStaticLdsBytes <= rthx::kMaxLdsBytes) {
-    p.clds = true;
+    p.clds = 1;
     p.lds_bytes = p.cl_offset + (size_t)dom->D.lat.bytes;
   }
   p.uniform = dom->uniform_beta[a->bin] > -0.1;  // traceRay.jl:4

@@ -94,6 +94,30 @@ struct LatticeLayout {
   double inv_x, inv_y;       // nx / (xs[nx] - xs[0]), ny / (ys[ny] - ys[0]): first guess of the cell
 };
 
+// Lattice form of a multi-polygon domain (MLAT kernels): the coarse polygons
+// are the ncx x ncy boxes of a coarse lattice (cxs, cys) and the fine
+// polygons of every coarse box are the boxes of one global fine lattice (xs,
+// ys) inside it, x fastest (meshQuad.jl:139-179) -- a layered medium such as
+// the greenhouse (67 layers of 201 x 3 cells: one 201 x 201 lattice).  Blob:
+// xs[nx+1], ys[ny+1], cxs[ncx+1], cys[ncy+1] (f64), cmap[ncy ncx] (i32:
+// coarse polygon of box (ci, cj)), MCoarse[n_coarse], then (staged per bin)
+// one beta per coarse polygon (-1 when its fine betas differ).
+struct MCoarse {
+  int32_t first;     // first fine polygon
+  int32_t i0, j0;    // its fine lattice box
+  int32_t nxf, nyf;  // fine boxes per row / column
+  int32_t ci, cj;    // coarse lattice box
+  uint32_t solid;    // bit w: coarse wall w solid
+};
+
+struct MLatLayout {
+  int32_t bytes;       // LDS block incl. the betas (0: not a lattice)
+  int32_t blob_bytes;  // staged from ml_blob
+  int32_t nx, ny, ncx, ncy;
+  int32_t off_ys, off_cxs, off_cys, off_cmap, off_cinfo, off_beta;
+  double inv_x, inv_y, inv_cx, inv_cy;  // first guesses of lattice_index
+};
+
 struct DevDomain {
   int32_t n_coarse, n_fine, n_surfaces, n_bins;
   // coarse polygons
@@ -132,6 +156,9 @@ struct DevDomain {
   const uint4 RTHX_GLOBAL* lat_blob;   // [lat.bytes / 16]
   const int32_t RTHX_GLOBAL* lat_map;  // [nx ny] when !identity
   LatticeLayout lat;
+  // lattice of a multi-polygon domain (MLatLayout)
+  const uint4 RTHX_GLOBAL* ml_blob;    // [ml.blob_bytes / 16]
+  MLatLayout ml;
 };
 
 struct TraceParams {
@@ -344,10 +371,8 @@ __device__ __forceinline__ double dist_to_polygon(double px, double py, double d
 // den_i = d.n_i is -dy, dx, dy, -dx (products with +-1 and +-0 are exact), so
 // the same candidates, comparisons and first-index ties as dist_to_polygon,
 // with 4 of its 16 geometry reads and no multiplies for num/den.
-template <class Poly>
-__device__ __forceinline__ double dist_to_rect(double px, double py, double dx, double dy, const Poly& q,
-                                               int& widx) {
-  const double x0 = q.x[0], x1 = q.x[1], y0 = q.y[0], y1 = q.y[2];
+__device__ __forceinline__ double dist_to_box(double px, double py, double dx, double dy, double x0, double x1,
+                                              double y0, double y1, int& widx) {
   const double num[4] = {py - y0, x1 - px, y1 - py, px - x0};
   const double den[4] = {-dy, dx, dy, -dx};
   double bn = 1.0, bd = 0.0;
@@ -364,6 +389,12 @@ __device__ __forceinline__ double dist_to_rect(double px, double py, double dx, 
   if (bd == 0.0) return __builtin_inf();
   double u = bn / bd;
   return u > 0.0 ? u : __builtin_inf();
+}
+
+template <class Poly>
+__device__ __forceinline__ double dist_to_rect(double px, double py, double dx, double dy, const Poly& q,
+                                               int& widx) {
+  return dist_to_box(px, py, dx, dy, q.x[0], q.x[1], q.y[0], q.y[2], widx);
 }
 
 template <bool AXIS, class Poly>
@@ -851,20 +882,28 @@ __device__ __forceinline__ CoarseLds coarse_lds_view(const char RTHX_LDS* base, 
   return v;
 }
 
-// segment() with the coarse mesh in LDS.  One more shortcut of the variable
-// path (traceRay.jl:87-103): when every fine polygon of coarse c has the same
+// segment() with the coarse mesh in LDS, in two parts.  walk_cl runs a
+// segment up to its end point: it returns kRayContinue after a crossing (p,
+// c, S / acc updated), -1 for a lost ray, or kRayEndGas / kRayEndWall with p
+// moved to the end point inside coarse c; end_cl then finds the absorber
+// (the fine polygon holding p and, for a wall, the fine wall).  The trace
+// kernel runs end_cl for many lanes at once (the ends of a wave's rays fall
+// on different iterations, and the fine locate would otherwise run for one
+// or two lanes per iteration).  One more shortcut of the variable path
+// (traceRay.jl:87-103): when every fine polygon of coarse c has the same
 // beta in this bin (the greenhouse's layers), beta is that value whichever
 // fine polygon holds the segment start, so the start is not located.  The
 // reference would lose a ray whose start lies in no fine polygon of c; such a
 // point lies within rounding of c's boundary (the fine polygons tile c), and
 // here that ray continues.
+constexpr int kRayEndGas = -4;   // walk_cl: the ray is absorbed by the gas at p (coarse c)
+constexpr int kRayEndWall = -5;  // walk_cl: the ray hits a solid wall of coarse c at p
+
 template <bool UNIFORM, bool AXIS>
-__device__ __forceinline__ int segment_cl(const DevDomain& D, const TraceParams& P, const CoarseLds& L, int& c,
-                                          double& px, double& py, double dx, double dy, double& S, double& acc) {
+__device__ __forceinline__ int walk_cl(const DevDomain& D, const TraceParams& P, const CoarseLds& L, int& c,
+                                       double& px, double& py, double dx, double dy, double& S, double& acc) {
   const double eta = P.eta;
   int k;
-  const int first = L.first[c];
-  const int count = L.first[c + 1] - first;
   const double u = dist_to_cell<AXIS>(px, py, dx, dy, L.poly[c], k);
   const uint32_t solid = L.solid[c];
   bool gas;
@@ -874,8 +913,9 @@ __device__ __forceinline__ int segment_cl(const DevDomain& D, const TraceParams&
   } else {
     beta = L.beta[c];
     if (beta < 0.0) {
+      const int first = L.first[c];
       const DevGrid fg = ld(L.fgrid + c);
-      const int f0 = locate_fine(D, fg, first, count, px, py);
+      const int f0 = locate_fine(D, fg, first, L.first[c + 1] - first, px, py);
       if (f0 < 0) return -1;
       beta = D.beta[(size_t)P.bin * D.n_fine + first + f0];
     }
@@ -887,14 +927,7 @@ __device__ __forceinline__ int segment_cl(const DevDomain& D, const TraceParams&
     const double t = gas ? (UNIFORM ? S : (S - acc) / beta) - eta : u - eta;
     px = px + __dmul_rn(t, dx);
     py = py + __dmul_rn(t, dy);
-    const DevGrid fg = ld(L.fgrid + c);
-    const int f = locate_fine(D, fg, first, count, px, py);
-    if (f < 0) return -1;
-    const int fg_idx = first + f;
-    if (gas) return D.n_surfaces + fg_idx;
-    int w;
-    dist_to_cell<AXIS>(px, py, dx, dy, D.f_poly[fg_idx], w);
-    return D.f_surf[4 * fg_idx + w];
+    return gas ? kRayEndGas : kRayEndWall;
   }
   const double t = u + eta;
   px = px + __dmul_rn(t, dx);
@@ -902,6 +935,120 @@ __device__ __forceinline__ int segment_cl(const DevDomain& D, const TraceParams&
   if (UNIFORM) S -= u; else acc += tau_b;
   c = locate(D.c_grid, D, L.cells, L.poly, L.bbox, 0, D.n_coarse, px, py);
   return c < 0 ? -1 : kRayContinue;
+}
+
+template <bool AXIS>
+__device__ __forceinline__ int end_cl(const DevDomain& D, const CoarseLds& L, int c, double px, double py, double dx,
+                                      double dy, bool gas) {
+  const int first = L.first[c];
+  const DevGrid fg = ld(L.fgrid + c);
+  const int f = locate_fine(D, fg, first, L.first[c + 1] - first, px, py);
+  if (f < 0) return -1;
+  const int fg_idx = first + f;
+  if (gas) return D.n_surfaces + fg_idx;
+  int w;
+  dist_to_cell<AXIS>(px, py, dx, dy, D.f_poly[fg_idx], w);
+  return D.f_surf[4 * fg_idx + w];
+}
+
+template <bool UNIFORM, bool AXIS>
+__device__ __forceinline__ int segment_cl(const DevDomain& D, const TraceParams& P, const CoarseLds& L, int& c,
+                                          double& px, double& py, double dx, double dy, double& S, double& acc) {
+  const int a = walk_cl<UNIFORM, AXIS>(D, P, L, c, px, py, dx, dy, S, acc);
+  return (a == kRayEndGas || a == kRayEndWall) ? end_cl<AXIS>(D, L, c, px, py, dx, dy, a == kRayEndGas) : a;
+}
+
+// ---------------------------------------------------------------------------
+// MLAT kernels: the walk of walk_cl / end_cl on a multi-polygon lattice
+// (MLatLayout, staged in LDS).  The coarse polygon after a crossing is the
+// coarse lattice box holding the nudged point and the fine polygon the fine
+// lattice box -- findFace2D's first hit, since the half-open boxes of a
+// lattice partition its rectangle (see segment_lat) -- and a point in no box
+// of the coarse polygon (within rounding of its boundary) is in none of its
+// fine polygons either: lost, as in the reference.
+// ---------------------------------------------------------------------------
+struct MLatLds {
+  const double RTHX_LDS* xs;
+  const double RTHX_LDS* ys;
+  const double RTHX_LDS* cxs;
+  const double RTHX_LDS* cys;
+  const int32_t RTHX_LDS* cmap;
+  const MCoarse RTHX_LDS* cinfo;
+  const double RTHX_LDS* beta;
+};
+
+__device__ __forceinline__ MLatLds mlat_lds_view(const char RTHX_LDS* base, const MLatLayout& G) {
+  MLatLds v;
+  v.xs = (const double RTHX_LDS*)base;
+  v.ys = (const double RTHX_LDS*)(base + G.off_ys);
+  v.cxs = (const double RTHX_LDS*)(base + G.off_cxs);
+  v.cys = (const double RTHX_LDS*)(base + G.off_cys);
+  v.cmap = (const int32_t RTHX_LDS*)(base + G.off_cmap);
+  v.cinfo = (const MCoarse RTHX_LDS*)(base + G.off_cinfo);
+  v.beta = (const double RTHX_LDS*)(base + G.off_beta);
+  return v;
+}
+
+// Fine polygon (global index) of coarse m holding p, or -1; (i, j) its box.
+__device__ __forceinline__ int ml_fine(const MLatLds& L, const MLatLayout& G, const MCoarse& m, double px, double py,
+                                       int& i, int& j) {
+  i = lattice_index(L.xs, G.nx, G.inv_x, px);
+  j = lattice_index(L.ys, G.ny, G.inv_y, py);
+  const int li = i - m.i0, lj = j - m.j0;
+  if (i < 0 || j < 0 || li < 0 || li >= m.nxf || lj < 0 || lj >= m.nyf) return -1;
+  return m.first + lj * m.nxf + li;
+}
+
+template <bool UNIFORM>
+__device__ __forceinline__ int walk_ml(const DevDomain& D, const TraceParams& P, const MLatLds& L,
+                                       const MLatLayout& G, int& c, double& px, double& py, double dx, double dy,
+                                       double& S, double& acc) {
+  const double eta = P.eta;
+  const MCoarse m = ld(L.cinfo + c);
+  int k;
+  const double u = dist_to_box(px, py, dx, dy, L.cxs[m.ci], L.cxs[m.ci + 1], L.cys[m.cj], L.cys[m.cj + 1], k);
+  bool gas;
+  double beta = 0.0, tau_b = 0.0;
+  if (UNIFORM) {
+    gas = S < u;
+  } else {
+    beta = L.beta[c];
+    if (beta < 0.0) {
+      int i, j;
+      const int f0 = ml_fine(L, G, m, px, py, i, j);
+      if (f0 < 0) return -1;
+      beta = D.beta[(size_t)P.bin * D.n_fine + f0];
+    }
+    tau_b = __dmul_rn(beta, u);
+    gas = acc + tau_b >= S;
+  }
+  const bool wall = !gas && ((m.solid >> k) & 1u);
+  if (gas || wall) {
+    const double t = gas ? (UNIFORM ? S : (S - acc) / beta) - eta : u - eta;
+    px = px + __dmul_rn(t, dx);
+    py = py + __dmul_rn(t, dy);
+    return gas ? kRayEndGas : kRayEndWall;
+  }
+  const double t = u + eta;
+  px = px + __dmul_rn(t, dx);
+  py = py + __dmul_rn(t, dy);
+  if (UNIFORM) S -= u; else acc += tau_b;
+  const int ci = lattice_index(L.cxs, G.ncx, G.inv_cx, px), cj = lattice_index(L.cys, G.ncy, G.inv_cy, py);
+  if (ci < 0 || cj < 0) return -1;
+  c = L.cmap[cj * G.ncx + ci];
+  return kRayContinue;
+}
+
+__device__ __forceinline__ int end_ml(const DevDomain& D, const MLatLds& L, const MLatLayout& G, int c, double px,
+                                      double py, double dx, double dy, bool gas) {
+  const MCoarse m = ld(L.cinfo + c);
+  int i, j;
+  const int fg = ml_fine(L, G, m, px, py, i, j);
+  if (fg < 0) return -1;
+  if (gas) return D.n_surfaces + fg;
+  int w;
+  dist_to_box(px, py, dx, dy, L.xs[i], L.xs[i + 1], L.ys[j], L.ys[j + 1], w);
+  return D.f_surf[4 * fg + w];
 }
 
 // S = -ln(u)/beta (uniform, traceRay.jl:25) or tau* = -ln(u) (variable, :79).

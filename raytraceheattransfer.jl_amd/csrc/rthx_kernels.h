@@ -72,7 +72,8 @@ struct LaunchCfg {
   hipStream_t stream;
   int tally;    // Tally
   int threads;  // workgroup size; 0 = the one with the most resident waves
-  bool uniform, faithful, single, axis, clds;
+  int clds;  // LDS behind the tally: 0 none, 1 coarse mesh (multi-polygon) or LAT (single), 2 MLAT
+  bool uniform, faithful, single, axis;
 };
 
 hipError_t launch_trace(const LaunchCfg& L);

@@ -34,11 +34,14 @@ namespace rthx {
 #ifndef RTHX_LAT_WAVES_PER_EU
 #define RTHX_LAT_WAVES_PER_EU 6  // LAT kernels (lattice locate): no cell records in registers
 #endif
+#ifndef RTHX_MULTI_WAVES_PER_EU
+#define RTHX_MULTI_WAVES_PER_EU 4  // multi-polygon kernels (walk state + batched ends)
+#endif
 #ifndef RTHX_REFILL
 #define RTHX_REFILL 16  // ray regeneration batch of the multi-polygon kernels (lanes)
 #endif
 #define RTHX_TRACE_WAVES \
-  __attribute__((amdgpu_waves_per_eu(SINGLE ? (CLDS ? RTHX_LAT_WAVES_PER_EU : RTHX_TRACE_WAVES_PER_EU) : RTHX_TRACE_WAVES_PER_EU - 1)))
+  __attribute__((amdgpu_waves_per_eu(SINGLE ? (CL ? RTHX_LAT_WAVES_PER_EU : RTHX_TRACE_WAVES_PER_EU) : RTHX_MULTI_WAVES_PER_EU)))
 
 // Decoupled look-back (Merrill & Garland 2016) over the rows of one launch:
 // row `slot` publishes its nnz as an aggregate (flag 1), walks back over its
@@ -286,7 +289,7 @@ __device__ __forceinline__ uint32_t hash_emit_bitmap(const uint32_t* keys, const
   return total;
 }
 
-template <bool UNIFORM, int TALLY, bool FAITHFUL, bool SINGLE, bool REC, bool SPLIT, bool AXIS, bool CLDS>
+template <bool UNIFORM, int TALLY, bool FAITHFUL, bool SINGLE, bool REC, bool SPLIT, bool AXIS, int CL>
 __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_exchange_kernel(const DevDomain* __restrict__ Dp,
                                                                      TraceParams P, TallyParams T,
                                                                      RecordParams rec) {
@@ -304,6 +307,11 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
   __shared__ SingleCoarse s_single;
   __shared__ double s_tab[kTableDoubles];  // cos and log tables (rthx_device.h)
 
+  // CL: what sits in LDS behind the row tally.  SINGLE: 1 = the lattice of
+  // the one coarse rectangle (LAT).  Multi-polygon: 1 = the coarse mesh
+  // (CLDS), 2 = the multi-polygon lattice (MLAT).
+  constexpr bool CLDS = CL != 0;
+  constexpr bool MLAT = CL == 2 && !SINGLE;
   const int tid = threadIdx.x;
   const int64_t slot = SPLIT ? (int64_t)(blockIdx.x / T.split) : (int64_t)blockIdx.x;
   const int64_t part = SPLIT ? (int64_t)(blockIdx.x % T.split) : 0;
@@ -322,6 +330,11 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
   if (CLDS && SINGLE) {  // LAT: the lattice of the single coarse rectangle (LatticeLayout)
     uint4* dst = (uint4*)cl_base;
     for (int i = tid; i < D.lat.bytes / 16; i += nthr) dst[i] = D.lat_blob[i];
+  } else if (MLAT) {
+    uint4* dst = (uint4*)cl_base;
+    for (int i = tid; i < D.ml.blob_bytes / 16; i += nthr) dst[i] = D.ml_blob[i];
+    double RTHX_LDS* cb = (double RTHX_LDS*)(cl_base + D.ml.off_beta);
+    for (int i = tid; i < D.n_coarse; i += nthr) cb[i] = D.c_beta[(size_t)P.bin * D.n_coarse + i];
   } else if (CLDS) {
     uint4* dst = (uint4*)cl_base;  // generic view (HIP vector assignment); stores stay ds_write
     for (int i = tid; i < D.cl.blob_bytes / 16; i += nthr) dst[i] = D.c_blob[i];
@@ -422,18 +435,32 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
     // Several domains' rays cross many coarse polygons (the greenhouse's 67
     // layers), and their segment counts differ widely.  Ray regeneration: a
     // lane whose ray ended takes the next ray index of the row from an LDS
-    // counter, so waves do not idle until their longest ray ends.  Refills
-    // are batched (a wave emits once at least kRefill of its lanes are idle)
-    // so the emission code runs for many lanes at a time.
+    // counter, so waves do not idle until their longest ray ends.  Work that
+    // only some lanes need in an iteration is batched: a wave emits new rays
+    // and (CLDS) finds the absorbers of the rays whose walk ended (end_cl)
+    // once at least kRefill of its lanes have stopped walking, so that the
+    // emission and the fine locate run for many lanes at a time.
     constexpr int kRefill = RTHX_REFILL;
     double px = 0.0, py = 0.0, dx = 0.0, dy = 0.0, S = 0.0, acc = 0.0, ox = 0.0, oy = 0.0;
     int c = 0, it = 0;
     uint32_t r = 0;
-    bool live = false, more = true;
+    bool live = false, ending = false, end_gas = false, more = true;
     while (true) {
-      if (more) {
-        const uint64_t idle = __ballot(!live);
-        if (__popcll(idle) >= kRefill || __ballot(live) == 0ull) {
+      const uint64_t walking = __ballot(live);
+      if (walking == 0ull || 64 - __popcll(walking) >= kRefill) {
+        if (CLDS && ending) {
+          int a;
+          if constexpr (MLAT) {
+            a = end_ml(D, mlat_lds_view(lds_opaque(cl_base), D.ml), D.ml, c, px, py, dx, dy, end_gas);
+          } else {
+            const CoarseLds L = coarse_lds_view(lds_opaque(cl_base), D.cl);
+            a = end_cl<AXIS>(D, L, c, px, py, dx, dy, end_gas);
+          }
+          tally(a);
+          record(r, a, ox, oy, px, py);
+          ending = false;
+        }
+        if (more) {
           if (!live) {
             r = atomicAdd(&s_next, 1u);
             if (r < (uint32_t)r_end) {
@@ -451,20 +478,26 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
           }
           more = __ballot(!live) == 0ull;  // a lane found the row exhausted: no more refills
         }
+        if (__ballot(live) == 0ull) break;  // (every ended ray was resolved above)
       }
-      if (__ballot(live) == 0ull) break;
       if (live) {
         int a = -1;
         if (it < 10000) {
-          if (CLDS) {
+          if constexpr (MLAT) {
+            a = walk_ml<UNIFORM>(D, P, mlat_lds_view(lds_opaque(cl_base), D.ml), D.ml, c, px, py, dx, dy, S, acc);
+          } else if constexpr (CLDS) {
             const CoarseLds L = coarse_lds_view(lds_opaque(cl_base), D.cl);
-            a = segment_cl<UNIFORM, AXIS>(D, P, L, c, px, py, dx, dy, S, acc);
+            a = walk_cl<UNIFORM, AXIS>(D, P, L, c, px, py, dx, dy, S, acc);
           } else {
             a = segment<UNIFORM, false, AXIS>(D, P, s_single, c, px, py, dx, dy, S, acc);
           }
         }
         ++it;
-        if (a != kRayContinue) {
+        if (a == kRayEndGas || a == kRayEndWall) {
+          live = false;
+          ending = true;
+          end_gas = a == kRayEndGas;
+        } else if (a != kRayContinue) {
           tally(a);
           record(r, a, ox, oy, px, py);
           live = false;
@@ -761,9 +794,9 @@ __global__ __launch_bounds__(256) void csr_pack_kernel(const uint32_t* __restric
 // ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
-template <bool UNIFORM, int TALLY, bool FAITHFUL, bool SINGLE, bool REC, bool SPLIT, bool AXIS, bool CLDS = false>
+template <bool UNIFORM, int TALLY, bool FAITHFUL, bool SINGLE, bool REC, bool SPLIT, bool AXIS, int CL = 0>
 static hipError_t launch_trace_t(const LaunchCfg& L) {
-  auto kern = trace_exchange_kernel<UNIFORM, TALLY, FAITHFUL, SINGLE, REC, SPLIT, AXIS, CLDS>;
+  auto kern = trace_exchange_kernel<UNIFORM, TALLY, FAITHFUL, SINGLE, REC, SPLIT, AXIS, CL>;
   if (L.lds_bytes > 64 * 1024) {  // (occupancy queries above 64 KiB need the attribute first)
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)L.lds_bytes);
@@ -793,20 +826,23 @@ static hipError_t launch_trace_t(const LaunchCfg& L) {
 
 template <bool UNIFORM, int TALLY, bool FAITHFUL, bool AXIS>
 static hipError_t launch_trace_a(const LaunchCfg& L) {
-  // SINGLE kernels with CLDS = the lattice locate (LAT; axis-aligned only)
+  // SINGLE kernels with CL = 1: the lattice locate (LAT; axis-aligned only);
+  // multi-polygon kernels: CL = 1 coarse mesh in LDS, 2 lattice (MLAT, axis only)
   if (L.T.split > 1) {
     if constexpr (AXIS) {
-      if (L.single && L.clds) return launch_trace_t<UNIFORM, TALLY, FAITHFUL, true, false, true, AXIS, true>(L);
+      if (L.single && L.clds) return launch_trace_t<UNIFORM, TALLY, FAITHFUL, true, false, true, AXIS, 1>(L);
+      if (!L.single && L.clds == 2) return launch_trace_t<UNIFORM, TALLY, FAITHFUL, false, false, true, AXIS, 2>(L);
     }
     if (L.single) return launch_trace_t<UNIFORM, TALLY, FAITHFUL, true, false, true, AXIS>(L);
-    if (L.clds) return launch_trace_t<UNIFORM, TALLY, FAITHFUL, false, false, true, AXIS, true>(L);
+    if (L.clds) return launch_trace_t<UNIFORM, TALLY, FAITHFUL, false, false, true, AXIS, 1>(L);
     return launch_trace_t<UNIFORM, TALLY, FAITHFUL, false, false, true, AXIS>(L);
   }
   if constexpr (AXIS) {
-    if (L.single && L.clds) return launch_trace_t<UNIFORM, TALLY, FAITHFUL, true, false, false, AXIS, true>(L);
+    if (L.single && L.clds) return launch_trace_t<UNIFORM, TALLY, FAITHFUL, true, false, false, AXIS, 1>(L);
+    if (!L.single && L.clds == 2) return launch_trace_t<UNIFORM, TALLY, FAITHFUL, false, false, false, AXIS, 2>(L);
   }
   if (L.single) return launch_trace_t<UNIFORM, TALLY, FAITHFUL, true, false, false, AXIS>(L);
-  if (L.clds) return launch_trace_t<UNIFORM, TALLY, FAITHFUL, false, false, false, AXIS, true>(L);
+  if (L.clds) return launch_trace_t<UNIFORM, TALLY, FAITHFUL, false, false, false, AXIS, 1>(L);
   return launch_trace_t<UNIFORM, TALLY, FAITHFUL, false, false, false, AXIS>(L);
 }
 

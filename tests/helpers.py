@@ -253,7 +253,7 @@ def element_keys(dom, nd=9):
 
 
 def greenhouse_domain(n_layers=67, nx=201, ny=3, n_bins=8, scale_height=15_900.0 / 100_000.0,
-                      kappa_vis=0.01, kappa_ir=100.0):
+                      kappa_vis=0.01, kappa_ir=100.0, uniform=False):
     """BASELINE configs[4] geometry: a 1x1 stack of coarse
     layers, side walls solid, bottom of layer 1 and top of the last layer
     solid, interfaces open; per-band kappa(y) = rho(y_mid) (k_ir s_b + k_vis
@@ -267,12 +267,29 @@ def greenhouse_domain(n_layers=67, nx=201, ny=3, n_bins=8, scale_height=15_900.0
         y0, y1 = j / n_layers, (j + 1) / n_layers
         rho = math.exp(-((y0 + y1) / 2) / scale_height)
         kap = rho * (kappa_ir * sig + kappa_vis * (1 - sig))
+        if uniform:  # (every layer the same kappa: traceRayUniform)
+            kap = np.full(n_bins, 0.7)
         f = PolyVolume2D([(0.0, y0), (1.0, y0), (1.0, y1), (0.0, y1)], [j == 0, True, j == n_layers - 1, True],
                          n_bins, kap, np.zeros(n_bins))
         f.epsilon = [np.ones(n_bins) for _ in range(4)]
         f.T_in_g = -1.0
         faces.append(f)
     return RayTracingDomain2D(faces, [(nx, ny)] * n_layers)
+
+
+def quad_lattice_domain(ncx=2, ncy=3, nxf=4, nyf=3, kappa=0.8):
+    """A unit square cut into an ncx x ncy lattice of coarse squares (outer
+    walls solid, interior walls open), each meshed nxf x nyf: a multi-polygon
+    lattice with more than one coarse column (MLAT kernels)."""
+    faces = []
+    for j in range(ncy):
+        for i in range(ncx):
+            x0, x1, y0, y1 = i / ncx, (i + 1) / ncx, j / ncy, (j + 1) / ncy
+            f = PolyVolume2D([(x0, y0), (x1, y0), (x1, y1), (x0, y1)],
+                             [j == 0, i == ncx - 1, j == ncy - 1, i == 0], 1, kappa * (1 + 0.3 * ((i + j) % 2)), 0.0)
+            f.T_in_g = -1.0
+            faces.append(f)
+    return RayTracingDomain2D(faces, [(nxf, nyf)] * len(faces))
 
 
 def icosphere(level=2, radius=0.3, center=(0.5, 0.5, 0.5)):

@@ -182,6 +182,37 @@ def test_coarse_lds_kernels_match_global_kernels(hip, case, monkeypatch):
         assert_same(a, oracle.trace_exchange(flat, args, 16))
 
 
+@pytest.mark.parametrize("case", ["greenhouse", "greenhouse_checker", "lattice_2x3", "uniform_layers"])
+def test_multi_polygon_lattice_kernels_match_coarse_lds_kernels(hip, case, monkeypatch):
+    """Layered axis-aligned domains take the MLAT kernels (rthx_device.h
+    walk_ml / end_ml: coarse and fine lattice locates); RTHX_NO_MLAT=1 (at
+    domain creation) keeps the coarse-mesh CLDS kernels.  Both equal the
+    oracle -- with uniform and per-cell betas, a 2 x 3 coarse lattice and a
+    uniform-beta (traceRayUniform) layered domain."""
+    bins = (0,)
+    if case == "greenhouse":
+        dom, bins = H.greenhouse_domain(n_layers=6, nx=9, ny=3, n_bins=8), (0, 4, 7)
+    elif case == "greenhouse_checker":
+        dom, bins = H.greenhouse_domain(n_layers=6, nx=9, ny=3, n_bins=8), (0, 7)
+        for c in (1, 4):
+            for k, f in enumerate(dom.fine_mesh[c]):
+                if k % 2:
+                    f.kappa_g = np.asarray(f.kappa_g) * 1.7
+    elif case == "lattice_2x3":
+        dom = H.quad_lattice_domain(2, 3, 4, 3)
+    else:
+        dom = H.greenhouse_domain(n_layers=5, nx=7, ny=2, n_bins=1, uniform=True)
+    flat = dom.flat()
+    for b in bins:
+        args, _k = _args(hip, flat, 1500, seed=17, bin0=b)
+        a = gpu_trace(hip, flat, args)
+        monkeypatch.setenv("RTHX_NO_MLAT", "1")
+        g = gpu_trace(hip, flat, args)
+        monkeypatch.delenv("RTHX_NO_MLAT")
+        assert_same(a, g)
+        assert_same(a, oracle.trace_exchange(flat, args, 16))
+
+
 def test_recorder_exact(hip):
     dom = H.wedge_domain(8, 3)
     flat = dom.flat()
