@@ -383,6 +383,7 @@ RTHX_EXPORT int rthx_domain_create(const rthx_domain_desc* desc, int32_t device,
     }
     D.cl = L;
   }
+  std::vector<double> cbeta_all;  // (per bin, per coarse polygon; MLAT reorders it by box)
   if (nc >= 2) {
     std::vector<double> cbeta((size_t)s.n_bins * nc, -1.0);
     for (int bn = 0; bn < s.n_bins; ++bn)
@@ -394,6 +395,7 @@ RTHX_EXPORT int rthx_domain_create(const rthx_domain_desc* desc, int32_t device,
         if (same) cbeta[(size_t)bn * nc + c] = bb[f0];
       }
     UP(cbeta.data(), cbeta.size(), D.c_beta);
+    cbeta_all = cbeta;
   }
   // Multi-polygon lattice (rthx_device.h MLatLayout; MLAT kernels): the
   // coarse rectangles are the boxes of a coarse lattice, and the fine
@@ -457,6 +459,8 @@ RTHX_EXPORT int rthx_domain_create(const rthx_domain_desc* desc, int32_t device,
       off = a16(off + 4 * cmap.size());
       G.off_cinfo = (int32_t)off;
       off = a16(off + sizeof(rthx::MCoarse) * nc);
+      G.off_bsolid = (int32_t)off;
+      off = a16(off + 4 * nc);
       G.off_beta = (int32_t)off;
       G.blob_bytes = (int32_t)off;
       off = a16(off + 8 * nc);
@@ -475,7 +479,16 @@ RTHX_EXPORT int rthx_domain_create(const rthx_domain_desc* desc, int32_t device,
         std::memcpy(b + G.off_cys, cys.data(), 8 * cys.size());
         std::memcpy(b + G.off_cmap, cmap.data(), 4 * cmap.size());
         std::memcpy(b + G.off_cinfo, info.data(), sizeof(rthx::MCoarse) * nc);
+        std::vector<uint32_t> bsolid(nc);
+        std::vector<double> bbeta((size_t)s.n_bins * nc);
+        for (size_t bx = 0; bx < nc; ++bx) {
+          const int c = cmap[bx];
+          bsolid[bx] = csolid[c];
+          for (int bn = 0; bn < s.n_bins; ++bn) bbeta[(size_t)bn * nc + bx] = cbeta_all[(size_t)bn * nc + c];
+        }
+        std::memcpy(b + G.off_bsolid, bsolid.data(), 4 * nc);
         UP(blob.data(), blob.size(), D.ml_blob);
+        UP(bbeta.data(), bbeta.size(), D.ml_bbeta);
         D.ml = G;
       }
     }

@@ -100,8 +100,9 @@ struct LatticeLayout {
 // ys) inside it, x fastest (meshQuad.jl:139-179) -- a layered medium such as
 // the greenhouse (67 layers of 201 x 3 cells: one 201 x 201 lattice).  Blob:
 // xs[nx+1], ys[ny+1], cxs[ncx+1], cys[ncy+1] (f64), cmap[ncy ncx] (i32:
-// coarse polygon of box (ci, cj)), MCoarse[n_coarse], then (staged per bin)
-// one beta per coarse polygon (-1 when its fine betas differ).
+// coarse polygon of box b = cj ncx + ci), MCoarse[n_coarse], bsolid[nbox]
+// (u32: solid walls of box b), then (staged per bin from ml_bbeta) one beta
+// per box (-1 when the fine betas of its polygon differ).
 struct MCoarse {
   int32_t first;     // first fine polygon
   int32_t i0, j0;    // its fine lattice box
@@ -114,7 +115,8 @@ struct MLatLayout {
   int32_t bytes;       // LDS block incl. the betas (0: not a lattice)
   int32_t blob_bytes;  // staged from ml_blob
   int32_t nx, ny, ncx, ncy;
-  int32_t off_ys, off_cxs, off_cys, off_cmap, off_cinfo, off_beta;
+  int32_t off_ys, off_cxs, off_cys, off_cmap, off_cinfo, off_bsolid, off_beta;
+  int32_t reserved;
   double inv_x, inv_y, inv_cx, inv_cy;  // first guesses of lattice_index
 };
 
@@ -158,6 +160,7 @@ struct DevDomain {
   LatticeLayout lat;
   // lattice of a multi-polygon domain (MLatLayout)
   const uint4 RTHX_GLOBAL* ml_blob;    // [ml.blob_bytes / 16]
+  const double RTHX_GLOBAL* ml_bbeta;  // [n_bins][n_coarse] beta of box b (-1: per fine polygon)
   MLatLayout ml;
 };
 
@@ -371,6 +374,7 @@ __device__ __forceinline__ double dist_to_polygon(double px, double py, double d
 // den_i = d.n_i is -dy, dx, dy, -dx (products with +-1 and +-0 are exact), so
 // the same candidates, comparisons and first-index ties as dist_to_polygon,
 // with 4 of its 16 geometry reads and no multiplies for num/den.
+// dist_to_rect on the box [x0, x1] x [y0, y1].
 __device__ __forceinline__ double dist_to_box(double px, double py, double dx, double dy, double x0, double x1,
                                               double y0, double y1, int& widx) {
   const double num[4] = {py - y0, x1 - px, y1 - py, px - x0};
@@ -388,6 +392,36 @@ __device__ __forceinline__ double dist_to_box(double px, double py, double dx, d
   widx = bi;
   if (bd == 0.0) return __builtin_inf();
   double u = bn / bd;
+  return u > 0.0 ? u : __builtin_inf();
+}
+
+// dist_to_box for a point in the half-open box [x0, x1) x [y0, y1) (MLAT
+// walks: the coarse box is always the one holding the point).  There every
+// wall's num is >= 0 (> 0 for the right and top walls), so a wall is a
+// candidate only if its den = d.n is positive: at most the wall on the side
+// dx points to (xb: x0 if dx < 0, else x1) and the one dy points to (yb),
+// compared in wall order as the four-wall loop does.  Two bounds are read
+// instead of four and two walls tested instead of four.
+__device__ __forceinline__ double dist_in_box(double px, double py, double dx, double dy, double xb, double yb,
+                                              int& widx) {
+  const bool xdn = dx < 0.0, ydn = dy < 0.0;
+  const double nx = fabs(xb - px), ny = fabs(yb - py), ax = fabs(dx), ay = fabs(dy);
+  // (num den > 0: den = |d| on the chosen side, > 0 unless d is 0 there)
+  const bool vx = ax >= 1e-10 && __dmul_rn(nx, ax) > 0.0;
+  const bool vy = ay >= 1e-10 && __dmul_rn(ny, ay) > 0.0;
+  const int ix = xdn ? 3 : 1, iy = ydn ? 0 : 2;
+  // wall order: the y wall comes first unless it is the top wall (2) and the
+  // x wall the right one (1)
+  const bool y_first = ydn || xdn;
+  const double fn = y_first ? ny : nx, fd = y_first ? ay : ax, sn = y_first ? nx : ny, sd = y_first ? ax : ay;
+  const bool fv = y_first ? vy : vx, sv = y_first ? vx : vy;
+  const bool second = sv && (!fv || __dmul_rn(sn, fd) < __dmul_rn(fn, sd));
+  if (!(second || fv)) {
+    widx = 0;
+    return __builtin_inf();
+  }
+  widx = second == y_first ? ix : iy;
+  const double u = second ? sn / sd : fn / fd;
   return u > 0.0 ? u : __builtin_inf();
 }
 
@@ -974,6 +1008,7 @@ struct MLatLds {
   const double RTHX_LDS* cys;
   const int32_t RTHX_LDS* cmap;
   const MCoarse RTHX_LDS* cinfo;
+  const uint32_t RTHX_LDS* bsolid;
   const double RTHX_LDS* beta;
 };
 
@@ -985,8 +1020,32 @@ __device__ __forceinline__ MLatLds mlat_lds_view(const char RTHX_LDS* base, cons
   v.cys = (const double RTHX_LDS*)(base + G.off_cys);
   v.cmap = (const int32_t RTHX_LDS*)(base + G.off_cmap);
   v.cinfo = (const MCoarse RTHX_LDS*)(base + G.off_cinfo);
+  v.bsolid = (const uint32_t RTHX_LDS*)(base + G.off_bsolid);
   v.beta = (const double RTHX_LDS*)(base + G.off_beta);
   return v;
+}
+
+// The walker's coarse box: lattice indices, box index b = cj ncx + ci and
+// bounds [x0, x1) x [y0, y1), kept in registers from one segment to the next.
+struct MBox {
+  int ci, cj, b;
+  double x0, x1, y0, y1;
+};
+
+__device__ __forceinline__ void ml_box(const MLatLds& L, const MLatLayout& G, int ci, int cj, MBox& B) {
+  B.ci = ci;
+  B.cj = cj;
+  B.b = cj * G.ncx + ci;
+  B.x0 = L.cxs[ci];
+  B.x1 = L.cxs[ci + 1];
+  B.y0 = L.cys[cj];
+  B.y1 = L.cys[cj + 1];
+}
+
+// the box of coarse polygon c (a ray's emitter)
+__device__ __forceinline__ void ml_enter(const MLatLds& L, const MLatLayout& G, int c, MBox& B) {
+  const MCoarse m = ld(L.cinfo + c);
+  ml_box(L, G, m.ci, m.cj, B);
 }
 
 // Fine polygon (global index) of coarse m holding p, or -1; (i, j) its box.
@@ -999,49 +1058,99 @@ __device__ __forceinline__ int ml_fine(const MLatLds& L, const MLatLayout& G, co
   return m.first + lj * m.nxf + li;
 }
 
+#ifndef RTHX_WALK_BATCH
+#define RTHX_WALK_BATCH 4  // MLAT segments per call of walk_ml (per iteration of the kernel's ray loop)
+#endif
+
+// Up to RTHX_WALK_BATCH segments of one ray in box B (`it` counts them
+// against traceRay's 10,000-step cap, traceRay.jl:27).  The point is always
+// in B's half-open box, so the distance to B's walls is dist_in_box with the
+// ray's direction data taken out of the loop: the candidate walls are the
+// one dx points to and the one dy points to, compared in wall order.  After
+// a crossing of wall k the point is looked for in the neighbouring box
+// across k first (one new bound read from LDS); a point that is not there (a
+// crossing through a corner, or rounding) is located on the coarse lattice:
+// findFace2D's answer either way.  Returns kRayContinue (the batch ended
+// inside the lattice), kRayEndGas / kRayEndWall (p at the end point, in B),
+// or -1 (lost).
 template <bool UNIFORM>
 __device__ __forceinline__ int walk_ml(const DevDomain& D, const TraceParams& P, const MLatLds& L,
-                                       const MLatLayout& G, int& c, double& px, double& py, double dx, double dy,
-                                       double& S, double& acc) {
+                                       const MLatLayout& G, MBox& B, double& px, double& py, double dx, double dy,
+                                       double& S, double& acc, int& it) {
   const double eta = P.eta;
-  const MCoarse m = ld(L.cinfo + c);
-  int k;
-  const double u = dist_to_box(px, py, dx, dy, L.cxs[m.ci], L.cxs[m.ci + 1], L.cys[m.cj], L.cys[m.cj + 1], k);
-  bool gas;
-  double beta = 0.0, tau_b = 0.0;
-  if (UNIFORM) {
-    gas = S < u;
-  } else {
-    beta = L.beta[c];
-    if (beta < 0.0) {
-      int i, j;
-      const int f0 = ml_fine(L, G, m, px, py, i, j);
-      if (f0 < 0) return -1;
-      beta = D.beta[(size_t)P.bin * D.n_fine + f0];
+  const bool xdn = dx < 0.0, ydn = dy < 0.0;
+  const double ax = fabs(dx), ay = fabs(dy);
+  const bool vxd = ax >= 1e-10, vyd = ay >= 1e-10;
+  const bool y_first = ydn || xdn;  // wall order: y wall first unless top (2) vs right (1)
+  const int ix = xdn ? 3 : 1, iy = ydn ? 0 : 2;
+  const int sx = xdn ? -1 : 1, sy = ydn ? -1 : 1;
+  const int xo = xdn ? 0 : 1, yo = ydn ? 0 : 1;
+#pragma unroll 1
+  for (int n = 0; n < RTHX_WALK_BATCH; ++n) {
+    if (it >= 10000) return -1;
+    ++it;
+    const double nx = fabs((xdn ? B.x0 : B.x1) - px), ny = fabs((ydn ? B.y0 : B.y1) - py);
+    const bool vx = vxd && __dmul_rn(nx, ax) > 0.0, vy = vyd && __dmul_rn(ny, ay) > 0.0;
+    const double cx = __dmul_rn(nx, ay), cy = __dmul_rn(ny, ax);
+    const bool xw = vx && (!vy || (y_first ? cx < cy : !(cy < cx)));
+    const bool any = vx || vy;
+    double u = (xw ? nx : ny) / (xw ? ax : ay);
+    u = (any && u > 0.0) ? u : __builtin_inf();
+    const int k = any ? (xw ? ix : iy) : 0;
+    bool gas;
+    double beta = 0.0, tau_b = 0.0;
+    if (UNIFORM) {
+      gas = S < u;
+    } else {
+      beta = L.beta[B.b];
+      if (beta < 0.0) {
+        const MCoarse m = ld(L.cinfo + L.cmap[B.b]);
+        int i, j;
+        const int f0 = ml_fine(L, G, m, px, py, i, j);
+        if (f0 < 0) return -1;
+        beta = D.beta[(size_t)P.bin * D.n_fine + f0];
+      }
+      tau_b = __dmul_rn(beta, u);
+      gas = acc + tau_b >= S;
     }
-    tau_b = __dmul_rn(beta, u);
-    gas = acc + tau_b >= S;
-  }
-  const bool wall = !gas && ((m.solid >> k) & 1u);
-  if (gas || wall) {
-    const double t = gas ? (UNIFORM ? S : (S - acc) / beta) - eta : u - eta;
+    const bool wall = !gas && ((L.bsolid[B.b] >> k) & 1u);
+    if (gas || wall) {
+      const double t = gas ? (UNIFORM ? S : (S - acc) / beta) - eta : u - eta;
+      px = px + __dmul_rn(t, dx);
+      py = py + __dmul_rn(t, dy);
+      return gas ? kRayEndGas : kRayEndWall;
+    }
+    const double t = u + eta;
     px = px + __dmul_rn(t, dx);
     py = py + __dmul_rn(t, dy);
-    return gas ? kRayEndGas : kRayEndWall;
+    if (UNIFORM) S -= u; else acc += tau_b;
+    // the neighbouring box across wall k (k is the x wall iff xw)
+    const int ci = B.ci + (xw ? sx : 0), cj = B.cj + (xw ? 0 : sy);
+    bool ok = (unsigned)ci < (unsigned)G.ncx && (unsigned)cj < (unsigned)G.ncy;
+    const double v = ok ? (xw ? L.cxs[ci + xo] : L.cys[cj + yo]) : 0.0;
+    const double x0 = xw ? (xdn ? v : B.x1) : B.x0, x1 = xw ? (xdn ? B.x0 : v) : B.x1;
+    const double y0 = xw ? B.y0 : (ydn ? v : B.y1), y1 = xw ? B.y1 : (ydn ? B.y0 : v);
+    ok = ok && x0 <= px && px < x1 && y0 <= py && py < y1;
+    if (ok) {
+      B.ci = ci;
+      B.cj = cj;
+      B.b += xw ? sx : sy * G.ncx;
+      B.x0 = x0;
+      B.x1 = x1;
+      B.y0 = y0;
+      B.y1 = y1;
+    } else {
+      const int li = lattice_index(L.cxs, G.ncx, G.inv_cx, px), lj = lattice_index(L.cys, G.ncy, G.inv_cy, py);
+      if (li < 0 || lj < 0) return -1;
+      ml_box(L, G, li, lj, B);
+    }
   }
-  const double t = u + eta;
-  px = px + __dmul_rn(t, dx);
-  py = py + __dmul_rn(t, dy);
-  if (UNIFORM) S -= u; else acc += tau_b;
-  const int ci = lattice_index(L.cxs, G.ncx, G.inv_cx, px), cj = lattice_index(L.cys, G.ncy, G.inv_cy, py);
-  if (ci < 0 || cj < 0) return -1;
-  c = L.cmap[cj * G.ncx + ci];
   return kRayContinue;
 }
 
-__device__ __forceinline__ int end_ml(const DevDomain& D, const MLatLds& L, const MLatLayout& G, int c, double px,
-                                      double py, double dx, double dy, bool gas) {
-  const MCoarse m = ld(L.cinfo + c);
+__device__ __forceinline__ int end_ml(const DevDomain& D, const MLatLds& L, const MLatLayout& G, const MBox& B,
+                                      double px, double py, double dx, double dy, bool gas) {
+  const MCoarse m = ld(L.cinfo + L.cmap[B.b]);
   int i, j;
   const int fg = ml_fine(L, G, m, px, py, i, j);
   if (fg < 0) return -1;

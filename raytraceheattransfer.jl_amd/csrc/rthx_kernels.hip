@@ -38,7 +38,7 @@ namespace rthx {
 #define RTHX_MULTI_WAVES_PER_EU 4  // multi-polygon kernels (walk state + batched ends)
 #endif
 #ifndef RTHX_REFILL
-#define RTHX_REFILL 16  // ray regeneration batch of the multi-polygon kernels (lanes)
+#define RTHX_REFILL 32  // refill / end batch of the multi-polygon kernels (lanes; C5: 16 24 32 40 -> 32)
 #endif
 #define RTHX_TRACE_WAVES \
   __attribute__((amdgpu_waves_per_eu(SINGLE ? (CL ? RTHX_LAT_WAVES_PER_EU : RTHX_TRACE_WAVES_PER_EU) : RTHX_MULTI_WAVES_PER_EU)))
@@ -334,7 +334,7 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
     uint4* dst = (uint4*)cl_base;
     for (int i = tid; i < D.ml.blob_bytes / 16; i += nthr) dst[i] = D.ml_blob[i];
     double RTHX_LDS* cb = (double RTHX_LDS*)(cl_base + D.ml.off_beta);
-    for (int i = tid; i < D.n_coarse; i += nthr) cb[i] = D.c_beta[(size_t)P.bin * D.n_coarse + i];
+    for (int i = tid; i < D.n_coarse; i += nthr) cb[i] = D.ml_bbeta[(size_t)P.bin * D.n_coarse + i];
   } else if (CLDS) {
     uint4* dst = (uint4*)cl_base;  // generic view (HIP vector assignment); stores stay ds_write
     for (int i = tid; i < D.cl.blob_bytes / 16; i += nthr) dst[i] = D.c_blob[i];
@@ -443,6 +443,16 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
     constexpr int kRefill = RTHX_REFILL;
     double px = 0.0, py = 0.0, dx = 0.0, dy = 0.0, S = 0.0, acc = 0.0, ox = 0.0, oy = 0.0;
     int c = 0, it = 0;
+    MBox box{};  // (MLAT: the coarse lattice box instead of c)
+#ifdef RTHX_MLAT_HOIST
+    const MLatLayout G_ml = D.ml;
+    const MLatLds L_ml = mlat_lds_view(cl_base, G_ml);
+#define RTHX_ML_VIEW L_ml
+#define RTHX_ML_G G_ml
+#else
+#define RTHX_ML_VIEW mlat_lds_view(lds_opaque(cl_base), D.ml)
+#define RTHX_ML_G D.ml
+#endif
     uint32_t r = 0;
     bool live = false, ending = false, end_gas = false, more = true;
     while (true) {
@@ -451,7 +461,7 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
         if (CLDS && ending) {
           int a;
           if constexpr (MLAT) {
-            a = end_ml(D, mlat_lds_view(lds_opaque(cl_base), D.ml), D.ml, c, px, py, dx, dy, end_gas);
+            a = end_ml(D, RTHX_ML_VIEW, RTHX_ML_G, box, px, py, dx, dy, end_gas);
           } else {
             const CoarseLds L = coarse_lds_view(lds_opaque(cl_base), D.cl);
             a = end_cl<AXIS>(D, L, c, px, py, dx, dy, end_gas);
@@ -472,6 +482,7 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
               oy = py;
               acc = 0.0;
               c = e.coarse;
+              if constexpr (MLAT) ml_enter(RTHX_ML_VIEW, RTHX_ML_G, c, box);
               it = 0;
               live = true;
             }
@@ -482,17 +493,17 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
       }
       if (live) {
         int a = -1;
-        if (it < 10000) {
-          if constexpr (MLAT) {
-            a = walk_ml<UNIFORM>(D, P, mlat_lds_view(lds_opaque(cl_base), D.ml), D.ml, c, px, py, dx, dy, S, acc);
-          } else if constexpr (CLDS) {
+        if constexpr (MLAT) {
+          a = walk_ml<UNIFORM>(D, P, RTHX_ML_VIEW, RTHX_ML_G, box, px, py, dx, dy, S, acc, it);  // (counts it)
+        } else if (it < 10000) {
+          if constexpr (CLDS) {
             const CoarseLds L = coarse_lds_view(lds_opaque(cl_base), D.cl);
             a = walk_cl<UNIFORM, AXIS>(D, P, L, c, px, py, dx, dy, S, acc);
           } else {
             a = segment<UNIFORM, false, AXIS>(D, P, s_single, c, px, py, dx, dy, S, acc);
           }
         }
-        ++it;
+        if constexpr (!MLAT) ++it;
         if (a == kRayEndGas || a == kRayEndWall) {
           live = false;
           ending = true;
