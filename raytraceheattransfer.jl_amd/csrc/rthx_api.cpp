@@ -712,7 +712,8 @@ int plan_trace(const rthx_domain* dom, const rthx_trace_args* a, TracePlan& p) {
   const bool axis = dom->axis_rect && !env_flag("RTHX_NO_AXIS");
   const bool no_clds = env_flag("RTHX_NO_CLDS");  // (tests: the global-memory multi-polygon kernels)
   if (!dom->single_convex && axis && dom->D.ml.bytes > 0 && !no_clds &&
-      p.cl_offset + (size_t)dom->D.ml.bytes + rthx::kStaticLdsBytes <= rthx::kMaxLdsBytes) {
+      p.cl_offset + (size_t)dom->D.ml.bytes + (size_t)rthx::kTraceThreads * rthx::kRaySlotBytes +
+              rthx::kStaticLdsBytes <= rthx::kMaxLdsBytes) {
     p.clds = 2;  // multi-polygon lattice (MLAT kernels)
     p.lds_bytes = p.cl_offset + (size_t)dom->D.ml.bytes;
   } else if (!dom->single_convex && dom->D.cl.bytes > 0 &&

@@ -1058,6 +1058,13 @@ __device__ __forceinline__ int ml_fine(const MLatLds& L, const MLatLayout& G, co
   return m.first + lj * m.nxf + li;
 }
 
+// One emitted ray in an MLAT kernel's per-wave queue (LDS).
+struct alignas(16) RaySlot {
+  double px, py, dx, dy, S;
+  double pad;
+};
+constexpr int kRaySlotBytes = (int)sizeof(RaySlot);  // 48: the queue takes 48 B per lane of the workgroup
+
 #ifndef RTHX_WALK_BATCH
 #define RTHX_WALK_BATCH 4  // MLAT segments per call of walk_ml (per iteration of the kernel's ray loop)
 #endif

@@ -37,6 +37,11 @@ namespace rthx {
 #ifndef RTHX_MULTI_WAVES_PER_EU
 #define RTHX_MULTI_WAVES_PER_EU 4  // multi-polygon kernels (walk state + batched ends)
 #endif
+#define RTHX_ML_VIEW mlat_lds_view(lds_opaque(cl_base), D.ml)
+#define RTHX_ML_G D.ml
+#ifndef RTHX_REFILL_Q
+#define RTHX_REFILL_Q 8  // MLAT kernels: idle lanes before a refill from the ray queue / end batch
+#endif
 #ifndef RTHX_REFILL
 #define RTHX_REFILL 32  // refill / end batch of the multi-polygon kernels (lanes; C5: 16 24 32 40 -> 32)
 #endif
@@ -431,6 +436,93 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
       const uint32_t pw = k == 0u ? b0 : k == 1u ? b1 : k == 2u ? b2 : b3;
       if (r >= rb && r < re) one_ray(r, true, pw);
     }
+  } else if constexpr (MLAT) {
+    // Layered / lattice domains.  Rays walk many coarse boxes and their walk
+    // lengths differ widely, so a lane whose ray ended takes the next one at
+    // once -- from a per-wave queue of 64 emitted rays in LDS (RaySlot):
+    // emission runs for every lane of the wave at a time (each lane emits
+    // one ray into the queue when the queue runs short), and a refill is a
+    // pop of a few LDS words.  The absorbers of the rays whose walk ended
+    // (end_ml) are found together once kRefillQ lanes have stopped walking.
+    constexpr int kRefillQ = RTHX_REFILL_Q;
+    const uint32_t lane = lane_id();
+    const uint64_t lt_mask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    RaySlot RTHX_LDS* q = (RaySlot RTHX_LDS*)(cl_base + D.ml.bytes) + (tid >> 6) * 64;
+    __shared__ MBox s_box0;  // the emitter's coarse box: every ray of the row starts there
+    if (tid == 0) ml_enter(mlat_lds_view(cl_base, D.ml), D.ml, s_emit.coarse, s_box0);
+    __syncthreads();
+    uint32_t q_head = 0, q_cnt = 0;  // wave-uniform ring of 64 slots
+    bool exhausted = false;          // the row has no rays left to emit
+    double px = 0.0, py = 0.0, dx = 0.0, dy = 0.0, S = 0.0, acc = 0.0;
+    int it = 0;
+    MBox box{};
+    bool live = false, ending = false, end_gas = false;
+    while (true) {
+      const uint64_t walking = __ballot(live);
+      if (walking == 0ull || 64 - __popcll(walking) >= kRefillQ) {
+        if (ending) {
+          const int a = end_ml(D, RTHX_ML_VIEW, RTHX_ML_G, box, px, py, dx, dy, end_gas);
+          tally(a);
+          ending = false;
+        }
+        const uint64_t idle = __ballot(!live);
+        if (!exhausted && q_cnt < (uint32_t)__popcll(idle)) {
+          // top the queue up: lane l emits ray base + l into slot q_head + q_cnt + l
+          const uint32_t want = 64u - q_cnt;
+          uint32_t base = 0;
+          if (lane == 0) base = atomicAdd(&s_next, want);
+          base = __shfl(base, 0);
+          const uint32_t rr = base + lane;
+          const bool valid = lane < want && rr < (uint32_t)r_end;
+          if (valid) {
+            const double RTHX_LDS* tab = lds_opaque(&s_tab[0]);
+            const Emitter RTHX_LDS* em = lds_opaque(&s_emit);
+            const Emitter& e = *(const Emitter*)em;
+            RaySlot sl;
+            start_ray<UNIFORM, FAITHFUL>(P, e, (const double*)tab, (uint32_t)g, rr, sl.px, sl.py, sl.dx, sl.dy, sl.S);
+            RaySlot RTHX_LDS* d = q + ((q_head + q_cnt + lane) & 63u);
+            d->px = sl.px;
+            d->py = sl.py;
+            d->dx = sl.dx;
+            d->dy = sl.dy;
+            d->S = sl.S;
+          }
+          const uint32_t n_new = (uint32_t)__popcll(__ballot(valid));
+          if (n_new < want) exhausted = true;
+          q_cnt += n_new;
+        }
+        if (q_cnt > 0) {
+          const uint32_t rank = (uint32_t)__popcll(idle & lt_mask);
+          if (!live && rank < q_cnt) {
+            const RaySlot RTHX_LDS* sl = q + ((q_head + rank) & 63u);
+            px = sl->px;
+            py = sl->py;
+            dx = sl->dx;
+            dy = sl->dy;
+            S = sl->S;
+            acc = 0.0;
+            it = 0;
+            box = s_box0;
+            live = true;
+          }
+          const uint32_t taken = q_cnt < (uint32_t)__popcll(idle) ? q_cnt : (uint32_t)__popcll(idle);
+          q_head = (q_head + taken) & 63u;
+          q_cnt -= taken;
+        }
+        if (__ballot(live) == 0ull) break;  // (queue empty, row exhausted, every end resolved)
+      }
+      if (live) {
+        const int a = walk_ml<UNIFORM>(D, P, RTHX_ML_VIEW, RTHX_ML_G, box, px, py, dx, dy, S, acc, it);
+        if (a == kRayEndGas || a == kRayEndWall) {
+          live = false;
+          ending = true;
+          end_gas = a == kRayEndGas;
+        } else if (a != kRayContinue) {
+          tally(a);
+          live = false;
+        }
+      }
+    }
   } else {
     // Several domains' rays cross many coarse polygons (the greenhouse's 67
     // layers), and their segment counts differ widely.  Ray regeneration: a
@@ -444,15 +536,6 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
     double px = 0.0, py = 0.0, dx = 0.0, dy = 0.0, S = 0.0, acc = 0.0, ox = 0.0, oy = 0.0;
     int c = 0, it = 0;
     MBox box{};  // (MLAT: the coarse lattice box instead of c)
-#ifdef RTHX_MLAT_HOIST
-    const MLatLayout G_ml = D.ml;
-    const MLatLds L_ml = mlat_lds_view(cl_base, G_ml);
-#define RTHX_ML_VIEW L_ml
-#define RTHX_ML_G G_ml
-#else
-#define RTHX_ML_VIEW mlat_lds_view(lds_opaque(cl_base), D.ml)
-#define RTHX_ML_G D.ml
-#endif
     uint32_t r = 0;
     bool live = false, ending = false, end_gas = false, more = true;
     while (true) {
@@ -814,7 +897,8 @@ static hipError_t launch_trace_t(const LaunchCfg& L) {
     if (e != hipSuccess) return e;
   }
   const int64_t blocks = L.T.n_rows * (SPLIT ? L.T.split : 1);
-  auto lds_for = [&](int) { return L.lds_bytes; };
+  // (MLAT kernels: a 64-slot ray queue per wave behind the lattice)
+  auto lds_for = [&](int t) { return L.lds_bytes + (CL == 2 && !SINGLE ? (size_t)t * kRaySlotBytes : 0); };
   // Workgroup size: the one that keeps most waves resident per CU.  With a
   // large LDS row histogram (large N) only one or two workgroups fit a CU,
   // and 1024-lane workgroups keep 16 waves busy instead of 4.
