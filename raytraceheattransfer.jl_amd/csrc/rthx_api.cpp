@@ -16,6 +16,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -64,6 +65,24 @@ void fill_tables(double* t) {
   }
 }
 
+
+hipError_t device_stream(int device, hipStream_t* out) {
+  static std::mutex mu;
+  static std::vector<hipStream_t> streams;
+  std::lock_guard<std::mutex> lock(mu);
+  if (device < 0) return hipErrorInvalidDevice;
+  if ((size_t)device >= streams.size()) streams.resize(device + 1, nullptr);
+  if (!streams[device]) {
+    hipError_t e = hipSetDevice(device);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&streams[device], hipStreamNonBlocking);
+    if (e != hipSuccess) {
+      streams[device] = nullptr;
+      return e;
+    }
+  }
+  *out = streams[device];
+  return hipSuccess;
+}
 }  // namespace rthx
 
 namespace {
@@ -241,7 +260,7 @@ RTHX_EXPORT int rthx_domain_create(const rthx_domain_desc* desc, int32_t device,
     delete d;
     return code;
   };
-  if (hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess) return bail(fail(RTHX_EDEVICE, "hipStreamCreate"));
+  if (rthx::device_stream(device, &d->stream) != hipSuccess) return bail(fail(RTHX_EDEVICE, "hipStreamCreate"));
   for (auto& e : d->ev)
     if (hipEventCreate(&e) != hipSuccess) return bail(fail(RTHX_EDEVICE, "hipEventCreate"));
 

@@ -88,4 +88,10 @@ inline double now_ms() {
   return duration<double, std::milli>(steady_clock::now().time_since_epoch()).count();
 }
 
+// The library's stream on `device`: one non-blocking stream per device for
+// the whole process, created on first use and never destroyed.  Creating a
+// stream creates a hardware queue (~0.1 s on MI355X), so domains, scenes,
+// smoothing results and solves share it instead of creating their own.
+hipError_t device_stream(int device, hipStream_t* out);
+
 }  // namespace rthx

@@ -40,7 +40,7 @@ struct rthx_domain {
     for (void* p : allocs) (void)hipFree(p);
     for (auto& e : ev)
       if (e) (void)hipEventDestroy(e);
-    if (stream) (void)hipStreamDestroy(stream);
+    // (stream: the device's shared stream, rthx::device_stream)
   }
 };
 

@@ -360,8 +360,7 @@ int smooth_core(const SmoothInput& in, const double* w_in, int64_t n_w, int32_t 
     return code;
   };
   res->device = args->device;
-  if (hipStreamCreateWithFlags(&res->stream, hipStreamNonBlocking) != hipSuccess)
-    return bail(fail(RTHX_EDEVICE, "hipStreamCreate"));
+  if (rthx::device_stream(args->device, &res->stream) != hipSuccess) return bail(fail(RTHX_EDEVICE, "hipStreamCreate"));
   Ctx c;
   c.s = res->stream;
   c.n = m;

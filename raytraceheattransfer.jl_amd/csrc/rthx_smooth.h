@@ -23,8 +23,7 @@ struct rthx_smooth_result {
     if (device >= 0) (void)hipSetDevice(device);
     F.release();
     rp.release();
-    ci.release();
-    if (stream) (void)hipStreamDestroy(stream);
+    ci.release();  // (stream: the device's shared stream)
   }
 };
 

@@ -179,11 +179,7 @@ RTHX_EXPORT int rthx_solve_grey(const int64_t* row_ptr, const int32_t* cols, con
   HIP_TRY(hipSetDevice(args->device), "hipSetDevice");
   Solver S;
   S.n = n;
-  HIP_TRY(hipStreamCreateWithFlags(&S.s, hipStreamNonBlocking), "hipStreamCreate");
-  struct StreamGuard {
-    hipStream_t s;
-    ~StreamGuard() { (void)hipStreamDestroy(s); }
-  } guard{S.s};
+  HIP_TRY(rthx::device_stream(args->device, &S.s), "hipStreamCreate");
   DevBuf Fd, trp, tci, tv;
   S.op.n = n;
   if (dense) {
@@ -244,11 +240,7 @@ RTHX_EXPORT int rthx_solve_grey_smoothed(const rthx_smooth_result* F, const doub
   HIP_TRY(hipSetDevice(F->device), "hipSetDevice");
   Solver S;
   S.n = F->n;
-  HIP_TRY(hipStreamCreateWithFlags(&S.s, hipStreamNonBlocking), "hipStreamCreate");
-  struct StreamGuard {
-    hipStream_t s;
-    ~StreamGuard() { (void)hipStreamDestroy(s); }
-  } guard{S.s};
+  HIP_TRY(rthx::device_stream(F->device, &S.s), "hipStreamCreate");
   HIP_TRY(S.part.reserve((size_t)rthx::gs::part_doubles(S.n) * 8), "hipMalloc");
   S.op.dense = true;
   S.op.n = S.n;

@@ -15,6 +15,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <numeric>
@@ -43,7 +45,7 @@ struct rthx_scene3d {
     (void)hipSetDevice(device);
     for (auto& e : ev)
       if (e) (void)hipEventDestroy(e);
-    if (stream) (void)hipStreamDestroy(stream);
+    // (stream: the device's shared stream, rthx::device_stream)
   }
 };
 
@@ -305,6 +307,7 @@ RTHX_EXPORT int rthx_scene3d_create_grouped(const double* xyz, const int32_t* nv
   *out = nullptr;
   if (!xyz || !nv || !normal || n < 2) return fail(RTHX_EINVAL, "null argument or fewer than 2 polygons");
   if (n >= (int64_t(1) << 30)) return fail(RTHX_ERANGE, "too many polygons");
+  const double t_start = now_ms();
   // groups: each a contiguous run of polygon indices ([glo, ghi) per polygon)
   std::vector<int32_t> glo(n), ghi(n);
   {
@@ -412,6 +415,7 @@ RTHX_EXPORT int rthx_scene3d_create_grouped(const double* xyz, const int32_t* nv
   std::vector<double> tables(rthx::kTableDoubles);
   rthx::fill_tables(tables.data());
 
+  const double t_bvh = now_ms();
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) return fail(RTHX_EDEVICE, "no HIP device visible");
   if (device < 0 || device >= ndev) return fail(RTHX_EINVAL, "device ordinal out of range");
@@ -424,7 +428,7 @@ RTHX_EXPORT int rthx_scene3d_create_grouped(const double* xyz, const int32_t* nv
     delete s;
     return code;
   };
-  if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) return bail(fail(RTHX_EDEVICE, "hipStreamCreate"));
+  if (rthx::device_stream(device, &s->stream) != hipSuccess) return bail(fail(RTHX_EDEVICE, "hipStreamCreate"));
   for (auto& e : s->ev)
     if (hipEventCreate(&e) != hipSuccess) return bail(fail(RTHX_EDEVICE, "hipEventCreate"));
   auto up = [&](DevBuf& b, const void* src, size_t bytes) {
@@ -445,6 +449,9 @@ RTHX_EXPORT int rthx_scene3d_create_grouped(const double* xyz, const int32_t* nv
   s->S.nodes = s->nodes.as<rthx::Bvh2Node>();
   s->S.tables = s->tables.as<double>();
   if (!up(s->scene, &s->S, sizeof(s->S))) return bail(fail(RTHX_ENOMEM, "uploading the 3D scene"));
+  if (getenv("RTHX_VERBOSE"))
+    std::fprintf(stderr, "rthx_scene3d_create: host geometry + BVH %.2f ms, device setup + upload %.2f ms\n",
+                 t_bvh - t_start, now_ms() - t_bvh);
   *out = s;
   return RTHX_OK;
 }

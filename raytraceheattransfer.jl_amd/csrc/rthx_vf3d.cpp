@@ -86,7 +86,7 @@ RTHX_EXPORT int rthx_view_factors_3d(const double* xyz, const int32_t* nv, int64
   if (a->device < 0 || a->device >= ndev) return fail(RTHX_EINVAL, "device ordinal out of range");
   HIP_TRY(hipSetDevice(a->device), "hipSetDevice");
   hipStream_t st = nullptr;
-  HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate");
+  HIP_TRY(rthx::device_stream(a->device, &st), "hipStreamCreate");
   hipEvent_t e0 = nullptr, e1 = nullptr;
   DevBuf d_polys, d_area, d_F;
   int rc = RTHX_OK;
@@ -126,7 +126,6 @@ RTHX_EXPORT int rthx_view_factors_3d(const double* xyz, const int32_t* nv, int64
   d_polys.release();
   d_area.release();
   d_F.release();
-  (void)hipStreamDestroy(st);
   if (rc != RTHX_OK) return rc;
   inf.pairs = n * (n - 1);
   inf.total_ms = now_ms() - t0;

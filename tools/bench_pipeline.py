@@ -28,6 +28,11 @@ def main():
         dom = H.square_domain(a.ndim)
         t0 = time.perf_counter()
         dom(int(a.rays), seed=1 + r, verbose=False)
+        t_first = time.perf_counter() - t0
+        # steady state: mesh() again on the same domain (flattened descriptor
+        # and device upload cached, as the reference builds its grids once)
+        t0 = time.perf_counter()
+        dom(int(a.rays), seed=1 + r, verbose=False)
         t1 = time.perf_counter()
         info = {}
         from rthx.equilibrium import equilibrium_grey
@@ -39,7 +44,8 @@ def main():
         t4 = time.perf_counter()
         sm = getattr(dom, "last_smooth_info", {})
         tr = dom.last_trace_info[0]
-        print(f"ndim {a.ndim} rays {a.rays:.0e}: mesh() {1e3 * (t1 - t0):.0f} ms (trace kernel "
+        print(f"ndim {a.ndim} rays {a.rays:.0e}: mesh() {1e3 * (t1 - t0):.0f} ms (first call on a new domain "
+              f"{1e3 * t_first:.0f} ms: flattening + upload; trace kernel "
               f"{tr['trace_ms']:.2f} ms), solve {1e3 * (t2 - t1):.0f} ms (GMRES {info['iterations']} iterations, "
               f"library {info['ms_total']:.1f} ms, residual {info['residual']:.2e}), energy error "
               f"{dom.energy_error:.2e}; smoothing library {sm.get('ms_total', float('nan')):.1f} ms (OP "

@@ -35,8 +35,12 @@ def main():
     xyz, nv, nrm, nc = H.cube_icosphere_scene(args.ndim, args.level, args.radius)
     n = len(nv)
     R = int(args.rays) // n
+    from rthx import _lib
+    _lib.load().rthx_device_synchronize(0)  # HIP context up before the build is timed
     t = time.perf_counter()
     groups = None if args.no_groups else H.cube_icosphere_groups(args.ndim, args.level)
+    t_groups = time.perf_counter() - t
+    t = time.perf_counter()
     scene = Scene3D(xyz, nv, nrm, groups=groups)
     t_build = time.perf_counter() - t
     scene.trace(R, device_only=True)
@@ -54,7 +58,7 @@ def main():
     c = float(np.median(cs)) * 1e3
     rays = n * R
     line = (f"config4 cube {args.ndim}x{args.ndim}/face + icosphere L{args.level} (n={n}, {n - nc} triangles, "
-            f"{int(np.sum(np.where(nv == 4, 2, 1)))} MT triangles, {'polygon' if args.no_groups else 'face'} groups)  R={R} rays={rays:.3e}  scene build {t_build * 1e3:.0f} ms  "
+            f"{int(np.sum(np.where(nv == 4, 2, 1)))} MT triangles, {'polygon' if args.no_groups else 'face'} groups)  R={R} rays={rays:.3e}  scene build {t_build * 1e3:.0f} ms (groups {t_groups * 1e3:.0f} ms)  "
             f"BVH {stats}  kernel {k:.2f} ms ({rays / k / 1e6:.2f} Grays/s)  call {c:.2f} ms  lost {info['lost_total']}  nnz {info['nnz']}")
     if args.cpu_rows > 0:
         from oracle import oracle
