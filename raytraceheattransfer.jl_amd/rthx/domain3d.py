@@ -108,23 +108,60 @@ def _mesh_quad_flat(face, Nx, Ny):
     return out
 
 
+def _mesh_triangle_flat(face, Nx, Ny):
+    """meshTriangle(face::Vector{Vector}, Nx, Ny) (meshTriangle.jl:106-220):
+    the flat triangle is mirrored across its longest edge (first maximum of
+    the three edge lengths) into a parallelogram, which is meshed as a quad
+    (meshQuad.jl:75-182); cells whose midpoint lies on that edge (within
+    1e-6) become triangles (the cell's corners other than the mirrored one's
+    position, p4 = p3), cells on the triangle's side are kept, the others
+    dropped.  Returns (p1, p2, p3, p4) lists of points with z = 0."""
+    from .geometry import PolyVolume2D, mesh_quad
+
+    P = [np.asarray(q, dtype=np.float64)[:2] for q in face]
+    tri_mid = (np.asarray(face[0], dtype=np.float64) + np.asarray(face[1], dtype=np.float64)
+               + np.asarray(face[2], dtype=np.float64))[:2] / 3
+    norms = [np.linalg.norm(P[0] - P[1]), np.linalg.norm(P[1] - P[2]), np.linalg.norm(P[2] - P[0])]
+    max_index = int(np.argmax(norms)) + 1  # findmax: first maximum, 1-based
+    to_mirror, start = {1: (P[2], P[0]), 2: (P[0], P[1]), 3: (P[1], P[2])}[max_index]
+    line = {1: P[1] - P[0], 2: P[2] - P[1], 3: P[0] - P[2]}[max_index]
+    mirror_ind = max_index + 1
+    lmid = start + line / 2
+    mirrored = -(to_mirror - lmid) + lmid
+    new_pts = [P[0], P[1], P[2]]
+    new_pts.insert(mirror_ind - 1, mirrored)
+    tria_ids = [i for i in (1, 2, 3, 4) if i != mirror_ind]
+    face2 = PolyVolume2D([tuple(q) for q in new_pts], [True] * 4, 1, 1.0, 1.0)
+    mesh_quad(face2, Nx, Ny)
+    t = float(np.dot(tri_mid - start, line) / np.dot(line, line))
+    nearest = start + min(max(t, 0.0), 1.0) * line
+    out = ([], [], [], [])
+    for sub in face2.subVolumes:
+        cos_sub = float(np.dot(tri_mid - nearest, np.asarray(sub.midPoint) - nearest))
+        if abs(cos_sub) <= 1e-6:  # isapprox(x, 0.0, atol=1e-6): cut by the diagonal
+            kv = [sub.vertices[i - 1] for i in tria_ids]
+            corners = (kv[0], kv[1], kv[2], kv[2])
+        elif cos_sub > 0.0 - 1e-6:
+            corners = tuple(sub.vertices)
+        else:
+            continue
+        for k in range(4):
+            out[k].append(np.array([corners[k][0], corners[k][1], 0.0]))
+    return out
+
+
 def mesh_faces(points: np.ndarray, faces: np.ndarray, Ndim: int):
     """meshFaces (meshFaces.jl:2-18): per face the sub-face corner lists
-    (p1, p2, p3, p4), meshed in the face's own plane and projected back.
-    Triangular faces are supported for Ndim = 1 (the face itself); the
-    reference's triangle subdivision (meshTriangle.jl:106-220) is not
-    restated."""
+    (p1, p2, p3, p4), meshed in the face's own plane (meshQuad, or
+    meshTriangle for triangles: N(N+1)/2 sub-faces) and projected back.
+    (The reference sizes every face's list by face 1's sub-face count,
+    ViewFactorDomain3D.jl:41; here each face keeps its own.)"""
     out = []
     for row in faces:
         pts = [np.asarray(points[i], dtype=np.float64) for i in row]
-        if len(pts) == 3:
-            if Ndim != 1:
-                raise NotImplementedError("triangular faces are meshed only with Ndim = 1")
-            out.append(([pts[0]], [pts[1]], [pts[2]], [pts[2]]))
-            continue
         R, T = _project_plane_flat(pts)
         flat = [R @ (p + T) for p in pts]
-        cells = _mesh_quad_flat(flat, Ndim, Ndim)
+        cells = _mesh_triangle_flat(flat, Ndim, Ndim) if len(pts) == 3 else _mesh_quad_flat(flat, Ndim, Ndim)
         Rinv = np.linalg.inv(R)
         out.append(tuple([Rinv @ q - T for q in corner] for corner in cells))
     return out

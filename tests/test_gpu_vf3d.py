@@ -182,3 +182,74 @@ def test_grey_surface_properties(hip):
     for s in dom.subfaces():
         assert 400.0 < s.T_w < 1100.0 and np.isfinite(s.q_w)
     assert abs(sum(s.q_w for s in dom.subfaces())) < REF["energy_tolerance_W"]
+
+
+def icosphere_domain(level, ndim, T_in_w=None, q_in_w=None, epsilon=None):
+    """An icosphere enclosure (readme.md:532-589): 20 * 4**level triangles,
+    each meshed by meshTriangle (meshTriangle.jl:106-220) into ndim(ndim+1)/2
+    sub-faces."""
+    from rthx import ViewFactorDomain3D
+
+    tris = H.icosphere(level, radius=1.0, center=(0.0, 0.0, 0.0))
+    pts = np.array([p for t in tris for p in t])
+    faces = np.arange(1, len(pts) + 1).reshape(-1, 3)  # 1-based, three own vertices per face
+    n = len(faces)
+    return ViewFactorDomain3D(pts, faces, ndim, [0.0] * n if q_in_w is None else q_in_w,
+                              [-1.0] * n if T_in_w is None else T_in_w, [1.0] * n if epsilon is None else epsilon)
+
+
+@pytest.mark.parametrize("ndim", [2, 3])
+def test_icosphere_triangle_subfaces_reciprocity_and_row_sums(hip, ndim):
+    """Triangular faces meshed at Ndim = 2 and 3: F over the N(N+1)/2
+    sub-faces of every face against the CPU restatement, reciprocity and row
+    sums (test/test_3d_viewfactors.jl:126-137 tolerances), F_smooth rows = 1."""
+    dom = icosphere_domain(0, ndim)
+    subs = dom.subfaces()
+    assert len(subs) == 20 * ndim * (ndim + 1) // 2
+    xyz, nv = dom.polygon_arrays()
+    assert np.sum(nv == 3) == 20 * ndim  # ndim triangles along each face's mirrored edge, the rest quads
+    F, area, _ = gpu_F(xyz, nv)
+    F0, area0 = oracle.view_factors_3d(xyz, nv, 16)
+    assert np.max(np.abs(F - F0)) <= 10 * ATOL
+    # sub-face areas add up to their face's area
+    for sf in dom.facesMesh:
+        assert sum(s.area for s in sf.subFaces) == pytest.approx(sf.area, rel=1e-12)
+    AF = area[:, None] * F
+    assert np.max(np.abs(AF - AF.T)) < 1e-10
+    np.testing.assert_allclose(F.sum(axis=1), 1.0, rtol=0, atol=2e-3)  # closed convex enclosure (closed-form sums)
+    dom()
+    np.testing.assert_allclose(dom.F_smooth.sum(axis=1), 1.0, rtol=0, atol=1e-10)
+
+
+def test_isothermal_icosphere_triangles(hip):
+    """test/test_3d_heat_transfer.jl:29-72 on a triangulated enclosure (Ndim = 3)."""
+    from rthx.equilibrium import solve_equilibrium
+
+    dom = icosphere_domain(1, 3, T_in_w=[1000.0] * 80)
+    dom()
+    solve_equilibrium(dom)
+    for s in dom.subfaces():
+        assert abs(s.T_w - 1000.0) <= REF["temp_tolerance_K"]
+        assert abs(s.q_w) < REF["energy_tolerance_W"]
+
+
+def test_icosphere_hot_cap_energy_conservation(hip):
+    """test/test_3d_heat_transfer.jl:78-128, :134-184 on triangles (Ndim = 2):
+    a hot and a cold polar cap, the rest adiabatic; every adiabatic face lies
+    between the two temperatures and the net flux sums to zero."""
+    from rthx.equilibrium import solve_equilibrium
+
+    tris = H.icosphere(1, radius=1.0, center=(0.0, 0.0, 0.0))
+    zc = np.array([np.mean([p[2] for p in t]) for t in tris])
+    T_in = [1000.0 if z > 0.75 else 500.0 if z < -0.75 else -1.0 for z in zc]
+    assert 1000.0 in T_in and 500.0 in T_in
+    dom = icosphere_domain(1, 2, T_in_w=T_in)
+    dom()
+    solve_equilibrium(dom)
+    for i, sf in enumerate(dom.facesMesh):
+        T = np.mean([s.T_w for s in sf.subFaces])
+        if T_in[i] < 0:
+            assert 500.0 - REF["temp_tolerance_K"] < T < 1000.0 + REF["temp_tolerance_K"]
+        else:
+            assert abs(T - T_in[i]) <= REF["temp_tolerance_K"]
+    assert abs(sum(s.q_w for s in dom.subfaces())) < REF["energy_tolerance_W"] * 10

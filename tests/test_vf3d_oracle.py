@@ -120,3 +120,42 @@ def test_view_factor_domain_meshing(ndim):
                            for j in range(6)] for i in range(6)])
         assert np.allclose(np.sort(Fface[np.triu_indices(6, 1)]),
                            np.sort(np.array(REF["F_EES"])[np.triu_indices(6, 1)]), rtol=0, atol=1e-9)
+
+
+@pytest.mark.parametrize("ndim", [1, 2, 3, 5])
+def test_triangle_faces_meshing(ndim):
+    """meshTriangle (meshTriangle.jl:106-220) through meshFaces: a triangular
+    face becomes ndim(ndim+1)/2 sub-faces in its own plane -- ndim(ndim-1)/2
+    quads and ndim triangles along the mirrored diagonal -- tiling it (areas
+    add up, every sub-face inside the face), inward normals toward the domain
+    midpoint; sub-face view factors add up to the whole-face ones."""
+    from rthx import ViewFactorDomain3D
+
+    pts = np.array([[0.1, 0.0, 0.0], [1.3, 0.2, 0.1], [0.2, 1.1, 0.0], [0.3, 0.4, 1.2]])
+    faces = np.array([[1, 3, 2], [1, 2, 4], [1, 4, 3], [2, 3, 4]])
+    dom = ViewFactorDomain3D(pts, faces, ndim, [0.0] * 4, [-1.0] * 4, [1.0] * 4)
+    mid = pts.mean(axis=0)
+    assert dom.num_elements == 4 * ndim * (ndim + 1) // 2
+    for sf in dom.facesMesh:
+        subs = sf.subFaces
+        assert sum(len(s.vertices) == 3 for s in subs) == ndim
+        assert sum(s.area for s in subs) == pytest.approx(sf.area, rel=1e-12)
+        v = sf.vertices
+        n = np.cross(v[1] - v[0], v[2] - v[0])
+        for s in subs:
+            assert np.dot(s.inwardNormal, mid - s.midPoint) > 0
+            for p in s.vertices:
+                assert abs(np.dot(n, p - v[0])) < 1e-12  # in the face's plane
+                # inside the face: barycentric coordinates >= 0
+                T = np.array([v[1] - v[0], v[2] - v[0]]).T
+                lam = np.linalg.lstsq(T, p - v[0], rcond=None)[0]
+                assert lam.min() > -1e-12 and lam.sum() < 1 + 1e-12
+    xyz, nv = dom.polygon_arrays()
+    F, area = oracle.view_factors_3d(xyz, nv, 8)
+    k = ndim * (ndim + 1) // 2
+    Fface = np.array([[np.sum(area[i * k:(i + 1) * k, None] * F[i * k:(i + 1) * k, j * k:(j + 1) * k])
+                       for j in range(4)] for i in range(4)])
+    one = ViewFactorDomain3D(pts, faces, 1, [0.0] * 4, [-1.0] * 4, [1.0] * 4)
+    x1, n1 = one.polygon_arrays()
+    F1, a1 = oracle.view_factors_3d(x1, n1, 8)
+    assert np.allclose(Fface, a1[:, None] * F1, rtol=0, atol=1e-9)
