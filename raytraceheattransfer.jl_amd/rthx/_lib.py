@@ -323,12 +323,15 @@ class HipBackend:
     """The product backend: trace one bin on an MI355X through librthx.
 
     ``devices``: trace on several devices (rthx_multi_trace_exchange, rows
-    split over them); default one device, the call's ``device``."""
+    split over them); default one device, the call's ``device``.
+    ``bands=True``: a :spectral_variable domain's bands go to the devices
+    whole, one band per device at a time (rthx.exchange), instead."""
 
     name = "hip"
 
-    def __init__(self, devices: Optional[Sequence[int]] = None):
+    def __init__(self, devices: Optional[Sequence[int]] = None, bands: bool = False):
         self.devices = [int(d) for d in devices] if devices else None
+        self.band_devices = list(self.devices) if (bands and self.devices) else None
 
     def _domain(self, dom, device: int):
         if self.devices and len(self.devices) > 1:

@@ -11,6 +11,14 @@ collective.  ``gather_csr`` brings the row blocks to one rank (or all) when
 the caller wants the whole F: tensor all-reduce / all-gather, over RCCL and
 xGMI on an NCCL group, over gloo on the host otherwise.  Inside one process,
 rthx_multi_trace_exchange splits rows over several devices instead.
+
+Spectral domains whose bands vary in space (:spectral_variable, BASELINE
+config C5: every band traced alone, parallelRayTracing.jl:20-42) also shard
+by band: each rank (or each device of one process,
+rthx.exchange.parallel_ray_tracing with band devices) traces whole bands,
+``bands_of`` picking its share of the traced bands.  Bands are independent,
+so again there is no collective on the data path; ``broadcast_csr`` hands a
+band's CSR to the other ranks when they want it.
 """
 from __future__ import annotations
 
@@ -116,3 +124,44 @@ def gather_csr(row_ptr, cols, counts, n: int, group=None, dst: int = 0):
     rows = [np.nonzero(owner == k + 1)[0] for k in range(world)]
     c, v = _place(rows, pieces, lens_g, g_rp, int(g_rp[-1]))
     return g_rp, c, v
+
+
+def traced_bands(dom) -> List[Tuple[int, List[int]]]:
+    """The traces a :spectral_variable mesh() runs, in the reference's order
+    (parallelRayTracing.jl:20-42): (traced bin, bins that share its F), 1-based
+    -- every non-uniform bin alone, then one trace per group of uniform bins
+    with equal beta (group_uniform_bins)."""
+    from .exchange import group_uniform_bins
+
+    groups, _reps, nonuniform = group_uniform_bins(dom.uniform_across_bin)
+    return [(b, [b]) for b in nonuniform] + [(g[0], list(g)) for g in groups]
+
+
+def bands_of(rank: int, world: int, traced: Sequence[Tuple[int, List[int]]]):
+    """`rank`'s share of the traced bands (every world-th, in trace order)."""
+    if not (0 <= rank < world):
+        raise ValueError("rank out of range")
+    return [t for k, t in enumerate(traced) if k % world == rank]
+
+
+def broadcast_csr(row_ptr, cols, counts, n: int, src: int, group=None):
+    """Rank `src`'s CSR (n rows) on every rank: the sizes, then the arrays,
+    as tensor broadcasts (over RCCL / xGMI on an NCCL group, gloo on the host).
+    Non-source ranks pass None for the arrays."""
+    import torch
+    import torch.distributed as dist
+
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else torch.device("cpu")
+    rank = dist.get_rank(group)
+    nnz = torch.tensor([int(row_ptr[-1]) if rank == src else 0], dtype=torch.int64, device=dev)
+    dist.broadcast(nnz, src, group=group)
+    m = int(nnz.item())
+    if rank == src:
+        buf = torch.from_numpy(np.concatenate([np.asarray(row_ptr, dtype=np.int64),
+                                               np.asarray(cols, dtype=np.int64)[:m],
+                                               np.asarray(counts, dtype=np.int64)[:m]])).to(dev)
+    else:
+        buf = torch.empty(n + 1 + 2 * m, dtype=torch.int64, device=dev)
+    dist.broadcast(buf, src, group=group)
+    b = buf.cpu().numpy()
+    return b[:n + 1], b[n + 1:n + 1 + m].astype(np.int32), b[n + 1 + m:].astype(np.uint32)

@@ -416,10 +416,14 @@ class RayTracingDomain2D:
 
     def __call__(self, rays_tot: int, method: str = "exchange", nudge: Optional[float] = None,
                  k_dykstra=None, max_iters: int = 1000, verbose: Optional[bool] = None,
-                 rec=None, seed: int = 1, device: int = 0, faithful: bool = False, smooth: bool = True):
+                 rec=None, seed: int = 1, device: int = 0, faithful: bool = False, smooth: bool = True,
+                 devices=None):
         """multiDispatchRayTrace2D.jl:1-18.  ``method="exchange"``: trace (F_raw)
         then smooth (F_smooth, exchangeRayTracing.jl:13-74) on the device;
-        ``smooth=False`` stops after tracing (F_smooth stays None).  The
+        ``smooth=False`` stops after tracing (F_smooth stays None).
+        ``devices``: several GPUs -- a :spectral_variable domain's bands are
+        traced whole on them side by side (band per GPU), any other domain's
+        emitter rows are split over them (rthx_multi_trace_exchange).  The
         results land in ``self.F_raw`` / ``self.F_smooth`` (copied from the
         device on first read); returns None.
         ``method="direct"``: directRayTracing! (directRayTracing.jl:1-17) on
@@ -435,8 +439,13 @@ class RayTracingDomain2D:
             # F_raw and F_smooth stay on the device (the counts are smoothed
             # where they were traced, the GERT solve reads F_smooth in place);
             # each is copied to the host once, when first read
+            backend = None
+            if devices is not None and len(devices) > 1:
+                from ._lib import HipBackend
+
+                backend = HipBackend(devices, bands=self.spectral_mode == "spectral_variable")
             exchange_ray_tracing(self, int(rays_tot), trace_nudge, verbose, rec, seed=seed, device=device,
-                                 faithful=faithful, lazy=True)
+                                 faithful=faithful, lazy=True, backend=backend)
             if smooth:
                 Fs = smooth_exchange_factors(self, None, max_iters=max_iters, k_dykstra=k_dykstra,
                                              verbose=verbose, device=device)

@@ -191,6 +191,8 @@ def parallel_ray_tracing(dom, rays_total: int, nudge: float, verbose: bool, rec=
     dom.last_trace_info = []
     release_device_results(dom)
     kw = dict(seed=seed, device=device, faithful=faithful, backend=backend, lazy=lazy)
+    if dom.spectral_mode == "spectral_variable" and len(getattr(backend, "band_devices", None) or []) > 1:
+        return _bands_over_devices(dom, rays_per_emitter, nudge, verbose, rec, kw), rays_per_emitter
     if dom.spectral_mode == "spectral_variable":
         F_vec: List[Optional[sp.csr_matrix]] = [None] * n_bins
         groups, _reps, nonuniform = group_uniform_bins(dom.uniform_across_bin)
@@ -208,6 +210,56 @@ def parallel_ray_tracing(dom, rays_total: int, nudge: float, verbose: bool, rec=
         return F_vec, rays_per_emitter
     F = compute_exchange_factors_bin(dom, rays_per_emitter, nudge, 1, verbose, rec, **kw)
     return F, rays_per_emitter
+
+
+def _bands_over_devices(dom, rays_per_emitter, nudge, verbose, rec, kw):
+    """:spectral_variable traces spread over devices, band by band (BASELINE
+    C5's band-per-GPU form): the k-th traced band (traced_bands order) runs on
+    band_devices[k % D], one host thread per device (the library call
+    releases the GIL), each band a whole single-device trace -- the counts
+    equal a one-device mesh() exactly.  Grouped bins share their trace's F as
+    in parallelRayTracing.jl:32-42."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from ._lib import HipBackend
+    from .distributed import traced_bands
+
+    from ._lib import DeviceDomain
+
+    class _Pinned(HipBackend):  # one worker's own upload (one in-flight call per domain handle)
+        def __init__(self, dd, dev):
+            super().__init__([dev])
+            self._dd = dd
+
+        def _domain(self, dom_, device):
+            return self._dd, self.devices[0]
+
+    backend = kw["backend"]
+    devices = list(backend.band_devices)
+    traced = traced_bands(dom)
+    workers = []
+    for w, d in enumerate(devices):  # uploads before the threads start, kept with the domain
+        key = ("band", w, d)
+        if key not in dom._device_domains:
+            dom._device_domains[key] = DeviceDomain(dom.flat(), d)
+        workers.append(_Pinned(dom._device_domains[key], d))
+    F_vec = [None] * dom.n_spectral_bins
+
+    def run(worker):
+        out = []
+        for k in range(worker, len(traced), len(devices)):
+            b, _aliases = traced[k]
+            kk = dict(kw, backend=workers[worker], device=devices[worker])
+            out.append((k, compute_exchange_factors_bin(dom, rays_per_emitter, nudge, b, verbose, rec, **kk)))
+        return out
+
+    with ThreadPoolExecutor(max_workers=len(devices)) as ex:
+        for part in ex.map(run, range(len(devices))):
+            for k, F in part:
+                for j in traced[k][1]:
+                    F_vec[j - 1] = F
+    dom.last_trace_info.sort(key=lambda i: i["bin"])
+    return F_vec
 
 
 def materialize_F_raw(F_raw, ns: int, surfaces_only: bool):

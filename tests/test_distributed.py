@@ -91,3 +91,53 @@ def test_two_rank_direct_allreduce_equals_single_process(tmp_path):
     counts, _total, _info = DR.direct_ray_tracing_single_bin(dom, 30_001, H.NUDGE, 1, seed=5,
                                                              backend=oracle.OracleBackend(4))
     assert np.array_equal(np.load(out), counts)
+
+
+def _band_worker(rank, world, port, out_path):
+    """C5's band-per-GPU form over processes: each rank traces its share of a
+    :spectral_variable domain's traced bands (rthx.distributed.bands_of), and
+    every band's CSR is then broadcast from its owner (broadcast_csr)."""
+    sys.path[:0] = [H.PKG, H.ROOT, os.path.join(H.ROOT, "tests")]
+    import torch.distributed as dist
+
+    from oracle import oracle
+    from rthx import _lib
+    from rthx.distributed import bands_of, broadcast_csr, traced_bands
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    dom = H.greenhouse_domain(n_layers=4, nx=5, ny=2, n_bins=5)
+    flat = dom.flat()
+    traced = traced_bands(dom)
+    mine = {b: None for b, _ in bands_of(rank, world, traced)}
+    for b in mine:
+        args, _k = _lib.make_args(b - 1, 300, H.NUDGE, 12, 0, flat.n_emitters, 1)
+        mine[b] = oracle.trace_exchange(flat, args, 2)[:3]
+    out = {}
+    for k, (b, _aliases) in enumerate(traced):
+        src = k % world
+        rp, c, v = mine[b] if src == rank else (None, None, None)
+        out[b] = broadcast_csr(rp, c, v, flat.n_emitters, src)
+    if rank == 1:
+        np.savez(out_path, **{f"b{b}_{i}": a for b, t in out.items() for i, a in enumerate(t)})
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_bands_equal_single_process(tmp_path):
+    out = str(tmp_path / "bands.npz")
+    mp.spawn(_band_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    from oracle import oracle
+    from rthx import _lib
+    from rthx.distributed import traced_bands
+
+    dom = H.greenhouse_domain(n_layers=4, nx=5, ny=2, n_bins=5)
+    flat = dom.flat()
+    m = np.load(out)
+    traced = traced_bands(dom)
+    assert len(traced) >= 2
+    for b, _aliases in traced:
+        args, _k = _lib.make_args(b - 1, 300, H.NUDGE, 12, 0, flat.n_emitters, 1)
+        rp, cols, cnt, _i, _ = oracle.trace_exchange(flat, args, 4)
+        assert np.array_equal(m[f"b{b}_0"], rp)
+        assert np.array_equal(m[f"b{b}_1"], cols)
+        assert np.array_equal(m[f"b{b}_2"], cnt)
