@@ -402,26 +402,37 @@ __device__ __forceinline__ double dist_to_box(double px, double py, double dx, d
 // dx points to (xb: x0 if dx < 0, else x1) and the one dy points to (yb),
 // compared in wall order as the four-wall loop does.  Two bounds are read
 // instead of four and two walls tested instead of four.
-__device__ __forceinline__ double dist_in_box(double px, double py, double dx, double dy, double xb, double yb,
-                                              int& widx) {
+struct BoxHit {
+  double num, den;  // the winning wall's |num|, |den| (parameter num / den)
+  int wall;         // its index (0 when no wall qualifies)
+  bool any;
+};
+
+__device__ __forceinline__ BoxHit box_hit_in(double px, double py, double dx, double dy, double xb, double yb) {
   const bool xdn = dx < 0.0, ydn = dy < 0.0;
   const double nx = fabs(xb - px), ny = fabs(yb - py), ax = fabs(dx), ay = fabs(dy);
   // (num den > 0: den = |d| on the chosen side, > 0 unless d is 0 there)
   const bool vx = ax >= 1e-10 && __dmul_rn(nx, ax) > 0.0;
   const bool vy = ay >= 1e-10 && __dmul_rn(ny, ay) > 0.0;
-  const int ix = xdn ? 3 : 1, iy = ydn ? 0 : 2;
   // wall order: the y wall comes first unless it is the top wall (2) and the
-  // x wall the right one (1)
+  // x wall the right one (1); the later wall wins only if strictly closer
   const bool y_first = ydn || xdn;
-  const double fn = y_first ? ny : nx, fd = y_first ? ay : ax, sn = y_first ? nx : ny, sd = y_first ? ax : ay;
-  const bool fv = y_first ? vy : vx, sv = y_first ? vx : vy;
-  const bool second = sv && (!fv || __dmul_rn(sn, fd) < __dmul_rn(fn, sd));
-  if (!(second || fv)) {
-    widx = 0;
-    return __builtin_inf();
-  }
-  widx = second == y_first ? ix : iy;
-  const double u = second ? sn / sd : fn / fd;
+  const double cx = __dmul_rn(nx, ay), cy = __dmul_rn(ny, ax);
+  const bool xw = vx && (!vy || (y_first ? cx < cy : !(cy < cx)));
+  BoxHit h;
+  h.any = vx || vy;
+  h.num = xw ? nx : ny;
+  h.den = xw ? ax : ay;
+  h.wall = h.any ? (xw ? (xdn ? 3 : 1) : (ydn ? 0 : 2)) : 0;
+  return h;
+}
+
+__device__ __forceinline__ double dist_in_box(double px, double py, double dx, double dy, double xb, double yb,
+                                              int& widx) {
+  const BoxHit h = box_hit_in(px, py, dx, dy, xb, yb);
+  widx = h.wall;
+  if (!h.any) return __builtin_inf();
+  const double u = h.num / h.den;
   return u > 0.0 ? u : __builtin_inf();
 }
 
@@ -836,7 +847,14 @@ __device__ __forceinline__ int segment_lat(const DevDomain& D, const TraceParams
                                            double dx, double dy, double& S, double& acc) {
   const double eta = P.eta;
   int k;
-  const double u = dist_to_rect(px, py, dx, dy, sc.poly, k);
+  // (an emitted point lies in the rectangle's half-open box: two candidate
+  // walls, dist_in_box; any other point takes the four-wall test)
+  const double cx0 = sc.poly.x[0], cx1 = sc.poly.x[1], cy0 = sc.poly.y[0], cy1 = sc.poly.y[2];
+  double u;
+  if (cx0 <= px && px < cx1 && cy0 <= py && py < cy1)
+    u = dist_in_box(px, py, dx, dy, dx < 0.0 ? cx0 : cx1, dy < 0.0 ? cy0 : cy1, k);
+  else
+    u = dist_to_box(px, py, dx, dy, cx0, cx1, cy0, cy1, k);
   bool gas;
   double beta = 0.0, tau_b = 0.0;
   if (UNIFORM) {
@@ -857,20 +875,11 @@ __device__ __forceinline__ int segment_lat(const DevDomain& D, const TraceParams
   const int i = lattice_index(L.xs, G.nx, G.inv_x, px), j = lattice_index(L.ys, G.ny, G.inv_y, py);
   if (i < 0 || j < 0) return -1;
   if (gas) return D.n_surfaces + (G.identity ? j * G.nx + i : D.lat_map[j * G.nx + i]);
-  const double x0 = L.xs[i], x1 = L.xs[i + 1], y0 = L.ys[j], y1 = L.ys[j + 1];
-  const double num[4] = {py - y0, x1 - px, y1 - py, px - x0};
-  const double den[4] = {-dy, dx, dy, -dx};
-  double bn = 1.0, bd = 0.0;
-  int w = 0;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const double an = fabs(num[q]), ad = fabs(den[q]);
-    const bool better = (ad >= 1e-10) && (__dmul_rn(num[q], den[q]) > 0.0) && (__dmul_rn(an, bd) < __dmul_rn(bn, ad));
-    bn = better ? an : bn;
-    bd = better ? ad : bd;
-    w = better ? q : w;
-  }
-  // (w = 0 when no wall qualifies, as dist_to_rect / distToSurface2D's findmin)
+  // the end point lies in fine box (i, j) (half-open: lattice_index): the
+  // wall is the nearer of the two the ray points to, in wall order, as the
+  // four-wall test of dist_to_rect would find it (w = 0 when none qualifies,
+  // distToSurface2D's findmin)
+  const int w = box_hit_in(px, py, dx, dy, dx < 0.0 ? L.xs[i] : L.xs[i + 1], dy < 0.0 ? L.ys[j] : L.ys[j + 1]).wall;
   return w == 0 ? (j == 0 ? L.bot[i] : -1)
        : w == 1 ? (i == G.nx - 1 ? L.right[j] : -1)
        : w == 2 ? (j == G.ny - 1 ? L.top[i] : -1)
