@@ -417,13 +417,15 @@ class RayTracingDomain2D:
     def __call__(self, rays_tot: int, method: str = "exchange", nudge: Optional[float] = None,
                  k_dykstra=None, max_iters: int = 1000, verbose: Optional[bool] = None,
                  rec=None, seed: int = 1, device: int = 0, faithful: bool = False, smooth: bool = True,
-                 devices=None):
+                 devices=None, bands: bool = False):
         """multiDispatchRayTrace2D.jl:1-18.  ``method="exchange"``: trace (F_raw)
         then smooth (F_smooth, exchangeRayTracing.jl:13-74) on the device;
         ``smooth=False`` stops after tracing (F_smooth stays None).
-        ``devices``: several GPUs -- a :spectral_variable domain's bands are
-        traced whole on them side by side (band per GPU), any other domain's
-        emitter rows are split over them (rthx_multi_trace_exchange).  The
+        ``devices``: several GPUs -- every traced bin's emitter rows are
+        split over them (rthx_multi_trace_exchange); with ``bands=True`` a
+        :spectral_variable domain's bands are traced whole on them side by
+        side instead (band per GPU; balanced only when the bands cost alike,
+        DESIGN.md §8).  The
         results land in ``self.F_raw`` / ``self.F_smooth`` (copied from the
         device on first read); returns None.
         ``method="direct"``: directRayTracing! (directRayTracing.jl:1-17) on
@@ -443,7 +445,7 @@ class RayTracingDomain2D:
             if devices is not None and len(devices) > 1:
                 from ._lib import HipBackend
 
-                backend = HipBackend(devices, bands=self.spectral_mode == "spectral_variable")
+                backend = HipBackend(devices, bands=bands and self.spectral_mode == "spectral_variable")
             exchange_ray_tracing(self, int(rays_tot), trace_nudge, verbose, rec, seed=seed, device=device,
                                  faithful=faithful, lazy=True, backend=backend)
             if smooth:

@@ -105,7 +105,7 @@ def test_bands_over_devices_equal_one_device(hip):
     one = [F.toarray() for F in dom.F_raw]
     one_s = [np.asarray(F.toarray() if hasattr(F, "toarray") else F) for F in dom.F_smooth]
     dom2 = _mixed_band_domain()
-    dom2(rays, seed=33, verbose=False, devices=[0, 0])
+    dom2(rays, seed=33, verbose=False, devices=[0, 0], bands=True)
     assert sorted(i["bin"] for i in dom2.last_trace_info) == [1, 2, 3, 5]
     two = dom2.F_raw
     assert two[1] is two[3]
@@ -114,3 +114,18 @@ def test_bands_over_devices_equal_one_device(hip):
         S = two_s = dom2.F_smooth[b]
         S = np.asarray(two_s.toarray() if hasattr(two_s, "toarray") else two_s)
         assert np.allclose(S, one_s[b], rtol=0, atol=1e-13)
+
+
+def test_rows_over_devices_per_band_equal_one_device(hip):
+    """mesh(devices=[0, 0]) without bands=True: each traced band's rows are
+    split over the devices (rthx_multi_trace_exchange); same F_raw."""
+    dom = _mixed_band_domain()
+    n = dom.flat().n_emitters
+    rays = 400 * n
+    dom(rays, seed=34, verbose=False, smooth=False)
+    one = [F.toarray() for F in dom.F_raw]
+    dom2 = _mixed_band_domain()
+    dom2(rays, seed=34, verbose=False, smooth=False, devices=[0, 0])
+    assert all(i["n_devices"] == 2 for i in dom2.last_trace_info)
+    for b in range(5):
+        assert np.array_equal(dom2.F_raw[b].toarray(), one[b])

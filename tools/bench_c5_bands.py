@@ -22,13 +22,15 @@ def main():
     ap.add_argument("--rays", type=float, default=1e9)
     ap.add_argument("--devices", default="")
     ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--rows", action="store_true", help="split each band's rows over the devices instead")
     a = ap.parse_args()
     n = _lib.device_count()
     devs = [int(x) for x in a.devices.split(",")] if a.devices else list(range(n))
     dom = H.greenhouse_domain()
     N = dom.flat().n_emitters
     R = int(a.rays) // N
-    kw = dict(seed=1, verbose=False, smooth=False, devices=devs if len(devs) > 1 else None, device=devs[0])
+    kw = dict(seed=1, verbose=False, smooth=False, devices=devs if len(devs) > 1 else None, device=devs[0],
+              bands=not a.rows)
     dom(R * N, **kw)  # uploads + warm-up
     best = None
     for _ in range(a.steps):
@@ -39,7 +41,7 @@ def main():
     info = sorted(dom.last_trace_info, key=lambda i: i["bin"])
     rays = sum(i["rays_traced"] for i in info)
     per = "  ".join(f"b{i['bin']} {i['trace_ms']:.1f}" for i in info)
-    print(f"C5 bands over devices {devs}: {len(info)} band traces, {rays:.3e} rays in {best * 1e3:.1f} ms "
+    print(f"C5 {'rows' if a.rows else 'bands'} over devices {devs}: {len(info)} band traces, {rays:.3e} rays in {best * 1e3:.1f} ms "
           f"({rays / best / 1e9:.2f} Grays/s whole call)  kernel ms: {per}", flush=True)
 
 
