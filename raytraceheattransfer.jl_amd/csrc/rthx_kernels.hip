@@ -449,6 +449,10 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
     const uint64_t lt_mask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     RaySlot RTHX_LDS* q = (RaySlot RTHX_LDS*)(cl_base + D.ml.bytes) + (tid >> 6) * 64;
     __shared__ MBox s_box0;  // the emitter's coarse box: every ray of the row starts there
+#ifdef RTHX_SEGSTAT
+    __shared__ unsigned long long s_segs;  // (diagnostic build: segments walked by the row)
+    if (tid == 0) s_segs = 0ull;
+#endif
     if (tid == 0) ml_enter(mlat_lds_view(cl_base, D.ml), D.ml, s_emit.coarse, s_box0);
     __syncthreads();
     uint32_t q_head = 0, q_cnt = 0;  // wave-uniform ring of 64 slots
@@ -512,7 +516,13 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
         if (__ballot(live) == 0ull) break;  // (queue empty, row exhausted, every end resolved)
       }
       if (live) {
+#ifdef RTHX_SEGSTAT
+        const int it0 = it;
+#endif
         const int a = walk_ml<UNIFORM>(D, P, RTHX_ML_VIEW, RTHX_ML_G, box, px, py, dx, dy, S, acc, it);
+#ifdef RTHX_SEGSTAT
+        atomicAdd(&s_segs, (unsigned long long)(it - it0));
+#endif
         if (a == kRayEndGas || a == kRayEndWall) {
           live = false;
           ending = true;
@@ -523,6 +533,12 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
         }
       }
     }
+#ifdef RTHX_SEGSTAT
+    __syncthreads();
+    if (tid == 0 && slot % 2048 == 0)
+      printf("SEGSTAT bin %d row %lld rays %lld segments %llu per_ray %.3f\n", P.bin, (long long)g,
+             (long long)(r_end - r_begin), s_segs, (double)s_segs / (double)(r_end - r_begin));
+#endif
   } else {
     // Several domains' rays cross many coarse polygons (the greenhouse's 67
     // layers), and their segment counts differ widely.  Ray regeneration: a
