@@ -138,3 +138,24 @@ def test_populate_workspace_matches_reference_order():
     assert np.allclose(ws["Tw"], a["Tw"]) and np.allclose(ws["Volume"], a["vol"])
     assert np.allclose(ws["kappa_g"], a["kappa"]) and np.allclose(ws["omega_g"], a["omega"])
     assert np.array_equal(ws["Qg_known"], (a["Tg"] < 0).astype(int))
+
+
+def test_traced_bands_and_band_shares():
+    """:spectral_variable traces in the reference's order (non-uniform bins
+    alone, then one trace per group of equal uniform beta,
+    parallelRayTracing.jl:20-42) and their split over ranks / devices."""
+    from rthx.distributed import bands_of, traced_bands
+
+    faces = []
+    for k in range(3):
+        y0, y1 = k / 3, (k + 1) / 3
+        kap = np.array([0.5 + k, 1.0, 2.0 * (k + 1), 1.0, 3.0])
+        faces.append(PolyVolume2D([(0, y0), (1, y0), (1, y1), (0, y1)], [k == 0, True, k == 2, True], 5, kap, 0.0))
+    dom = RayTracingDomain2D(faces, [(2, 2)] * 3)
+    traced = traced_bands(dom)
+    assert traced == [(1, [1]), (3, [3]), (2, [2, 4]), (5, [5])]
+    shares = [bands_of(r, 3, traced) for r in range(3)]
+    assert shares == [[(1, [1]), (5, [5])], [(3, [3])], [(2, [2, 4])]]
+    assert sorted(b for s in shares for b, _ in s) == [1, 2, 3, 5]
+    with pytest.raises(ValueError):
+        bands_of(3, 3, traced)
