@@ -659,12 +659,16 @@ uint64_t lookback_wait_ticks() {
 
 // Launch geometry of one trace call (rows, split, LDS histogram layout).
 struct TracePlan {
-  int64_t N = 0, R = 0, end = 0, n_rows = 0, split = 1, row_cap = 1, hash_cap = 0, bm_words = 0;
+  int64_t N = 0, R = 0, end = 0, n_rows = 0, split = 1, row_cap = 1, hash_cap = 0, bm_words = 0, part_cap = 0;
+  bool part_lists = false;  // split rows as sorted part lists + part_merge_kernel (else the dense merge)
   int tally = rthx::kTallyU16;
   int clds = 0;  // rthx_kernels.h LaunchCfg::clds
   bool recording = false, uniform = true;
   size_t lds_bytes = 0, cl_offset = 0;
 };
+
+// Split rows as part lists: staging + merge scratch (16 B per reserved entry) allowed
+constexpr int64_t kPartListBudget = int64_t(24) << 30;
 
 // Hash tallies (large N): the largest table the trace kernel's LDS holds
 // (keys + counts, 8 B per slot); a workgroup traces at most 3/4 as many rays.
@@ -723,7 +727,25 @@ int plan_trace(const rthx_domain* dom, const rthx_trace_args* a, TracePlan& p) {
       p.bm_words = bm;
       p.lds_bytes += 4 * (size_t)bm;
     }
-    if (p.split > 1) p.row_cap = std::max<int64_t>(1, R);  // part lists at p * chunk
+    if (p.split > 1) {  // part lists at p * chunk
+      p.row_cap = std::max<int64_t>(1, R);
+      p.part_cap = (R + p.split - 1) / p.split;
+      p.part_lists = true;
+    }
+  } else if (p.split > 1) {
+    // Split rows with LDS histograms: RTHX_PART_LISTS=1 writes each slice's
+    // counts as a sorted list (min(N, chunk) entries reserved per slice)
+    // merged by part_merge_kernel instead of adding them into a dense
+    // [rows][N] buffer that row_compact_kernel compacts.  The lists are ~1/3
+    // of N at C2 shards, but the merge's binary searches in global memory
+    // are latency-bound: 0.62 / 1.60 ms against the dense merge's 0.15 /
+    // 0.09 ms at 4 / 8 emulated ranks, so the dense merge stays the default.
+    const int64_t pc = std::min<int64_t>(N, (R + p.split - 1) / p.split);
+    if (p.n_rows * p.split * pc * 16 <= kPartListBudget && env_flag("RTHX_PART_LISTS")) {
+      p.part_cap = pc;
+      p.row_cap = p.split * pc;
+      p.part_lists = true;
+    }
   }
   // multi-polygon domains: the coarse mesh goes behind the histogram in LDS
   // when it fits (CLDS kernels, rthx_device.h segment_cl)
@@ -775,11 +797,10 @@ int run_trace(rthx_domain* dom, const rthx_trace_args* a, const TracePlan& p, rt
     HIP_TRY(res->stage_cols.reserve((size_t)n_rows * p.row_cap * 4), "hipMalloc stage_cols");
     HIP_TRY(res->stage_cnt.reserve((size_t)n_rows * p.row_cap * 4), "hipMalloc stage_cnt");
   }
-  const bool hash = p.tally == rthx::kTallyHash;
-  // split rows: the dense per-row counts, or (hash tallies) the part merge's
+  // split rows: the dense per-row counts, or (part lists) the part merge's
   // scratch [2][n_rows][row_cap] followed by part_nnz [n_rows][split]
-  const size_t dense_bytes = hash ? (size_t)n_rows * p.row_cap * 8 + (size_t)n_rows * p.split * 4
-                                  : (size_t)n_rows * N * 4;
+  const size_t dense_bytes = p.part_lists ? (size_t)n_rows * p.row_cap * 8 + (size_t)n_rows * p.split * 4
+                                          : (size_t)n_rows * N * 4;
   if (p.split > 1) HIP_TRY(res->dense.reserve(dense_bytes), "hipMalloc dense rows");
   else res->dense.release();
 
@@ -805,7 +826,8 @@ int run_trace(rthx_domain* dom, const rthx_trace_args* a, const TracePlan& p, rt
   T.row_nnz = res->row_nnz.as<uint32_t>();
   T.row_tallied = res->row_tallied.as<uint32_t>();
   T.dense = p.split > 1 ? res->dense.as<uint32_t>() : nullptr;
-  T.part_nnz = p.split > 1 && hash ? T.dense + 2 * (size_t)n_rows * p.row_cap : nullptr;
+  T.part_nnz = p.split > 1 && p.part_lists ? T.dense + 2 * (size_t)n_rows * p.row_cap : nullptr;
+  T.part_cap = p.part_cap;
   T.hash_cap = (int32_t)p.hash_cap;
   int32_t shift = 32;
   for (int64_t c = p.hash_cap; c > 1; c >>= 1) --shift;
@@ -823,7 +845,7 @@ int run_trace(rthx_domain* dom, const rthx_trace_args* a, const TracePlan& p, rt
   }
   HIP_TRY(hipMemsetAsync(res->totals.p, 0, 32, st), "hipMemset totals");
   if (p.split > 1 && n_rows > 0) {
-    if (!hash) HIP_TRY(hipMemsetAsync(T.dense, 0, (size_t)n_rows * N * 4, st), "hipMemset dense rows");
+    if (!p.part_lists) HIP_TRY(hipMemsetAsync(T.dense, 0, (size_t)n_rows * N * 4, st), "hipMemset dense rows");
     HIP_TRY(hipMemsetAsync(T.row_tallied, 0, (size_t)n_rows * 4, st), "hipMemset row_tallied");
   }
   HIP_TRY(hipEventRecord(dom->ev[0], st), "hipEventRecord");
@@ -850,7 +872,7 @@ int run_trace(rthx_domain* dom, const rthx_trace_args* a, const TracePlan& p, rt
     HIP_TRY(hipMemcpyAsync(totals, res->totals.p, 32, hipMemcpyDeviceToHost, st), "hipMemcpy totals");
     HIP_TRY(hipStreamSynchronize(st), "trace kernel");
   } else {
-    const int merge = p.split == 1 ? rthx::kNoMerge : hash ? rthx::kMergeParts : rthx::kMergeDense;
+    const int merge = p.split == 1 ? rthx::kNoMerge : p.part_lists ? rthx::kMergeParts : rthx::kMergeDense;
     int rc = rthx::finish_staged(res, T, merge, st, dom->ev[2], totals);
     if (rc) return rc;
   }

@@ -47,7 +47,8 @@ struct TallyParams {
   uint32_t* row_nnz;
   uint32_t* row_tallied;
   uint32_t* dense;      // split only: [n_rows][N] (dense tallies) or merge scratch [2][n_rows][row_cap] (hash)
-  uint32_t* part_nnz;   // split hash tallies: [n_rows][split]
+  uint32_t* part_nnz;   // split rows as sorted part lists (hash tallies, or PART_LISTS): [n_rows][split]; null = dense merge
+  int64_t part_cap;     // part lists: entries reserved per part in a row's staging slot
   int32_t hash_cap;     // hash tallies: table slots (power of two; keys then counts in dynamic LDS)
   int32_t hash_shift;   // 32 - log2(hash_cap)
   int64_t bm_words;     // hash tallies: N-bit absorber bitmap after the table (words), 0 = sort the table

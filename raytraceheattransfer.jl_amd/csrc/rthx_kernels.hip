@@ -645,7 +645,7 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
     // output pointers of the row (or part); the look-back runs once every lane knows nnz
     auto out = [&](uint32_t nnz, uint32_t*& oc, uint32_t*& on) {
       if (SPLIT) {
-        const int64_t o = slot * T.row_cap + part * chunk;
+        const int64_t o = slot * T.row_cap + part * T.part_cap;
         oc = T.stage_cols + o;
         on = T.stage_cnt + o;
       } else if (SINGLE && T.lb_status) {
@@ -685,6 +685,22 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
     return;
   }
 
+  auto count2 = [&](int64_t w, uint32_t& lo, uint32_t& hi) {
+    uint32_t v = hist[w];
+    lo = PACK16 ? (v & 0xFFFFu) : v;
+    hi = PACK16 ? (v >> 16) : 0u;
+  };
+  if (SPLIT && T.part_nnz) {
+    // this slice's counts as an ascending list at part * part_cap of the
+    // row's staging slot; part_merge_kernel merges the row's slices
+    const int64_t o = slot * T.row_cap + part * T.part_cap;
+    const uint32_t nnz = compact_row<PACK16>(n_words, count2, T.stage_cols + o, T.stage_cnt + o, wave_sum);
+    if (tid == 0) {
+      T.part_nnz[blockIdx.x] = nnz;
+      atomicAdd(&T.row_tallied[slot], s_tallied);
+    }
+    return;
+  }
   if (SPLIT) {
     // add this slice's nonzero counters into the row's dense buffer
     uint32_t* dense = T.dense + slot * T.n_emitters;
@@ -701,11 +717,6 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
     if (tid == 0) atomicAdd(&T.row_tallied[slot], s_tallied);
     return;
   }
-  auto count2 = [&](int64_t w, uint32_t& lo, uint32_t& hi) {
-    uint32_t v = hist[w];
-    lo = PACK16 ? (v & 0xFFFFu) : v;
-    hi = PACK16 ? (v >> 16) : 0u;
-  };
   if (SINGLE && T.lb_status) {  // (host: single-polygon domains only; keeps the other kernels lean)
     auto base_of = [&](uint32_t nnz) -> uint64_t {
       if (tid == 0) s_base = lookback_offset(T.lb_status, slot, nnz, &T.totals[3], T.lb_wait_ticks);
@@ -762,8 +773,8 @@ __global__ __launch_bounds__(kTraceThreads) void row_compact_kernel(TallyParams 
   if (threadIdx.x == 0) T.row_nnz[slot] = nnz;
 }
 
-// Split rows with hash tallies: merge the row's `split` sorted part lists
-// (stage_*[slot*row_cap + p*chunk ..], part_nnz) into one ascending list in
+// Split rows (hash tallies, or part lists): merge the row's `split` sorted
+// part lists (stage_*[slot*row_cap + p*part_cap ..], part_nnz) into one ascending list in
 // the row's staging slot.  Each entry goes to its rank in the merged order
 // (its index in its own list plus, by binary search, the entries of the
 // other lists that precede it: equal keys of earlier parts first), in the
@@ -772,7 +783,7 @@ __global__ __launch_bounds__(kTraceThreads) void row_compact_kernel(TallyParams 
 __global__ __launch_bounds__(kTraceThreads) void part_merge_kernel(TallyParams T) {
   __shared__ uint32_t wave_sum[kTraceThreads / 64];
   const int64_t slot = blockIdx.x, S = T.split;
-  const int64_t chunk = (T.R + S - 1) / S;
+  const int64_t chunk = T.part_cap;
   const uint32_t tid = threadIdx.x, lane = lane_id();
   const int wave = (int)(tid >> 6);
   const uint32_t* pn = T.part_nnz + slot * S;

@@ -255,6 +255,29 @@ def test_split_rows_exact(hip):
     assert_same(gpu_trace(hip, flat, args), oracle.trace_exchange(flat, args, 16))
 
 
+@pytest.mark.parametrize("case", ["square_pack16", "square_u32", "wedges", "greenhouse"])
+def test_split_part_lists_equal_dense_merge(hip, case, monkeypatch):
+    """Split rows: each slice's counts as a sorted list merged by
+    part_merge_kernel (RTHX_PART_LISTS=1) against the dense row buffer +
+    row_compact_kernel (default), and both against the oracle -- packed and
+    u32 LDS counters, single- and multi-polygon kernels."""
+    if case == "square_pack16":
+        dom, R, kw = H.square_domain(11), 20_000, {}
+    elif case == "square_u32":
+        dom, R, kw = H.square_domain(11), 80_000, dict(begin=3, stride=8)
+    elif case == "wedges":
+        dom, R, kw = H.wedge_domain(16, 4), 9_000, {}
+    else:
+        dom, R, kw = H.greenhouse_domain(n_layers=6, nx=9, ny=3, n_bins=8), 9_000, dict(bin0=2)
+    flat = dom.flat()
+    args, _k = _args(hip, flat, R, seed=41, **kw)
+    a = gpu_trace(hip, flat, args)
+    monkeypatch.setenv("RTHX_PART_LISTS", "1")
+    b = gpu_trace(hip, flat, args)
+    assert_same(a, b)
+    assert_same(a, oracle.trace_exchange(flat, args, 16))
+
+
 def test_edge_cases(hip):
     dom = H.square_domain(5)
     flat = dom.flat()
