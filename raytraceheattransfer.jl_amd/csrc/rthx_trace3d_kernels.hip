@@ -29,6 +29,9 @@ namespace t3 {
 
 constexpr int kThreads = kTrace3dThreads;
 
+#ifndef RTHX_T3_LEAF_LAG
+#define RTHX_T3_LEAF_LAG 8  // the descent stops once at most this many descending lanes hold no leaf yet (0 16 32: slower)
+#endif
 #ifndef RTHX_T3_REFILL
 #define RTHX_T3_REFILL 16  // ray regeneration: refill batch (lanes); 0 = one ray per lane per pass
 #endif
@@ -134,9 +137,9 @@ struct Walk {
     }
   }
 
-  // One round of the walk: descend (speculatively) until every live lane of
-  // the wave holds a leaf, then test the leaves; false once this lane's walk
-  // is over.
+  // One round of the walk: descend (speculatively) until all but
+  // RTHX_T3_LEAF_LAG of the wave's descending lanes hold a leaf, then test
+  // the leaves; false once this lane's walk is over.
   __device__ __forceinline__ bool step(const DevScene3D& S, const Bvh2Node RTHX_LDS* top, int n_top, int group,
                                        int glo, int glen, int RTHX_LDS* stk) {
     while (node >= 0) {
@@ -175,7 +178,7 @@ struct Walk {
         pending = node;
         node = sp > 0 ? stk[--sp * kThreads] : kWalkDone;
       }
-      if (__ballot(pending == 0) == 0ull) break;
+      if (__popcll(__ballot(pending == 0)) <= RTHX_T3_LEAF_LAG) break;
     }
     while (pending < 0) {
       leaf(S, glo, glen, pending);
