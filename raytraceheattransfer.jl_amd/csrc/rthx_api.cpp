@@ -702,7 +702,18 @@ int plan_trace(const rthx_domain* dom, const rthx_trace_args* a, TracePlan& p) {
   const int64_t words = p.tally == rthx::kTallyU16 ? (N + 1) / 2 : N;
   p.lds_bytes = (size_t)words * 4;
   p.row_cap = std::max<int64_t>(1, std::min<int64_t>(N, R));
-  if (p.lds_bytes + rthx::kStaticLdsBytes > rthx::kMaxLdsBytes || env_flag("RTHX_FORCE_HASH")) {
+  // Short rows over many emitters (C5 at 1e8 rays per band: R = 2426, N =
+  // 41205): a hash table of the row's few distinct absorbers plus an N-bit
+  // bitmap is less than half the packed histogram, so more workgroups fit a
+  // CU and the per-row zeroing and compaction shrink: C5 12.97 -> 8.79 ms
+  // per band.  Only unsplit rows (no part merge) of packed histograms.
+  bool short_rows = false;
+  if (p.tally == rthx::kTallyU16 && p.split == 1 && !env_flag("RTHX_NO_SHORT_HASH")) {
+    int64_t h = 256;
+    while (h * 75 < 100 * R) h *= 2;
+    short_rows = h <= kMaxHashCap && 2 * (8 * h + 4 * ((N + 31) / 32)) <= (int64_t)p.lds_bytes;
+  }
+  if (p.lds_bytes + rthx::kStaticLdsBytes > rthx::kMaxLdsBytes || short_rows || env_flag("RTHX_FORCE_HASH")) {
     // Large N: the row is an LDS hash table (rthx_kernels.hip hash_tally)
     // filled at most to load_pct, so a workgroup traces at most 3/4 x
     // kMaxHashCap rays by default; longer rows are split, and their sorted
