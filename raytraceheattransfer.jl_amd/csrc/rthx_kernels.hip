@@ -791,23 +791,55 @@ __global__ __launch_bounds__(kTraceThreads) void part_merge_kernel(TallyParams T
   uint32_t* sn = T.stage_cnt + slot * T.row_cap;
   uint32_t* xk = T.dense + slot * T.row_cap;
   uint32_t* xn = T.dense + (T.n_rows + slot) * T.row_cap;
+  // A row whose parts hold at most kMergeLdsKeys keys (and at most
+  // kMergeMaxParts parts) is merged from an LDS copy of its keys: the binary
+  // searches then run on LDS instead of dependent global loads.
+  constexpr uint32_t kMergeLdsKeys = 8192;
+  constexpr int kMergeMaxParts = 64;
+  __shared__ uint32_t s_keys[kMergeLdsKeys];
+  __shared__ uint32_t s_off[kMergeMaxParts + 1];
   uint32_t total = 0;
+  for (int64_t p = 0; p < S; ++p) total += pn[p];
+  const bool in_lds = total <= kMergeLdsKeys && S <= kMergeMaxParts;
+  if (in_lds) {
+    if (tid == 0) {
+      uint32_t o = 0;
+      for (int64_t p = 0; p < S; ++p) {
+        s_off[p] = o;
+        o += pn[p];
+      }
+      s_off[S] = o;
+    }
+    __syncthreads();
+    for (int64_t p = 0; p < S; ++p)
+      for (uint32_t i = tid; i < pn[p]; i += kTraceThreads) s_keys[s_off[p] + i] = sc[p * chunk + i];
+    __syncthreads();
+  }
   for (int64_t p = 0; p < S; ++p) {
     const uint32_t n = pn[p];
-    total += n;
     const uint32_t* lk = sc + p * chunk;
     for (uint32_t i = tid; i < n; i += kTraceThreads) {
-      const uint32_t k = lk[i];
+      const uint32_t k = in_lds ? s_keys[s_off[p] + i] : lk[i];
       uint32_t rank = i;
       for (int64_t q = 0; q < S; ++q) {
         if (q == p) continue;
-        const uint32_t* qk = sc + q * chunk;
         uint32_t lo = 0, hi = pn[q];
-        while (lo < hi) {
-          const uint32_t mid = (lo + hi) >> 1;
-          const uint32_t v = qk[mid];
-          if (q < p ? v <= k : v < k) lo = mid + 1;
-          else hi = mid;
+        if (in_lds) {
+          const uint32_t* qk = s_keys + s_off[q];
+          while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            const uint32_t v = qk[mid];
+            if (q < p ? v <= k : v < k) lo = mid + 1;
+            else hi = mid;
+          }
+        } else {
+          const uint32_t* qk = sc + q * chunk;
+          while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            const uint32_t v = qk[mid];
+            if (q < p ? v <= k : v < k) lo = mid + 1;
+            else hi = mid;
+          }
         }
         rank += lo;
       }
