@@ -141,6 +141,11 @@ int check_grid(const rthx_grid_desc& g, int32_t count, const char* what) {
 #define RTHX_SPLIT_TARGET 4096
 #endif
 constexpr int64_t kSplitTargetBlocks = RTHX_SPLIT_TARGET;
+// Rows are split only below this many rows: a 4-rank C2 shard (2651 rows)
+// traced unsplit takes 1.058 ms per step against 1.155 ms split in two with
+// the dense merge; an 8-rank shard (1325 rows) keeps its split to ~4096
+// workgroups (1.093 ms; 1.365 unsplit) -- bench.py --emulate-world, round 2.
+constexpr int64_t kSplitBelowRows = 2048;
 constexpr int64_t kSplitMinRays = 2048;
 
 // Device point-location grids: rthx_grid.cpp.  Cells per mean polygon extent
@@ -692,8 +697,10 @@ int plan_trace(const rthx_domain* dom, const rthx_trace_args* a, TracePlan& p) {
   // counters of a large row); each workgroup then traces R/split rays.
   p.recording = a->n_record > 0 && a->record_bin == a->bin;
   p.split = 1;
-  if (!p.recording && p.n_rows > 0 && p.n_rows < kSplitTargetBlocks && R >= 2 * kSplitMinRays)
-    p.split = std::min<int64_t>((kSplitTargetBlocks + p.n_rows - 1) / p.n_rows, R / kSplitMinRays);
+  const int64_t split_target = env_int("RTHX_SPLIT_TARGET", kSplitTargetBlocks, 1, 1 << 20);
+  const int64_t split_below = env_int("RTHX_SPLIT_BELOW", kSplitBelowRows, 1, 1 << 20);
+  if (!p.recording && p.n_rows > 0 && p.n_rows < split_below && R >= 2 * kSplitMinRays)
+    p.split = std::min<int64_t>((split_target + p.n_rows - 1) / p.n_rows, R / kSplitMinRays);
   if (!p.recording && R >= 65536 && ((N + 1) / 2) * 4 + rthx::kStaticLdsBytes <= (int64_t)rthx::kMaxLdsBytes &&
       N * 4 + rthx::kStaticLdsBytes > (int64_t)rthx::kMaxLdsBytes)
     p.split = std::max<int64_t>(p.split, (R + 65534) / 65535);
