@@ -668,6 +668,13 @@ __device__ __forceinline__ void iso_dir(uint32_t w_th, uint32_t w_ph, const doub
   dy = ct;
 }
 
+// EK: the emitter's kind when the caller knows it for the whole workgroup
+// (kEmitAny: read from e; kEmitVolRect: an axis-aligned rectangle volume
+// emitter, e.rect) -- the kind tests then fold away instead of reading the
+// Emitter's flags from LDS for every ray.
+constexpr int kEmitAny = 0, kEmitVolRect = 2;
+template <int EK> struct EmitKind { static constexpr int value = EK; };
+
 // emitVolumeRay2D.jl:1-33: uniform point (quad = triangles ABC / CDA chosen
 // by area), nudged toward the midpoint, isotropic 3D direction projected on
 // the plane (sin(theta) cos(phi), cos(theta)).  cos_tab: the kCosTable
@@ -676,18 +683,18 @@ __device__ __forceinline__ void iso_dir(uint32_t w_th, uint32_t w_ph, const doub
 // directly, (x0 + u1 (x1 - x0), y0 + u2 (y1 - y0)): the same distribution as
 // the reference's two triangles without the square root and the selection
 // draw (faithful sampling keeps the reference's construction).
-template <bool FAITHFUL>
+template <bool FAITHFUL, int EK = kEmitAny>
 __device__ __forceinline__ void emit_volume(const Emitter& e, double eta, const RayWords& rw, const double* cos_tab,
                                             double& px, double& py, double& dx, double& dy) {
   const double R1 = u32(rw.a[0]), R2 = u32(rw.a[1]);
-  if (!FAITHFUL && e.rect) {
+  if (!FAITHFUL && (EK == kEmitVolRect || e.rect)) {
     px = e.v[0] + __dmul_rn(e.v[2] - e.v[0], R1);
     py = e.v[1] + __dmul_rn(e.v[5] - e.v[1], R2);
   } else {
     double s1 = FAITHFUL ? sqrt(R1) : sqrt_unit(R1);
     double wa = 1.0 - s1, wb = __dmul_rn(s1, 1.0 - R2), wc = __dmul_rn(s1, R2);
     double Ax = e.v[0], Ay = e.v[1], Bx = e.v[2], By = e.v[3], Cx = e.v[4], Cy = e.v[5];
-    if (e.nv == 4) {
+    if (EK == kEmitVolRect || e.nv == 4) {
       double sel = u32(rw.sw);
       if (!(sel < e.tri_frac)) {  // (C, D, A)
         Ax = e.v[4]; Ay = e.v[5]; Bx = e.v[6]; By = e.v[7]; Cx = e.v[0]; Cy = e.v[1];
@@ -1190,13 +1197,17 @@ __device__ __forceinline__ double free_path(const TraceParams& P, const double* 
 // The words of ray (g, r) of emitter e (RayWords); pw: the free-path word
 // when the caller already holds the ray's word of block (r >> 2, g, 1, b)
 // (SINGLE kernels amortise that block over four consecutive rays).
+template <int EK = kEmitAny>
+__device__ __forceinline__ bool emitter_surface(const Emitter& e) { return EK == kEmitAny ? e.surface : false; }
+
+template <int EK = kEmitAny>
 __device__ __forceinline__ RayWords ray_words(const TraceParams& P, const Emitter& e, uint32_t g, uint32_t r,
                                               bool have_pw, uint32_t pw, bool faithful) {
   RayWords rw;
   philox_words(r, g, 0u, (uint32_t)P.bin, P.key0, P.key1, rw.a);
   rw.pw = 0u;
   rw.sw = 0u;
-  if (!e.surface) {
+  if (!emitter_surface<EK>(e)) {
     if (have_pw) {
       rw.pw = pw;
     } else {
@@ -1205,7 +1216,8 @@ __device__ __forceinline__ RayWords ray_words(const TraceParams& P, const Emitte
       const uint32_t j = r & 3u;
       rw.pw = j == 0 ? b[0] : j == 1 ? b[1] : j == 2 ? b[2] : b[3];
     }
-    if (e.need_sel || (faithful && e.nv == 4)) {
+    // (a rectangle: need_sel false, nv 4)
+    if (EK == kEmitVolRect ? faithful : (e.need_sel || (faithful && e.nv == 4))) {
       uint32_t c[4];
       philox_words(r, g, 2u, (uint32_t)P.bin, P.key0, P.key1, c);
       rw.sw = c[0];
@@ -1215,19 +1227,20 @@ __device__ __forceinline__ RayWords ray_words(const TraceParams& P, const Emitte
 }
 
 // Emission of ray (g, r): point, direction and free path / tau*.
-template <bool UNIFORM, bool FAITHFUL>
+template <bool UNIFORM, bool FAITHFUL, int EK = kEmitAny>
 __device__ __forceinline__ void start_ray_w(const TraceParams& P, const Emitter& e, const double* tabs,
                                             const RayWords& rw, double& px, double& py, double& dx, double& dy,
                                             double& S) {
-  if (e.surface)
+  const bool surface = emitter_surface<EK>(e);
+  if (surface)
     emit_surface<FAITHFUL>(e, P.eta, rw, px, py, dx, dy);
   else
-    emit_volume<FAITHFUL>(e, P.eta, rw, tabs, px, py, dx, dy);
+    emit_volume<FAITHFUL, EK>(e, P.eta, rw, tabs, px, py, dx, dy);
   // (opaque copies: a select between the two struct fields becomes a
   // dynamically indexed scratch load)
   uint32_t w_surf = rw.a[3], w_vol = rw.pw;
   __asm__ volatile("" : "+v"(w_surf), "+v"(w_vol));
-  S = free_path<UNIFORM, FAITHFUL>(P, tabs, u32(e.surface ? w_surf : w_vol));
+  S = free_path<UNIFORM, FAITHFUL>(P, tabs, u32(surface ? w_surf : w_vol));
 }
 
 template <bool UNIFORM, bool FAITHFUL>
@@ -1240,13 +1253,13 @@ __device__ __forceinline__ void start_ray(const TraceParams& P, const Emitter& e
 // One ray (g, r) of emitter e traced to the end (SINGLE domains: one
 // segment), from its random words.  Returns absorber (-1 = lost); (ox, oy)
 // emission point, (px, py) end point.
-template <bool UNIFORM, bool FAITHFUL, bool SINGLE, bool AXIS, bool LAT = false>
+template <bool UNIFORM, bool FAITHFUL, bool SINGLE, bool AXIS, bool LAT = false, int EK = kEmitAny>
 __device__ __forceinline__ int trace_one_w(const DevDomain& D, const TraceParams& P, const Emitter& e,
                                            const SingleCoarse& sc, const double* tabs, const RayWords& rw,
                                            double& ox, double& oy, double& px, double& py,
                                            const char RTHX_LDS* lat_base = nullptr) {
   double dx, dy, S, acc = 0.0;
-  start_ray_w<UNIFORM, FAITHFUL>(P, e, tabs, rw, px, py, dx, dy, S);
+  start_ray_w<UNIFORM, FAITHFUL, EK>(P, e, tabs, rw, px, py, dx, dy, S);
   ox = px;
   oy = py;
   if (LAT) return segment_lat<UNIFORM>(D, P, sc, lattice_lds_view(lat_base, D.lat), D.lat, px, py, dx, dy, S, acc);

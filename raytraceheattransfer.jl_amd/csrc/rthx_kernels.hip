@@ -396,7 +396,8 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
     // round over the lanes are traced one ray per lane, each drawing its
     // own free-path block, so that no lane traces more than one ray beyond
     // the row's average.
-    auto one_ray = [&](uint32_t r, bool have_pw, uint32_t pw) {
+    auto one_ray = [&](uint32_t r, bool have_pw, uint32_t pw, auto ek) {
+      constexpr int EK = decltype(ek)::value;
       double ox, oy, px, py;
       // Opaque LDS addresses: re-read the loop-invariant coarse record and cos
       // table at their point of use instead of hoisting ~40 values into VGPRs.
@@ -404,8 +405,8 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
       const double RTHX_LDS* tab = lds_opaque(&s_tab[0]);
       const Emitter RTHX_LDS* em = lds_opaque(&s_emit);
       const Emitter& e = *(const Emitter*)em;
-      const RayWords rw = ray_words(P, e, (uint32_t)g, r, have_pw, pw, FAITHFUL);
-      int a = trace_one_w<UNIFORM, FAITHFUL, SINGLE, AXIS, CLDS && AXIS>(
+      const RayWords rw = ray_words<EK>(P, e, (uint32_t)g, r, have_pw, pw, FAITHFUL);
+      int a = trace_one_w<UNIFORM, FAITHFUL, SINGLE, AXIS, CLDS && AXIS, EK>(
           D, P, e, *(const SingleCoarse*)sc, (const double*)tab, rw, ox, oy, px, py, lds_opaque(cl_base));
       tally(a);
       record(r, a, ox, oy, px, py);
@@ -413,7 +414,9 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
     const uint32_t rb = (uint32_t)r_begin, re = (uint32_t)r_end;
     const uint32_t q0 = rb >> 2, q1 = (re + 3u) >> 2;
     const uint32_t q_full = q0 + ((q1 - q0) / (uint32_t)nthr) * (uint32_t)nthr;
-    const bool volume = !lds_opaque(&s_emit)->surface;
+    // (workgroup-uniform flags, in scalar registers)
+    const bool volume = __builtin_amdgcn_readfirstlane((int)lds_opaque(&s_emit)->surface) == 0;
+    const bool vrect = volume && __builtin_amdgcn_readfirstlane((int)lds_opaque(&s_emit)->rect) != 0;
     // Every lane runs the same number of group rounds (q_full - q0 is a
     // multiple of nthr), then the tail rays one per lane: the iteration
     // count and the phase are uniform over the workgroup (scalar registers),
@@ -422,6 +425,10 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
     const uint32_t n_grp = 4u * ((q_full - q0) / (uint32_t)nthr);
     const uint32_t r_tail = 4u * q_full > rb ? 4u * q_full : rb;
     const uint32_t n_it = n_grp + (re > r_tail ? (re - r_tail + (uint32_t)nthr - 1u) / (uint32_t)nthr : 0u);
+    // The loop is compiled twice: for an axis-aligned rectangle volume
+    // emitter (the cells of a lattice: the kind tests of the emission fold
+    // away, EmitKind) and for any emitter.
+    auto rounds = [&](auto ek) {
     uint32_t b0 = 0u, b1 = 0u, b2 = 0u, b3 = 0u;
     for (uint32_t it = 0; it < n_it; ++it) {
       const bool grp = it < n_grp;
@@ -434,7 +441,17 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
       }
       const uint32_t k = r & 3u;
       const uint32_t pw = k == 0u ? b0 : k == 1u ? b1 : k == 2u ? b2 : b3;
-      if (r >= rb && r < re) one_ray(r, true, pw);
+      if (r >= rb && r < re) one_ray(r, true, pw, ek);
+    }
+    };
+    if constexpr (!FAITHFUL) {
+      if (vrect)
+        rounds(EmitKind<kEmitVolRect>{});
+      else
+        rounds(EmitKind<kEmitAny>{});
+    } else {
+      (void)vrect;
+      rounds(EmitKind<kEmitAny>{});
     }
   } else if constexpr (MLAT) {
     // Layered / lattice domains.  Rays walk many coarse boxes and their walk
