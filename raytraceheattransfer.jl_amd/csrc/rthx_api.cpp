@@ -809,9 +809,16 @@ int run_trace(rthx_domain* dom, const rthx_trace_args* a, const TracePlan& p, rt
     res->stage_cnt.release();
     HIP_TRY(res->cols.reserve((size_t)n_rows * p.row_cap * 4), "hipMalloc cols");
     HIP_TRY(res->cnt.reserve((size_t)n_rows * p.row_cap * 4), "hipMalloc cnt");
-    HIP_TRY(res->lb_status.reserve((size_t)n_rows * 8), "hipMalloc look-back words");
+    // fresh words or totals (or a wrapped epoch): zero them once, epoch 1
+    const size_t lb_bytes = (size_t)n_rows * 8;
+    if (!res->lb_status.p || lb_bytes > res->lb_status.cap || !res->lb_totals.p) res->lb_epoch = 0;
+    HIP_TRY(res->lb_status.reserve(lb_bytes), "hipMalloc look-back words");
+    HIP_TRY(res->lb_totals.reserve(8 * 8), "hipMalloc look-back totals");
+    HIP_TRY(res->h_totals.reserve(4 * 8), "hipHostMalloc totals");
   } else {
     res->lb_status.release();
+    res->lb_totals.release();
+    res->lb_epoch = 0;
     HIP_TRY(res->stage_cols.reserve((size_t)n_rows * p.row_cap * 4), "hipMalloc stage_cols");
     HIP_TRY(res->stage_cnt.reserve((size_t)n_rows * p.row_cap * 4), "hipMalloc stage_cnt");
   }
@@ -858,10 +865,23 @@ int run_trace(rthx_domain* dom, const rthx_trace_args* a, const TracePlan& p, rt
     T.out_cols = res->cols.as<uint32_t>();
     T.out_cnt = res->cnt.as<uint32_t>();
     T.row_off = res->row_off.as<int64_t>();
-    T.totals = res->totals.as<unsigned long long>();
-    HIP_TRY(hipMemsetAsync(T.lb_status, 0, (size_t)n_rows * 8, st), "hipMemset look-back words");
+    // The words carry the launch's epoch and row 0 zeroes the other set of
+    // totals for the next launch, so nothing is zeroed between launches but
+    // at the first and after 65535 (the epoch's wrap).
+    uint32_t e = res->lb_epoch;
+    if (e == 0 || e >= rthx::kLbEpochMax) {
+      HIP_TRY(hipMemsetAsync(T.lb_status, 0, res->lb_status.cap, st), "hipMemset look-back words");
+      HIP_TRY(hipMemsetAsync(res->lb_totals.p, 0, 8 * 8, st), "hipMemset look-back totals");
+      e = 0;
+    }
+    ++e;
+    res->lb_epoch = 0;  // set again once the launch has completed
+    T.lb_epoch = e;
+    T.totals = res->lb_totals.as<unsigned long long>() + 4 * (e & 1);
+    T.totals_next = res->lb_totals.as<unsigned long long>() + 4 * ((e + 1) & 1);
+  } else {
+    HIP_TRY(hipMemsetAsync(res->totals.p, 0, 32, st), "hipMemset totals");
   }
-  HIP_TRY(hipMemsetAsync(res->totals.p, 0, 32, st), "hipMemset totals");
   if (p.split > 1 && n_rows > 0) {
     if (!p.part_lists) HIP_TRY(hipMemsetAsync(T.dense, 0, (size_t)n_rows * N * 4, st), "hipMemset dense rows");
     HIP_TRY(hipMemsetAsync(T.row_tallied, 0, (size_t)n_rows * 4, st), "hipMemset row_tallied");
@@ -887,8 +907,10 @@ int run_trace(rthx_domain* dom, const rthx_trace_args* a, const TracePlan& p, rt
   HIP_TRY(hipEventRecord(dom->ev[1], st), "hipEventRecord");
   if (lookback) {
     HIP_TRY(hipEventRecord(dom->ev[2], st), "hipEventRecord");
-    HIP_TRY(hipMemcpyAsync(totals, res->totals.p, 32, hipMemcpyDeviceToHost, st), "hipMemcpy totals");
+    HIP_TRY(hipMemcpyAsync(res->h_totals.p, T.totals, 32, hipMemcpyDeviceToHost, st), "hipMemcpy totals");
     HIP_TRY(hipStreamSynchronize(st), "trace kernel");
+    std::memcpy(totals, res->h_totals.p, 32);
+    res->lb_epoch = T.lb_epoch;
   } else {
     const int merge = p.split == 1 ? rthx::kNoMerge : p.part_lists ? rthx::kMergeParts : rthx::kMergeDense;
     int rc = rthx::finish_staged(res, T, merge, st, dom->ev[2], totals);
@@ -963,7 +985,8 @@ int trace_exchange_one(rthx_domain* dom, const rthx_trace_args* a, rthx_result* 
   // layers), and a row waiting on a slower predecessor idles its CU slot
   // (C5 greenhouse: 15.2 -> 17.6 ms per band with the look-back).  The
   // recorder's kernels stage.
-  const bool lookback = p.split == 1 && n_rows > 0 && dom->single_convex && !p.recording && !env_flag("RTHX_NO_LOOKBACK");
+  const bool lookback = p.split == 1 && n_rows > 0 && dom->single_convex && !p.recording &&
+                        (uint64_t)n_rows * (uint64_t)p.row_cap <= rthx::kLbValMax && !env_flag("RTHX_NO_LOOKBACK");
   int64_t totals[4] = {0, 0, 0, 0};
   float ms_trace = 0.f, ms_pack = 0.f;
   rc = run_trace(dom, a, p, res, lookback, rec, totals, &ms_trace, &ms_pack);
@@ -1265,8 +1288,9 @@ RTHX_EXPORT int rthx_multi_trace_exchange(rthx_multi* m, const rthx_trace_args* 
     (void)hipSetDevice(res->device);
     rthx::DevBuf* all[] = {&res->stage_cols, &res->stage_cnt, &res->row_nnz, &res->row_tallied, &res->row_off,
                            &res->totals,     &res->cols,      &res->cnt,     &res->dense,       &res->rec_ids,
-                           &res->rec_ok,     &res->rec_orig,  &res->rec_end, &res->lb_status};
+                           &res->rec_ok,     &res->rec_orig,  &res->rec_end, &res->lb_status, &res->lb_totals};
     for (rthx::DevBuf* b : all) b->release();
+    res->lb_epoch = 0;
     res->device = -1;
   }
   while (res->parts.size() < nd) res->parts.push_back(new rthx_result());

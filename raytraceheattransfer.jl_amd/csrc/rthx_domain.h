@@ -54,6 +54,9 @@ struct rthx_result {
   rthx::DevBuf stage_cols, stage_cnt, row_nnz, row_tallied, row_off, totals, cols, cnt, dense;
   rthx::DevBuf rec_ids, rec_ok, rec_orig, rec_end;
   rthx::DevBuf lb_status;  // direct-CSR look-back words (unsplit launches)
+  rthx::DevBuf lb_totals;  // look-back launches' totals, two sets of 4 (launch e uses set e & 1)
+  uint32_t lb_epoch = 0;   // epoch of the last look-back launch; 0 = words and totals not yet zeroed
+  rthx::HostBuf h_totals;  // pinned copy of a look-back launch's totals
   rthx::DevBuf fvals;      // F_raw values (rthx_result_copy_F)
   bool valid = false;
   bool host_row_off = false;
@@ -69,11 +72,12 @@ struct rthx_result {
     for (rthx_result* p : parts) delete p;
     if (device >= 0) (void)hipSetDevice(device);
     rthx::DevBuf* all[] = {&stage_cols, &stage_cnt, &row_nnz,  &row_tallied, &row_off,  &totals, &cols,
-                     &cnt,        &dense,     &rec_ids,  &rec_ok,      &rec_orig, &rec_end, &lb_status, &fvals};
+                     &cnt,        &dense,     &rec_ids,  &rec_ok,      &rec_orig, &rec_end, &lb_status, &lb_totals, &fvals};
     for (rthx::DevBuf* b : all) b->release();
     h_cols.release();
     h_cnt.release();
     h_vals.release();
+    h_totals.release();
   }
 };
 

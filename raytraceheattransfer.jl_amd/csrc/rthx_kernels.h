@@ -54,15 +54,25 @@ struct TallyParams {
   int64_t bm_words;     // hash tallies: N-bit absorber bitmap after the table (words), 0 = sort the table
   // Unsplit 2D launches: rows go straight into the final CSR (cols / cnt at
   // the row's offset, found by a decoupled look-back over lb_status, one
-  // zeroed u64 per row); nullptr = staging + row_scan_kernel + csr_pack_kernel.
+  // u64 per row tagged with the launch's epoch, so the words need no zeroing
+  // between launches); nullptr = staging + row_scan_kernel + csr_pack_kernel.
   unsigned long long* lb_status;
   uint32_t* out_cols;
   uint32_t* out_cnt;
   int64_t* row_off;              // [n_rows + 1]
   unsigned long long* totals;    // nnz, lost rays, max lost per row, look-back stalls (zeroed)
+  unsigned long long* totals_next;  // look-back launches: the next launch's totals, zeroed by row 0
   int64_t R;
   uint64_t lb_wait_ticks;        // longest look-back wait (s_memrealtime ticks, 100 MHz) before giving up
+  uint32_t lb_epoch;             // 1 .. kLbEpochMax: tag of this launch's look-back words
 };
+
+// Look-back word: flag (1 aggregate, 2 inclusive prefix) in bits 62-63, the
+// launch epoch in bits 46-61, the value below.  A word of another epoch
+// (or a zeroed one: epochs start at 1) is not yet published.
+constexpr int kLbEpochShift = 46;
+constexpr uint32_t kLbEpochMax = 0xFFFF;
+constexpr unsigned long long kLbValMax = (1ull << kLbEpochShift) - 1;
 
 struct LaunchCfg {
   const DevDomain* D;

@@ -52,8 +52,9 @@ namespace rthx {
 // row `slot` publishes its nnz as an aggregate (flag 1), walks back over its
 // predecessors' words adding aggregates until it meets an inclusive prefix
 // (flag 2), then publishes its own inclusive prefix.  One u64 per row: flag
-// in bits 62-63, value below.  Agent-scope atomics (coherent across the
-// XCDs' L2s).
+// in bits 62-63, the launch epoch in bits 46-61 (a word of an earlier launch
+// reads as unpublished, so the words are zeroed only when the epoch wraps),
+// value below.  Agent-scope atomics (coherent across the XCDs' L2s).
 // Progress: workgroups are dispatched in order within each XCD (not across
 // the chip), so the lowest unfinished row m is always resident or next in
 // line: every row ahead of it in its XCD's queue has a smaller index and has
@@ -65,20 +66,23 @@ namespace rthx {
 // ones, so the misplaced rows stay inside cols / counts, and the host then
 // traces the launch again on the staging path (rthx_api.cpp run_trace).
 __device__ __forceinline__ uint64_t lookback_offset(unsigned long long* status, int64_t slot, uint32_t nnz,
-                                                    unsigned long long* stalled, uint64_t wait_ticks) {
-  constexpr unsigned long long kAgg = 1ull << 62, kInc = 2ull << 62, kVal = (1ull << 62) - 1;
+                                                    unsigned long long* stalled, uint64_t wait_ticks,
+                                                    uint32_t epoch) {
+  constexpr unsigned long long kAgg = 1ull << 62, kInc = 2ull << 62, kVal = kLbValMax;
+  const unsigned long long tag = (unsigned long long)epoch << kLbEpochShift;
   if (slot == 0) {
-    __hip_atomic_store(&status[0], kInc | nnz, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&status[0], kInc | tag | nnz, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return 0;
   }
-  __hip_atomic_store(&status[slot], kAgg | nnz, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(&status[slot], kAgg | tag | nnz, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   unsigned long long excl = 0;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   bool gave_up = false;
   uint32_t polls = 0;
   for (int64_t j = slot - 1; !gave_up; --j) {
     unsigned long long v;
-    while (((v = __hip_atomic_load(&status[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 62) == 0) {
+    while ((((v = __hip_atomic_load(&status[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> kLbEpochShift) &
+            kLbEpochMax) != epoch) {
       __builtin_amdgcn_s_sleep(1);
       // the clock is read every 16th poll (a scalar-memory round trip each);
       // a zero bound (tests) gives up at the first unpublished predecessor
@@ -92,7 +96,7 @@ __device__ __forceinline__ uint64_t lookback_offset(unsigned long long* status, 
     excl += v & kVal;
     if ((v >> 62) == 2) break;
   }
-  __hip_atomic_store(&status[slot], kInc | (excl + nnz), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(&status[slot], kInc | tag | (excl + nnz), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return excl;
 }
 
@@ -653,6 +657,8 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
         T.row_off[T.n_rows] = (int64_t)(b + nnz);
         T.totals[0] = b + nnz;
       }
+      if (slot == 0)  // the next look-back launch's totals (rthx_api.cpp run_trace)
+        for (int i = 0; i < 4; ++i) T.totals_next[i] = 0ull;
     }
   };
   if constexpr (HASH) {
@@ -666,7 +672,7 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
         oc = T.stage_cols + o;
         on = T.stage_cnt + o;
       } else if (SINGLE && T.lb_status) {
-        if (tid == 0) s_base = lookback_offset(T.lb_status, slot, nnz, &T.totals[3], T.lb_wait_ticks);
+        if (tid == 0) s_base = lookback_offset(T.lb_status, slot, nnz, &T.totals[3], T.lb_wait_ticks, T.lb_epoch);
         __syncthreads();
         oc = T.out_cols + s_base;
         on = T.out_cnt + s_base;
@@ -736,7 +742,7 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
   }
   if (SINGLE && T.lb_status) {  // (host: single-polygon domains only; keeps the other kernels lean)
     auto base_of = [&](uint32_t nnz) -> uint64_t {
-      if (tid == 0) s_base = lookback_offset(T.lb_status, slot, nnz, &T.totals[3], T.lb_wait_ticks);
+      if (tid == 0) s_base = lookback_offset(T.lb_status, slot, nnz, &T.totals[3], T.lb_wait_ticks, T.lb_epoch);
       __syncthreads();
       return s_base;
     };

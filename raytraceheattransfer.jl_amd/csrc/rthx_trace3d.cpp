@@ -512,6 +512,8 @@ RTHX_EXPORT int rthx_trace_exchange_3d(rthx_scene3d* sc, const rthx_trace_args* 
   res->info.rays_traced = n_rows * R;
   res->info.n_devices = 1;
   res->lb_status.release();
+  res->lb_totals.release();
+  res->lb_epoch = 0;
   HIP_TRY(res->stage_cols.reserve((size_t)n_rows * row_cap * 4), "hipMalloc stage_cols");
   HIP_TRY(res->stage_cnt.reserve((size_t)n_rows * row_cap * 4), "hipMalloc stage_cnt");
   HIP_TRY(res->row_nnz.reserve((size_t)n_rows * 4), "hipMalloc row_nnz");

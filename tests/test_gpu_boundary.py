@@ -187,6 +187,55 @@ def test_lookback_stall_falls_back_to_staging(hip, monkeypatch):
     assert np.array_equal(ref[2], small[2])
 
 
+def _open_square(ndim):
+    """A square whose top wall is open (rays through it are lost), so the
+    look-back launch's lost-ray totals (atomics) are non-zero."""
+    face = H.PolyVolume2D([(0.0, 0.0), (1.0, 0.0), (1.0, 1.0), (0.0, 1.0)], [True, True, False, True], 1, 1.0, 0.0)
+    face.T_in_w = [1000.0, 0.0, 0.0, 0.0]
+    face.epsilon = [1.0] * 4
+    face.T_in_g = -1.0
+    face.q_in_g = 0.0
+    return H.RayTracingDomain2D([face], [(ndim, ndim)])
+
+
+def test_reused_result_across_lookback_launches(hip, monkeypatch):
+    """One result object traced again and again (as bench.py does): the
+    look-back words are tagged with the launch's epoch and row 0 zeroes the
+    next launch's totals, so nothing is zeroed between launches.  Every call
+    (growing and shrinking row counts, a staging launch in between) must
+    give the counts and totals of a fresh result, and the totals must not
+    accumulate over calls."""
+    small, big = _open_square(23), _open_square(37)
+    fs, fb = small.flat(), big.flat()
+    ds, db = hip.DeviceDomain(fs, 0), hip.DeviceDomain(fb, 0)
+    a_s, _k1 = _args(hip, fs, 2000, seed=11)
+    a_b, _k2 = _args(hip, fb, 1500, seed=12)
+    want_s, want_b = _trace(hip, ds, a_s), _trace(hip, db, a_b)
+    assert want_s[3]["lost_total"] > 0 and want_b[3]["lost_total"] > 0
+    res = hip.DeviceResult()
+    try:
+        plan = ["s", "s", "b", "s", "staging", "b", "b", "s"] + ["s"] * 8
+        for step in plan:
+            if step == "staging":
+                monkeypatch.setenv("RTHX_NO_LOOKBACK", "1")
+            dd, args, want = (db, a_b, want_b) if step == "b" else (ds, a_s, want_s)
+            res.trace(dd, args)
+            monkeypatch.delenv("RTHX_NO_LOOKBACK", raising=False)
+            info = res.info()
+            rp, cols, cnt = res.csr()
+            for x, y in zip(want[:3], (rp, cols, cnt)):
+                assert np.array_equal(x, y), step
+            for k in ("nnz", "lost_total", "lost_max_row"):
+                assert info[k] == want[3][k], (step, k)
+            assert info["lookback_fallbacks"] == 0
+    finally:
+        res.close()
+        ds.close()
+        db.close()
+    ref = oracle.trace_exchange(fs, a_s, 16)
+    assert np.array_equal(want_s[2], ref[2]) and want_s[3]["lost_total"] == ref[3]["lost_total"]
+
+
 @pytest.mark.parametrize("case", ["grey11", "transparent", "scatter"])
 def test_smooth_from_device_result_equals_host_csr_smoothing(hip, case):
     """rthx_smooth_F_result (counts never leave the device) equals
