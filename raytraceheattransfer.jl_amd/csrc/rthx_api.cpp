@@ -813,8 +813,8 @@ int run_trace(rthx_domain* dom, const rthx_trace_args* a, const TracePlan& p, rt
     const size_t lb_bytes = (size_t)n_rows * 8;
     if (!res->lb_status.p || lb_bytes > res->lb_status.cap || !res->lb_totals.p) res->lb_epoch = 0;
     HIP_TRY(res->lb_status.reserve(lb_bytes), "hipMalloc look-back words");
-    HIP_TRY(res->lb_totals.reserve(8 * 8), "hipMalloc look-back totals");
-    HIP_TRY(res->h_totals.reserve(4 * 8), "hipHostMalloc totals");
+    HIP_TRY(res->lb_totals.reserve(2 * 8 * 8), "hipMalloc look-back totals");
+    HIP_TRY(res->h_totals.reserve(8 * 8), "hipHostMalloc totals");
   } else {
     res->lb_status.release();
     res->lb_totals.release();
@@ -871,14 +871,14 @@ int run_trace(rthx_domain* dom, const rthx_trace_args* a, const TracePlan& p, rt
     uint32_t e = res->lb_epoch;
     if (e == 0 || e >= rthx::kLbEpochMax) {
       HIP_TRY(hipMemsetAsync(T.lb_status, 0, res->lb_status.cap, st), "hipMemset look-back words");
-      HIP_TRY(hipMemsetAsync(res->lb_totals.p, 0, 8 * 8, st), "hipMemset look-back totals");
+      HIP_TRY(hipMemsetAsync(res->lb_totals.p, 0, 2 * 8 * 8, st), "hipMemset look-back totals");
       e = 0;
     }
     ++e;
     res->lb_epoch = 0;  // set again once the launch has completed
     T.lb_epoch = e;
-    T.totals = res->lb_totals.as<unsigned long long>() + 4 * (e & 1);
-    T.totals_next = res->lb_totals.as<unsigned long long>() + 4 * ((e + 1) & 1);
+    T.totals = res->lb_totals.as<unsigned long long>() + 8 * (e & 1);
+    T.totals_next = res->lb_totals.as<unsigned long long>() + 8 * ((e + 1) & 1);
   } else {
     HIP_TRY(hipMemsetAsync(res->totals.p, 0, 32, st), "hipMemset totals");
   }
@@ -907,6 +907,9 @@ int run_trace(rthx_domain* dom, const rthx_trace_args* a, const TracePlan& p, rt
   HIP_TRY(hipEventRecord(dom->ev[1], st), "hipEventRecord");
   if (lookback) {
     HIP_TRY(hipEventRecord(dom->ev[2], st), "hipEventRecord");
+    // (a last-row hand-over of the totals into page-locked memory, counting
+    // finished rows with one more atomic per row, measured 14 us slower per
+    // launch than this copy: profiles/round2/hosttot_ab.txt)
     HIP_TRY(hipMemcpyAsync(res->h_totals.p, T.totals, 32, hipMemcpyDeviceToHost, st), "hipMemcpy totals");
     HIP_TRY(hipStreamSynchronize(st), "trace kernel");
     std::memcpy(totals, res->h_totals.p, 32);

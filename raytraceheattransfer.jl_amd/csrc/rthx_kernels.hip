@@ -18,6 +18,8 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <map>
+#include <mutex>
 
 #include "rthx_device.h"
 #include "rthx_kernels.h"
@@ -970,30 +972,68 @@ __global__ __launch_bounds__(256) void csr_pack_kernel(const uint32_t* __restric
 // ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
+// Workgroup size chosen for a (kernel, dynamic LDS bytes, device); 0 = not yet.
+struct OccKey {
+  const void* kern;
+  size_t lds;
+  int device;
+  bool operator<(const OccKey& o) const {
+    return kern != o.kern ? kern < o.kern : lds != o.lds ? lds < o.lds : device < o.device;
+  }
+};
+static std::mutex g_occ_mu;
+static std::map<OccKey, int> g_occ;
+static int occ_device() {
+  int d = 0;
+  (void)hipGetDevice(&d);
+  return d;
+}
+static int occupancy_cache_get(const void* kern, size_t lds) {
+  const OccKey k{kern, lds, occ_device()};
+  std::lock_guard<std::mutex> g(g_occ_mu);
+  auto it = g_occ.find(k);
+  return it == g_occ.end() ? 0 : it->second;
+}
+static void occupancy_cache_put(const void* kern, size_t lds, int threads) {
+  const OccKey k{kern, lds, occ_device()};
+  std::lock_guard<std::mutex> g(g_occ_mu);
+  g_occ[k] = threads;
+}
+
 template <bool UNIFORM, int TALLY, bool FAITHFUL, bool SINGLE, bool REC, bool SPLIT, bool AXIS, int CL = 0>
 static hipError_t launch_trace_t(const LaunchCfg& L) {
   auto kern = trace_exchange_kernel<UNIFORM, TALLY, FAITHFUL, SINGLE, REC, SPLIT, AXIS, CL>;
-  if (L.lds_bytes > 64 * 1024) {  // (occupancy queries above 64 KiB need the attribute first)
-    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)L.lds_bytes);
-    if (e != hipSuccess) return e;
-  }
   const int64_t blocks = L.T.n_rows * (SPLIT ? L.T.split : 1);
   // (MLAT kernels: a 64-slot ray queue per wave behind the lattice)
   auto lds_for = [&](int t) { return L.lds_bytes + (CL == 2 && !SINGLE ? (size_t)t * kRaySlotBytes : 0); };
   // Workgroup size: the one that keeps most waves resident per CU.  With a
   // large LDS row histogram (large N) only one or two workgroups fit a CU,
-  // and 1024-lane workgroups keep 16 waves busy instead of 4.
-  int threads = kTraceThreads, best_waves = 0;
-  for (int t = kTraceThreads; t <= kMaxTraceThreads; t *= 2) {
-    if (lds_for(t) + (size_t)kStaticLdsBytes > kMaxLdsBytes) break;
-    int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, t, lds_for(t)) != hipSuccess)
-      break;
-    if (per_cu * (t / 64) > best_waves) {
-      best_waves = per_cu * (t / 64);
-      threads = t;
+  // and 1024-lane workgroups keep 16 waves busy instead of 4.  The choice is
+  // cached per (kernel, LDS bytes, device): the queries cost more host time
+  // per call than the rest of the launch.
+  if (L.lds_bytes > 64 * 1024) {  // (occupancy queries above 64 KiB need the attribute first)
+    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)L.lds_bytes);
+    if (e != hipSuccess) return e;
+  }
+  int threads = occupancy_cache_get((const void*)kern, L.lds_bytes);
+  if (threads == 0) {
+    int best_waves = 0;
+    threads = kTraceThreads;
+    bool queried = true;
+    for (int t = kTraceThreads; t <= kMaxTraceThreads; t *= 2) {
+      if (lds_for(t) + (size_t)kStaticLdsBytes > kMaxLdsBytes) break;
+      int per_cu = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, t, lds_for(t)) != hipSuccess) {
+        queried = false;
+        break;
+      }
+      if (per_cu * (t / 64) > best_waves) {
+        best_waves = per_cu * (t / 64);
+        threads = t;
+      }
     }
+    if (queried) occupancy_cache_put((const void*)kern, L.lds_bytes, threads);
   }
   if (L.threads == 256 || L.threads == 512 || L.threads == 1024) threads = L.threads;
   const size_t lds = lds_for(threads);
