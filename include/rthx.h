@@ -207,6 +207,37 @@ int rthx_result_copy_rays(const rthx_result* res, double* origins_xy,
                           double* endpoints_xy, int64_t* emitter, int64_t cap,
                           int64_t* n_out);
 
+/* The count matrix where it lies, in device memory, for a collective (RCCL
+ * over xGMI) to send without a round trip through the host -- the rows a
+ * rank or device traced are its block of the gather that assembles F
+ * (the reference's per-thread blocks,
+ * parallelRayTracing.jl:81-102,154).  Block k = 0 .. n_rows-1 holds emitter
+ * emitter_begin + k * emitter_stride; row_off[n_rows+1] (int64), cols[nnz]
+ * and counts[nnz] (uint32) are device pointers on `device`, valid until the
+ * result is traced into again or destroyed.  A result of
+ * rthx_multi_trace_exchange holds one block per device: `part` selects it
+ * (n_parts receives their number; 1 for a one-device trace). */
+typedef struct rthx_device_csr {
+  int32_t device;
+  int32_t n_parts;
+  int64_t n_rows;
+  int64_t nnz;
+  int64_t emitter_begin;
+  int64_t emitter_stride;
+  const int64_t* row_off;
+  const uint32_t* cols;
+  const uint32_t* counts;
+} rthx_device_csr;
+
+int rthx_result_get_device_csr(const rthx_result* res, int32_t part, rthx_device_csr* out);
+
+/* Device-to-device copy of block `part` into caller buffers on the same
+ * device (e.g. the tensors a collective sends): row_off[n_rows+1],
+ * cols[nnz], counts[nnz]; any pointer may be NULL.  Returns when the copy is
+ * complete. */
+int rthx_result_copy_csr_device(const rthx_result* res, int32_t part, int64_t* row_off, uint32_t* cols,
+                                uint32_t* counts);
+
 /* ------------------------------------------------------------------------
  * Several devices: the GPU counterpart of the reference's
  * static emitter partition over threads (parallelRayTracing.jl:81-102).  The

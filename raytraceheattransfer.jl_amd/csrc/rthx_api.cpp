@@ -513,6 +513,9 @@ RTHX_EXPORT int rthx_domain_create(const rthx_domain_desc* desc, int32_t device,
         std::memcpy(b + G.off_bsolid, bsolid.data(), 4 * nc);
         UP(blob.data(), blob.size(), D.ml_blob);
         UP(bbeta.data(), bbeta.size(), D.ml_bbeta);
+        d->ml_mixed.assign((size_t)s.n_bins, 0);
+        for (int bn = 0; bn < s.n_bins; ++bn)
+          for (size_t bx = 0; bx < nc; ++bx) d->ml_mixed[bn] |= bbeta[(size_t)bn * nc + bx] < 0.0 ? 1 : 0;
         D.ml = G;
       }
     }
@@ -837,6 +840,7 @@ int run_trace(rthx_domain* dom, const rthx_trace_args* a, const TracePlan& p, rt
   P.key0 = (uint32_t)a->seed;
   P.key1 = (uint32_t)(a->seed >> 32);
   P.bin = a->bin;
+  P.mixed = p.clds == 2 && !dom->ml_mixed.empty() ? dom->ml_mixed[a->bin] : 1;
   P.beta_uniform = dom->beta_first[a->bin];
   P.inv_beta_uniform = P.beta_uniform > 0 ? 1.0 / P.beta_uniform : 0.0;
 
@@ -1213,6 +1217,58 @@ RTHX_EXPORT int rthx_result_copy_F(const rthx_result* cres, int64_t* row_ptr, in
   if (!cres) return fail(RTHX_EINVAL, "null result");
   if (!cres->valid) return fail(RTHX_ESTATE, "result holds no trace");
   return copy_result(const_cast<rthx_result*>(cres), row_ptr, cols, nullptr, vals);
+}
+
+namespace {
+// Block `part` of a result (itself for a one-device trace).
+int device_block(const rthx_result* cres, int32_t part, rthx_result** out, int32_t* n_parts) {
+  if (!cres) return fail(RTHX_EINVAL, "null result");
+  if (!cres->valid) return fail(RTHX_ESTATE, "result holds no trace");
+  rthx_result* res = const_cast<rthx_result*>(cres);
+  const int32_t np = res->parts.empty() ? 1 : (int32_t)res->parts.size();
+  if (part < 0 || part >= np) return fail(RTHX_EINVAL, "part out of range");
+  *out = res->parts.empty() ? res : res->parts[part];
+  if (n_parts) *n_parts = np;
+  return RTHX_OK;
+}
+}  // namespace
+
+RTHX_EXPORT int rthx_result_get_device_csr(const rthx_result* cres, int32_t part, rthx_device_csr* out) {
+  if (!out) return fail(RTHX_EINVAL, "null output");
+  rthx_result* q = nullptr;
+  int32_t np = 1;
+  int rc = device_block(cres, part, &q, &np);
+  if (rc) return rc;
+  *out = rthx_device_csr{};
+  out->device = q->device;
+  out->n_parts = np;
+  out->n_rows = q->n_rows;
+  out->nnz = q->info.nnz;
+  out->emitter_begin = q->begin;
+  out->emitter_stride = q->stride;
+  out->row_off = q->row_off.as<int64_t>();
+  out->cols = q->cols.as<uint32_t>();
+  out->counts = q->cnt.as<uint32_t>();
+  return RTHX_OK;
+}
+
+RTHX_EXPORT int rthx_result_copy_csr_device(const rthx_result* cres, int32_t part, int64_t* row_off, uint32_t* cols,
+                                            uint32_t* counts) {
+  rthx_result* q = nullptr;
+  int rc = device_block(cres, part, &q, nullptr);
+  if (rc) return rc;
+  HIP_TRY(hipSetDevice(q->device), "hipSetDevice");
+  hipStream_t st = nullptr;
+  HIP_TRY(rthx::device_stream(q->device, &st), "device stream");
+  const size_t nnz = (size_t)q->info.nnz;
+  if (row_off && q->n_rows >= 0)
+    HIP_TRY(hipMemcpyAsync(row_off, q->row_off.p, (size_t)(q->n_rows + 1) * 8, hipMemcpyDeviceToDevice, st),
+            "hipMemcpy row_off D2D");
+  if (cols && nnz) HIP_TRY(hipMemcpyAsync(cols, q->cols.p, nnz * 4, hipMemcpyDeviceToDevice, st), "hipMemcpy cols D2D");
+  if (counts && nnz)
+    HIP_TRY(hipMemcpyAsync(counts, q->cnt.p, nnz * 4, hipMemcpyDeviceToDevice, st), "hipMemcpy counts D2D");
+  HIP_TRY(hipStreamSynchronize(st), "device CSR copy");
+  return RTHX_OK;
 }
 
 RTHX_EXPORT int rthx_result_copy_rays(const rthx_result* cres, double* origins_xy, double* endpoints_xy,

@@ -170,7 +170,7 @@ struct TraceParams {
   double eta;              // nudge
   uint32_t key0, key1;     // Philox key (seed)
   int32_t bin;
-  int32_t reserved;
+  int32_t mixed;           // MLAT kernels: some coarse box has no single beta in `bin` (walk_ml)
   double beta_uniform;     // beta of fine face 0 in `bin` (uniform path, traceRay.jl:6-11)
   double inv_beta_uniform; // 1 / beta_uniform (0 when beta_uniform <= 0)
 };
@@ -279,7 +279,7 @@ __host__ __device__ __forceinline__ double neg_log_tab(double u, const double* t
   const uint64_t ix = dbits(u);
   const uint64_t tmp = ix - kLogOff;
   const int i = (int)((tmp >> 45) & (kLogTable - 1));
-  const int64_t k = (int64_t)tmp >> 52;
+  const int32_t k = (int32_t)(uint32_t)(tmp >> 32) >> 20;  // the exponent k (|k| < 1100): a 32-bit conversion
   const double z = bitsd(ix - (tmp & 0xFFF0000000000000ull));
   const double invc = tab[4 * i], t_hi = tab[4 * i + 1], t_lo = tab[4 * i + 2];
   const double r = __builtin_fma(z, invc, -1.0);
@@ -815,9 +815,12 @@ __device__ __forceinline__ int segment(const DevDomain& D, const TraceParams& P,
 // walk that corrects it runs only then (for every lane of a wave only when
 // one of them needs it).
 __device__ __forceinline__ int lattice_index(const double RTHX_LDS* b, int n, double inv, double x) {
-  double fi = floor(__dmul_rn(x - b[0], inv));
-  fi = fmin(fmax(fi, 0.0), (double)(n - 1));
-  int i = (int)fi;
+  // the guess's floor clamped to [0, n-1]: v_cvt_i32_f64 truncates toward
+  // zero (and saturates), which equals floor for guesses >= 0, and every
+  // negative guess clamps to 0 either way
+  int i;
+  __asm__("v_cvt_i32_f64 %0, %1" : "=v"(i) : "v"(__dmul_rn(x - b[0], inv)));
+  i = i < 0 ? 0 : (i > n - 1 ? n - 1 : i);
   if (b[i] <= x && x < b[i + 1]) return i;
   while (i > 0 && x < b[i]) --i;
   while (i < n - 1 && !(x < b[i + 1])) ++i;
@@ -848,7 +851,10 @@ __device__ __forceinline__ LatticeLds lattice_lds_view(const char RTHX_LDS* base
 // gas / wall end point's cell, and for a wall hit the fine wall of that cell
 // (dist_to_rect on its lattice bounds: the same candidates and ties as on its
 // DevPoly) and the wall's surface index from the boundary arrays.
-template <bool UNIFORM>
+// INSIDE: the caller knows p lies in the rectangle's half-open box (a ray
+// of an axis-aligned rectangle volume emitter: its uniform point, nudged
+// toward the cell's midpoint, lies in the cell, and the cell in the box).
+template <bool UNIFORM, bool INSIDE = false>
 __device__ __forceinline__ int segment_lat(const DevDomain& D, const TraceParams& P, const SingleCoarse& sc,
                                            const LatticeLds& L, const LatticeLayout& G, double& px, double& py,
                                            double dx, double dy, double& S, double& acc) {
@@ -858,7 +864,7 @@ __device__ __forceinline__ int segment_lat(const DevDomain& D, const TraceParams
   // walls, dist_in_box; any other point takes the four-wall test)
   const double cx0 = sc.poly.x[0], cx1 = sc.poly.x[1], cy0 = sc.poly.y[0], cy1 = sc.poly.y[2];
   double u;
-  if (cx0 <= px && px < cx1 && cy0 <= py && py < cy1)
+  if (INSIDE || (cx0 <= px && px < cx1 && cy0 <= py && py < cy1))
     u = dist_in_box(px, py, dx, dy, dx < 0.0 ? cx0 : cx1, dy < 0.0 ? cy0 : cy1, k);
   else
     u = dist_to_box(px, py, dx, dy, cx0, cx1, cy0, cy1, k);
@@ -1074,101 +1080,268 @@ __device__ __forceinline__ int ml_fine(const MLatLds& L, const MLatLayout& G, co
   return m.first + lj * m.nxf + li;
 }
 
-// One emitted ray in an MLAT kernel's per-wave queue (LDS).
-struct alignas(16) RaySlot {
-  double px, py, dx, dy, S;
-  double pad;
+// The emitted rays of an MLAT kernel wait in a per-wave queue in LDS: 64
+// slots of kRaySlotDoubles doubles, stored field-major (field f of slot s at
+// q[f * 64 + s]) so that the lanes of a wave read consecutive words.
+// Fields: px, py, dx, dy, S (free path / tau*), RN(1/|dx|), RN(1/|dy|).
+constexpr int kRaySlotDoubles = 7;
+constexpr int kRaySlotBytes = 8 * kRaySlotDoubles;  // 56: the queue takes 56 B per lane of the workgroup
+
+// A walking ray's direction with what its walk reuses at every segment: the
+// signs, |d| and the correctly rounded reciprocals of |dx| and |dy| (the
+// segment parameter num / |d| is then q = num r, corrected once by an fma:
+// Markstein's theorem gives the correctly rounded quotient for r = RN(1/|d|),
+// so the walk divides once per ray instead of once per segment).
+struct MRay {
+  double dx, dy;
+  double rax, ray;  // RN(1 / |dx|), RN(1 / |dy|) (inf for a zero component)
 };
-constexpr int kRaySlotBytes = (int)sizeof(RaySlot);  // 48: the queue takes 48 B per lane of the workgroup
 
-#ifndef RTHX_WALK_BATCH
-#define RTHX_WALK_BATCH 4  // MLAT segments per call of walk_ml (per iteration of the kernel's ray loop)
-#endif
+// num / den, correctly rounded, from rec = RN(1 / den) (num >= 0, den in
+// [1e-10, 2], num / den far from overflow and underflow: the walk's
+// operands): q = RN(num rec) is within an ulp of num / den, e = num - q den
+// is exact (fma), and RN(q + e rec) is RN(num / den) (Markstein; Muller et
+// al., Handbook of Floating-Point Arithmetic, Thm. 4.10).
+__device__ __forceinline__ double div_by_rcp(double num, double den, double rec) {
+  const double q = __dmul_rn(num, rec);
+  const double e = __builtin_fma(-q, den, num);
+  return __builtin_fma(e, rec, q);
+}
 
-// Up to RTHX_WALK_BATCH segments of one ray in box B (`it` counts them
-// against traceRay's 10,000-step cap, traceRay.jl:27).  The point is always
-// in B's half-open box, so the distance to B's walls is dist_in_box with the
-// ray's direction data taken out of the loop: the candidate walls are the
-// one dx points to and the one dy points to, compared in wall order.  After
-// a crossing of wall k the point is looked for in the neighbouring box
-// across k first (one new bound read from LDS); a point that is not there (a
-// crossing through a corner, or rounding) is located on the coarse lattice:
-// findFace2D's answer either way.  Returns kRayContinue (the batch ended
-// inside the lattice), kRayEndGas / kRayEndWall (p at the end point, in B),
-// or -1 (lost).
+// The walk of one ray through the boxes of a multi-polygon lattice (the loop
+// of traceRay.jl:27-68 / :85-145), starting in box B: segments until the ray
+// ends, or until at most `stop` lanes of the wave still walk (the kernel then
+// resolves the ended rays and hands new rays to the idle lanes).  `it`
+// counts segments against traceRay's 10,000-step cap (traceRay.jl:27).
+// The point is always in B's half-open box, so only the wall dx points to
+// and the one dy points to can be hit (dist_in_box's candidates, compared in
+// wall order).  After a crossing of wall k the point is looked for in the
+// neighbouring box across k first (one new bound read from LDS); a point
+// that is not there (a crossing through a corner, or rounding) is located on
+// the coarse lattice: findFace2D's answer either way.  The segment's
+// arithmetic is the CPU restatement's: u = num / |d| (correctly rounded,
+// div_by_rcp), tau_b = beta u, the gas test acc + tau_b >= tau*, and
+// p + (u + eta) d with separately rounded products.  MIXED: some box of
+// this bin has no single beta (its fine betas differ); its segments read
+// beta from the fine cell holding the segment's start (traceRay.jl:87-100).
+// Returns kRayContinue (still walking: stopped for the wave), kRayEndGas /
+// kRayEndWall (p at the segment start, in B; u_end the segment's wall
+// parameter: end_move_ml finishes the ray), or -1 (lost).
 template <bool UNIFORM>
 __device__ __forceinline__ int walk_ml(const DevDomain& D, const TraceParams& P, const MLatLds& L,
-                                       const MLatLayout& G, MBox& B, double& px, double& py, double dx, double dy,
-                                       double& S, double& acc, int& it) {
+                                       const MLatLayout& G, MBox& B, double& px, double& py, const MRay& r,
+                                       double& S, double& acc, int& it, double& u_end, uint32_t stop) {
   const double eta = P.eta;
-  const bool xdn = dx < 0.0, ydn = dy < 0.0;
-  const double ax = fabs(dx), ay = fabs(dy);
+  const bool mixed = P.mixed != 0;
+  const bool xdn = r.dx < 0.0, ydn = r.dy < 0.0;
+  const double ax = fabs(r.dx), ay = fabs(r.dy);
   const bool vxd = ax >= 1e-10, vyd = ay >= 1e-10;
   const bool y_first = ydn || xdn;  // wall order: y wall first unless top (2) vs right (1)
   const int ix = xdn ? 3 : 1, iy = ydn ? 0 : 2;
   const int sx = xdn ? -1 : 1, sy = ydn ? -1 : 1;
   const int xo = xdn ? 0 : 1, yo = ydn ? 0 : 1;
+  bool walking = true;
+  int status = kRayContinue;
 #pragma unroll 1
-  for (int n = 0; n < RTHX_WALK_BATCH; ++n) {
-    if (it >= 10000) return -1;
-    ++it;
-    const double nx = fabs((xdn ? B.x0 : B.x1) - px), ny = fabs((ydn ? B.y0 : B.y1) - py);
-    const bool vx = vxd && __dmul_rn(nx, ax) > 0.0, vy = vyd && __dmul_rn(ny, ay) > 0.0;
-    const double cx = __dmul_rn(nx, ay), cy = __dmul_rn(ny, ax);
-    const bool xw = vx && (!vy || (y_first ? cx < cy : !(cy < cx)));
-    const bool any = vx || vy;
-    double u = (xw ? nx : ny) / (xw ? ax : ay);
-    u = (any && u > 0.0) ? u : __builtin_inf();
-    const int k = any ? (xw ? ix : iy) : 0;
-    bool gas;
-    double beta = 0.0, tau_b = 0.0;
+  while (true) {
+    if (walking) {
+      const double nx = fabs((xdn ? B.x0 : B.x1) - px), ny = fabs((ydn ? B.y0 : B.y1) - py);
+      // a wall is a candidate when its parameter num / den is > 0: den >= 1e-10
+      // and num > 0 (num / den > 0 exactly then, for den <= 1)
+      const bool vx = vxd && nx > 0.0, vy = vyd && ny > 0.0;
+      const double cx = __dmul_rn(nx, ay), cy = __dmul_rn(ny, ax);
+      const bool xw = vx && (!vy || (y_first ? cx < cy : !(cy < cx)));
+      const bool any = vx || vy;
+      const double u = any ? div_by_rcp(xw ? nx : ny, xw ? ax : ay, xw ? r.rax : r.ray) : __builtin_inf();
+      const int k = any ? (xw ? ix : iy) : 0;
+      bool gas;
+      double accn = 0.0;
+      if (UNIFORM) {
+        gas = S < u;
+      } else {
+        double beta = L.beta[B.b];
+        if (mixed && beta < 0.0) {
+          const MCoarse m = ld(L.cinfo + L.cmap[B.b]);
+          int i, j;
+          const int f0 = ml_fine(L, G, m, px, py, i, j);
+          if (f0 < 0) {  // the segment start lies in no fine cell: lost (traceRay.jl:89-91)
+            walking = false;
+            status = -1;
+          } else {
+            beta = D.beta[(size_t)P.bin * D.n_fine + f0];
+          }
+        }
+        accn = acc + __dmul_rn(beta, u);
+        gas = accn >= S;
+      }
+      const bool wall = !gas && ((L.bsolid[B.b] >> k) & 1u);
+      if (walking && (gas || wall)) {
+        walking = false;
+        status = gas ? kRayEndGas : kRayEndWall;
+        u_end = u;
+      }
+      if (walking) {
+        const double t = u + eta;
+        px = px + __dmul_rn(t, r.dx);
+        py = py + __dmul_rn(t, r.dy);
+        if (UNIFORM) S -= u; else acc = accn;
+        // the neighbouring box across wall k (k is the x wall iff xw)
+        const int ci = B.ci + (xw ? sx : 0), cj = B.cj + (xw ? 0 : sy);
+        bool ok = (unsigned)ci < (unsigned)G.ncx && (unsigned)cj < (unsigned)G.ncy;
+        const double v = ok ? (xw ? L.cxs[ci + xo] : L.cys[cj + yo]) : 0.0;
+        const double x0 = xw ? (xdn ? v : B.x1) : B.x0, x1 = xw ? (xdn ? B.x0 : v) : B.x1;
+        const double y0 = xw ? B.y0 : (ydn ? v : B.y1), y1 = xw ? B.y1 : (ydn ? B.y0 : v);
+        ok = ok && x0 <= px && px < x1 && y0 <= py && py < y1;
+        if (ok) {
+          B.ci = ci;
+          B.cj = cj;
+          B.b += xw ? sx : sy * G.ncx;
+          B.x0 = x0;
+          B.x1 = x1;
+          B.y0 = y0;
+          B.y1 = y1;
+        } else {
+          const int li = lattice_index(L.cxs, G.ncx, G.inv_cx, px), lj = lattice_index(L.cys, G.ncy, G.inv_cy, py);
+          if (li < 0 || lj < 0) {
+            walking = false;
+            status = -1;
+          } else {
+            ml_box(L, G, li, lj, B);
+          }
+        }
+        if (walking && ++it >= 10000) {  // traceRay.jl:27: no end within 10,000 steps
+          walking = false;
+          status = -1;
+        }
+      }
+    }
+    if ((uint32_t)__popcll(__ballot(walking)) <= stop) break;
+  }
+  return status;
+}
+
+// walk_ml on a layered lattice: one coarse column (ncx == 1), the boxes a
+// stack of layers j with bounds cys[j], cys[j + 1] (the greenhouse of C5).
+// A ray crosses only layer boundaries (an x wall is the lattice's side:
+// solid, or the ray leaves), so the walker keeps just its layer index and
+// reads the layer's bounds, beta and solid walls from LDS at each segment.
+// The point is checked against its layer's box at the start of every
+// segment instead of after each crossing: the same test of the neighbouring
+// box (the layer across the crossed boundary; across a side wall or the
+// lattice's top or bottom the box is kept, which the check then fails), and
+// a point outside it -- a crossing through a corner, a nudge that did not
+// carry the point across, or a point outside the lattice -- is located on
+// the lattice as in walk_ml (findFace2D, lost when in no box).  Same
+// arithmetic, candidates, ties, step count and results as walk_ml.
+template <bool UNIFORM>
+__device__ __forceinline__ int walk_layers(const DevDomain& D, const TraceParams& P, const MLatLds& L,
+                                           const MLatLayout& G, MBox& B, double& px, double& py, const MRay& r,
+                                           double& S, double& acc, int& it, double& u_end, uint32_t stop) {
+  const double eta = P.eta;
+  const bool mixed = P.mixed != 0;
+  const int ncy = G.ncy;
+  const bool xdn = r.dx < 0.0, ydn = r.dy < 0.0;
+  const double ax = fabs(r.dx), ay = fabs(r.dy);
+  const bool vxd = ax >= 1e-10, vyd = ay >= 1e-10;
+  const bool y_first = ydn | xdn;  // wall order: y wall first unless top (2) vs right (1)
+  const int kx = xdn ? 3 : 1, ky = ydn ? 0 : 2;
+  const int sy = ydn ? -1 : 1;
+  const double x0 = L.cxs[0], x1 = L.cxs[1];
+  const double xf = xdn ? x0 : x1;
+  int cj = B.cj;
+  bool walking = true;
+  int status = kRayContinue;
+#pragma unroll 1
+  while (true) {
+    if (walking) {
+      const double y0 = L.cys[cj], y1 = L.cys[cj + 1];
+      const bool inside = (x0 <= px) & (px < x1) & (y0 <= py) & (py < y1);
+      if (!inside) {
+        const int li = lattice_index(L.cxs, 1, G.inv_cx, px), lj = lattice_index(L.cys, ncy, G.inv_cy, py);
+        if ((li < 0) | (lj < 0)) {
+          walking = false;
+          status = -1;
+        } else {
+          cj = lj;
+        }
+      } else {
+        const double yf = ydn ? y0 : y1;
+        const double nx = fabs(xf - px), ny = fabs(yf - py);
+        const bool vx = vxd & (nx > 0.0), vy = vyd & (ny > 0.0);
+        const double cx = __dmul_rn(nx, ay), cy = __dmul_rn(ny, ax);
+        const bool xw = vx & (!vy | (y_first ? (cx < cy) : !(cy < cx)));
+        const bool any = vx | vy;
+        const double u = any ? div_by_rcp(xw ? nx : ny, xw ? ax : ay, xw ? r.rax : r.ray) : __builtin_inf();
+        const int k = any ? (xw ? kx : ky) : 0;
+        bool gas;
+        double accn = 0.0;
+        bool lost = false;
+        if (UNIFORM) {
+          gas = S < u;
+        } else {
+          double beta = L.beta[cj];
+          if (mixed && beta < 0.0) {
+            const MCoarse m = ld(L.cinfo + L.cmap[cj]);
+            int i, j;
+            const int f0 = ml_fine(L, G, m, px, py, i, j);
+            lost = f0 < 0;  // the segment start lies in no fine cell (traceRay.jl:89-91)
+            beta = lost ? 0.0 : D.beta[(size_t)P.bin * D.n_fine + f0];
+          }
+          accn = acc + __dmul_rn(beta, u);
+          gas = accn >= S;
+        }
+        const bool wall = !gas & (((L.bsolid[cj] >> k) & 1u) != 0u);
+        if (lost | gas | wall) {
+          walking = false;
+          status = lost ? -1 : gas ? kRayEndGas : kRayEndWall;
+          u_end = u;
+        } else {
+          const double t = u + eta;
+          px = px + __dmul_rn(t, r.dx);
+          py = py + __dmul_rn(t, r.dy);
+          if (UNIFORM) S -= u; else acc = accn;
+          const int cjn = cj + sy;
+          cj = (!xw & ((unsigned)cjn < (unsigned)ncy)) ? cjn : cj;
+          if (++it >= 10000) {  // traceRay.jl:27: no end within 10,000 steps
+            walking = false;
+            status = -1;
+          }
+        }
+      }
+    }
+    if ((uint32_t)__popcll(__ballot(walking)) <= stop) break;
+  }
+  B.ci = 0;
+  B.cj = cj;
+  B.b = cj;
+  return status;
+}
+
+// The end point of a ray whose walk ended (kRayEndGas / kRayEndWall, p at
+// the last segment's start): p + (t - eta) d with t = (tau* - acc) / beta
+// (gas, traceRay.jl:105-116; S for the uniform path, :31-40) or the wall
+// parameter u (:42-52 / :118-128).
+template <bool UNIFORM>
+__device__ __forceinline__ void end_move_ml(const DevDomain& D, const TraceParams& P, const MLatLds& L,
+                                            const MLatLayout& G, const MBox& B, double& px, double& py,
+                                            const MRay& r, double S, double acc, double u_end, bool gas) {
+  double t = u_end;
+  if (gas) {
     if (UNIFORM) {
-      gas = S < u;
+      t = S;
     } else {
-      beta = L.beta[B.b];
-      if (beta < 0.0) {
+      double beta = L.beta[B.b];
+      if (P.mixed && beta < 0.0) {  // (the walk found the start's fine cell)
         const MCoarse m = ld(L.cinfo + L.cmap[B.b]);
         int i, j;
-        const int f0 = ml_fine(L, G, m, px, py, i, j);
-        if (f0 < 0) return -1;
-        beta = D.beta[(size_t)P.bin * D.n_fine + f0];
+        beta = D.beta[(size_t)P.bin * D.n_fine + ml_fine(L, G, m, px, py, i, j)];
       }
-      tau_b = __dmul_rn(beta, u);
-      gas = acc + tau_b >= S;
-    }
-    const bool wall = !gas && ((L.bsolid[B.b] >> k) & 1u);
-    if (gas || wall) {
-      const double t = gas ? (UNIFORM ? S : (S - acc) / beta) - eta : u - eta;
-      px = px + __dmul_rn(t, dx);
-      py = py + __dmul_rn(t, dy);
-      return gas ? kRayEndGas : kRayEndWall;
-    }
-    const double t = u + eta;
-    px = px + __dmul_rn(t, dx);
-    py = py + __dmul_rn(t, dy);
-    if (UNIFORM) S -= u; else acc += tau_b;
-    // the neighbouring box across wall k (k is the x wall iff xw)
-    const int ci = B.ci + (xw ? sx : 0), cj = B.cj + (xw ? 0 : sy);
-    bool ok = (unsigned)ci < (unsigned)G.ncx && (unsigned)cj < (unsigned)G.ncy;
-    const double v = ok ? (xw ? L.cxs[ci + xo] : L.cys[cj + yo]) : 0.0;
-    const double x0 = xw ? (xdn ? v : B.x1) : B.x0, x1 = xw ? (xdn ? B.x0 : v) : B.x1;
-    const double y0 = xw ? B.y0 : (ydn ? v : B.y1), y1 = xw ? B.y1 : (ydn ? B.y0 : v);
-    ok = ok && x0 <= px && px < x1 && y0 <= py && py < y1;
-    if (ok) {
-      B.ci = ci;
-      B.cj = cj;
-      B.b += xw ? sx : sy * G.ncx;
-      B.x0 = x0;
-      B.x1 = x1;
-      B.y0 = y0;
-      B.y1 = y1;
-    } else {
-      const int li = lattice_index(L.cxs, G.ncx, G.inv_cx, px), lj = lattice_index(L.cys, G.ncy, G.inv_cy, py);
-      if (li < 0 || lj < 0) return -1;
-      ml_box(L, G, li, lj, B);
+      t = (S - acc) / beta;
     }
   }
-  return kRayContinue;
+  t = t - P.eta;
+  px = px + __dmul_rn(t, r.dx);
+  py = py + __dmul_rn(t, r.dy);
 }
 
 __device__ __forceinline__ int end_ml(const DevDomain& D, const MLatLds& L, const MLatLayout& G, const MBox& B,
@@ -1178,8 +1351,10 @@ __device__ __forceinline__ int end_ml(const DevDomain& D, const MLatLds& L, cons
   const int fg = ml_fine(L, G, m, px, py, i, j);
   if (fg < 0) return -1;
   if (gas) return D.n_surfaces + fg;
-  int w;
-  dist_to_box(px, py, dx, dy, L.xs[i], L.xs[i + 1], L.ys[j], L.ys[j + 1], w);
+  // the end point lies in fine box (i, j) (half-open: lattice_index), so the
+  // four-wall test of dist_to_box reduces to the two walls the ray points to
+  // (box_hit_in, as segment_lat)
+  const int w = box_hit_in(px, py, dx, dy, dx < 0.0 ? L.xs[i] : L.xs[i + 1], dy < 0.0 ? L.ys[j] : L.ys[j + 1]).wall;
   return D.f_surf[4 * fg + w];
 }
 
@@ -1262,7 +1437,9 @@ __device__ __forceinline__ int trace_one_w(const DevDomain& D, const TraceParams
   start_ray_w<UNIFORM, FAITHFUL, EK>(P, e, tabs, rw, px, py, dx, dy, S);
   ox = px;
   oy = py;
-  if (LAT) return segment_lat<UNIFORM>(D, P, sc, lattice_lds_view(lat_base, D.lat), D.lat, px, py, dx, dy, S, acc);
+  if (LAT)
+    return segment_lat<UNIFORM, EK == kEmitVolRect>(D, P, sc, lattice_lds_view(lat_base, D.lat), D.lat, px, py, dx,
+                                                     dy, S, acc);
   int c = e.coarse;
   for (int it = 0; it < (SINGLE ? 1 : 10000); ++it) {  // traceRay.jl:27 (10,000 steps, then lost)
     const int a = segment<UNIFORM, SINGLE, AXIS>(D, P, sc, c, px, py, dx, dy, S, acc);

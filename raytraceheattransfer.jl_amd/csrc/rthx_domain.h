@@ -34,6 +34,7 @@ struct rthx_domain {
   std::vector<double> beta_first;    // beta of fine face 0 per bin (traceRay.jl:6-11)
   bool single_convex = false;        // one convex coarse polygon (SINGLE kernels)
   bool axis_rect = false;            // every polygon an axis-aligned rectangle in canonical order (AXIS kernels)
+  std::vector<uint8_t> ml_mixed;     // MLAT: per bin, 1 if some coarse box has no single beta (TraceParams::mixed)
   rthx::DirectWork* direct = nullptr;  // created by the first rthx_trace_direct call
   ~rthx_domain() {
     if (direct) rthx::destroy_direct_work(direct);

@@ -445,8 +445,10 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
         philox_words(r >> 2, (uint32_t)g, 1u, (uint32_t)P.bin, P.key0, P.key1, b);
         b0 = b[0]; b1 = b[1]; b2 = b[2]; b3 = b[3];
       }
+      // (word r & 3 of the block by bit selects: a compare chain becomes a
+      // branchy switch)
       const uint32_t k = r & 3u;
-      const uint32_t pw = k == 0u ? b0 : k == 1u ? b1 : k == 2u ? b2 : b3;
+      const uint32_t pw = (k & 2u) ? ((k & 1u) ? b3 : b2) : ((k & 1u) ? b1 : b0);
       if (r >= rb && r < re) one_ray(r, true, pw, ek);
     }
     };
@@ -467,10 +469,10 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
     // one ray into the queue when the queue runs short), and a refill is a
     // pop of a few LDS words.  The absorbers of the rays whose walk ended
     // (end_ml) are found together once kRefillQ lanes have stopped walking.
-    constexpr int kRefillQ = RTHX_REFILL_Q;
+    constexpr uint32_t kRefillQ = RTHX_REFILL_Q;
     const uint32_t lane = lane_id();
     const uint64_t lt_mask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-    RaySlot RTHX_LDS* q = (RaySlot RTHX_LDS*)(cl_base + D.ml.bytes) + (tid >> 6) * 64;
+    double RTHX_LDS* q = (double RTHX_LDS*)(cl_base + D.ml.bytes) + (tid >> 6) * (64 * kRaySlotDoubles);
     __shared__ MBox s_box0;  // the emitter's coarse box: every ray of the row starts there
 #ifdef RTHX_SEGSTAT
     __shared__ unsigned long long s_segs;  // (diagnostic build: segments walked by the row)
@@ -480,80 +482,84 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
     __syncthreads();
     uint32_t q_head = 0, q_cnt = 0;  // wave-uniform ring of 64 slots
     bool exhausted = false;          // the row has no rays left to emit
-    double px = 0.0, py = 0.0, dx = 0.0, dy = 0.0, S = 0.0, acc = 0.0;
+    const bool layered = D.ml.ncx == 1;  // a stack of layers (walk_layers)
+    double px = 0.0, py = 0.0, S = 0.0, acc = 0.0, u_end = 0.0;
+    MRay ry{};
     int it = 0;
     MBox box{};
-    bool live = false, ending = false, end_gas = false;
+    // kRayContinue: walking; kRayEndGas / kRayEndWall: the walk ended, the
+    // absorber not yet found; anything else: idle
+    int state = -1;
     while (true) {
-      const uint64_t walking = __ballot(live);
-      if (walking == 0ull || 64 - __popcll(walking) >= kRefillQ) {
-        if (ending) {
-          const int a = end_ml(D, RTHX_ML_VIEW, RTHX_ML_G, box, px, py, dx, dy, end_gas);
-          tally(a);
-          ending = false;
-        }
-        const uint64_t idle = __ballot(!live);
-        if (!exhausted && q_cnt < (uint32_t)__popcll(idle)) {
-          // top the queue up: lane l emits ray base + l into slot q_head + q_cnt + l
-          const uint32_t want = 64u - q_cnt;
-          uint32_t base = 0;
-          if (lane == 0) base = atomicAdd(&s_next, want);
-          base = __shfl(base, 0);
-          const uint32_t rr = base + lane;
-          const bool valid = lane < want && rr < (uint32_t)r_end;
-          if (valid) {
-            const double RTHX_LDS* tab = lds_opaque(&s_tab[0]);
-            const Emitter RTHX_LDS* em = lds_opaque(&s_emit);
-            const Emitter& e = *(const Emitter*)em;
-            RaySlot sl;
-            start_ray<UNIFORM, FAITHFUL>(P, e, (const double*)tab, (uint32_t)g, rr, sl.px, sl.py, sl.dx, sl.dy, sl.S);
-            RaySlot RTHX_LDS* d = q + ((q_head + q_cnt + lane) & 63u);
-            d->px = sl.px;
-            d->py = sl.py;
-            d->dx = sl.dx;
-            d->dy = sl.dy;
-            d->S = sl.S;
-          }
-          const uint32_t n_new = (uint32_t)__popcll(__ballot(valid));
-          if (n_new < want) exhausted = true;
-          q_cnt += n_new;
-        }
-        if (q_cnt > 0) {
-          const uint32_t rank = (uint32_t)__popcll(idle & lt_mask);
-          if (!live && rank < q_cnt) {
-            const RaySlot RTHX_LDS* sl = q + ((q_head + rank) & 63u);
-            px = sl->px;
-            py = sl->py;
-            dx = sl->dx;
-            dy = sl->dy;
-            S = sl->S;
-            acc = 0.0;
-            it = 0;
-            box = s_box0;
-            live = true;
-          }
-          const uint32_t taken = q_cnt < (uint32_t)__popcll(idle) ? q_cnt : (uint32_t)__popcll(idle);
-          q_head = (q_head + taken) & 63u;
-          q_cnt -= taken;
-        }
-        if (__ballot(live) == 0ull) break;  // (queue empty, row exhausted, every end resolved)
+      // Resolve the ended rays, then hand the queue's rays to the idle lanes.
+      if (state == kRayEndGas || state == kRayEndWall) {
+        const bool gas = state == kRayEndGas;
+        end_move_ml<UNIFORM>(D, P, RTHX_ML_VIEW, RTHX_ML_G, box, px, py, ry, S, acc, u_end, gas);
+        tally(end_ml(D, RTHX_ML_VIEW, RTHX_ML_G, box, px, py, ry.dx, ry.dy, gas));
       }
+      bool live = state == kRayContinue;
+      const uint64_t idle = __ballot(!live);
+      const uint32_t n_idle = (uint32_t)__popcll(idle);
+      if (!exhausted && q_cnt < n_idle) {
+        // top the queue up: lane l emits ray base + l into slot q_head + q_cnt + l
+        const uint32_t want = 64u - q_cnt;
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(&s_next, want);
+        base = __shfl(base, 0);
+        const uint32_t rr = base + lane;
+        const bool valid = lane < want && rr < (uint32_t)r_end;
+        if (valid) {
+          const double RTHX_LDS* tab = lds_opaque(&s_tab[0]);
+          const Emitter RTHX_LDS* em = lds_opaque(&s_emit);
+          const Emitter& e = *(const Emitter*)em;
+          double v[kRaySlotDoubles];
+          start_ray<UNIFORM, FAITHFUL>(P, e, (const double*)tab, (uint32_t)g, rr, v[0], v[1], v[2], v[3], v[4]);
+          v[5] = 1.0 / fabs(v[2]);
+          v[6] = 1.0 / fabs(v[3]);
+          double RTHX_LDS* d = q + ((q_head + q_cnt + lane) & 63u);
+#pragma unroll
+          for (int f = 0; f < kRaySlotDoubles; ++f) d[64 * f] = v[f];
+        }
+        const uint32_t n_new = (uint32_t)__popcll(__ballot(valid));
+        if (n_new < want) exhausted = true;
+        q_cnt += n_new;
+      }
+      if (q_cnt > 0) {
+        const uint32_t rank = (uint32_t)__popcll(idle & lt_mask);
+        if (!live && rank < q_cnt) {
+          const double RTHX_LDS* sl = q + ((q_head + rank) & 63u);
+          px = sl[0];
+          py = sl[64];
+          ry.dx = sl[128];
+          ry.dy = sl[192];
+          S = sl[256];
+          ry.rax = sl[320];
+          ry.ray = sl[384];
+          acc = 0.0;
+          it = 0;
+          box = s_box0;
+          live = true;
+        }
+        const uint32_t taken = q_cnt < n_idle ? q_cnt : n_idle;
+        q_head = (q_head + taken) & 63u;
+        q_cnt -= taken;
+      }
+      state = live ? kRayContinue : -1;
+      if (__ballot(live) == 0ull) break;  // (queue empty, row exhausted, every end resolved)
+      // Walk until kRefillQ lanes are idle, or to the end of every walk when
+      // the row has no rays left to hand out.
+      const uint32_t stop = (!exhausted || q_cnt > 0) ? 64u - kRefillQ : 0u;
       if (live) {
 #ifdef RTHX_SEGSTAT
         const int it0 = it;
 #endif
-        const int a = walk_ml<UNIFORM>(D, P, RTHX_ML_VIEW, RTHX_ML_G, box, px, py, dx, dy, S, acc, it);
+        if (layered)
+          state = walk_layers<UNIFORM>(D, P, RTHX_ML_VIEW, RTHX_ML_G, box, px, py, ry, S, acc, it, u_end, stop);
+        else
+          state = walk_ml<UNIFORM>(D, P, RTHX_ML_VIEW, RTHX_ML_G, box, px, py, ry, S, acc, it, u_end, stop);
 #ifdef RTHX_SEGSTAT
         atomicAdd(&s_segs, (unsigned long long)(it - it0));
 #endif
-        if (a == kRayEndGas || a == kRayEndWall) {
-          live = false;
-          ending = true;
-          end_gas = a == kRayEndGas;
-        } else if (a != kRayContinue) {
-          tally(a);
-          live = false;
-        }
       }
     }
 #ifdef RTHX_SEGSTAT
@@ -574,20 +580,14 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
     constexpr int kRefill = RTHX_REFILL;
     double px = 0.0, py = 0.0, dx = 0.0, dy = 0.0, S = 0.0, acc = 0.0, ox = 0.0, oy = 0.0;
     int c = 0, it = 0;
-    MBox box{};  // (MLAT: the coarse lattice box instead of c)
     uint32_t r = 0;
     bool live = false, ending = false, end_gas = false, more = true;
     while (true) {
       const uint64_t walking = __ballot(live);
       if (walking == 0ull || 64 - __popcll(walking) >= kRefill) {
         if (CLDS && ending) {
-          int a;
-          if constexpr (MLAT) {
-            a = end_ml(D, RTHX_ML_VIEW, RTHX_ML_G, box, px, py, dx, dy, end_gas);
-          } else {
-            const CoarseLds L = coarse_lds_view(lds_opaque(cl_base), D.cl);
-            a = end_cl<AXIS>(D, L, c, px, py, dx, dy, end_gas);
-          }
+          const CoarseLds L = coarse_lds_view(lds_opaque(cl_base), D.cl);
+          const int a = end_cl<AXIS>(D, L, c, px, py, dx, dy, end_gas);
           tally(a);
           record(r, a, ox, oy, px, py);
           ending = false;
@@ -604,7 +604,6 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
               oy = py;
               acc = 0.0;
               c = e.coarse;
-              if constexpr (MLAT) ml_enter(RTHX_ML_VIEW, RTHX_ML_G, c, box);
               it = 0;
               live = true;
             }
@@ -615,9 +614,7 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
       }
       if (live) {
         int a = -1;
-        if constexpr (MLAT) {
-          a = walk_ml<UNIFORM>(D, P, RTHX_ML_VIEW, RTHX_ML_G, box, px, py, dx, dy, S, acc, it);  // (counts it)
-        } else if (it < 10000) {
+        if (it < 10000) {
           if constexpr (CLDS) {
             const CoarseLds L = coarse_lds_view(lds_opaque(cl_base), D.cl);
             a = walk_cl<UNIFORM, AXIS>(D, P, L, c, px, py, dx, dy, S, acc);
@@ -625,7 +622,7 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
             a = segment<UNIFORM, false, AXIS>(D, P, s_single, c, px, py, dx, dy, S, acc);
           }
         }
-        if constexpr (!MLAT) ++it;
+        ++it;
         if (a == kRayEndGas || a == kRayEndWall) {
           live = false;
           ending = true;
@@ -1011,9 +1008,15 @@ static hipError_t launch_trace_t(const LaunchCfg& L) {
   // and 1024-lane workgroups keep 16 waves busy instead of 4.  The choice is
   // cached per (kernel, LDS bytes, device): the queries cost more host time
   // per call than the rest of the launch.
-  if (L.lds_bytes > 64 * 1024) {  // (occupancy queries above 64 KiB need the attribute first)
-    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)L.lds_bytes);
+  // Occupancy queries and launches above 64 KiB of dynamic LDS need the
+  // attribute first, set to the most any workgroup size below may use (the
+  // MLAT ray queue grows with the workgroup).
+  size_t lds_max = L.lds_bytes;
+  for (int t = kTraceThreads; t <= kMaxTraceThreads; t *= 2)
+    if (lds_for(t) + (size_t)kStaticLdsBytes <= kMaxLdsBytes) lds_max = std::max(lds_max, lds_for(t));
+  if (L.threads == 256 || L.threads == 512 || L.threads == 1024) lds_max = std::max(lds_max, lds_for(L.threads));
+  if (lds_max > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_max);
     if (e != hipSuccess) return e;
   }
   int threads = occupancy_cache_get((const void*)kern, L.lds_bytes);

@@ -63,6 +63,8 @@ def load(path: Optional[str] = None) -> C.CDLL:
                                        C.POINTER(C.c_double)]
     lib.rthx_result_copy_rays.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double),
                                           C.POINTER(C.c_int64), C.c_int64, C.POINTER(C.c_int64)]
+    lib.rthx_result_get_device_csr.argtypes = [C.c_void_p, C.c_int32, C.POINTER(abi.DeviceCsr)]
+    lib.rthx_result_copy_csr_device.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p]
     lib.rthx_host_register.argtypes = [C.c_void_p, C.c_size_t]
     lib.rthx_host_unregister.argtypes = [C.c_void_p]
     lib.rthx_multi_create.argtypes = [C.POINTER(abi.DomainDesc), C.POINTER(C.c_int32), C.c_int32,
@@ -258,6 +260,36 @@ class DeviceResult:
         inf = abi.ResultInfo()
         check(self._lib.rthx_result_get_info(self.handle, C.byref(inf)))
         return inf.as_dict()
+
+    def device_csr(self, part: int = 0) -> dict:
+        """Where block `part` of the count matrix lies in device memory
+        (rthx_result_get_device_csr): device, n_parts, n_rows, nnz,
+        emitter_begin, emitter_stride and the device pointers row_off, cols,
+        counts."""
+        d = abi.DeviceCsr()
+        check(self._lib.rthx_result_get_device_csr(self.handle, int(part), C.byref(d)))
+        return d.as_dict()
+
+    @property
+    def device(self) -> int:
+        """The device holding a one-device trace's counts."""
+        return int(self.device_csr()["device"])
+
+    def torch_csr(self, part: int = 0):
+        """Block `part` as torch tensors on its device, copied device to
+        device (rthx_result_copy_csr_device; no host round trip): row_off
+        (int64, n_rows + 1), cols and counts (int32; the uint32 counts
+        reinterpreted, lossless), plus the block's dict (device_csr)."""
+        import torch
+
+        d = self.device_csr(part)
+        dev = torch.device("cuda", d["device"])
+        row_off = torch.empty(d["n_rows"] + 1, dtype=torch.int64, device=dev)
+        pairs = torch.empty((2, max(d["nnz"], 1)), dtype=torch.int32, device=dev)
+        check(self._lib.rthx_result_copy_csr_device(self.handle, int(part), C.c_void_p(row_off.data_ptr()),
+                                                    C.c_void_p(pairs[0].data_ptr()),
+                                                    C.c_void_p(pairs[1].data_ptr())))
+        return row_off, pairs[:, :d["nnz"]], d
 
     def csr(self, pinned: Optional[PinnedArrays] = None):
         """(row_ptr, cols, counts) on the host.  With `pinned`, cols and

@@ -205,6 +205,24 @@ class DirectInfo(C.Structure):
         return {name: getattr(self, name) for name, _ in self._fields_}
 
 
+class DeviceCsr(C.Structure):
+    """rthx_device_csr (include/rthx.h): a result's count matrix in device memory."""
+    _fields_ = [
+        ("device", C.c_int32),
+        ("n_parts", C.c_int32),
+        ("n_rows", C.c_int64),
+        ("nnz", C.c_int64),
+        ("emitter_begin", C.c_int64),
+        ("emitter_stride", C.c_int64),
+        ("row_off", C.c_void_p),
+        ("cols", C.c_void_p),
+        ("counts", C.c_void_p),
+    ]
+
+    def as_dict(self) -> dict:
+        return {name: getattr(self, name) for name, _ in self._fields_}
+
+
 class Vf3dArgs(C.Structure):
     """rthx_vf3d_args (include/rthx.h)."""
     _fields_ = [("device", C.c_int32), ("reserved0", C.c_int32)]
@@ -233,6 +251,8 @@ EXPORTED_SYMBOLS = (
     "rthx_result_copy_csr",
     "rthx_result_copy_rays",
     "rthx_result_copy_F",
+    "rthx_result_get_device_csr",
+    "rthx_result_copy_csr_device",
     "rthx_host_register",
     "rthx_host_unregister",
     "rthx_multi_create",

@@ -81,49 +81,120 @@ def _place(pieces_rows, pieces, lens_global, row_ptr, nnz):
     return cols, counts
 
 
-def gather_csr(row_ptr, cols, counts, n: int, group=None, dst: int = 0):
-    """Bring every rank's CSR block (disjoint row sets, each over all n rows)
-    to rank `dst` (dst = -1: to every rank) with tensor collectives: one
-    all-reduce of the row lengths and owners, one all-gather of the padded
-    (col, count) pairs.  On an NCCL (= RCCL on ROCm) group the tensors travel
-    over xGMI from device memory; on gloo through the host.  Returns the
-    merged CSR (row_ptr, cols, counts) where requested, else None."""
+def _device_of(group):
+    import torch
+    import torch.distributed as dist
+
+    if dist.get_backend(group) == "nccl":
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
+def _pairs_tensor(cols, counts, dev):
+    """(cols, counts) as one int32 [2, nnz] tensor on `dev`: the uint32
+    counts travel bit for bit as int32 (8 bytes per nonzero)."""
+    import torch
+
+    if isinstance(cols, torch.Tensor):
+        return torch.stack([cols.to(dev, torch.int32), counts.to(dev).view(torch.int32)
+                            if counts.dtype == torch.int32 else counts.to(dev, torch.int32)])
+    c = np.ascontiguousarray(cols, dtype=np.int32)
+    v = np.ascontiguousarray(counts, dtype=np.uint32).view(np.int32)
+    return torch.from_numpy(np.stack([c, v])).to(dev)
+
+
+def _gather_blocks(rows, lens, pairs, n: int, group, dst: int, as_tensors: bool):
+    """The gather behind gather_csr / gather_result.  rows: this rank's
+    traced rows (global ids, ascending), lens: their entry counts, pairs: the
+    int32 [2, nnz] (col, count) tensor of those rows in row order (on the
+    group's device)."""
     import torch
     import torch.distributed as dist
 
     rank = dist.get_rank(group)
     world = dist.get_world_size(group)
-    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else torch.device("cpu")
+    dev = pairs.device
+    rows = torch.as_tensor(rows, dtype=torch.int64, device=dev)
+    lens = torch.as_tensor(lens, dtype=torch.int64, device=dev)
+    nnz_local = int(pairs.shape[1])
+    # row lengths and owners over all n rows (disjoint rows: the sums are
+    # the values), to dst only when dst >= 0
+    meta = torch.zeros(2 * n, dtype=torch.int64, device=dev)
+    meta[rows] = lens
+    meta[n + rows] = rank + 1
+    sizes = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
+    dist.all_gather(sizes, torch.tensor([nnz_local], dtype=torch.int64, device=dev), group=group)
+    cap = max(max(int(x.item()) for x in sizes), 1)
+    buf = torch.zeros((2, cap), dtype=torch.int32, device=dev)
+    buf[:, :nnz_local] = pairs
+    if dst >= 0:
+        dist.reduce(meta, dst, group=group)
+        out = [torch.empty_like(buf) for _ in range(world)] if rank == dst else None
+        dist.gather(buf, out, dst=dst, group=group)
+        if rank != dst:
+            return None
+    else:
+        dist.all_reduce(meta, group=group)
+        out = [torch.empty_like(buf) for _ in range(world)]
+        dist.all_gather(out, buf, group=group)
+    lens_g, owner = meta[:n], meta[n:]
+    g_rp = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(lens_g, 0, out=g_rp[1:])
+    total = int(g_rp[-1].item())
+    cols = torch.zeros(total, dtype=torch.int32, device=dev)
+    counts = torch.zeros(total, dtype=torch.int32, device=dev)
+    for k in range(world):
+        rk = torch.nonzero(owner == k + 1).flatten()
+        lk = lens_g[rk]
+        tot = int(lk.sum().item()) if rk.numel() else 0
+        if tot == 0:
+            continue
+        start = torch.cumsum(lk, 0) - lk  # each row's first entry in rank k's block
+        idx = torch.repeat_interleave(g_rp[rk] - start, lk) + torch.arange(tot, device=dev)
+        cols[idx] = out[k][0, :tot]
+        counts[idx] = out[k][1, :tot]
+    if as_tensors:
+        return g_rp, cols, counts
+    return g_rp.cpu().numpy(), cols.cpu().numpy(), counts.cpu().numpy().view(np.uint32)
+
+
+def gather_csr(row_ptr, cols, counts, n: int, group=None, dst: int = 0, as_tensors: bool = False):
+    """Bring every rank's CSR block (disjoint row sets, each over all n rows)
+    to rank `dst` (dst = -1: to every rank) with tensor collectives: the
+    (col, count) pairs as int32 (8 bytes per nonzero) gathered to dst alone
+    (all-gathered only for dst = -1), the row lengths and owners reduced
+    there.  On an NCCL (= RCCL on ROCm) group the tensors travel over xGMI
+    from device memory; on gloo through the host.  Returns the merged CSR
+    (row_ptr, cols, counts) on the receiving ranks (numpy, or tensors on the
+    group's device with as_tensors), None elsewhere."""
+    dev = _device_of(group)
     rp = np.asarray(row_ptr, dtype=np.int64)
     lens = np.diff(rp)
+    rows = np.nonzero(lens)[0]
     nnz_local = int(rp[-1])
-    mine = np.zeros(n, dtype=np.int64)
-    mine[lens > 0] = rank + 1
-    meta = torch.from_numpy(np.concatenate([lens, mine, [nnz_local]])).to(dev)
-    # lengths and owners (disjoint rows: the sums are the values), and the
-    # largest block for the padding
-    sizes = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
-    dist.all_gather(sizes, meta[-1:].clone(), group=group)
-    meta = meta[:-1]
-    dist.all_reduce(meta, group=group)
-    meta = meta.cpu().numpy()
-    lens_g, owner = meta[:n], meta[n:]
-    nnz_k = [int(x.item()) for x in sizes]
-    cap = max(max(nnz_k), 1)
-    buf = np.zeros((2, cap), dtype=np.int64)
-    buf[0, :nnz_local] = np.asarray(cols, dtype=np.int64)[:nnz_local]
-    buf[1, :nnz_local] = np.asarray(counts, dtype=np.int64)[:nnz_local]
-    t = torch.from_numpy(buf).to(dev)
-    out = [torch.empty_like(t) for _ in range(world)]
-    dist.all_gather(out, t, group=group)
-    if dst >= 0 and rank != dst:
-        return None
-    g_rp = np.zeros(n + 1, dtype=np.int64)
-    np.cumsum(lens_g, out=g_rp[1:])
-    pieces = [(o[0].cpu().numpy(), o[1].cpu().numpy()) for o in out]
-    rows = [np.nonzero(owner == k + 1)[0] for k in range(world)]
-    c, v = _place(rows, pieces, lens_g, g_rp, int(g_rp[-1]))
-    return g_rp, c, v
+    pairs = _pairs_tensor(np.asarray(cols)[:nnz_local], np.asarray(counts)[:nnz_local], dev)
+    return _gather_blocks(rows, lens[rows], pairs, n, group, dst, as_tensors)
+
+
+def gather_result(res, n: int, group=None, dst: int = 0, as_tensors: bool = False):
+    """gather_csr of a traced rthx result (rthx._lib.DeviceResult).  On an NCCL
+    group the counts never leave device memory before the collective: the
+    block is copied device to device into the tensors RCCL sends
+    (rthx_result_copy_csr_device; its rows are emitter_begin + k *
+    emitter_stride).  On gloo the host CSR is gathered."""
+    import torch
+
+    dev = _device_of(group)
+    if dev.type == "cuda":
+        row_off, pairs, d = res.torch_csr()
+        if row_off.device != dev:
+            raise ValueError("the result lives on another device than this rank's")
+        lens = row_off[1:] - row_off[:-1]
+        rows = d["emitter_begin"] + d["emitter_stride"] * torch.arange(d["n_rows"], dtype=torch.int64, device=dev)
+        keep = lens > 0
+        return _gather_blocks(rows[keep], lens[keep], pairs, n, group, dst, as_tensors)
+    rp, c, v = res.csr()
+    return gather_csr(rp, c, v, n, group=group, dst=dst, as_tensors=as_tensors)
 
 
 def traced_bands(dom) -> List[Tuple[int, List[int]]]:
@@ -145,23 +216,25 @@ def bands_of(rank: int, world: int, traced: Sequence[Tuple[int, List[int]]]):
 
 
 def broadcast_csr(row_ptr, cols, counts, n: int, src: int, group=None):
-    """Rank `src`'s CSR (n rows) on every rank: the sizes, then the arrays,
-    as tensor broadcasts (over RCCL / xGMI on an NCCL group, gloo on the host).
+    """Rank `src`'s CSR (n rows) on every rank: the sizes, the row pointers
+    (int64) and the (col, count) pairs (int32, 8 bytes per nonzero) as tensor
+    broadcasts (over RCCL / xGMI on an NCCL group, gloo on the host).
     Non-source ranks pass None for the arrays."""
     import torch
     import torch.distributed as dist
 
-    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else torch.device("cpu")
+    dev = _device_of(group)
     rank = dist.get_rank(group)
     nnz = torch.tensor([int(row_ptr[-1]) if rank == src else 0], dtype=torch.int64, device=dev)
     dist.broadcast(nnz, src, group=group)
     m = int(nnz.item())
     if rank == src:
-        buf = torch.from_numpy(np.concatenate([np.asarray(row_ptr, dtype=np.int64),
-                                               np.asarray(cols, dtype=np.int64)[:m],
-                                               np.asarray(counts, dtype=np.int64)[:m]])).to(dev)
+        rp = torch.from_numpy(np.ascontiguousarray(row_ptr, dtype=np.int64)).to(dev)
+        pairs = _pairs_tensor(np.asarray(cols)[:m], np.asarray(counts)[:m], dev)
     else:
-        buf = torch.empty(n + 1 + 2 * m, dtype=torch.int64, device=dev)
-    dist.broadcast(buf, src, group=group)
-    b = buf.cpu().numpy()
-    return b[:n + 1], b[n + 1:n + 1 + m].astype(np.int32), b[n + 1 + m:].astype(np.uint32)
+        rp = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        pairs = torch.empty((2, m), dtype=torch.int32, device=dev)
+    dist.broadcast(rp, src, group=group)
+    dist.broadcast(pairs, src, group=group)
+    p = pairs.cpu().numpy()
+    return rp.cpu().numpy(), p[0].copy(), p[1].view(np.uint32).copy()

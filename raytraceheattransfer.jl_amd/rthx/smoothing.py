@@ -145,6 +145,11 @@ def smooth_F(F_raw, w, num_surfaces: int, max_iters: int = 1000, smooth_surfaces
     return out
 
 
+def result_device(res) -> int:
+    """The device a one-device trace result lives on (rthx_result_get_device_csr)."""
+    return res.device
+
+
 def smooth_exchange_factors(dom, F_raw, max_iters: int = 1000, k_dykstra: Optional[int] = None,
                             verbose: bool = True, device: int = 0):
     """The smoothing half of exchangeRayTracing! (exchangeRayTracing.jl:13-71):
@@ -163,7 +168,7 @@ def smooth_exchange_factors(dom, F_raw, max_iters: int = 1000, k_dykstra: Option
         # keep F_smooth there for the solve; the host copy of F_smooth is made
         # on first access (dom.F_smooth)
         info = {}
-        handle = smooth_F_device(res, n_block, get_w(dom), ns, info=info, **kw)
+        handle = smooth_F_device(res, n_block, get_w(dom), ns, info=info, **dict(kw, device=result_device(res)))
         dom._set_F_smooth_device(handle)
         dom.last_smooth_info = info
         return None
@@ -179,7 +184,9 @@ def smooth_exchange_factors(dom, F_raw, max_iters: int = 1000, k_dykstra: Option
         def smooth_bin(b):
             r = held.get(b)
             if r is not None and r.info()["n_devices"] == 1:  # counts still on the device
-                h = smooth_F_device(r, n_block, get_w(dom, b), ns, **kw)
+                # on the device that traced the band (band workers spread the
+                # bands over devices: rthx.exchange._bands_over_devices)
+                h = smooth_F_device(r, n_block, get_w(dom, b), ns, **dict(kw, device=result_device(r)))
                 try:
                     return h.host()
                 finally:

@@ -30,7 +30,7 @@ def _worker(rank, world, port, out_path):
 
     from oracle import oracle
     from rthx import _lib
-    from rthx.distributed import gather_csr, shard
+    from rthx.distributed import gather_csr, gather_result, shard
 
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     dom = H.wedge_domain(8, 3)
@@ -38,9 +38,26 @@ def _worker(rank, world, port, out_path):
     begin, stride = shard(rank, world)
     args, _k = _lib.make_args(0, 500, H.NUDGE, 9, begin, flat.n_emitters, stride)
     rp, cols, cnt, info, _ = oracle.trace_exchange(flat, args, 2)
-    merged = gather_csr(rp, cols, cnt, flat.n_emitters)
+    merged = gather_csr(rp, cols, cnt, flat.n_emitters)  # to rank 0 only
+    assert (merged is None) == (rank != 0)
+    everyone = gather_csr(rp, cols, cnt, flat.n_emitters, dst=-1)  # every rank
+
+    class HostResult:  # gather_result on a gloo group gathers the result's host CSR
+        def csr(self):
+            return rp, cols, cnt
+
+    via_result = gather_result(HostResult(), flat.n_emitters, dst=1)
+    assert (via_result is None) == (rank != 1)
+    # uint32 counts travel bit for bit (as int32): a count above 2^31
+    big = np.array([0, 0, 1] if rank == 0 else [0, 1, 1], dtype=np.int64)
+    bg = gather_csr(big, np.array([1], np.int32), np.array([3_000_000_000 + rank], np.uint32), 2, dst=-1)
+    assert bg[2].dtype == np.uint32 and list(bg[2]) == [3_000_000_001, 3_000_000_000]
     if rank == 0:
-        np.savez(out_path, row_ptr=merged[0], cols=merged[1], counts=merged[2])
+        np.savez(out_path, row_ptr=merged[0], cols=merged[1], counts=merged[2], all_rp=everyone[0],
+                 all_cols=everyone[1], all_counts=everyone[2])
+    if rank == 1:
+        for x, y in zip(via_result, everyone):
+            assert np.array_equal(x, y)
     dist.barrier()
     dist.destroy_process_group()
 
@@ -56,9 +73,10 @@ def test_two_rank_gather_equals_single_process(tmp_path):
     args, _k = _lib.make_args(0, 500, H.NUDGE, 9, 0, flat.n_emitters, 1)
     rp, cols, cnt, _info, _ = oracle.trace_exchange(flat, args, 4)
     m = np.load(out)
-    assert np.array_equal(m["row_ptr"], rp)
-    assert np.array_equal(m["cols"], cols)
-    assert np.array_equal(m["counts"], cnt)
+    for pre in ("", "all_"):
+        assert np.array_equal(m[pre + "row_ptr" if not pre else "all_rp"], rp)
+        assert np.array_equal(m[pre + "cols"], cols)
+        assert np.array_equal(m[pre + "counts"], cnt)
 
 
 def _direct_worker(rank, world, port, out_path):

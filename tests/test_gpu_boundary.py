@@ -324,3 +324,36 @@ def test_bench_two_gpus_as_a_plain_command(hip, mode):
                      "--rays-per-gpu", "20000000", "--mode", mode])
     assert d["n_gpus"] == 2 and d["value"] > 0
     assert d["config"]["rays_per_step"] == (40_000_000 // 10605) * 10605
+
+
+@pytest.mark.parametrize("case", ["square", "greenhouse", "shard"])
+def test_device_csr_equals_host_csr(hip, case):
+    """rthx_result_get_device_csr / rthx_result_copy_csr_device: the block a
+    collective sends from device memory (rthx.distributed.gather_result on
+    NCCL groups) holds exactly the host CSR's rows -- single- and
+    multi-polygon kernels, and a strided shard (rows begin + k stride)."""
+    torch = pytest.importorskip("torch")
+    dom = H.greenhouse_domain(n_layers=6, nx=9, ny=3, n_bins=8) if case == "greenhouse" else H.square_domain(13)
+    flat = dom.flat()
+    begin, stride = (1, 3) if case == "shard" else (0, 1)
+    args = _args(hip, flat, 3000, seed=4, begin=begin, stride=stride)[0]
+    dd = hip.DeviceDomain(flat, 0)
+    res = hip.DeviceResult()
+    try:
+        res.trace(dd, args)
+        rp, cols, cnt = res.csr()
+        d = res.device_csr()
+        assert d["device"] == 0 and d["n_parts"] == 1 and res.device == 0
+        assert d["emitter_begin"] == begin and d["emitter_stride"] == stride
+        assert d["nnz"] == rp[-1] and d["row_off"] and d["cols"] and d["counts"]
+        row_off, pairs, _d = res.torch_csr()
+        assert row_off.device.type == "cuda" and pairs.device.type == "cuda"
+        rows = np.arange(begin, flat.n_emitters, stride)
+        assert d["n_rows"] == rows.size
+        ro = row_off.cpu().numpy()
+        assert np.array_equal(np.diff(ro), np.diff(rp)[rows])
+        p = pairs.cpu().numpy()
+        assert np.array_equal(p[0], cols) and np.array_equal(p[1].view(np.uint32), cnt)
+    finally:
+        res.close()
+        dd.close()

@@ -159,3 +159,40 @@ def test_traced_bands_and_band_shares():
     assert sorted(b for s in shares for b, _ in s) == [1, 2, 3, 5]
     with pytest.raises(ValueError):
         bands_of(3, 3, traced)
+
+
+def test_band_results_are_smoothed_on_their_own_device(monkeypatch):
+    """mesh(devices=[...], bands=True) leaves each band's counts on the device
+    that traced it (rthx.exchange._bands_over_devices); the smoothing of a
+    band must run there (rthx_smooth_F_result refuses another device).  The
+    results are mocks, so no GPU is needed: bands 1..8 on devices b % 3."""
+    from rthx import smoothing
+
+    dom = H.greenhouse_domain(n_layers=4, nx=3, ny=2, n_bins=8)
+
+    class FakeResult:
+        def __init__(self, device):
+            self.device = device
+
+        def info(self):
+            return {"n_devices": 1}
+
+    dom._trace_results = {b: FakeResult(b % 3) for b in range(1, 9)}
+    seen = []
+
+    class FakeHandle:
+        def host(self):
+            return np.zeros((1, 1))
+
+        def close(self):
+            pass
+
+    def fake_smooth(res, n, w, ns, **kw):
+        seen.append((res.device, kw["device"]))
+        return FakeHandle()
+
+    monkeypatch.setattr(smoothing, "smooth_F_device", fake_smooth)
+    out = smoothing.smooth_exchange_factors(dom, None, verbose=False, device=0)
+    assert len(out) == 8
+    assert len(seen) == 8 and all(r == d for r, d in seen)
+    assert {d for _r, d in seen} == {0, 1, 2}
