@@ -258,6 +258,12 @@ def main():
                          "threads: this one process drives N devices through rthx_multi_trace_exchange")
     ap.add_argument("--emulate-world", type=int, default=0,
                     help="diagnostic: run rank 0's shard of a W-GPU job on this one GPU (no value claim)")
+    ap.add_argument("--strong", action="store_true",
+                    help="strong scaling: --rays-per-gpu is the whole job's ray count, split over the GPUs "
+                         "(default: weak scaling, that many rays per GPU)")
+    ap.add_argument("--faithful-steps", type=int, default=10,
+                    help="steps of the faithful-sampling leg (the reference's acos/sin/cos emission, "
+                         "emitVolumeRay2D.jl:26-31), reported beside value; 0 skips it")
     args = ap.parse_args()
 
     if args.mode == "ranks" and args.gpus > 1 and "WORLD_SIZE" not in os.environ and args.emulate_world <= 1:
@@ -291,7 +297,7 @@ def main():
     N = flat.n_emitters
     ndev = _lib.device_count()
     n_units = args.gpus if args.mode == "threads" else world  # GPUs doing the work
-    total_rays = args.rays_per_gpu * n_units
+    total_rays = args.rays_per_gpu * (1 if args.strong else n_units)
     R = total_rays // N
     if args.mode == "threads":
         devices = [d % max(ndev, 1) for d in range(args.gpus)]
@@ -353,6 +359,29 @@ def main():
         rays_all, nnz_all = int(r[0]), int(r[1])
     else:
         rays_all, nnz_all = rays_rank, nnz_rank
+
+    # The reference's own sampling (faithful: acos/sin/cos as
+    # emitVolumeRay2D.jl:26-31, Float32 Lambert draws), same launch otherwise;
+    # reported beside `value`, never as it.
+    faithful = None
+    if rank == 0 and args.faithful_steps > 0:
+        fargs, _kf = _lib.make_args(0, R, nudge, args.seed, targs.emitter_begin, N, targs.emitter_stride,
+                                    device=device, flags=abi.RTHX_FLAG_DEVICE_ONLY | abi.RTHX_FLAG_FAITHFUL_SAMPLING)
+        for _ in range(3):
+            res.trace(dd, fargs)
+        sync_all()
+        f_ms = []
+        t = time.perf_counter()
+        for _ in range(args.faithful_steps):
+            res.trace(dd, fargs)
+            f_ms.append(res.info()["trace_ms"])
+        sync_all()
+        f_el = time.perf_counter() - t
+        f_rays = res.info()["rays_traced"]
+        faithful = {"value": round(f_rays * args.faithful_steps / f_el / 1e6, 3), "unit": "Mrays/s",
+                    "ms_per_step": round(f_el / args.faithful_steps * 1e3, 4),
+                    "avg_kernel_ms": round(float(np.mean(f_ms)), 4), "steps": args.faithful_steps,
+                    "gpus": 1, "note": "faithful sampling (RTHX_FLAG_FAITHFUL_SAMPLING), rank 0's launch"}
 
     # PCIe-inclusive end-to-end passes, reported aside (never `value`): the
     # trace plus the CSR of counts DMA'd into page-locked caller arrays that a
@@ -424,13 +453,15 @@ def main():
             "prewarm_steps": prewarm_steps,
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.strong else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic",
             "config": {
                 "workload": (f"101x101 grey kappa=1 sigma_s=0 unit-square enclosure (BASELINE configs[1]); "
-                             f"{args.rays_per_gpu:.0e} rays per GPU, emitter rows sharded over {n_units} GPU(s)"),
+                             + (f"{args.rays_per_gpu:.0e} rays per job" if args.strong else
+                                f"{args.rays_per_gpu:.0e} rays per GPU")
+                             + f", emitter rows sharded over {n_units} GPU(s)"),
                 "n_emitters": N,
                 "rays_per_emitter": R,
                 "rays_per_step": rays_all,
@@ -455,6 +486,7 @@ def main():
             "pack_ms": round(float(np.mean(pack_ms)), 4),
             "roofline_fp64": fp64_roof,
             "roofline_valu": valu_roof,
+            "faithful_sampling": faithful,
             "e2e_with_d2h_mrays_s": round(e2e, 3) if e2e else None,
             "e2e_F_with_d2h_mrays_s": round(e2e_F, 3) if e2e_F else None,
         }

@@ -146,8 +146,10 @@ typedef struct rthx_result_info {
                               (about 0 when the trace kernel wrote the CSR itself) */
   double total_ms;         /* host wall time of the whole call */
   int32_t n_devices;       /* devices that traced rows (rthx_multi_trace_exchange: > 1) */
-  int32_t lookback_fallbacks; /* launches whose direct-CSR look-back gave up waiting on a
-                              predecessor row and were re-traced on the staging path */
+  int32_t lookback_fallbacks; /* launches traced again: a direct-CSR look-back gave up waiting
+                              on a predecessor row (re-traced on the staging path), or the
+                              rows outgrew the CSR reserved from the previous launch's nnz
+                              (re-traced into buffers of the exact size) */
 } rthx_result_info;
 
 typedef struct rthx_domain rthx_domain;

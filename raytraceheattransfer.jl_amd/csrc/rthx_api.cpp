@@ -488,6 +488,10 @@ RTHX_EXPORT int rthx_domain_create(const rthx_domain_desc* desc, int32_t device,
       G.off_beta = (int32_t)off;
       G.blob_bytes = (int32_t)off;
       off = a16(off + 8 * nc);
+      if (ncx == 1) {  // layer records (walk_layers), staged per bin
+        G.off_lay = (int32_t)off;
+        off = a16(off + sizeof(rthx::LayerRec) * (size_t)ncy);
+      }
       G.inv_x = (double)nx / (xs[nx] - xs[0]);
       G.inv_y = (double)ny / (ys[ny] - ys[0]);
       G.inv_cx = (double)ncx / (cxs[ncx] - cxs[0]);
@@ -732,8 +736,7 @@ int plan_trace(const rthx_domain* dom, const rthx_trace_args* a, TracePlan& p) {
     const int64_t cap_max = env_int("RTHX_HASH_MAX", kMaxHashCap, 256, kMaxHashCap);
     const int64_t load_pct = env_int("RTHX_HASH_LOAD_PCT", 75, 10, 90);  // most slots a workgroup fills (A/B: tools/hash_ab.sh)
     const int64_t max_rays = cap_max * load_pct / 100;
-    if (rays_per_block > max_rays) {
-      if (p.recording) return fail(RTHX_ERANGE, "recording a large-N domain needs fewer rays_per_emitter");
+    if (rays_per_block > max_rays) {  // (recorded rows too: the recorder indexes rays by (emitter, ray))
       p.split = (R + max_rays - 1) / max_rays;
       rays_per_block = (R + p.split - 1) / p.split;
     }
@@ -798,25 +801,37 @@ int plan_trace(const rthx_domain* dom, const rthx_trace_args* a, TracePlan& p) {
 // to staging slots, then row_scan + csr_pack.  Fills totals (see
 // finish_staged; totals[3] > 0: a look-back wait gave up).
 int run_trace(rthx_domain* dom, const rthx_trace_args* a, const TracePlan& p, rthx_result* res, bool lookback,
-              const rthx::RecordParams& rec, int64_t totals[4], float* ms_trace, float* ms_pack) {
+              const rthx::RecordParams& rec, int64_t totals[rthx::kLbTotals], float* ms_trace, float* ms_pack) {
   const int64_t n_rows = p.n_rows, N = p.N, R = p.R;
   hipStream_t st = dom->stream;
   HIP_TRY(res->row_nnz.reserve((size_t)n_rows * 4), "hipMalloc row_nnz");
   HIP_TRY(res->row_tallied.reserve((size_t)n_rows * 4), "hipMalloc row_tallied");
   HIP_TRY(res->row_off.reserve((size_t)(n_rows + 1) * 8), "hipMalloc row_off");
   HIP_TRY(res->totals.reserve(4 * 8), "hipMalloc totals");
-  // Staging slots only when the rows are staged; the direct CSR writes
-  // cols / counts in place, sized to the worst case n_rows x min(N, R).
+  // Staging slots only when the rows are staged.  The direct CSR writes
+  // cols / counts in place: sized from the previous launch's nnz (plus an
+  // eighth), or on a first launch from a guess (2048 entries per row); rows
+  // that would end past them write nothing and
+  // flag an overflow, and the host then traces the launch again with the
+  // exact size, which the look-back's prefix sums give (trace_exchange_one).
+  // Never more than the worst case n_rows x min(N, R).
   if (lookback) {
     res->stage_cols.release();
     res->stage_cnt.release();
-    HIP_TRY(res->cols.reserve((size_t)n_rows * p.row_cap * 4), "hipMalloc cols");
-    HIP_TRY(res->cnt.reserve((size_t)n_rows * p.row_cap * 4), "hipMalloc cnt");
+    const int64_t worst = n_rows * p.row_cap;
+    int64_t want = res->lb_nnz_hint > 0 ? res->lb_nnz_hint + res->lb_nnz_hint / 8 + 65536
+                                        : std::max<int64_t>(1 << 20, n_rows * std::min<int64_t>(p.row_cap, 2048));
+    want = std::min<int64_t>(worst, (int64_t)env_int("RTHX_CSR_CAP", want, 1, worst));
+    want = std::max<int64_t>(want, 1);
+    for (rthx::DevBuf* b : {&res->cols, &res->cnt}) {
+      if (b->cap > 2 * (size_t)want * 4 + (64u << 20)) b->release();  // (a much larger earlier trace)
+      HIP_TRY(b->reserve((size_t)want * 4), "hipMalloc direct CSR");
+    }
     // fresh words or totals (or a wrapped epoch): zero them once, epoch 1
     const size_t lb_bytes = (size_t)n_rows * 8;
     if (!res->lb_status.p || lb_bytes > res->lb_status.cap || !res->lb_totals.p) res->lb_epoch = 0;
     HIP_TRY(res->lb_status.reserve(lb_bytes), "hipMalloc look-back words");
-    HIP_TRY(res->lb_totals.reserve(2 * 8 * 8), "hipMalloc look-back totals");
+    HIP_TRY(res->lb_totals.reserve(2 * 8 * 8), "hipMalloc look-back totals");  // (2 sets of kLbTotals <= 8)
     HIP_TRY(res->h_totals.reserve(8 * 8), "hipHostMalloc totals");
   } else {
     res->lb_status.release();
@@ -868,6 +883,7 @@ int run_trace(rthx_domain* dom, const rthx_trace_args* a, const TracePlan& p, rt
     T.lb_wait_ticks = lookback_wait_ticks();
     T.out_cols = res->cols.as<uint32_t>();
     T.out_cnt = res->cnt.as<uint32_t>();
+    T.out_cap = (int64_t)(std::min(res->cols.cap, res->cnt.cap) / 4);
     T.row_off = res->row_off.as<int64_t>();
     // The words carry the launch's epoch and row 0 zeroes the other set of
     // totals for the next launch, so nothing is zeroed between launches but
@@ -914,9 +930,10 @@ int run_trace(rthx_domain* dom, const rthx_trace_args* a, const TracePlan& p, rt
     // (a last-row hand-over of the totals into page-locked memory, counting
     // finished rows with one more atomic per row, measured 14 us slower per
     // launch than this copy: profiles/round2/hosttot_ab.txt)
-    HIP_TRY(hipMemcpyAsync(res->h_totals.p, T.totals, 32, hipMemcpyDeviceToHost, st), "hipMemcpy totals");
+    HIP_TRY(hipMemcpyAsync(res->h_totals.p, T.totals, 8 * rthx::kLbTotals, hipMemcpyDeviceToHost, st),
+            "hipMemcpy totals");
     HIP_TRY(hipStreamSynchronize(st), "trace kernel");
-    std::memcpy(totals, res->h_totals.p, 32);
+    std::memcpy(totals, res->h_totals.p, 8 * rthx::kLbTotals);
     res->lb_epoch = T.lb_epoch;
   } else {
     const int merge = p.split == 1 ? rthx::kNoMerge : p.part_lists ? rthx::kMergeParts : rthx::kMergeDense;
@@ -994,21 +1011,35 @@ int trace_exchange_one(rthx_domain* dom, const rthx_trace_args* a, rthx_result* 
   // recorder's kernels stage.
   const bool lookback = p.split == 1 && n_rows > 0 && dom->single_convex && !p.recording &&
                         (uint64_t)n_rows * (uint64_t)p.row_cap <= rthx::kLbValMax && !env_flag("RTHX_NO_LOOKBACK");
-  int64_t totals[4] = {0, 0, 0, 0};
+  int64_t totals[rthx::kLbTotals] = {0, 0, 0, 0, 0};
   float ms_trace = 0.f, ms_pack = 0.f;
   rc = run_trace(dom, a, p, res, lookback, rec, totals, &ms_trace, &ms_pack);
   if (rc) return rc;
+  if (lookback && totals[3] == 0 && totals[4] != 0) {
+    // Rows outgrew the reserved direct CSR: the look-back's totals hold the
+    // exact nnz, so the same launch -- same draws, same counts -- is traced
+    // again into buffers of that size.
+    res->info.lookback_fallbacks += 1;
+    res->lb_nnz_hint = totals[0];
+    float ms2 = 0.f, mp2 = 0.f;
+    rc = run_trace(dom, a, p, res, true, rec, totals, &ms2, &mp2);
+    if (rc) return rc;
+    ms_trace += ms2;
+    ms_pack += mp2;
+    if (totals[4] != 0) return fail(RTHX_ESTATE, "direct CSR overflow after resizing");
+  }
   if (lookback && totals[3] != 0) {
     // A look-back wait gave up (a predecessor row did not publish its nnz in
     // time): the direct CSR may be misplaced, so the same launch -- same
     // draws, same counts -- is traced again on the staging path.
-    res->info.lookback_fallbacks = 1;
+    res->info.lookback_fallbacks += 1;
     float ms2 = 0.f, mp2 = 0.f;
     rc = run_trace(dom, a, p, res, false, rec, totals, &ms2, &mp2);
     if (rc) return rc;
     ms_trace += ms2;
     ms_pack += mp2;
   }
+  if (lookback) res->lb_nnz_hint = totals[0];
   res->info.nnz = totals[0];
   res->info.lost_total = totals[1];
   res->info.lost_max_row = totals[2];

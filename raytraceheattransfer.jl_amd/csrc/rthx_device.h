@@ -116,8 +116,18 @@ struct MLatLayout {
   int32_t blob_bytes;  // staged from ml_blob
   int32_t nx, ny, ncx, ncy;
   int32_t off_ys, off_cxs, off_cys, off_cmap, off_cinfo, off_bsolid, off_beta;
-  int32_t reserved;
+  int32_t off_lay;     // one coarse column (ncx == 1): LayerRec[ncy] staged per bin after the betas; else 0
   double inv_x, inv_y, inv_cx, inv_cy;  // first guesses of lattice_index
+};
+
+// One layer of a one-column lattice as walk_layers reads it: its bounds,
+// this bin's beta and its solid walls in one 32-byte LDS record (two
+// ds_read_b128 per segment).
+struct alignas(16) LayerRec {
+  double y0, y1;
+  double beta;     // -1: the fine betas of the layer differ (MIXED)
+  uint32_t solid;  // bit w: wall w solid
+  uint32_t pad;
 };
 
 struct DevDomain {
@@ -1032,6 +1042,7 @@ struct MLatLds {
   const MCoarse RTHX_LDS* cinfo;
   const uint32_t RTHX_LDS* bsolid;
   const double RTHX_LDS* beta;
+  const LayerRec RTHX_LDS* lay;  // (one-column lattices)
 };
 
 __device__ __forceinline__ MLatLds mlat_lds_view(const char RTHX_LDS* base, const MLatLayout& G) {
@@ -1044,6 +1055,7 @@ __device__ __forceinline__ MLatLds mlat_lds_view(const char RTHX_LDS* base, cons
   v.cinfo = (const MCoarse RTHX_LDS*)(base + G.off_cinfo);
   v.bsolid = (const uint32_t RTHX_LDS*)(base + G.off_bsolid);
   v.beta = (const double RTHX_LDS*)(base + G.off_beta);
+  v.lay = (const LayerRec RTHX_LDS*)(base + G.off_lay);
   return v;
 }
 
@@ -1224,97 +1236,105 @@ __device__ __forceinline__ int walk_ml(const DevDomain& D, const TraceParams& P,
 // stack of layers j with bounds cys[j], cys[j + 1] (the greenhouse of C5).
 // A ray crosses only layer boundaries (an x wall is the lattice's side:
 // solid, or the ray leaves), so the walker keeps just its layer index and
-// reads the layer's bounds, beta and solid walls from LDS at each segment.
-// The point is checked against its layer's box at the start of every
-// segment instead of after each crossing: the same test of the neighbouring
-// box (the layer across the crossed boundary; across a side wall or the
-// lattice's top or bottom the box is kept, which the check then fails), and
-// a point outside it -- a crossing through a corner, a nudge that did not
-// carry the point across, or a point outside the lattice -- is located on
-// the lattice as in walk_ml (findFace2D, lost when in no box).  Same
-// arithmetic, candidates, ties, step count and results as walk_ml.
-template <bool UNIFORM>
+// reads the layer's record (bounds, beta, solid walls: LayerRec, two LDS
+// reads) at each segment.  The point is checked against its layer's box at
+// the start of every segment instead of after each crossing: the same test
+// of the neighbouring box (the layer across the crossed boundary; across a
+// side wall or the lattice's top or bottom the layer is kept, which the
+// check then fails).  A point outside it -- a crossing through a corner, a
+// nudge that did not carry the point across, a point outside the lattice --
+// ends the walk with kRayRelocate; the kernel locates it on the lattice
+// (relocate_layers: findFace2D's answer, lost when in no box) and the walk
+// goes on.  Same arithmetic, candidates, ties, step count and results as
+// walk_ml.  The loop body is straight-line code: a lane whose ray ends
+// leaves the loop, the wave leaves it when at most `stop` lanes still walk.
+// MIXED: some layer of this bin has no single beta.
+constexpr int kRayRelocate = -6;  // walk_layers: p is not in its layer's box
+
+template <bool UNIFORM, bool MIXED>
 __device__ __forceinline__ int walk_layers(const DevDomain& D, const TraceParams& P, const MLatLds& L,
                                            const MLatLayout& G, MBox& B, double& px, double& py, const MRay& r,
                                            double& S, double& acc, int& it, double& u_end, uint32_t stop) {
   const double eta = P.eta;
-  const bool mixed = P.mixed != 0;
   const int ncy = G.ncy;
   const bool xdn = r.dx < 0.0, ydn = r.dy < 0.0;
   const double ax = fabs(r.dx), ay = fabs(r.dy);
   const bool vxd = ax >= 1e-10, vyd = ay >= 1e-10;
-  const bool y_first = ydn | xdn;  // wall order: y wall first unless top (2) vs right (1)
+  // wall order: the y wall comes first unless it is the top wall (2) and the
+  // x wall the right one (1); the later wall wins only if strictly closer
+  const bool y_first = ydn | xdn;
   const int kx = xdn ? 3 : 1, ky = ydn ? 0 : 2;
   const int sy = ydn ? -1 : 1;
   const double x0 = L.cxs[0], x1 = L.cxs[1];
   const double xf = xdn ? x0 : x1;
   int cj = B.cj;
-  bool walking = true;
   int status = kRayContinue;
 #pragma unroll 1
   while (true) {
-    if (walking) {
-      const double y0 = L.cys[cj], y1 = L.cys[cj + 1];
-      const bool inside = (x0 <= px) & (px < x1) & (y0 <= py) & (py < y1);
-      if (!inside) {
-        const int li = lattice_index(L.cxs, 1, G.inv_cx, px), lj = lattice_index(L.cys, ncy, G.inv_cy, py);
-        if ((li < 0) | (lj < 0)) {
-          walking = false;
-          status = -1;
-        } else {
-          cj = lj;
-        }
-      } else {
-        const double yf = ydn ? y0 : y1;
-        const double nx = fabs(xf - px), ny = fabs(yf - py);
-        const bool vx = vxd & (nx > 0.0), vy = vyd & (ny > 0.0);
-        const double cx = __dmul_rn(nx, ay), cy = __dmul_rn(ny, ax);
-        const bool xw = vx & (!vy | (y_first ? (cx < cy) : !(cy < cx)));
-        const bool any = vx | vy;
-        const double u = any ? div_by_rcp(xw ? nx : ny, xw ? ax : ay, xw ? r.rax : r.ray) : __builtin_inf();
-        const int k = any ? (xw ? kx : ky) : 0;
-        bool gas;
-        double accn = 0.0;
-        bool lost = false;
-        if (UNIFORM) {
-          gas = S < u;
-        } else {
-          double beta = L.beta[cj];
-          if (mixed && beta < 0.0) {
-            const MCoarse m = ld(L.cinfo + L.cmap[cj]);
-            int i, j;
-            const int f0 = ml_fine(L, G, m, px, py, i, j);
-            lost = f0 < 0;  // the segment start lies in no fine cell (traceRay.jl:89-91)
-            beta = lost ? 0.0 : D.beta[(size_t)P.bin * D.n_fine + f0];
-          }
-          accn = acc + __dmul_rn(beta, u);
-          gas = accn >= S;
-        }
-        const bool wall = !gas & (((L.bsolid[cj] >> k) & 1u) != 0u);
-        if (lost | gas | wall) {
-          walking = false;
-          status = lost ? -1 : gas ? kRayEndGas : kRayEndWall;
-          u_end = u;
-        } else {
-          const double t = u + eta;
-          px = px + __dmul_rn(t, r.dx);
-          py = py + __dmul_rn(t, r.dy);
-          if (UNIFORM) S -= u; else acc = accn;
-          const int cjn = cj + sy;
-          cj = (!xw & ((unsigned)cjn < (unsigned)ncy)) ? cjn : cj;
-          if (++it >= 10000) {  // traceRay.jl:27: no end within 10,000 steps
-            walking = false;
-            status = -1;
-          }
+    const LayerRec rec = ld(L.lay + cj);
+    const bool inside = (x0 <= px) & (px < x1) & (rec.y0 <= py) & (py < rec.y1);
+    const double yf = ydn ? rec.y0 : rec.y1;
+    const double nx = fabs(xf - px), ny = fabs(yf - py);
+    // a wall is a candidate when its parameter num / den is > 0: den >= 1e-10
+    // and num > 0 (num / den > 0 exactly then, for den <= 1)
+    const bool vx = vxd & (nx > 0.0), vy = vyd & (ny > 0.0);
+    const double cx = __dmul_rn(nx, ay), cy = __dmul_rn(ny, ax);
+    const bool xw = vx & (!vy | (y_first & (cx < cy)) | (!y_first & (cx <= cy)));
+    const bool any = vx | vy;
+    const double u = any ? div_by_rcp(xw ? nx : ny, xw ? ax : ay, xw ? r.rax : r.ray) : __builtin_inf();
+    const int k = any ? (xw ? kx : ky) : 0;
+    bool gas, lost = false;
+    double accn = 0.0;
+    if (UNIFORM) {
+      gas = S < u;
+    } else {
+      double beta = rec.beta;
+      if (MIXED) {
+        if (beta < 0.0) {
+          const MCoarse m = ld(L.cinfo + L.cmap[cj]);
+          int i, j;
+          const int f0 = ml_fine(L, G, m, px, py, i, j);
+          lost = f0 < 0;  // the segment start lies in no fine cell (traceRay.jl:89-91)
+          beta = lost ? 0.0 : D.beta[(size_t)P.bin * D.n_fine + f0];
         }
       }
+      accn = acc + __dmul_rn(beta, u);
+      gas = accn >= S;
     }
-    if ((uint32_t)__popcll(__ballot(walking)) <= stop) break;
+    const bool wall = !gas & (((rec.solid >> k) & 1u) != 0u);
+    if (!inside | lost | gas | wall) {
+      status = !inside ? kRayRelocate : lost ? -1 : gas ? kRayEndGas : kRayEndWall;
+      u_end = u;
+      break;
+    }
+    const double t = u + eta;
+    px = px + __dmul_rn(t, r.dx);
+    py = py + __dmul_rn(t, r.dy);
+    if (UNIFORM) S -= u; else acc = accn;
+    const int cjn = cj + sy;
+    cj = (!xw & ((unsigned)cjn < (unsigned)ncy)) ? cjn : cj;
+    if (++it >= 10000) {  // traceRay.jl:27: no end within 10,000 steps
+      status = -1;
+      break;
+    }
+    if ((uint32_t)__popcll(__ballot(1)) <= stop) break;  // (the lanes still walking)
   }
   B.ci = 0;
   B.cj = cj;
   B.b = cj;
   return status;
+}
+
+// kRayRelocate: the layer of p by the lattice locate (findFace2D's answer);
+// false when p lies in no box (the ray is lost).
+__device__ __forceinline__ bool relocate_layers(const MLatLds& L, const MLatLayout& G, MBox& B, double px,
+                                                double py) {
+  const int li = lattice_index(L.cxs, 1, G.inv_cx, px), lj = lattice_index(L.cys, G.ncy, G.inv_cy, py);
+  if ((li < 0) | (lj < 0)) return false;
+  B.ci = 0;
+  B.cj = lj;
+  B.b = lj;
+  return true;
 }
 
 // The end point of a ray whose walk ended (kRayEndGas / kRayEndWall, p at

@@ -59,8 +59,9 @@ struct TallyParams {
   unsigned long long* lb_status;
   uint32_t* out_cols;
   uint32_t* out_cnt;
+  int64_t out_cap;               // entries out_cols / out_cnt hold (rows past it flag totals[4])
   int64_t* row_off;              // [n_rows + 1]
-  unsigned long long* totals;    // nnz, lost rays, max lost per row, look-back stalls (zeroed)
+  unsigned long long* totals;    // nnz, lost rays, max lost per row, look-back stalls, CSR overflows (zeroed)
   unsigned long long* totals_next;  // look-back launches: the next launch's totals, zeroed by row 0
   int64_t R;
   uint64_t lb_wait_ticks;        // longest look-back wait (s_memrealtime ticks, 100 MHz) before giving up
@@ -71,6 +72,7 @@ struct TallyParams {
 // launch epoch in bits 46-61, the value below.  A word of another epoch
 // (or a zeroed one: epochs start at 1) is not yet published.
 constexpr int kLbEpochShift = 46;
+constexpr int kLbTotals = 5;  // totals words of a look-back launch (TallyParams::totals)
 constexpr uint32_t kLbEpochMax = 0xFFFF;
 constexpr unsigned long long kLbValMax = (1ull << kLbEpochShift) - 1;
 

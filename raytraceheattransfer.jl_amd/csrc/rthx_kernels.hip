@@ -114,7 +114,8 @@ __device__ __forceinline__ uint64_t lookback_offset(unsigned long long* status, 
 // row's output offset (0 for staging slots; the look-back for the direct CSR).
 template <bool PAIRS, class F, class B>
 __device__ __forceinline__ uint32_t compact_row(int64_t n_words, F count2, uint32_t* __restrict__ out_c_,
-                                                uint32_t* __restrict__ out_n_, uint32_t* wave_sum, B base_of) {
+                                                uint32_t* __restrict__ out_n_, uint32_t* wave_sum, B base_of,
+                                                uint64_t cap = ~0ull) {
   const int kWaves = (int)(blockDim.x >> 6);
   const uint32_t lane = lane_id();
   const int wave = threadIdx.x >> 6;
@@ -140,7 +141,9 @@ __device__ __forceinline__ uint32_t compact_row(int64_t n_words, F count2, uint3
   const uint64_t gbase = base_of(total);
   uint32_t* __restrict__ out_c = out_c_ + gbase;
   uint32_t* __restrict__ out_n = out_n_ + gbase;
-  for (int64_t w0 = wb; w0 < we; w0 += 64) {
+  // (a row that would end past the `cap` entries reserved writes nothing:
+  // base_of has flagged the overflow and the host re-traces)
+  for (int64_t w0 = wb; w0 < (gbase + total <= cap ? we : wb); w0 += 64) {
     const int64_t w = w0 + lane;
     uint32_t lo = 0u, hi = 0u;
     if (w < we) count2(w, lo, hi);
@@ -287,7 +290,7 @@ __device__ __forceinline__ uint32_t hash_emit_bitmap(const uint32_t* keys, const
   uint32_t *oc, *on;
   out(total, oc, on);
   uint32_t pos = base + incl - c;
-  for (uint32_t w = w0; w < w1; ++w) {
+  for (uint32_t w = w0; w < (oc ? w1 : w0); ++w) {  // (null: the row overflows the reserved CSR)
     uint32_t bits = bm[w];
     while (bits) {
       const uint32_t a = 32u * w + (uint32_t)(__ffs(bits) - 1);
@@ -346,6 +349,21 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
     for (int i = tid; i < D.ml.blob_bytes / 16; i += nthr) dst[i] = D.ml_blob[i];
     double RTHX_LDS* cb = (double RTHX_LDS*)(cl_base + D.ml.off_beta);
     for (int i = tid; i < D.n_coarse; i += nthr) cb[i] = D.ml_bbeta[(size_t)P.bin * D.n_coarse + i];
+    if (D.ml.off_lay > 0) {  // one coarse column: the layer records of walk_layers (box b = layer b)
+      LayerRec* lay = (LayerRec*)(cl_base + D.ml.off_lay);  // (generic view; stores stay ds_write)
+      const char RTHX_GLOBAL* blob = (const char RTHX_GLOBAL*)D.ml_blob;
+      const double RTHX_GLOBAL* cys = (const double RTHX_GLOBAL*)(blob + D.ml.off_cys);
+      const uint32_t RTHX_GLOBAL* bs = (const uint32_t RTHX_GLOBAL*)(blob + D.ml.off_bsolid);
+      for (int i = tid; i < D.ml.ncy; i += nthr) {
+        LayerRec r;
+        r.y0 = cys[i];
+        r.y1 = cys[i + 1];
+        r.beta = D.ml_bbeta[(size_t)P.bin * D.n_coarse + i];
+        r.solid = bs[i];
+        r.pad = 0u;
+        lay[i] = r;
+      }
+    }
   } else if (CLDS) {
     uint4* dst = (uint4*)cl_base;  // generic view (HIP vector assignment); stores stay ds_write
     for (int i = tid; i < D.cl.blob_bytes / 16; i += nthr) dst[i] = D.c_blob[i];
@@ -497,6 +515,8 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
         end_move_ml<UNIFORM>(D, P, RTHX_ML_VIEW, RTHX_ML_G, box, px, py, ry, S, acc, u_end, gas);
         tally(end_ml(D, RTHX_ML_VIEW, RTHX_ML_G, box, px, py, ry.dx, ry.dy, gas));
       }
+      if (state == kRayRelocate)  // (walk_layers: a corner crossing or a nudge that fell short)
+        state = relocate_layers(RTHX_ML_VIEW, RTHX_ML_G, box, px, py) ? kRayContinue : -1;
       bool live = state == kRayContinue;
       const uint64_t idle = __ballot(!live);
       const uint32_t n_idle = (uint32_t)__popcll(idle);
@@ -553,8 +573,10 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
 #ifdef RTHX_SEGSTAT
         const int it0 = it;
 #endif
-        if (layered)
-          state = walk_layers<UNIFORM>(D, P, RTHX_ML_VIEW, RTHX_ML_G, box, px, py, ry, S, acc, it, u_end, stop);
+        if (layered && P.mixed)
+          state = walk_layers<UNIFORM, true>(D, P, RTHX_ML_VIEW, RTHX_ML_G, box, px, py, ry, S, acc, it, u_end, stop);
+        else if (layered)
+          state = walk_layers<UNIFORM, false>(D, P, RTHX_ML_VIEW, RTHX_ML_G, box, px, py, ry, S, acc, it, u_end, stop);
         else
           state = walk_ml<UNIFORM>(D, P, RTHX_ML_VIEW, RTHX_ML_G, box, px, py, ry, S, acc, it, u_end, stop);
 #ifdef RTHX_SEGSTAT
@@ -657,7 +679,7 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
         T.totals[0] = b + nnz;
       }
       if (slot == 0)  // the next look-back launch's totals (rthx_api.cpp run_trace)
-        for (int i = 0; i < 4; ++i) T.totals_next[i] = 0ull;
+        for (int i = 0; i < kLbTotals; ++i) T.totals_next[i] = 0ull;
     }
   };
   if constexpr (HASH) {
@@ -671,10 +693,14 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
         oc = T.stage_cols + o;
         on = T.stage_cnt + o;
       } else if (SINGLE && T.lb_status) {
-        if (tid == 0) s_base = lookback_offset(T.lb_status, slot, nnz, &T.totals[3], T.lb_wait_ticks, T.lb_epoch);
+        if (tid == 0) {
+          s_base = lookback_offset(T.lb_status, slot, nnz, &T.totals[3], T.lb_wait_ticks, T.lb_epoch);
+          if (s_base + nnz > (uint64_t)T.out_cap) atomicAdd(&T.totals[4], 1ull);  // (the host re-traces)
+        }
         __syncthreads();
-        oc = T.out_cols + s_base;
-        on = T.out_cnt + s_base;
+        const bool fits = s_base + nnz <= (uint64_t)T.out_cap;
+        oc = fits ? T.out_cols + s_base : nullptr;
+        on = fits ? T.out_cnt + s_base : nullptr;
       } else {
         oc = T.stage_cols + slot * T.row_cap;
         on = T.stage_cnt + slot * T.row_cap;
@@ -688,7 +714,7 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
       nnz = hash_sort(hist, hist + cap, cap, wave_sum);
       uint32_t *oc, *on;
       out(nnz, oc, on);
-      for (uint32_t i = (uint32_t)tid; i < nnz; i += (uint32_t)nthr) {
+      for (uint32_t i = (uint32_t)tid; i < (oc ? nnz : 0u); i += (uint32_t)nthr) {
         oc[i] = keys[i] - 1u;
         on[i] = cnts[i];
       }
@@ -741,11 +767,14 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
   }
   if (SINGLE && T.lb_status) {  // (host: single-polygon domains only; keeps the other kernels lean)
     auto base_of = [&](uint32_t nnz) -> uint64_t {
-      if (tid == 0) s_base = lookback_offset(T.lb_status, slot, nnz, &T.totals[3], T.lb_wait_ticks, T.lb_epoch);
+      if (tid == 0) {
+        s_base = lookback_offset(T.lb_status, slot, nnz, &T.totals[3], T.lb_wait_ticks, T.lb_epoch);
+        if (s_base + nnz > (uint64_t)T.out_cap) atomicAdd(&T.totals[4], 1ull);  // (the host re-traces)
+      }
       __syncthreads();
       return s_base;
     };
-    lb_finish(compact_row<PACK16>(n_words, count2, T.out_cols, T.out_cnt, wave_sum, base_of));
+    lb_finish(compact_row<PACK16>(n_words, count2, T.out_cols, T.out_cnt, wave_sum, base_of, (uint64_t)T.out_cap));
     return;
   }
   uint32_t nnz = compact_row<PACK16>(n_words, count2, T.stage_cols + slot * T.row_cap, T.stage_cnt + slot * T.row_cap,
@@ -1068,9 +1097,15 @@ static hipError_t launch_trace_a(const LaunchCfg& L) {
 
 template <bool UNIFORM, int TALLY, bool FAITHFUL>
 static hipError_t launch_trace_u(const LaunchCfg& L) {
-  // Recording is a plotting aid: generic (non-SINGLE, unsplit, general
-  // polygon) instances carry it.
-  if (L.rec.n > 0) return launch_trace_t<UNIFORM, TALLY, FAITHFUL, false, true, false, false>(L);
+  // Recording is a plotting aid: generic (non-SINGLE, general polygon)
+  // instances carry it, unsplit -- or split into hash-tallied parts when a
+  // large-N row holds more rays than one table (the recorder writes ray r of
+  // a recorded emitter at (emitter, r), whichever part traces it).
+  if (L.rec.n > 0) {
+    if constexpr (TALLY == kTallyHash)
+      if (L.T.split > 1) return launch_trace_t<UNIFORM, TALLY, FAITHFUL, false, true, true, false>(L);
+    return launch_trace_t<UNIFORM, TALLY, FAITHFUL, false, true, false, false>(L);
+  }
   return L.axis ? launch_trace_a<UNIFORM, TALLY, FAITHFUL, true>(L) : launch_trace_a<UNIFORM, TALLY, FAITHFUL, false>(L);
 }
 

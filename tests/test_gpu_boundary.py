@@ -357,3 +357,64 @@ def test_device_csr_equals_host_csr(hip, case):
     finally:
         res.close()
         dd.close()
+
+
+def test_direct_csr_overflow_retraces_with_exact_size(hip, monkeypatch):
+    """The direct CSR is reserved from the previous launch's nnz (a guess on
+    the first): rows that outgrow it write nothing, flag the overflow, and the
+    host traces the launch again into buffers of the exact size.  A forced
+    tiny reservation (RTHX_CSR_CAP) must give the same CSR, report one extra
+    launch, and the next launch of the same result must fit."""
+    dom = H.square_domain(31)
+    flat = dom.flat()
+    args = _args(hip, flat, 4000, seed=21)[0]
+    dd = hip.DeviceDomain(flat, 0)
+    try:
+        want = _trace(hip, dd, args)
+        assert want[3]["lookback_fallbacks"] == 0  # (worst case 1085 x 1085 entries: reserved outright)
+        monkeypatch.setenv("RTHX_CSR_CAP", "1000")
+        res = hip.DeviceResult()
+        try:
+            res.trace(dd, args)
+            assert res.info()["lookback_fallbacks"] == 1
+            got = res.csr()
+            monkeypatch.delenv("RTHX_CSR_CAP")
+            res.trace(dd, args)  # sized from the last nnz now: no second launch
+            assert res.info()["lookback_fallbacks"] == 0
+            again = res.csr()
+        finally:
+            res.close()
+        for x, y, z in zip(want[:3], got, again):
+            assert np.array_equal(x, y) and np.array_equal(x, z)
+    finally:
+        dd.close()
+
+
+def test_c2_direct_csr_working_set(hip):
+    """C2 (101 x 101, 1e8 rays): after the first launch the direct CSR is
+    sized from the measured nnz (~30.5 M entries: ~275 MB for cols and
+    counts) instead of rows x min(N, R) (800 MB)."""
+    torch = pytest.importorskip("torch")
+    flat = H.square_domain(101).flat()
+    N = flat.n_emitters
+    args = _args(hip, flat, 100_000_000 // N, seed=1, flags=hip.abi.RTHX_FLAG_DEVICE_ONLY)[0]
+    dd = hip.DeviceDomain(flat, 0)
+    res = hip.DeviceResult()
+    try:
+        res.trace(dd, args)  # first launch: guessed size (may re-trace once)
+        res.trace(dd, args)
+        free0 = torch.cuda.mem_get_info(0)[0]
+        res2 = hip.DeviceResult()
+        try:
+            res2.trace(dd, args)
+            res2.trace(dd, args)
+            used = free0 - torch.cuda.mem_get_info(0)[0]
+            nnz = res2.info()["nnz"]
+        finally:
+            res2.close()
+        assert nnz > 2e7
+        assert used < 0.5 * N * (100_000_000 // N) * 8, used  # well under the 800 MB worst case
+        assert used < 400e6, used
+    finally:
+        res.close()
+        dd.close()

@@ -314,26 +314,26 @@ def test_errors_do_not_crash(hip):
     dd.close()
 
 
-def test_large_n_recording_limit_reports_erange(hip):
-    """N above the packed LDS histogram (hash tallies): the recorder's
-    kernels are unsplit, so recording with more rays per emitter than one
-    table holds (12,288) is refused, not faulted; without recording the same
-    call traces."""
-    import ctypes as C
-
-    from rthx import abi
-
-    dom = H.square_domain(286)  # N = 1144 + 81796 > 76800
+def test_large_n_recording_with_split_rows_exact(hip):
+    """N above the packed LDS histogram (hash tallies) and more rays per
+    emitter than one hash table holds (12,288): recorded rows are split into
+    hash-tallied parts like any other (parallelRayTracing.jl:108,120-123,
+    135-138 records any emitter at any R); counts and recorded rays equal the
+    CPU restatement's."""
+    dom = H.square_domain(301)  # N = 1204 + 90601 = 91805
     flat = dom.flat()
-    dd = hip.DeviceDomain(flat, 0)
-    res = hip.DeviceResult()
-    a, _k = _args(hip, flat, 13_000, end=1, rec=[0])
-    assert hip.load().rthx_trace_exchange(dd.handle, C.byref(a), res.handle) == abi.RTHX_ERANGE
-    a, _k = _args(hip, flat, 13_000, end=1)
-    assert hip.load().rthx_trace_exchange(dd.handle, C.byref(a), res.handle) == abi.RTHX_OK
-    assert res.info()["rays_traced"] == 13_000
-    res.close()
-    dd.close()
+    ids = [0, 7, flat.n_emitters - 1]
+    args, _k = _args(hip, flat, 13_000, seed=23, end=8, rec=ids)
+    g = gpu_trace(hip, flat, args)
+    assert g[3]["rays_traced"] == 8 * 13_000
+    o = oracle.trace_exchange(flat, args, 16)
+    assert_same(g, o)
+    (go, ge, gg), (oo, oe, og) = g[4], o[4]
+    assert gg.size > 0 and set(np.unique(gg)) == {0, 7}  # (the last id is not in the traced range)
+    order = np.lexsort((np.arange(len(og)), og))
+    assert np.array_equal(gg, og[order])
+    assert np.allclose(go, oo[order], rtol=0, atol=1e-12)
+    assert np.allclose(ge, oe[order], rtol=0, atol=1e-9)
 
 
 # ---------------------------------------------------------------------------

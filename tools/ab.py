@@ -40,15 +40,22 @@ def main():
     ap.add_argument("--rounds", type=int, default=8)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--ndim", type=int, default=101)
+    ap.add_argument("--c5-bin", type=int, default=-1, help="time one band of the C5 greenhouse instead of C2")
     args = ap.parse_args()
     import bench
 
-    dom = bench.build_domain(args.ndim)
+    if args.c5_bin >= 0:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import helpers as H
+
+        dom = H.greenhouse_domain()
+    else:
+        dom = bench.build_domain(args.ndim)
     flat = dom.flat()
     N = flat.n_emitters
     R = args.rays // N
     nudge = 10_000 * np.finfo(np.float64).eps
-    targs, _k = _lib.make_args(0, R, nudge, 1, 0, N, 1, flags=abi.RTHX_FLAG_DEVICE_ONLY)
+    targs, _k = _lib.make_args(max(args.c5_bin, 0), R, nudge, 1, 0, N, 1, flags=abi.RTHX_FLAG_DEVICE_ONLY)
     runs = []
     for p in args.libs:
         lib = open_lib(p)

@@ -28,27 +28,39 @@ from rthx import _lib, abi  # noqa: E402
 
 
 def run(name, dom, rays, steps, bins=(0,)):
+    """Median kernel and call time per band; with several bands (C5) every
+    band's line and the whole configuration: all bands' rays over the sum of
+    the bands' median times (a mean or median band would hide the slow
+    bands)."""
     flat = dom.flat()
     N = flat.n_emitters
     R = rays // N
     dd = _lib.DeviceDomain(flat, 0)
     res = _lib.DeviceResult()
-    t_k, t_c = [], []
+    tot_k = tot_c = 0.0
     for b in bins:
         a, _k = _lib.make_args(b, R, H.NUDGE, 1, 0, N, 1, flags=abi.RTHX_FLAG_DEVICE_ONLY)
         for _ in range(3):
             res.trace(dd, a)
+        t_k, t_c = [], []
         for _ in range(steps):
             t = time.perf_counter()
             res.trace(dd, a)
             t_c.append(time.perf_counter() - t)
             t_k.append(res.info()["trace_ms"])
-    k = float(np.median(t_k))
-    c = float(np.median(t_c)) * 1e3
-    info = res.info()
-    print(f"{name:4s} N={N:6d} R={R:6d} bins={len(bins)} rays/call={N * R:.3e}  kernel {k:.3f} ms "
-          f"({N * R / k / 1e6:.1f} Grays/s)  call {c:.3f} ms ({N * R / c / 1e6:.1f} Grays/s)  "
-          f"nnz {info['nnz']}", flush=True)
+        k = float(np.median(t_k))
+        c = float(np.median(t_c)) * 1e3
+        tot_k += k
+        tot_c += c
+        info = res.info()
+        tag = f"{name} band {b}" if len(bins) > 1 else name
+        print(f"{tag:10s} N={N:6d} R={R:6d} rays={N * R:.3e}  kernel {k:.3f} ms ({N * R / k / 1e6:.1f} Grays/s)  "
+              f"call {c:.3f} ms ({N * R / c / 1e6:.1f} Grays/s)  nnz {info['nnz']}", flush=True)
+    if len(bins) > 1:
+        rays_all = len(bins) * N * R
+        print(f"{name} total: {len(bins)} bands, {rays_all:.3e} rays  kernels {tot_k:.1f} ms "
+              f"({rays_all / tot_k / 1e6:.2f} Grays/s)  calls {tot_c:.1f} ms ({rays_all / tot_c / 1e6:.2f} Grays/s)",
+              flush=True)
     res.close()
     dd.close()
 
