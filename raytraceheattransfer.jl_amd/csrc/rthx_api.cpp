@@ -809,9 +809,9 @@ int run_trace(rthx_domain* dom, const rthx_trace_args* a, const TracePlan& p, rt
   HIP_TRY(res->row_off.reserve((size_t)(n_rows + 1) * 8), "hipMalloc row_off");
   HIP_TRY(res->totals.reserve(4 * 8), "hipMalloc totals");
   // Staging slots only when the rows are staged.  The direct CSR writes
-  // cols / counts in place: sized from the previous launch's nnz (plus an
-  // eighth), or on a first launch from a guess (2048 entries per row); rows
-  // that would end past them write nothing and
+  // cols / counts in place: sized from the nnz of the previous launch of the
+  // same shape (N, rows, R) plus an eighth, or else from a guess (2048
+  // entries per row); rows that would end past them write nothing and
   // flag an overflow, and the host then traces the launch again with the
   // exact size, which the look-back's prefix sums give (trace_exchange_one).
   // Never more than the worst case n_rows x min(N, R).
@@ -819,9 +819,12 @@ int run_trace(rthx_domain* dom, const rthx_trace_args* a, const TracePlan& p, rt
     res->stage_cols.release();
     res->stage_cnt.release();
     const int64_t worst = n_rows * p.row_cap;
-    int64_t want = res->lb_nnz_hint > 0 ? res->lb_nnz_hint + res->lb_nnz_hint / 8 + 65536
-                                        : std::max<int64_t>(1 << 20, n_rows * std::min<int64_t>(p.row_cap, 2048));
-    want = std::min<int64_t>(worst, (int64_t)env_int("RTHX_CSR_CAP", want, 1, worst));
+    const bool same = res->lb_hint_shape[0] == N && res->lb_hint_shape[1] == n_rows && res->lb_hint_shape[2] == R;
+    int64_t want = same && res->lb_nnz_hint > 0
+                       ? res->lb_nnz_hint + res->lb_nnz_hint / 8 + 65536
+                       : env_int("RTHX_CSR_CAP", std::max<int64_t>(1 << 20, n_rows * std::min<int64_t>(p.row_cap, 2048)),
+                                 1, worst);  // (tests force a small first guess)
+    want = std::min<int64_t>(worst, want);
     want = std::max<int64_t>(want, 1);
     for (rthx::DevBuf* b : {&res->cols, &res->cnt}) {
       if (b->cap > 2 * (size_t)want * 4 + (64u << 20)) b->release();  // (a much larger earlier trace)
@@ -1021,6 +1024,9 @@ int trace_exchange_one(rthx_domain* dom, const rthx_trace_args* a, rthx_result* 
     // again into buffers of that size.
     res->info.lookback_fallbacks += 1;
     res->lb_nnz_hint = totals[0];
+    res->lb_hint_shape[0] = p.N;
+    res->lb_hint_shape[1] = n_rows;
+    res->lb_hint_shape[2] = R;
     float ms2 = 0.f, mp2 = 0.f;
     rc = run_trace(dom, a, p, res, true, rec, totals, &ms2, &mp2);
     if (rc) return rc;
@@ -1039,7 +1045,12 @@ int trace_exchange_one(rthx_domain* dom, const rthx_trace_args* a, rthx_result* 
     ms_trace += ms2;
     ms_pack += mp2;
   }
-  if (lookback) res->lb_nnz_hint = totals[0];
+  if (lookback) {
+    res->lb_nnz_hint = totals[0];
+    res->lb_hint_shape[0] = p.N;
+    res->lb_hint_shape[1] = n_rows;
+    res->lb_hint_shape[2] = R;
+  }
   res->info.nnz = totals[0];
   res->info.lost_total = totals[1];
   res->info.lost_max_row = totals[2];

@@ -57,7 +57,8 @@ struct rthx_result {
   rthx::DevBuf lb_status;  // direct-CSR look-back words (unsplit launches)
   rthx::DevBuf lb_totals;  // look-back launches' totals, two sets of 4 (launch e uses set e & 1)
   uint32_t lb_epoch = 0;   // epoch of the last look-back launch; 0 = words and totals not yet zeroed
-  int64_t lb_nnz_hint = 0; // nnz of the last look-back launch (sizes the next direct CSR)
+  int64_t lb_nnz_hint = 0; // nnz of the last look-back launch (sizes the next one of the same shape)
+  int64_t lb_hint_shape[3] = {0, 0, 0};  // its (N, rows, R)
   rthx::HostBuf h_totals;  // pinned copy of a look-back launch's totals
   rthx::DevBuf fvals;      // F_raw values (rthx_result_copy_F)
   bool valid = false;

@@ -34,7 +34,7 @@ namespace rthx {
 #define RTHX_TRACE_WAVES_PER_EU 5
 #endif
 #ifndef RTHX_LAT_WAVES_PER_EU
-#define RTHX_LAT_WAVES_PER_EU 6  // LAT kernels (lattice locate): no cell records in registers
+#define RTHX_LAT_WAVES_PER_EU 8  // LAT kernels (lattice locate): 64 VGPRs, the ray loop spill-free (6: 80 VGPRs, 3 % slower)
 #endif
 #ifndef RTHX_MULTI_WAVES_PER_EU
 #define RTHX_MULTI_WAVES_PER_EU 4  // multi-polygon kernels (walk state + batched ends)
@@ -42,13 +42,15 @@ namespace rthx {
 #define RTHX_ML_VIEW mlat_lds_view(lds_opaque(cl_base), D.ml)
 #define RTHX_ML_G D.ml
 #ifndef RTHX_REFILL_Q
-#define RTHX_REFILL_Q 8  // MLAT kernels: idle lanes before a refill from the ray queue / end batch
+#define RTHX_REFILL_Q 24  // MLAT kernels: idle lanes before the ends are resolved and the queue refills (C5 band 0 / 7 at 1e9 rays: 8 69.7 / 43.3 ms, 16 59.2 / 36.6, 24 57.0 / 34.3, 32 59.5 / 35.5, 40 61.9 / 34.6)
 #endif
 #ifndef RTHX_REFILL
 #define RTHX_REFILL 32  // refill / end batch of the multi-polygon kernels (lanes; C5: 16 24 32 40 -> 32)
 #endif
-#define RTHX_TRACE_WAVES \
-  __attribute__((amdgpu_waves_per_eu(SINGLE ? (CL ? RTHX_LAT_WAVES_PER_EU : RTHX_TRACE_WAVES_PER_EU) : RTHX_MULTI_WAVES_PER_EU)))
+// (faithful sampling's acos / sin / cos need more registers: the general budget)
+#define RTHX_TRACE_WAVES                                                                                   \
+  __attribute__((amdgpu_waves_per_eu(SINGLE ? (CL && !FAITHFUL ? RTHX_LAT_WAVES_PER_EU : RTHX_TRACE_WAVES_PER_EU) \
+                                            : RTHX_MULTI_WAVES_PER_EU)))
 
 // Decoupled look-back (Merrill & Garland 2016) over the rows of one launch:
 // row `slot` publishes its nnz as an aggregate (flag 1), walks back over its
