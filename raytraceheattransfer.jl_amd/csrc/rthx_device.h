@@ -16,12 +16,6 @@
 #define RTHX_GLOBAL
 #endif
 
-// Diagnostic builds only (tools/ablate.sh): RTHX_ABLATE replaces parts of the
-// ray with cheap stand-ins to price them.  Results are wrong in such builds;
-// the product build has RTHX_ABLATE == 0.
-#ifndef RTHX_ABLATE
-#define RTHX_ABLATE 0
-#endif
 // 1: keep the Philox key schedule out of loop-invariant SGPRs (A/B knob)
 #ifndef RTHX_PHILOX_OPAQUE_KEY
 #define RTHX_PHILOX_OPAQUE_KEY 1
@@ -200,7 +194,7 @@ __device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32
   __asm__ volatile("" : "+s"(k0), "+s"(k1));
 #endif
 #pragma unroll
-  for (int i = 0; i < ((RTHX_ABLATE & 1) ? 1 : 10); ++i) {
+  for (int i = 0; i < 10; ++i) {
     // one 32x32->64 multiply per product (v_mad_u64_u32) instead of mul_lo + mul_hi
     uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
     uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
@@ -725,7 +719,7 @@ __device__ __forceinline__ void emit_volume(const Emitter& e, double eta, const 
   } else {
     ct = 1.0 - 2.0 * u4;                       // cos(acos(x)) = x
     st = 2.0 * sqrt_unit(__dmul_rn(u4, 1.0 - u4));  // sin(acos(x)) = sqrt((1-x)(1+x))
-    cphi = (RTHX_ABLATE & 4) ? (1.0 - 2.0 * u32(rw.a[3])) : cos_2pi_u32(rw.a[3], cos_tab);
+    cphi = cos_2pi_u32(rw.a[3], cos_tab);
   }
   dx = __dmul_rn(st, cphi);
   dy = ct;
@@ -1382,9 +1376,8 @@ __device__ __forceinline__ int end_ml(const DevDomain& D, const MLatLds& L, cons
 template <bool UNIFORM, bool FAITHFUL>
 __device__ __forceinline__ double free_path(const TraceParams& P, const double* tabs, double u) {
   if (UNIFORM)
-    return P.beta_uniform > 0 ? ((RTHX_ABLATE & 2) ? (1.0 - u)
-                                 : FAITHFUL        ? -log(u) / P.beta_uniform
-                                                   : neg_log_tab(u, tabs + kLogTableOffset) * P.inv_beta_uniform)
+    return P.beta_uniform > 0 ? (FAITHFUL ? -log(u) / P.beta_uniform
+                                          : neg_log_tab(u, tabs + kLogTableOffset) * P.inv_beta_uniform)
                               : __builtin_inf();
   return FAITHFUL ? -log(u) : neg_log_tab(u, tabs + kLogTableOffset);
 }

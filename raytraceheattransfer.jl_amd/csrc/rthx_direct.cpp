@@ -180,6 +180,10 @@ RTHX_EXPORT int rthx_trace_direct(rthx_domain* dom, const double* weights, const
   L.faithful = (a->flags & RTHX_FLAG_FAITHFUL_SAMPLING) != 0;
   L.single = dom->single_convex;
   L.axis = dom->axis_rect && !(getenv("RTHX_NO_AXIS") && getenv("RTHX_NO_AXIS")[0] == '1');
+  // the lattice in LDS behind the counters (the exchange kernels' LAT locate)
+  L.lat = L.single && L.axis && dom->D.lat.bytes > 0 && !(getenv("RTHX_NO_LAT") && getenv("RTHX_NO_LAT")[0] == '1') &&
+          (3 * n * 4 > rthx::kHistBytes || 3 * n * 4 + 16 + dom->D.lat.bytes <= rthx::kHistBytes);
+  L.lat_bytes = L.lat ? dom->D.lat.bytes : 0;
   rthx::DirectParams& Q = L.Q;
   Q.P.eta = a->nudge;
   Q.P.key0 = (uint32_t)a->seed;

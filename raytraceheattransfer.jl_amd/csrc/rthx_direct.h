@@ -60,6 +60,9 @@ struct DirectLaunch {
   DirectParams Q;
   hipStream_t stream;
   bool uniform, faithful, single, axis;
+  bool lat;                       // single axis-aligned rectangle meshed as a lattice: its LatticeLayout
+                                  // staged in LDS behind the counters (segment_lat, as the exchange kernels)
+  int32_t lat_bytes;              // (its blob, D.lat.bytes)
   int threads, blocks;            // from direct_shape
 };
 

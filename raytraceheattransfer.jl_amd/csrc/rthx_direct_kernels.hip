@@ -57,7 +57,15 @@ __device__ __forceinline__ void philox_block(uint32_t w[4], uint32_t r0, uint32_
 #define RTHX_DIRECT_ATTR
 #endif
 
-template <bool UNIFORM, bool FAITHFUL, bool SINGLE, bool AXIS>
+// LDS bytes of the counters (copies of [3][n] u32) before the lattice blob.
+__host__ __device__ __forceinline__ size_t direct_lat_offset(int copies, int32_t n) {
+  return ((size_t)copies * 3 * (size_t)n * 4 + 15) & ~(size_t)15;
+}
+
+// LAT: the single coarse rectangle's lattice in LDS (LatticeLayout); legs
+// run segment_lat -- the exchange kernels' lattice locate, the same answers
+// as segment<UNIFORM, SINGLE, AXIS> on the cell records.
+template <bool UNIFORM, bool FAITHFUL, bool SINGLE, bool AXIS, bool LAT = false>
 __global__ __launch_bounds__(FAITHFUL ? kDirectThreads : kDirectMaxThreads) RTHX_DIRECT_ATTR void trace_direct_kernel(const DevDomain* __restrict__ Dp,
                                                                       DirectParams Q) {
   // Q.hist: Q.hist copies of the [3][n_elem] counters; wave v adds into copy
@@ -75,6 +83,11 @@ __global__ __launch_bounds__(FAITHFUL ? kDirectThreads : kDirectMaxThreads) RTHX
   const bool replay = Q.replay != nullptr;
   if (use_hist)
     for (int i = tid; i < copies * 3 * n; i += nthr) hist[i] = 0u;
+  char RTHX_LDS* lat_base = (char RTHX_LDS*)hist + direct_lat_offset(use_hist ? copies : 0, n);
+  if (LAT) {
+    uint4* dst = (uint4*)lat_base;  // generic view; stores stay ds_write
+    for (int i = tid; i < D.lat.bytes / 16; i += nthr) dst[i] = D.lat_blob[i];
+  }
   if (!FAITHFUL)
     for (int i = tid; i < kTableDoubles; i += nthr) s_tab[i] = D.tables[i];
   if (SINGLE && tid == 0) {
@@ -179,7 +192,13 @@ __global__ __launch_bounds__(FAITHFUL ? kDirectThreads : kDirectMaxThreads) RTHX
     if (live) {
       // traceRay (traceRay.jl:20-147) one coarse segment at a time, 10,000 per call
       int a;
-      if (SINGLE) {
+      if (LAT) {
+        const SingleCoarse RTHX_LDS* sc = lds_opaque(&s_single);
+        a = seg < 10000 ? segment_lat<UNIFORM>(D, Q.P, *(const SingleCoarse*)sc,
+                                               lattice_lds_view(lds_opaque(lat_base), D.lat), D.lat, px, py, dx, dy,
+                                               S, acc)
+                        : -1;
+      } else if (SINGLE) {
         const SingleCoarse RTHX_LDS* sc = lds_opaque(&s_single);
         a = seg < 10000 ? segment<UNIFORM, SINGLE, AXIS>(D, Q.P, *(const SingleCoarse*)sc, c, px, py, dx, dy, S, acc)
                         : -1;
@@ -313,9 +332,10 @@ static int counter_copies(int t, int32_t n_elem) {
   return (int)(fit < 1 ? 1 : (fit < waves ? fit : waves));
 }
 
-template <bool UNIFORM, bool FAITHFUL, bool SINGLE, bool AXIS>
+template <bool UNIFORM, bool FAITHFUL, bool SINGLE, bool AXIS, bool LAT = false>
 static hipError_t direct_shape_t(const DirectLaunch& L, int* threads, int* blocks, int* copies) {
-  auto kern = trace_direct_kernel<UNIFORM, FAITHFUL, SINGLE, AXIS>;
+  auto kern = trace_direct_kernel<UNIFORM, FAITHFUL, SINGLE, AXIS, LAT>;
+  const size_t lat_bytes = LAT ? (size_t)L.lat_bytes : 0;
   int dev = 0, cus = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
@@ -326,7 +346,7 @@ static hipError_t direct_shape_t(const DirectLaunch& L, int* threads, int* block
   int best_t = kDirectThreads, best_b = 0, best_w = 0, best_c = 1;
   for (int t = kDirectThreads; t <= (FAITHFUL ? kDirectThreads : kDirectMaxThreads); t *= 2) {
     const int c = L.Q.hist ? counter_copies(t, L.Q.n_elem) : 0;
-    const size_t lds = (size_t)c * 3 * L.Q.n_elem * 4;
+    const size_t lds = direct_lat_offset(c, L.Q.n_elem) + lat_bytes;
     if (lds > 64 * 1024) {
       e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       if (e != hipSuccess) return e;
@@ -347,10 +367,10 @@ static hipError_t direct_shape_t(const DirectLaunch& L, int* threads, int* block
   return hipSuccess;
 }
 
-template <bool UNIFORM, bool FAITHFUL, bool SINGLE, bool AXIS>
+template <bool UNIFORM, bool FAITHFUL, bool SINGLE, bool AXIS, bool LAT = false>
 static hipError_t launch_direct_t(const DirectLaunch& L) {
-  auto kern = trace_direct_kernel<UNIFORM, FAITHFUL, SINGLE, AXIS>;
-  const size_t lds = (size_t)L.Q.hist * 3 * L.Q.n_elem * 4;
+  auto kern = trace_direct_kernel<UNIFORM, FAITHFUL, SINGLE, AXIS, LAT>;
+  const size_t lds = direct_lat_offset(L.Q.hist, L.Q.n_elem) + (LAT ? (size_t)L.lat_bytes : 0);
   if (lds > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
@@ -362,6 +382,9 @@ static hipError_t launch_direct_t(const DirectLaunch& L) {
 template <bool SHAPE, bool UNIFORM, bool FAITHFUL>
 static hipError_t dispatch_u(const DirectLaunch& L, int* t, int* b, int* c) {
   if (L.single) {
+    if (L.axis && L.lat)
+      return SHAPE ? direct_shape_t<UNIFORM, FAITHFUL, true, true, true>(L, t, b, c)
+                   : launch_direct_t<UNIFORM, FAITHFUL, true, true, true>(L);
     if (L.axis)
       return SHAPE ? direct_shape_t<UNIFORM, FAITHFUL, true, true>(L, t, b, c)
                    : launch_direct_t<UNIFORM, FAITHFUL, true, true>(L);
