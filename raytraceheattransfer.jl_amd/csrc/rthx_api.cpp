@@ -178,6 +178,17 @@ extern "C" __attribute__((visibility("default"))) int rthx_debug_neg_log(const d
   return 0;
 }
 
+// The same log taken from a 32-bit draw w (neg_log_u32, the trace kernels'
+// free path): tests check it equals neg_log_tab(w 2^-32) bit for bit.
+extern "C" __attribute__((visibility("default"))) int rthx_debug_neg_log_u32(const uint32_t* w, int64_t n,
+                                                                             double* out) {
+  if ((!w || !out) && n > 0) return -1;
+  std::vector<double> t(rthx::kTableDoubles);
+  rthx::fill_tables(t.data());
+  for (int64_t k = 0; k < n; ++k) out[k] = rthx::neg_log_u32(w[k], t.data() + rthx::kLogTableOffset);
+  return 0;
+}
+
 RTHX_EXPORT int rthx_abi_version(void) { return RTHX_ABI_VERSION; }
 
 RTHX_EXPORT const char* rthx_last_error(void) { return rthx::g_last_error.c_str(); }

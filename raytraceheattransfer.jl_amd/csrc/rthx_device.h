@@ -300,6 +300,49 @@ __host__ __device__ __forceinline__ double neg_log_tab(double u, const double* t
   return u > 0.0 ? v : __builtin_inf();
 }
 
+// neg_log_tab(u32(w)) without forming u: (double)w is exact and its bits are
+// u's plus 32 in the exponent field, so the table index and z are the same
+// and only k moves by 32 (an integer subtract instead of v_ldexp_f64).
+// Bit-identical to neg_log_tab(u32(w)) for every w (w = 0 -> +inf).
+__host__ __device__ __forceinline__ double neg_log_u32(uint32_t w, const double* tab) {
+  const uint64_t ix = dbits((double)w);
+  const uint64_t tmp = ix - kLogOff;
+  const int i = (int)((tmp >> 45) & (kLogTable - 1));
+  const int32_t k = ((int32_t)(uint32_t)(tmp >> 32) >> 20) - 32;
+  const double z = bitsd(ix - (tmp & 0xFFF0000000000000ull));
+  const double invc = tab[4 * i], t_hi = tab[4 * i + 1], t_lo = tab[4 * i + 2];
+  const double r = __builtin_fma(z, invc, -1.0);
+  double q = __builtin_fma(r, 1.0 / 7.0, -1.0 / 6.0);
+  q = __builtin_fma(r, q, 1.0 / 5.0);
+  q = __builtin_fma(r, q, -1.0 / 4.0);
+  q = __builtin_fma(r, q, 1.0 / 3.0);
+  q = __builtin_fma(r, q, -0.5);
+  const double l1p = __builtin_fma(r * r, q, r);
+  const double kd = (double)k;
+  const double hi = __builtin_fma(-kd, 6.93147180369123816490e-01, t_hi);
+  const double lo = __builtin_fma(-kd, 1.90821492927058770002e-10, t_lo) - l1p;
+  const double v = hi + lo;
+  return w != 0u ? v : __builtin_inf();
+}
+
+// n / d, correctly rounded, for d > 0 and operands far from the range ends
+// (n = 0 or 2^-900 < |n| < 2^900, 2^-900 < d < 2^900): the IEEE division
+// sequence the compiler emits (v_rcp_f64, two Newton steps, the quotient and
+// one correction) without v_div_scale / v_div_fmas / v_div_fixup, which only
+// rescale operands near overflow / underflow and patch special values, so the
+// result is bit-identical on this range (distances of in-domain points to
+// walls over direction components >= 1e-10, and free-path quotients).
+__device__ __forceinline__ double div_pos(double n, double d) {
+  double r = __builtin_amdgcn_rcp(d);
+  double e = __builtin_fma(-d, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  e = __builtin_fma(-d, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  const double q = n * r;
+  const double rem = __builtin_fma(-d, q, n);
+  return __builtin_fma(rem, r, q);
+}
+
 // sqrt(x) for x in {0} U [2^-60, 1]: the rsq + Newton sequence of the
 // correctly rounded IEEE sqrt without its subnormal/overflow rescaling
 // (the operands here are unit draws, far from either).
@@ -395,7 +438,7 @@ __device__ __forceinline__ double dist_to_box(double px, double py, double dx, d
   }
   widx = bi;
   if (bd == 0.0) return __builtin_inf();
-  double u = bn / bd;
+  double u = div_pos(bn, bd);  // (bd >= 1e-10)
   return u > 0.0 ? u : __builtin_inf();
 }
 
@@ -436,7 +479,7 @@ __device__ __forceinline__ double dist_in_box(double px, double py, double dx, d
   const BoxHit h = box_hit_in(px, py, dx, dy, xb, yb);
   widx = h.wall;
   if (!h.any) return __builtin_inf();
-  const double u = h.num / h.den;
+  const double u = div_pos(h.num, h.den);  // (num in [0, domain size], den >= 1e-10)
   return u > 0.0 ? u : __builtin_inf();
 }
 
@@ -561,6 +604,7 @@ struct Emitter {
   double mx, my;      // fine midpoint (nudge target)
   double tri_frac;    // area(ABC)/V (quad volume)
   double tx, ty;      // unit tangent of the emitting wall (surface)
+  double sx, sy;      // the uniform point's extents times 2^-32 (surface: p2 - p1; rectangle: x1 - x0, y1 - y0)
   int nv;
   int coarse;
   bool surface;
@@ -615,6 +659,11 @@ __device__ __forceinline__ Emitter load_emitter(const DevDomain& D, int64_t g) {
                     v[3] == v[1] && v[7] == v[5];
   e.rect = rect;
   e.need_sel = !surface && nv == 4 && !rect;
+  // (x1 - x0) u32(w) = (double)w ((x1 - x0) 2^-32) exactly: emission takes
+  // fma(w, s, x0), the same value as fma(u32(w), x1 - x0, x0) without the
+  // per-ray subtract and scaling
+  e.sx = (v[2] - v[0]) * 0x1.0p-32;
+  e.sy = (surface ? v[3] - v[1] : v[5] - v[1]) * 0x1.0p-32;
   return e;
 }
 
@@ -642,9 +691,10 @@ __device__ __forceinline__ void lambert_dir(double tx, double ty, double l1, dou
 template <bool FAITHFUL>
 __device__ __forceinline__ void emit_surface(const Emitter& e, double eta, const RayWords& rw, double& px,
                                              double& py, double& dx, double& dy) {
-  double R = u32(rw.a[0]);
-  px = e.v[0] + __dmul_rn(e.v[2] - e.v[0], R);
-  py = e.v[1] + __dmul_rn(e.v[3] - e.v[1], R);
+  // p1 + (p2 - p1) u32(a0), contracted (Emitter::sx)
+  const double w0 = (double)rw.a[0];
+  px = __builtin_fma(w0, e.sx, e.v[0]);
+  py = __builtin_fma(w0, e.sy, e.v[1]);
   px = px + __dmul_rn(e.mx - px, eta);
   py = py + __dmul_rn(e.my - py, eta);
   lambert_dir<FAITHFUL>(e.tx, e.ty, u32(rw.a[1]), u32(rw.a[2]), dx, dy);
@@ -692,8 +742,9 @@ __device__ __forceinline__ void emit_volume(const Emitter& e, double eta, const 
                                             double& px, double& py, double& dx, double& dy) {
   const double R1 = u32(rw.a[0]), R2 = u32(rw.a[1]);
   if (!FAITHFUL && (EK == kEmitVolRect || e.rect)) {
-    px = e.v[0] + __dmul_rn(e.v[2] - e.v[0], R1);
-    py = e.v[1] + __dmul_rn(e.v[5] - e.v[1], R2);
+    // x0 + (x1 - x0) R1, contracted (Emitter::sx)
+    px = __builtin_fma((double)rw.a[0], e.sx, e.v[0]);
+    py = __builtin_fma((double)rw.a[1], e.sy, e.v[1]);
   } else {
     double s1 = FAITHFUL ? sqrt(R1) : sqrt_unit(R1);
     double wa = 1.0 - s1, wb = __dmul_rn(s1, 1.0 - R2), wc = __dmul_rn(s1, R2);
@@ -709,16 +760,21 @@ __device__ __forceinline__ void emit_volume(const Emitter& e, double eta, const 
   }
   px = px + __dmul_rn(e.mx - px, eta);
   py = py + __dmul_rn(e.my - py, eta);
-  double u4 = u32(rw.a[2]);
   double st, ct, cphi;
   if (FAITHFUL) {
+    double u4 = u32(rw.a[2]);
     double theta = acos(1.0 - 2.0 * u4);
     st = sin(theta);
     ct = cos(theta);
     cphi = cos(RTHX_TWO_PI * u32(rw.a[3]));
   } else {
-    ct = 1.0 - 2.0 * u4;                       // cos(acos(x)) = x
-    st = 2.0 * sqrt_unit(__dmul_rn(u4, 1.0 - u4));  // sin(acos(x)) = sqrt((1-x)(1+x))
+    // u4 = u32(a2) without forming it: ct = 1 - 2 u4 = fma(w, -2^-31, 1) and
+    // u4 (1 - u4) = w ((1 - u4) 2^-32), the factor an exact power-of-two
+    // scaling of RN(1 - u4) -- the same values as from u4
+    const double w4 = (double)rw.a[2];
+    ct = __builtin_fma(w4, -0x1.0p-31, 1.0);           // cos(acos(x)) = x
+    const double om = __builtin_fma(w4, -0x1.0p-64, 0x1.0p-32);
+    st = 2.0 * sqrt_unit(w4 * om);                      // sin(acos(x)) = sqrt((1-x)(1+x))
     cphi = cos_2pi_u32(rw.a[3], cos_tab);
   }
   dx = __dmul_rn(st, cphi);
@@ -1382,6 +1438,15 @@ __device__ __forceinline__ double free_path(const TraceParams& P, const double* 
   return FAITHFUL ? -log(u) : neg_log_tab(u, tabs + kLogTableOffset);
 }
 
+// free_path(u32(w)), the table log taken from w directly (neg_log_u32).
+template <bool UNIFORM, bool FAITHFUL>
+__device__ __forceinline__ double free_path_u32(const TraceParams& P, const double* tabs, uint32_t w) {
+  if (FAITHFUL) return free_path<UNIFORM, true>(P, tabs, u32(w));
+  const double l = neg_log_u32(w, tabs + kLogTableOffset);
+  if (UNIFORM) return P.beta_uniform > 0 ? l * P.inv_beta_uniform : __builtin_inf();
+  return l;
+}
+
 // The words of ray (g, r) of emitter e (RayWords); pw: the free-path word
 // when the caller already holds the ray's word of block (r >> 2, g, 1, b)
 // (SINGLE kernels amortise that block over four consecutive rays).
@@ -1428,7 +1493,7 @@ __device__ __forceinline__ void start_ray_w(const TraceParams& P, const Emitter&
   // dynamically indexed scratch load)
   uint32_t w_surf = rw.a[3], w_vol = rw.pw;
   __asm__ volatile("" : "+v"(w_surf), "+v"(w_vol));
-  S = free_path<UNIFORM, FAITHFUL>(P, tabs, u32(surface ? w_surf : w_vol));
+  S = free_path_u32<UNIFORM, FAITHFUL>(P, tabs, surface ? w_surf : w_vol);
 }
 
 template <bool UNIFORM, bool FAITHFUL>

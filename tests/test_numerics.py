@@ -54,3 +54,20 @@ def test_neg_log_edges(neg_log):
     assert np.abs(got[small] - ref[small]).max() <= 1e-18
     assert neg_log(np.array([0.0]))[0] == np.inf
     assert neg_log(np.array([1.0]))[0] == 0.0
+
+
+def test_neg_log_from_u32_draw_is_bit_identical(neg_log):
+    """neg_log_u32(w), the trace kernels' free-path log taken from the draw
+    word itself, equals neg_log_tab(w 2^-32) bit for bit (w = 0 -> +inf)."""
+    lib = _lib.load()
+    f = lib.rthx_debug_neg_log_u32
+    f.argtypes = [C.POINTER(C.c_uint32), C.c_int64, C.POINTER(C.c_double)]
+    rng = np.random.default_rng(11)
+    edges = [0, 1, 2, 3, 0xFFFFFFFF, 0xFFFFFFFE, 0x80000000, 0x7FFFFFFF, 0xB0000000, 0xAFFFFFFF]
+    edges += [1 << k for k in range(32)] + [(1 << k) - 1 for k in range(1, 33)]
+    w = np.concatenate([np.array(edges, dtype=np.uint32), rng.integers(0, 2**32, size=1_000_000, dtype=np.uint64).astype(np.uint32)])
+    out = np.empty(w.size)
+    assert f(w.ctypes.data_as(C.POINTER(C.c_uint32)), w.size, out.ctypes.data_as(C.POINTER(C.c_double))) == 0
+    ref = neg_log(w.astype(np.float64) * 2.0**-32)
+    assert out[0] == np.inf and ref[0] == np.inf
+    assert np.array_equal(out.view(np.uint64), ref.view(np.uint64))
