@@ -880,8 +880,10 @@ __device__ __forceinline__ int lattice_index(const double RTHX_LDS* b, int n, do
   // negative guess clamps to 0 either way
   int i;
   __asm__("v_cvt_i32_f64 %0, %1" : "=v"(i) : "v"(__dmul_rn(x - b[0], inv)));
-  i = i < 0 ? 0 : (i > n - 1 ? n - 1 : i);
-  if (b[i] <= x && x < b[i + 1]) return i;
+  i = __builtin_elementwise_min(__builtin_elementwise_max(i, 0), n - 1);  // (v_med3_i32)
+  // both bounds in one paired read, tested without a branch
+  const double lo = b[i], hi = b[i + 1];
+  if ((lo <= x) & (x < hi)) return i;
   while (i > 0 && x < b[i]) --i;
   while (i < n - 1 && !(x < b[i + 1])) ++i;
   return (b[i] <= x && x < b[i + 1]) ? i : -1;
@@ -953,10 +955,13 @@ __device__ __forceinline__ int segment_lat(const DevDomain& D, const TraceParams
   // four-wall test of dist_to_rect would find it (w = 0 when none qualifies,
   // distToSurface2D's findmin)
   const int w = box_hit_in(px, py, dx, dy, dx < 0.0 ? L.xs[i] : L.xs[i + 1], dy < 0.0 ? L.ys[j] : L.ys[j + 1]).wall;
-  return w == 0 ? (j == 0 ? L.bot[i] : -1)
-       : w == 1 ? (i == G.nx - 1 ? L.right[j] : -1)
-       : w == 2 ? (j == G.ny - 1 ? L.top[i] : -1)
-                : (i == 0 ? L.left[j] : -1);
+  // w 0 / 1 / 2 / 3: bot[i] if j = 0, right[j] if i = nx - 1, top[i] if
+  // j = ny - 1, left[j] if i = 0, else an interior wall (-1); one read at a
+  // selected address instead of a branch per wall
+  const bool wy = (w & 1) == 0;  // bottom or top: indexed by i
+  const int32_t RTHX_LDS* arr = w == 0 ? L.bot : w == 1 ? L.right : w == 2 ? L.top : L.left;
+  const int edge = w == 0 ? j : w == 1 ? G.nx - 1 - i : w == 2 ? G.ny - 1 - j : i;
+  return edge == 0 ? arr[wy ? i : j] : -1;
 }
 
 // ---------------------------------------------------------------------------
