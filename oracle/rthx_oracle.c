@@ -869,9 +869,9 @@ ORACLE_API int oracle_trace_ray(const rthx_domain_desc* d, const rthx_trace_args
 /* (traceSingleRay.jl:1-83), restated per ray with the Philox blocks the    */
 /* HIP kernel draws (csrc/rthx_direct_kernels.hip header):                  */
 /*   blk 0: emitter (alias table); blk 1, 2: emission words (words_t);      */
-/*   blk 2i+2: interaction of iteration i (choice, direction);              */
-/*   blk 2i+1 (i >= 2): roulette + free path of iteration i;                */
-/*   blk 3: roulette of iteration 1 when roulette_after == 0.               */
+/*   blk 2i+2: interaction of iteration i (choice u32(w0), direction u32    */
+/*             (w1), u32(w2), free path of iteration i+1 u32(w3));          */
+/*   blk 2i+1: roulette of iteration i, drawn only past roulette_after.     */
 /* Path events are buffered per ray and committed only when the ray ends    */
 /* absorbed, as the reference does (traceSingleRay returns `nothing` for a  */
 /* lost ray and directRayTracing.jl:101 then skips its path).               */
@@ -1035,7 +1035,7 @@ static void direct_ray(dworker_t* W, uint64_t ray) {
     c = h.coarse;
     block_at(a->seed, r0, r1, 2u * (uint32_t)it + 2u, tag, w);
     int wall = e < ns;
-    int lt = u52(w[0], w[1]) < (wall ? W->eps[e] : W->omega[e - ns]);
+    int lt = u32(w[0]) < (wall ? W->eps[e] : W->omega[e - ns]);
     int redirect = wall ? !lt : lt;
     if (!redirect && !W->reemit[e]) {
       /* true absorption (:42-43 / :72-74): commit the path (:103-125) */
@@ -1076,18 +1076,21 @@ static void direct_ray(dworker_t* W, uint64_t ray) {
         p[0] = p[0] + (m[0] - p[0]) * a->nudge;
         p[1] = p[1] + (m[1] - p[1]) * a->nudge;
       }
-      lambert_dir(ex / len, ey / len, u32(w[2]), u32(w[3]), faithful, dir);
+      lambert_dir(ex / len, ey / len, u32(w[1]), u32(w[2]), faithful, dir);
     } else {
       /* isotropicScatter2D from the interaction point (:60-61, :68-69) */
       p[0] = h.end[0];
       p[1] = h.end[1];
-      iso_dir(u32(w[2]), u32(w[3]), faithful, dir);
+      iso_dir(u32(w[1]), u32(w[2]), faithful, dir);
     }
     if (it >= a->max_iters) { W->capped++; break; } /* while iteration_count < max_iters (:7) */
     ++it;
-    block_at(a->seed, r0, r1, 2u * (uint32_t)it + 1u, tag, w);
-    if (it > a->roulette_after && u52(w[0], w[1]) > a->roulette_kill) { W->rouletted++; break; } /* :12-14 */
-    u_path = u52(w[2], w[3]);
+    if (it > a->roulette_after) { /* :12-14 */
+      uint32_t v[4];
+      block_at(a->seed, r0, r1, 2u * (uint32_t)it + 1u, tag, v);
+      if (u52(v[0], v[1]) > a->roulette_kill) { W->rouletted++; break; }
+    }
+    u_path = u32(w[3]);
   }
   if (np > 0) W->replayed++; /* lost with path events: the library rolls them back */
 }

@@ -674,30 +674,51 @@ __device__ __forceinline__ Emitter load_emitter(const DevDomain& D, int64_t g) {
 // lambertSample2D.jl:1-10 rotated by emitSurfaceRay2D.jl:17-24: cosine-law
 // direction from the Float32-rounded draws l1, l2, in the frame (tangent t,
 // left normal (-t_y, t_x)) of the wall, un-normalised.
+// The draws are the words w1, w2: l = u32(w), rounded to Float32.
+// cos(2 pi r2) of the Float32 draw r2 = RN24(w2) 2^-32 is the table cosine
+// of the word RN24(w2) (cos_2pi_u32; RN24(w2) = 2^32, i.e. r2 = 1, wraps to
+// the word 0: cos(2 pi) = cos(0)); the faithful path calls libm.
+__device__ __forceinline__ uint32_t f32_draw_word(uint32_t w) {
+  const float x = (float)w;  // RN24(w): Float32(u32(w)) 2^32, exactly
+  return x >= 4294967296.0f ? 0u : (uint32_t)x;
+}
+
 template <bool FAITHFUL>
-__device__ __forceinline__ void lambert_dir(double tx, double ty, double l1, double l2, double& dx, double& dy) {
-  float r1 = (float)l1;
-  float ct = (float)sqrt((double)r1);  // correctly rounded Float32 sqrt
-  float ct2 = __fmul_rn(ct, ct);
-  double st = sqrt(1.0 - (double)ct2);
-  float r2 = (float)l2;
-  double cpsi = FAITHFUL ? cos(RTHX_TWO_PI * (double)r2) : cospi(2.0 * (double)r2);
+__device__ __forceinline__ void lambert_dir(double tx, double ty, uint32_t w1, uint32_t w2, const double* cos_tab,
+                                            double& dx, double& dy) {
+  float r1 = (float)u32(w1);
+  double st, cpsi;
+  float ct;
+  if (FAITHFUL) {
+    ct = (float)sqrt((double)r1);  // correctly rounded Float32 sqrt
+    const float ct2 = __fmul_rn(ct, ct);
+    st = sqrt(1.0 - (double)ct2);
+    cpsi = cos(RTHX_TWO_PI * (double)(float)u32(w2));
+  } else {
+    // (sqrt_unit is the correctly rounded sqrt on {0} U [2^-60, 1]: r1 is 0
+    // or >= 2^-32, 1 - ct^2 is 0 or >= 2^-24)
+    ct = (float)sqrt_unit((double)r1);
+    const float ct2 = __fmul_rn(ct, ct);
+    st = sqrt_unit(1.0 - (double)ct2);
+    cpsi = cos_2pi_u32(f32_draw_word(w2), cos_tab);
+  }
   double xl = __dmul_rn(st, cpsi);
   double zl = (double)ct;
   dx = __dmul_rn(tx, xl) + __dmul_rn(-ty, zl);
   dy = __dmul_rn(ty, xl) + __dmul_rn(tx, zl);
 }
 
+
 template <bool FAITHFUL>
-__device__ __forceinline__ void emit_surface(const Emitter& e, double eta, const RayWords& rw, double& px,
-                                             double& py, double& dx, double& dy) {
+__device__ __forceinline__ void emit_surface(const Emitter& e, double eta, const RayWords& rw, const double* cos_tab,
+                                             double& px, double& py, double& dx, double& dy) {
   // p1 + (p2 - p1) u32(a0), contracted (Emitter::sx)
   const double w0 = (double)rw.a[0];
   px = __builtin_fma(w0, e.sx, e.v[0]);
   py = __builtin_fma(w0, e.sy, e.v[1]);
   px = px + __dmul_rn(e.mx - px, eta);
   py = py + __dmul_rn(e.my - py, eta);
-  lambert_dir<FAITHFUL>(e.tx, e.ty, u32(rw.a[1]), u32(rw.a[2]), dx, dy);
+  lambert_dir<FAITHFUL>(e.tx, e.ty, rw.a[1], rw.a[2], cos_tab, dx, dy);
 }
 
 // isotropicScatter2D.jl:1-4: theta = acos(2u - 1), phi = 2 pi v, direction
@@ -720,6 +741,39 @@ __device__ __forceinline__ void iso_dir(uint32_t w_th, uint32_t w_ph, const doub
   }
   dx = __dmul_rn(st, cphi);
   dy = ct;
+}
+
+// A redirected ray of the direct method (traceSingleRay.jl:36-62): a wall
+// reflects or re-emits it with a Lambert direction in the wall's frame
+// (lambert_dir), the gas scatters it isotropically (iso_dir, frame (1, 0)).
+// The non-faithful form shares one code path between the two, so a wave
+// with walls and gas among its lanes does not run both samplers:
+//   ct  = Float32 sqrt(Float32 u1)            (wall)   2 u1 - 1           (gas)
+//   st  = sqrt(1 - ct^2)                                sqrt(4 u1 (1 - u1)) = 2 sqrt(u1 (1 - u1))
+//   phi word  RN24(w2)                                  w2
+// then (st cos phi, ct) rotated into (t, left normal); the gas frame t =
+// (1, 0) rotates exactly (products with 1 and 0).  Each lane's direction is
+// the one lambert_dir / iso_dir give it.
+template <bool FAITHFUL>
+__device__ __forceinline__ void redirect_dir(bool wall, double tx, double ty, uint32_t w1, uint32_t w2,
+                                             const double* cos_tab, double& dx, double& dy) {
+  if (FAITHFUL) {
+    if (wall)
+      lambert_dir<true>(tx, ty, w1, w2, cos_tab, dx, dy);
+    else
+      iso_dir<true>(w1, w2, cos_tab, dx, dy);
+    return;
+  }
+  const double u = u32(w1);
+  const float ct_w = (float)sqrt_unit((double)(float)u);
+  const double ct = wall ? (double)ct_w : 2.0 * u - 1.0;
+  const double arg = wall ? 1.0 - (double)__fmul_rn(ct_w, ct_w) : 4.0 * __dmul_rn(u, 1.0 - u);
+  const double st = sqrt_unit(arg);
+  const double cpsi = cos_2pi_u32(wall ? f32_draw_word(w2) : w2, cos_tab);
+  const double fx = wall ? tx : 1.0, fy = wall ? ty : 0.0;
+  const double xl = __dmul_rn(st, cpsi);
+  dx = __dmul_rn(fx, xl) + __dmul_rn(-fy, ct);
+  dy = __dmul_rn(fy, xl) + __dmul_rn(fx, ct);
 }
 
 // EK: the emitter's kind when the caller knows it for the whole workgroup
@@ -1491,7 +1545,7 @@ __device__ __forceinline__ void start_ray_w(const TraceParams& P, const Emitter&
                                             double& S) {
   const bool surface = emitter_surface<EK>(e);
   if (surface)
-    emit_surface<FAITHFUL>(e, P.eta, rw, px, py, dx, dy);
+    emit_surface<FAITHFUL>(e, P.eta, rw, tabs, px, py, dx, dy);
   else
     emit_volume<FAITHFUL, EK>(e, P.eta, rw, tabs, px, py, dx, dy);
   // (opaque copies: a select between the two struct fields becomes a

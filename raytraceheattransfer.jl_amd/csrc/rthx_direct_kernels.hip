@@ -13,9 +13,10 @@
 // (r lo, r hi, blk, bin | kDirectTag):
 //   blk 0            emitter draw: column = mulhi(w0, n), accept w1 < threshold (alias table)
 //   blk 1, 2         emission (RayWords: block 1 = a, words 0, 1 of block 2 = free path, triangle selection)
-//   blk 2i+2, i >= 1 interaction of iteration i: choice u52(w0,w1), direction draws w2, w3
-//   blk 2i+1, i >= 2 start of iteration i: roulette u52(w0,w1), free path u52(w2,w3)
-//   blk 3            roulette of iteration 1 (only when roulette_after == 0)
+//   blk 2i+2, i >= 1 interaction of iteration i: choice u32(w0), direction draws w1, w2,
+//                    free path of iteration i + 1 u32(w3)
+//   blk 2i+1, i >= 1 roulette of iteration i, u52(w0,w1) -- drawn only past roulette_after
+// One Philox block per leg (32-bit draws, as the exchange tracer's).
 // oracle/rthx_oracle.c (oracle_trace_direct) draws the same blocks.
 //
 // Bookkeeping (directRayTracing.jl:72-128): the emission count is added when
@@ -211,11 +212,13 @@ __global__ __launch_bounds__(FAITHFUL ? kDirectThreads : kDirectMaxThreads) RTHX
         if (a < 0) {
           fate = kStatEscaped;  // traceRay returned nothing (traceSingleRay.jl:20-22)
         } else {
+          // interaction of iteration it: choice u32(w0), direction draws w1,
+          // w2, and the next leg's free path u32(w3)
           uint32_t w[4];
           philox_block(w, r0, r1, 2u * (uint32_t)it + 2u, tag, k0, k1);
           const DirectElem E = Q.el[a];
           const bool wall = a < Ns;
-          const bool lt = u52(w[0], w[1]) < E.p;
+          const bool lt = u32(w[0]) < E.p;
           // wall: rand() < epsilon absorbs (:35), else reflects (:45-49);
           // gas: rand() < omega scatters (:58-62), else absorbs (:63-75)
           const bool redirect = wall ? !lt : lt;
@@ -232,25 +235,28 @@ __global__ __launch_bounds__(FAITHFUL ? kDirectThreads : kDirectMaxThreads) RTHX
             dirty = true;
             ++ev;
             const double* tab = (const double*)lds_opaque(&s_tab[0]);
-            if (wall) {
-              const SurfGeo sg = Q.sgeo[a];
-              if (!redirect) {  // re-emission point nudged toward the fine midpoint (traceSingleRay.jl:40)
-                px = px + __dmul_rn(sg.mx - px, eta);
-                py = py + __dmul_rn(sg.my - py, eta);
-              }
-              lambert_dir<FAITHFUL>(sg.tx, sg.ty, u32(w[2]), u32(w[3]), dx, dy);
-            } else {
-              iso_dir<FAITHFUL>(w[2], w[3], tab, dx, dy);
+            // the wall's frame (tangent, midpoint); the gas scatters in (1, 0)
+            SurfGeo sg{1.0, 0.0, 0.0, 0.0};
+            if (wall) sg = Q.sgeo[a];
+            if (wall && !redirect) {  // re-emission point nudged toward the fine midpoint (traceSingleRay.jl:40)
+              px = px + __dmul_rn(sg.mx - px, eta);
+              py = py + __dmul_rn(sg.my - py, eta);
             }
+            redirect_dir<FAITHFUL>(wall, sg.tx, sg.ty, w[1], w[2], tab, dx, dy);
             if (it >= Q.max_iters) {
               fate = kStatCapped;  // while iteration_count < max_iters (traceSingleRay.jl:7)
             } else {
               ++it;
-              philox_block(w, r0, r1, 2u * (uint32_t)it + 1u, tag, k0, k1);
-              if (it > Q.roulette_after && u52(w[0], w[1]) > Q.roulette_kill) {
-                fate = kStatRoulette;  // traceSingleRay.jl:12-14
+              bool killed = false;
+              if (it > Q.roulette_after) {  // traceSingleRay.jl:12-14 (block 2 it + 1, drawn only then)
+                uint32_t v[4];
+                philox_block(v, r0, r1, 2u * (uint32_t)it + 1u, tag, k0, k1);
+                killed = u52(v[0], v[1]) > Q.roulette_kill;
+              }
+              if (killed) {
+                fate = kStatRoulette;
               } else {
-                S = free_path<UNIFORM, FAITHFUL>(Q.P, tab, u52(w[2], w[3]));
+                S = free_path_u32<UNIFORM, FAITHFUL>(Q.P, tab, w[3]);
                 acc = 0.0;
                 seg = 0;
               }
