@@ -1012,10 +1012,17 @@ __device__ __forceinline__ int segment_lat(const DevDomain& D, const TraceParams
   // w 0 / 1 / 2 / 3: bot[i] if j = 0, right[j] if i = nx - 1, top[i] if
   // j = ny - 1, left[j] if i = 0, else an interior wall (-1); one read at a
   // selected address instead of a branch per wall
+  // (the array is picked by its byte offset in the blob: selecting among the
+  // four LDS pointers made the compiler index a scratch copy of them)
   const bool wy = (w & 1) == 0;  // bottom or top: indexed by i
-  const int32_t RTHX_LDS* arr = w == 0 ? L.bot : w == 1 ? L.right : w == 2 ? L.top : L.left;
+  // (the four offsets are uniform: read into scalars, then selected per lane,
+  // not a per-lane load from a selected address)
+  const int o_bot = __builtin_amdgcn_readfirstlane(G.off_bot), o_right = __builtin_amdgcn_readfirstlane(G.off_right);
+  const int o_top = __builtin_amdgcn_readfirstlane(G.off_top), o_left = __builtin_amdgcn_readfirstlane(G.off_left);
+  const int off = w == 0 ? o_bot : w == 1 ? o_right : w == 2 ? o_top : o_left;
   const int edge = w == 0 ? j : w == 1 ? G.nx - 1 - i : w == 2 ? G.ny - 1 - j : i;
-  return edge == 0 ? arr[wy ? i : j] : -1;
+  const char RTHX_LDS* base = (const char RTHX_LDS*)L.xs;  // (xs opens the blob)
+  return edge == 0 ? *(const int32_t RTHX_LDS*)(base + off + 4 * (wy ? i : j)) : -1;
 }
 
 // ---------------------------------------------------------------------------

@@ -2,7 +2,7 @@
 restatement (oracle_trace_direct).
 
 Both sides draw every ray from the same Philox blocks (emitter, emission,
-one pair of blocks per bounce), so the per-element counts -- emitted,
+one block per bounce), so the per-element counts -- emitted,
 absorbed, reflected/scattered -- are compared exactly, including the rays
 the GPU rolls back by replay (escaped, rouletted or capped after path events).
 Tolerance: exact equality.  The kernel evaluates log/cos/sqrt with its own
@@ -102,6 +102,17 @@ def test_variable_extinction_bins_exact(hip):
     for b in range(4):
         eps, om, re = DR.element_data(dom, b + 1)
         assert_same(dom, w, eps, om, re, DR.make_direct_args(b, 60_000, H.NUDGE, 7))
+
+
+def test_emission_batches_ended_by_roulette_exact(hip):
+    """roulette_after = 0 with a 95 % kill: whole refill batches of a wave can
+    die at emission, before any leg; the wave must emit again rather than
+    retire while rays are left (every ray is traced, counts as the oracle's)."""
+    dom = H.square_domain(15, kappa=1.0, sigma_s=3.0, epsilon=0.5)
+    w, eps, om, re = _inputs(dom)
+    args = DR.make_direct_args(0, 200_000, H.NUDGE, 13, roulette_after=0, roulette_kill=0.05)
+    _, info = assert_same(dom, w, eps, om, re, args)
+    assert info["rays_traced"] == 200_000 and info["rouletted"] > 0.9 * 200_000
 
 
 @pytest.mark.parametrize("nd", [51, 101, 121])
