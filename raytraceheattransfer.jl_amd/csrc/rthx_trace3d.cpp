@@ -40,7 +40,9 @@ struct rthx_scene3d {
   DevBuf polys, tris, nodes, tables, scene;
   rthx::DevScene3D S{};
   int64_t n_poly = 0;
-  int top_choice[4] = {-1, -1, -1, -1};  // LDS node-cache size per kernel variant (launch_trace3d)
+  int top_choice[8] = {-1, -1, -1, -1, -1, -1, -1, -1};  // LDS node-cache size per kernel variant (launch_trace3d)
+  int ghist_choice[4] = {-1, -1, -1, -1};  // per (faithful, pack16, N, R): global-histogram form chosen (1) or not (0)
+  int64_t ghist_key[4] = {-1, -1, -1, -1};
   ~rthx_scene3d() {
     (void)hipSetDevice(device);
     for (auto& e : ev)
@@ -556,6 +558,24 @@ RTHX_EXPORT int rthx_trace_exchange_3d(rthx_scene3d* sc, const rthx_trace_args* 
     L.faithful = (a->flags & RTHX_FLAG_FAITHFUL_SAMPLING) != 0;
     L.pack16 = pack16;
     L.top_choice = sc->top_choice;
+    // The global-histogram form when its LDS (the stacks alone) keeps more
+    // workgroups resident than the LDS histogram's (RTHX_T3_GHIST=0/1 forces).
+    const char* gh = getenv("RTHX_T3_GHIST");
+    if (gh && (gh[0] == '0' || gh[0] == '1')) {
+      L.ghist = gh[0] == '1';
+    } else {
+      const int slot_k = (L.faithful ? 2 : 0) + (pack16 ? 1 : 0);
+      const int64_t key = N * 2 + (pack16 ? 1 : 0);
+      if (sc->ghist_key[slot_k] != key) {
+        int wh = 0, wg = 0;
+        HIP_TRY(rthx::trace3d_occupancy(L, lds_bytes, rthx::trace3d_dynamic_lds(0, sc->S.stack), &wh, &wg),
+                "3D tracer occupancy");
+        sc->ghist_choice[slot_k] = wg > wh ? 1 : 0;
+        sc->ghist_key[slot_k] = key;
+      }
+      L.ghist = sc->ghist_choice[slot_k] == 1;
+    }
+    if (L.ghist) L.lds_bytes = rthx::trace3d_dynamic_lds(0, sc->S.stack);
     HIP_TRY(rthx::launch_trace3d(L), "trace_exchange_3d_kernel launch");
   }
   HIP_TRY(hipEventRecord(sc->ev[1], st), "hipEventRecord");

@@ -83,9 +83,11 @@ struct Trace3dLaunch {
   hipStream_t stream;
   bool faithful;
   bool pack16;  // < 65536 rays per workgroup: u16 row-histogram counters
-  int* top_choice;  // [faithful * 2 + pack16]: LDS node-cache size (64 / 128), -1 = not chosen yet
+  bool ghist;   // counts straight to the dense rows (no LDS histogram)
+  int* top_choice;  // [ghist * 4 + faithful * 2 + pack16]: LDS node-cache size (64 / 128), -1 = not chosen yet
 };
 
 hipError_t launch_trace3d(const Trace3dLaunch& L);
+hipError_t trace3d_occupancy(const Trace3dLaunch& L, size_t lds_hist, size_t lds_gh, int* wg_hist, int* wg_gh);
 
 }  // namespace rthx

@@ -231,10 +231,14 @@ __device__ __forceinline__ void emit_ray(const Emit3& E, const double* tab, uint
 // staged in static LDS; the walk reads nodes < TOP there.  A small cache
 // serves the nodes most lanes share (larger ones measured slower: lanes
 // reading different deep nodes conflict in LDS banks).
-template <bool FAITHFUL, bool PACK16, int TOP>
+// GH: the row's counts go straight to its dense row in global memory (one
+// returnless atomic per ray) instead of an LDS histogram flushed at the end:
+// the histogram's LDS then holds walk stacks of more resident workgroups
+// (large N, where LDS limits occupancy).
+template <bool FAITHFUL, bool PACK16, int TOP, bool GH = false>
 __global__ __launch_bounds__(kThreads) RTHX_T3_ATTR void trace_exchange_3d_kernel(const DevScene3D* __restrict__ Sp,
                                                                                   TraceParams P, TallyParams T) {
-  // dynamic LDS: [row histogram][walk stacks]
+  // dynamic LDS: [row histogram][walk stacks] (GH: the stacks only)
   extern __shared__ uint32_t hist[];
   __shared__ Bvh2Node s_top[TOP];
   Bvh2Node RTHX_LDS* top = (Bvh2Node RTHX_LDS*)&s_top[0];
@@ -254,8 +258,9 @@ __global__ __launch_bounds__(kThreads) RTHX_T3_ATTR void trace_exchange_3d_kerne
   const int64_t g = P.g_begin + slot * P.g_stride;
   const int64_t N = T.n_emitters;
   // PACK16 (fewer than 65536 rays per workgroup): two u16 counters per word
-  const int64_t words = PACK16 ? (N + 1) / 2 : N;
+  const int64_t words = GH ? 0 : PACK16 ? (N + 1) / 2 : N;
   for (int64_t i = tid; i < words; i += kThreads) hist[i] = 0u;
+  uint32_t* dense = T.dense + slot * N;
   if (!FAITHFUL)
     for (int i = tid; i < 2 * kCosTable; i += kThreads) s_tab[i] = S.tables[i];
   // breadth-first top of the BVH (rthx_trace3d.cpp layout_nodes)
@@ -279,7 +284,9 @@ __global__ __launch_bounds__(kThreads) RTHX_T3_ATTR void trace_exchange_3d_kerne
   int RTHX_LDS* stk = (int RTHX_LDS*)(hist + trace3d_stack_offset(words)) + tid;
   auto tally = [&](int a) {
     if (a >= 0) {
-      if (PACK16)
+      if (GH)
+        __hip_atomic_fetch_add(&dense[a], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else if (PACK16)
         atomicAdd(&hist[a >> 1], 1u << ((a & 1) * 16));
       else
         atomicAdd(&hist[a], 1u);
@@ -329,11 +336,11 @@ __global__ __launch_bounds__(kThreads) RTHX_T3_ATTR void trace_exchange_3d_kerne
   for (int off = 32; off > 0; off >>= 1) tallied += __shfl_xor(tallied, off);
   if (lane_id() == 0) atomicAdd(&s_tallied, tallied);
   __syncthreads();
-  uint32_t* dense = T.dense + slot * N;
-  for (int64_t i = tid; i < N; i += kThreads) {
-    const uint32_t v = PACK16 ? (hist[i >> 1] >> ((i & 1) * 16)) & 0xFFFFu : hist[i];
-    if (v) atomicAdd(&dense[i], v);
-  }
+  if (!GH)
+    for (int64_t i = tid; i < N; i += kThreads) {
+      const uint32_t v = PACK16 ? (hist[i >> 1] >> ((i & 1) * 16)) & 0xFFFFu : hist[i];
+      if (v) atomicAdd(&dense[i], v);
+    }
   if (tid == 0) atomicAdd(&T.row_tallied[slot], s_tallied);
 }
 
@@ -341,24 +348,24 @@ __global__ __launch_bounds__(kThreads) RTHX_T3_ATTR void trace_exchange_3d_kerne
 
 namespace {
 
-template <bool FAITHFUL, bool PACK16>
+template <bool FAITHFUL, bool PACK16, bool GH>
 hipError_t launch_variant(const Trace3dLaunch& L) {
   // The 128-node cache when it costs no workgroup per CU against the 64-node
   // one (occupancy queries are slow host calls: the choice is kept per scene
   // and kernel variant in L.top_choice).
-  int& top = L.top_choice[(FAITHFUL ? 2 : 0) + (PACK16 ? 1 : 0)];
+  int& top = L.top_choice[(GH ? 4 : 0) + (FAITHFUL ? 2 : 0) + (PACK16 ? 1 : 0)];
   if (top < 0) {
     int pc64 = 0, pc128 = 0;
     hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &pc64, (const void*)t3::trace_exchange_3d_kernel<FAITHFUL, PACK16, 64>, t3::kThreads, L.lds_bytes);
+        &pc64, (const void*)t3::trace_exchange_3d_kernel<FAITHFUL, PACK16, 64, GH>, t3::kThreads, L.lds_bytes);
     if (e != hipSuccess) return e;
     e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &pc128, (const void*)t3::trace_exchange_3d_kernel<FAITHFUL, PACK16, 128>, t3::kThreads, L.lds_bytes);
+        &pc128, (const void*)t3::trace_exchange_3d_kernel<FAITHFUL, PACK16, 128, GH>, t3::kThreads, L.lds_bytes);
     if (e != hipSuccess) return e;
     top = pc128 > 0 && pc128 >= pc64 ? 128 : 64;
   }
-  auto kern = top == 128 ? t3::trace_exchange_3d_kernel<FAITHFUL, PACK16, 128>
-                         : t3::trace_exchange_3d_kernel<FAITHFUL, PACK16, 64>;
+  auto kern = top == 128 ? t3::trace_exchange_3d_kernel<FAITHFUL, PACK16, 128, GH>
+                         : t3::trace_exchange_3d_kernel<FAITHFUL, PACK16, 64, GH>;
   if (L.lds_bytes > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.lds_bytes);
     if (e != hipSuccess) return e;
@@ -371,8 +378,25 @@ hipError_t launch_variant(const Trace3dLaunch& L) {
 }  // namespace
 
 hipError_t launch_trace3d(const Trace3dLaunch& L) {
-  if (L.faithful) return L.pack16 ? launch_variant<true, true>(L) : launch_variant<true, false>(L);
-  return L.pack16 ? launch_variant<false, true>(L) : launch_variant<false, false>(L);
+  if (L.ghist) return L.faithful ? launch_variant<true, false, true>(L) : launch_variant<false, false, true>(L);
+  if (L.faithful) return L.pack16 ? launch_variant<true, true, false>(L) : launch_variant<true, false, false>(L);
+  return L.pack16 ? launch_variant<false, true, false>(L) : launch_variant<false, false, false>(L);
+}
+
+// Resident workgroups per CU of the LDS-histogram and the global-histogram
+// forms (the host keeps the global one when it fits more).
+hipError_t trace3d_occupancy(const Trace3dLaunch& L, size_t lds_hist, size_t lds_gh, int* wg_hist, int* wg_gh) {
+  const void* kh = L.faithful ? (L.pack16 ? (const void*)t3::trace_exchange_3d_kernel<true, true, 64, false>
+                                          : (const void*)t3::trace_exchange_3d_kernel<true, false, 64, false>)
+                              : (L.pack16 ? (const void*)t3::trace_exchange_3d_kernel<false, true, 64, false>
+                                          : (const void*)t3::trace_exchange_3d_kernel<false, false, 64, false>);
+  const void* kg = L.faithful ? (const void*)t3::trace_exchange_3d_kernel<true, false, 64, true>
+                              : (const void*)t3::trace_exchange_3d_kernel<false, false, 64, true>;
+  hipError_t e = hipSuccess;
+  if (lds_hist > 64 * 1024) e = hipFuncSetAttribute(kh, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_hist);
+  if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(wg_hist, kh, t3::kThreads, lds_hist);
+  if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(wg_gh, kg, t3::kThreads, lds_gh);
+  return e;
 }
 
 }  // namespace rthx

@@ -1,0 +1,14 @@
+#!/bin/bash
+# 3D tracer: its GPU tests on the in-tree build, then config 4 (L3, L4) per library.
+#   bash tools/gpu_t3_ab.sh TAG lib1.so lib2.so ...
+set -o pipefail
+TAG=$1; shift
+mkdir -p gpurun_out
+timeout -k 10 400 python -u -m pytest tests/test_gpu_trace3d.py -m gpu -x -q --timeout 200 --timeout-method thread -p no:cacheprovider \
+  > gpurun_out/pt_$TAG.log 2>&1 || { tail -40 gpurun_out/pt_$TAG.log; exit 1; }
+tail -n 1 gpurun_out/pt_$TAG.log
+for lib in "$@"; do
+  n=$(basename $(dirname $lib))
+  RTHX_LIB=$lib timeout -k 10 200 python tools/bench_trace3d.py --ndim 10 --level 3 --cpu-rows 0 2>&1 | grep config4 | sed "s|^|$n |" | tee -a gpurun_out/t3_$TAG.log || exit 1
+  RTHX_LIB=$lib timeout -k 10 200 python tools/bench_trace3d.py --ndim 20 --level 4 --cpu-rows 0 2>&1 | grep config4 | sed "s|^|$n |" | tee -a gpurun_out/t3_$TAG.log || exit 1
+done
