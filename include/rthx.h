@@ -245,7 +245,9 @@ int rthx_result_copy_csr_device(const rthx_result* res, int32_t part, int64_t* r
  * static emitter partition over threads (parallelRayTracing.jl:81-102).  The
  * domain is uploaded to every listed device; rthx_multi_trace_exchange splits
  * the selected rows into one block per device, traces the blocks
- * concurrently (one host thread and HIP stream per device) and fills one
+ * concurrently on distinct devices (one host thread per listed device, each
+ * on its device's one shared library stream; a device listed twice runs its
+ * blocks one after another) and fills one
  * rthx_result whose info / copy calls cover all rows, exactly as a
  * one-device trace of the same arguments would (every row is a pure
  * function of (seed, bin, emitter, ray), so the counts are bit-identical for

@@ -1372,8 +1372,9 @@ RTHX_EXPORT int rthx_multi_create(const rthx_domain_desc* desc, const int32_t* d
   if (!out) return fail(RTHX_EINVAL, "null out");
   *out = nullptr;
   if (!devices || n_devices < 1) return fail(RTHX_EINVAL, "empty device list");
-  // (a device may be listed more than once: its blocks then run on
-  // concurrent streams of that device)
+  // (a device may be listed more than once: its blocks then run one after
+  // another on that device's one shared stream, rthx::device_stream -- a
+  // correctness configuration for tests, not a way to overlap work)
   rthx_multi* m = new (std::nothrow) rthx_multi();
   if (!m) return fail(RTHX_ENOMEM, "host allocation failed");
   m->doms.assign(n_devices, nullptr);

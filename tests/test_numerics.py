@@ -71,3 +71,28 @@ def test_neg_log_from_u32_draw_is_bit_identical(neg_log):
     ref = neg_log(w.astype(np.float64) * 2.0**-32)
     assert out[0] == np.inf and ref[0] == np.inf
     assert np.array_equal(out.view(np.uint64), ref.view(np.uint64))
+
+
+def test_u32_free_paths_match_52_bit_free_paths(neg_log):
+    """The 32-bit draws' free paths (-ln u32(w), capped at
+    22.18) against 52-bit ones (the reference's Float64 rand()) and the
+    exact exponential: two-sample and one-sample Kolmogorov-Smirnov tests,
+    first two moments within 5 sigma, and the cap."""
+    stats = pytest.importorskip("scipy.stats")
+    lib = _lib.load()
+    f = lib.rthx_debug_neg_log_u32
+    f.argtypes = [C.POINTER(C.c_uint32), C.c_int64, C.POINTER(C.c_double)]
+    rng = np.random.default_rng(2024)
+    n = 1_000_000
+    w = rng.integers(0, 2**32, size=n, dtype=np.uint64).astype(np.uint32)
+    s32 = np.empty(n)
+    assert f(w.ctypes.data_as(C.POINTER(C.c_uint32)), n, s32.ctypes.data_as(C.POINTER(C.c_double))) == 0
+    s32 = s32[np.isfinite(s32)]  # (w = 0, probability 2^-32: an infinite path)
+    u52 = (rng.integers(1, 2**52, size=n, dtype=np.int64)).astype(np.float64) * 2.0**-52
+    s52 = neg_log(u52)
+    assert stats.ks_2samp(s32, s52).pvalue > 1e-3
+    assert stats.kstest(s32, "expon").pvalue > 1e-3
+    for s in (s32, s52):
+        assert abs(s.mean() - 1.0) < 5 / np.sqrt(n)
+        assert abs(s.var() - 1.0) < 5 * np.sqrt(8.0 / n)
+    assert s32.max() <= -np.log(2.0**-32) + 1e-12
