@@ -47,9 +47,15 @@ namespace rthx {
 #ifndef RTHX_REFILL
 #define RTHX_REFILL 32  // refill / end batch of the multi-polygon kernels (lanes; C5: 16 24 32 40 -> 32)
 #endif
-// (faithful sampling's acos / sin / cos need more registers: the general budget)
-#define RTHX_TRACE_WAVES                                                                                   \
-  __attribute__((amdgpu_waves_per_eu(SINGLE ? (CL && !FAITHFUL ? RTHX_LAT_WAVES_PER_EU : RTHX_TRACE_WAVES_PER_EU) \
+// (faithful sampling's acos / sin / cos need more registers, and so do the
+// hash-tally kernels: the general budget.  L301, N = 91,805: 20.5 Grays/s at
+// 8 waves, 23.4 at the general budget.  The split-row kernels spill a few
+// registers at 8 waves but still run faster there: the emulated 8-rank C2
+// shard 0.888 ms per step against 1.069; profiles/round3/ab/waves_spin_zero_ab.log)
+#define RTHX_TRACE_WAVES                                                                                    \
+  __attribute__((amdgpu_waves_per_eu(SINGLE ? (CL && !FAITHFUL && TALLY != kTallyHash                       \
+                                                   ? RTHX_LAT_WAVES_PER_EU                                  \
+                                                   : RTHX_TRACE_WAVES_PER_EU)                               \
                                             : RTHX_MULTI_WAVES_PER_EU)))
 
 // Decoupled look-back (Merrill & Garland 2016) over the rows of one launch:
