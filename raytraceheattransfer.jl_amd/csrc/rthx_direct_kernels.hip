@@ -189,12 +189,9 @@ __global__ __launch_bounds__(FAITHFUL ? kDirectThreads : kDirectMaxThreads) RTHX
         more = __ballot(!live && !got) == 0ull;
       }
     }
-    if (__ballot(live) == 0ull) {
-      // (no ray in flight: done once nothing is left to emit; else a batch
-      // that roulette ended at emission -- emit again)
-      if (!more) break;
-      continue;
-    }
+    // (no ray in flight: done once nothing is left to emit; else a batch
+    // that roulette ended at emission -- the next trip emits again)
+    if (!more && __ballot(live) == 0ull) break;
     if (live) {
       // traceRay (traceRay.jl:20-147) one coarse segment at a time, 10,000 per call
       int a;
