@@ -868,7 +868,8 @@ ORACLE_API int oracle_trace_ray(const rthx_domain_desc* d, const rthx_trace_args
 /* (DirectTracing2D/directRayTracing.jl:19-152) and traceSingleRay          */
 /* (traceSingleRay.jl:1-83), restated per ray with the Philox blocks the    */
 /* HIP kernel draws (csrc/rthx_direct_kernels.hip header):                  */
-/*   blk 0: emitter (alias table); blk 1, 2: emission words (words_t);      */
+/*   blk 1: emission words a; blk 2: free path w0, triangle selection w1,  */
+/*          the emitter by the alias table from w2 (column) and w3;        */
 /*   blk 2i+2: interaction of iteration i (choice u32(w0), direction u32    */
 /*             (w1), u32(w2), free path of iteration i+1 u32(w3));          */
 /*   blk 2i+1: roulette of iteration i, drawn only past roulette_after.     */
@@ -992,21 +993,17 @@ static void direct_ray(dworker_t* W, uint64_t ray) {
   const int faithful = (a->flags & RTHX_FLAG_FAITHFUL_SAMPLING) != 0;
   const uint32_t r0 = (uint32_t)ray, r1 = (uint32_t)(ray >> 32), tag = (uint32_t)a->bin | DIRECT_TAG;
   uint32_t w[4];
-  /* emitter = sample(local_rng, emitters, Weights(energy)) (:70) */
-  block_at(a->seed, r0, r1, 0u, tag, w);
-  uint32_t col = (uint32_t)(((uint64_t)w[0] * (uint64_t)n) >> 32);
-  uint64_t at = W->alias[col];
-  int64_t g = (w[1] < (uint32_t)at) ? (int64_t)col : (int64_t)(at >> 32);
   /* emission words: a = block 1, free path / triangle selection = words 0,
-   * 1 of block 2 (the device's RayWords) */
+   * 1 of block 2 (the device's RayWords); emitter = sample(local_rng,
+   * emitters, Weights(energy)) (:70) from words 2, 3 of block 2 */
   words_t rw;
+  block_at(a->seed, r0, r1, 2u, tag, w);
+  rw.pw = w[0];
+  rw.sw = w[1];
+  uint32_t col = (uint32_t)(((uint64_t)w[2] * (uint64_t)n) >> 32);
+  uint64_t at = W->alias[col];
+  int64_t g = (w[3] < (uint32_t)at) ? (int64_t)col : (int64_t)(at >> 32);
   block_words(a->seed, r0, r1, 1u, tag, rw.a);
-  {
-    uint32_t c2[4];
-    block_words(a->seed, r0, r1, 2u, tag, c2);
-    rw.pw = c2[0];
-    rw.sw = c2[1];
-  }
   double p[2], dir[2];
   int f;
   double u_path;

@@ -31,7 +31,7 @@ using rthx::now_ms;
 namespace rthx {
 
 struct DirectWork {
-  DevBuf alias, el, sgeo, counts, stats, next, lost, n_lost, partial;
+  DevBuf alias, el, sgeo, emit, counts, stats, next, lost, n_lost, partial;
   bool have_frames = false;
 };
 
@@ -165,6 +165,8 @@ RTHX_EXPORT int rthx_trace_direct(rthx_domain* dom, const double* weights, const
   if (!Wk.have_frames) {
     HIP_TRY(Wk.sgeo.reserve(std::max<int64_t>(ns, 1) * sizeof(rthx::SurfGeo)), "hipMalloc surface frames");
     HIP_TRY(rthx::launch_surface_frames(dom->d_dom, ns, Wk.sgeo.as<rthx::SurfGeo>(), st), "surface_frames launch");
+    HIP_TRY(Wk.emit.reserve(n * sizeof(rthx::Emitter)), "hipMalloc emitter records");
+    HIP_TRY(rthx::launch_emitter_table(dom->d_dom, n, Wk.emit.as<rthx::Emitter>(), st), "emitter_table launch");
     Wk.have_frames = true;
   }
   HIP_TRY(hipMemcpyAsync(Wk.alias.p, alias.data(), n * 8, hipMemcpyHostToDevice, st), "hipMemcpy alias");
@@ -195,6 +197,7 @@ RTHX_EXPORT int rthx_trace_direct(rthx_domain* dom, const double* weights, const
   Q.alias = Wk.alias.as<uint64_t>();
   Q.el = Wk.el.as<rthx::DirectElem>();
   Q.sgeo = Wk.sgeo.as<rthx::SurfGeo>();
+  Q.emitters = Wk.emit.as<rthx::Emitter>();
   Q.counts = Wk.counts.as<unsigned long long>();
   Q.lost = Wk.lost.as<uint32_t>();
   Q.n_lost = Wk.n_lost.as<uint32_t>();

@@ -42,6 +42,7 @@ struct DirectParams {
   const uint64_t* alias;          // [n_elem] (alias index << 32) | acceptance threshold
   const DirectElem* el;           // [n_elem]
   const SurfGeo* sgeo;            // [Ns]
+  const Emitter* emitters;        // [n_elem] emission records (load_emitter, built once per domain)
   unsigned long long* counts;     // [3][n_elem] emitted, absorbed, redirected
   uint32_t* lost;                 // first pass: items of lost rays that committed path events
   uint32_t* n_lost;
@@ -73,5 +74,6 @@ hipError_t launch_direct(const DirectLaunch& L);
 hipError_t launch_counter_reduce(const uint32_t* partial, int32_t n_blocks, int64_t len, bool is_signed,
                                  unsigned long long* counts, hipStream_t stream);
 hipError_t launch_surface_frames(const DevDomain* D, int32_t n_surfaces, SurfGeo* out, hipStream_t stream);
+hipError_t launch_emitter_table(const DevDomain* D, int64_t n, Emitter* out, hipStream_t stream);
 
 }  // namespace rthx

@@ -11,8 +11,9 @@
 //
 // Random numbers: ray r (64-bit) owns the Philox blocks with counter
 // (r lo, r hi, blk, bin | kDirectTag):
-//   blk 0            emitter draw: column = mulhi(w0, n), accept w1 < threshold (alias table)
-//   blk 1, 2         emission (RayWords: block 1 = a, words 0, 1 of block 2 = free path, triangle selection)
+//   blk 1            emission words a (RayWords)
+//   blk 2            free path (w0) and triangle selection (w1) of the emission; the emitter by the
+//                    alias table: column = mulhi(w2, n), accept w3 < threshold
 //   blk 2i+2, i >= 1 interaction of iteration i: choice u32(w0), direction draws w1, w2,
 //                    free path of iteration i + 1 u32(w3)
 //   blk 2i+1, i >= 1 roulette of iteration i, u52(w0,w1) -- drawn only past roulette_after
@@ -150,24 +151,21 @@ __global__ __launch_bounds__(FAITHFUL ? kDirectThreads : kDirectMaxThreads) RTHX
           const uint64_t ray = (uint64_t)Q.ray_begin + (replay ? (uint64_t)Q.replay[item] : (uint64_t)item);
           r0 = (uint32_t)ray;
           r1 = (uint32_t)(ray >> 32);
-          // emitter: sample(emitters, Weights(energy)) (directRayTracing.jl:70) by the alias method
-          uint32_t w[4];
-          philox_block(w, r0, r1, 0u, tag, k0, k1);
-          const uint32_t col = (uint32_t)(((uint64_t)w[0] * (uint64_t)(uint32_t)n) >> 32);
-          const uint64_t at = Q.alias[col];
-          const int g = (w[1] < (uint32_t)at) ? (int)col : (int)(at >> 32);
-          const double* tab = (const double*)lds_opaque(&s_tab[0]);
-          const Emitter e = load_emitter(D, g);
           // emission words (RayWords): a = block 1; free path and triangle
-          // selection of volume emitters = words 0 and 1 of block 2
+          // selection of volume emitters = words 0 and 1 of block 2; the
+          // emitter, sample(emitters, Weights(energy)) (directRayTracing.jl:70),
+          // by the alias method from words 2 and 3
+          uint32_t w[4];
           RayWords rw;
+          philox_block(w, r0, r1, 2u, tag, k0, k1);
+          rw.pw = w[0];
+          rw.sw = w[1];
+          const uint32_t col = (uint32_t)(((uint64_t)w[2] * (uint64_t)(uint32_t)n) >> 32);
+          const uint64_t at = Q.alias[col];
+          const int g = (w[3] < (uint32_t)at) ? (int)col : (int)(at >> 32);
+          const double* tab = (const double*)lds_opaque(&s_tab[0]);
+          const Emitter e = Q.emitters[g];  // (load_emitter's record, precomputed)
           philox_block(rw.a, r0, r1, 1u, tag, k0, k1);
-          {
-            uint32_t c2[4];
-            philox_block(c2, r0, r1, 2u, tag, k0, k1);
-            rw.pw = c2[0];
-            rw.sw = c2[1];
-          }
           start_ray_w<UNIFORM, FAITHFUL>(Q.P, e, tab, rw, px, py, dx, dy, S);
           acc = 0.0;
           c = e.coarse;
@@ -420,6 +418,22 @@ hipError_t launch_counter_reduce(const uint32_t* partial, int32_t n_blocks, int6
   const unsigned slices = (unsigned)(n_blocks < kReduceSlices ? n_blocks : kReduceSlices);
   hipLaunchKernelGGL(counter_reduce_kernel, dim3((unsigned)((len + 255) / 256), slices), dim3(256), 0, stream, partial,
                      n_blocks, len, is_signed ? 1 : 0, counts);
+  return hipGetLastError();
+}
+
+// The emission record of every emitter (load_emitter), once per domain: the
+// direct kernel's emission reads it instead of rebuilding it from the
+// polygon (a surface's tangent costs a square root and two divisions).
+__global__ __launch_bounds__(256) void emitter_table_kernel(const DevDomain* __restrict__ Dp, int64_t n,
+                                                            Emitter* __restrict__ out) {
+  const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (g >= n) return;
+  out[g] = load_emitter(*Dp, g);
+}
+
+hipError_t launch_emitter_table(const DevDomain* D, int64_t n, Emitter* out, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(emitter_table_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, D, n, out);
   return hipGetLastError();
 }
 

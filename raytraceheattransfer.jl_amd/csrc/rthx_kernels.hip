@@ -1068,8 +1068,13 @@ static hipError_t launch_trace_t(const LaunchCfg& L) {
         queried = false;
         break;
       }
-      if (per_cu * (t / 64) > best_waves) {
-        best_waves = per_cu * (t / 64);
+      // (on a tie 512 lanes win over 256: half the workgroups, so a launch
+      // of few long rows ends in fewer rounds -- C3, 2805 rows: 113.6 ->
+      // 118.2 Grays/s; 1024 lanes lose at C2, 9429 rays per row, 0.852 ->
+      // 0.942 ms; profiles/round3/ab/wgsize.log)
+      const int waves = per_cu * (t / 64);
+      if (waves > best_waves || (waves == best_waves && t <= 512)) {
+        best_waves = waves;
         threads = t;
       }
     }
