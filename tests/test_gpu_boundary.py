@@ -418,3 +418,45 @@ def test_c2_direct_csr_working_set(hip):
     finally:
         res.close()
         dd.close()
+
+
+def test_gather_and_broadcast_over_rccl(hip):
+    """The NCCL (= RCCL on ROCm) branches of rthx.distributed on a real GPU:
+    a one-rank NCCL group (a one-GPU box cannot hold two ranks on one
+    device) gathers a traced result from device memory
+    (rthx_result_copy_csr_device -> the tensors RCCL sends), to one rank and
+    to all, and broadcasts a CSR; every form equals the host CSR."""
+    torch = pytest.importorskip("torch")
+    import socket
+
+    import torch.distributed as dist
+    from rthx import distributed as RD
+
+    flat = H.square_domain(15).flat()
+    N = flat.n_emitters
+    args = _args(hip, flat, 2000, seed=9, begin=1, stride=2)[0]
+    dd = hip.DeviceDomain(flat, 0)
+    res = hip.DeviceResult()
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        assert dist.get_backend() == "nccl"
+        res.trace(dd, args)
+        rp, cols, cnt = res.csr()
+        for dst in (0, -1):
+            g_rp, g_c, g_v = RD.gather_result(res, N, dst=dst)
+            assert np.array_equal(g_rp, rp) and np.array_equal(g_c, cols) and np.array_equal(g_v, cnt)
+        t_rp, t_c, t_v = RD.gather_result(res, N, dst=0, as_tensors=True)
+        assert t_rp.device.type == "cuda" and t_c.device.type == "cuda"
+        assert np.array_equal(t_v.cpu().numpy().view(np.uint32), cnt)
+        h_rp, h_c, h_v = RD.gather_csr(rp, cols, cnt, N, dst=0)
+        assert np.array_equal(h_rp, rp) and np.array_equal(h_c, cols) and np.array_equal(h_v, cnt)
+        b_rp, b_c, b_v = RD.broadcast_csr(rp, cols, cnt, N, src=0)
+        assert np.array_equal(np.asarray(b_rp), rp) and np.array_equal(np.asarray(b_c), cols)
+        assert np.array_equal(np.asarray(b_v).view(np.uint32), cnt)
+    finally:
+        dist.destroy_process_group()
+        res.close()
