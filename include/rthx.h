@@ -247,7 +247,8 @@ int rthx_result_copy_csr_device(const rthx_result* res, int32_t part, int64_t* r
  * the selected rows into one block per device, traces the blocks
  * concurrently on distinct devices (one host thread per listed device, each
  * on its device's one shared library stream; a device listed twice runs its
- * blocks one after another) and fills one
+ * blocks one after another, and their per-part event timings may then
+ * include each other's kernels) and fills one
  * rthx_result whose info / copy calls cover all rows, exactly as a
  * one-device trace of the same arguments would (every row is a pure
  * function of (seed, bin, emitter, ray), so the counts are bit-identical for
