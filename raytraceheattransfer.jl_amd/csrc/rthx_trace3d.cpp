@@ -69,7 +69,7 @@ constexpr int kLeafTris = RTHX_T3_LEAF;  // triangles per BVH leaf (at most)
 #ifndef RTHX_T3_SAH_BINS
 #define RTHX_T3_SAH_BINS 16
 #endif
-constexpr int64_t kSplitTargetBlocks = 8192;
+constexpr int64_t kSplitTargetBlocks = 16384;  // workgroups per launch (RTHX_T3_SPLIT_TARGET; 4096 / 8192 / 32768: slower at config 4)
 constexpr int64_t kSplitMinRays = 1024;
 
 struct BuildTri {
@@ -486,8 +486,10 @@ RTHX_EXPORT int rthx_trace_exchange_3d(rthx_scene3d* sc, const rthx_trace_args* 
   const int64_t end = std::min<int64_t>(a->emitter_end, N);
   const int64_t n_rows = end > a->emitter_begin ? (end - a->emitter_begin + a->emitter_stride - 1) / a->emitter_stride : 0;
   int64_t split = 1;
+  int64_t split_target = kSplitTargetBlocks;
+  if (const char* e = getenv("RTHX_T3_SPLIT_TARGET")) split_target = std::max<int64_t>(1, std::atoll(e));
   if (n_rows > 0 && R >= 2 * kSplitMinRays)
-    split = std::max<int64_t>(1, std::min<int64_t>((kSplitTargetBlocks + n_rows - 1) / n_rows, R / kSplitMinRays));
+    split = std::max<int64_t>(1, std::min<int64_t>((split_target + n_rows - 1) / n_rows, R / kSplitMinRays));
   const bool pack16 = (R + split - 1) / split < 65536;
   const size_t lds_bytes = rthx::trace3d_dynamic_lds(pack16 ? (N + 1) / 2 : N, sc->S.stack);
   if (lds_bytes + rthx::kTrace3dStaticLds > rthx::kMaxLdsBytes)
@@ -570,7 +572,10 @@ RTHX_EXPORT int rthx_trace_exchange_3d(rthx_scene3d* sc, const rthx_trace_args* 
         int wh = 0, wg = 0;
         HIP_TRY(rthx::trace3d_occupancy(L, lds_bytes, rthx::trace3d_dynamic_lds(0, sc->S.stack), &wh, &wg),
                 "3D tracer occupancy");
-        sc->ghist_choice[slot_k] = wg > wh ? 1 : 0;
+        // (more than a quarter more workgroups: at config 4 L3 the GH form's
+        // 6 against the histogram's 5 measured 4 % slower -- a returnless
+        // global atomic per ray -- at L4 its 6 against 2 is 3 % faster)
+        sc->ghist_choice[slot_k] = 4 * wg > 5 * wh ? 1 : 0;
         sc->ghist_key[slot_k] = key;
       }
       L.ghist = sc->ghist_choice[slot_k] == 1;

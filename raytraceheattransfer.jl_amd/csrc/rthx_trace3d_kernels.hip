@@ -38,6 +38,10 @@ constexpr int kThreads = kTrace3dThreads;
 #ifndef RTHX_T3_WAVES
 #define RTHX_T3_WAVES 0  // > 0: amdgpu_waves_per_eu floor (register budget) for variants
 #endif
+#ifndef RTHX_T3_GH_WAVES
+#define RTHX_T3_GH_WAVES 6  // waves per SIMD the global-histogram kernels are built for (1 = compiler's choice)
+#endif
+constexpr int kGhWaves = RTHX_T3_GH_WAVES;
 #if RTHX_T3_WAVES > 0
 #define RTHX_T3_ATTR __attribute__((amdgpu_waves_per_eu(RTHX_T3_WAVES)))
 #else
@@ -235,8 +239,13 @@ __device__ __forceinline__ void emit_ray(const Emit3& E, const double* tab, uint
 // returnless atomic per ray) instead of an LDS histogram flushed at the end:
 // the histogram's LDS then holds walk stacks of more resident workgroups
 // (large N, where LDS limits occupancy).
+//
+// GH kernels run where LDS (the row histogram) would cap the resident
+// workgroups; they are built for 6 waves per SIMD (80 VGPRs, no spills;
+// config 4 L4 7.59 -> 7.83 Grays/s), the LDS-histogram ones keep the
+// compiler's 86 (5 waves: a 6-wave budget measured 1 % slower at L3).
 template <bool FAITHFUL, bool PACK16, int TOP, bool GH = false>
-__global__ __launch_bounds__(kThreads) RTHX_T3_ATTR void trace_exchange_3d_kernel(const DevScene3D* __restrict__ Sp,
+__global__ __launch_bounds__(kThreads) RTHX_T3_ATTR __attribute__((amdgpu_waves_per_eu(GH ? kGhWaves : 1))) void trace_exchange_3d_kernel(const DevScene3D* __restrict__ Sp,
                                                                                   TraceParams P, TallyParams T) {
   // dynamic LDS: [row histogram][walk stacks] (GH: the stacks only)
   extern __shared__ uint32_t hist[];
