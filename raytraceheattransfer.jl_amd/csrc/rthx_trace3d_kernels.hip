@@ -35,6 +35,12 @@ constexpr int kThreads = kTrace3dThreads;
 #ifndef RTHX_T3_REFILL
 #define RTHX_T3_REFILL 16  // ray regeneration: refill batch (lanes); 0 = one ray per lane per pass
 #endif
+#ifndef RTHX_T3_FLATNODE
+#define RTHX_T3_FLATNODE 0  // 1: node records by one flat load from either the LDS top or the global array (A/B)
+#endif
+#ifndef RTHX_T3_BRANCHY
+#define RTHX_T3_BRANCHY 1  // 0: straight-line child selection (config 4 L3 9.5 -> 9.3 Grays/s: slower)
+#endif
 #ifndef RTHX_T3_WAVES
 #define RTHX_T3_WAVES 0  // > 0: amdgpu_waves_per_eu floor (register budget) for variants
 #endif
@@ -148,6 +154,16 @@ struct Walk {
                                        int glo, int glen, int RTHX_LDS* stk) {
     while (node >= 0) {
       Bvh2Node nd;
+#if RTHX_T3_FLATNODE
+      // one flat load for either address space (no branch between the LDS
+      // copy of the top nodes and the global array)
+      {
+        typedef float f4 __attribute__((ext_vector_type(4)));
+        const f4* q = node < n_top ? (const f4*)(const Bvh2Node*)(top + node) : (const f4*)(S.nodes + node);
+        const f4 w[4] = {q[0], q[1], q[2], q[3]};
+        __builtin_memcpy(&nd, w, sizeof(nd));
+      }
+#else
       if (node < n_top) {
         typedef float f4 __attribute__((ext_vector_type(4)));
         const f4 RTHX_LDS* q = (const f4 RTHX_LDS*)(top + node);
@@ -155,6 +171,7 @@ struct Walk {
         __builtin_memcpy(&nd, w, sizeof(nd));
       } else
         nd = S.nodes[node];
+#endif
       float tn[2], tf[2];
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
@@ -167,7 +184,8 @@ struct Walk {
         tf[c] = fminf(fminf(fmaxf(a0, b0), fmaxf(a1, b1)), fminf(fmaxf(a2, b2), best_tf));
       }
       // a child whose triangles all belong to the emitter's group is never entered
-      const bool h0 = tn[0] <= tf[0] && nd.group[0] != group, h1 = tn[1] <= tf[1] && nd.group[1] != group;
+      const bool h0 = (tn[0] <= tf[0]) & (nd.group[0] != group), h1 = (tn[1] <= tf[1]) & (nd.group[1] != group);
+#if RTHX_T3_BRANCHY
       if (h0 && h1) {
         const bool near0 = tn[0] <= tn[1];
         stk[sp * kThreads] = near0 ? nd.child[1] : nd.child[0];
@@ -182,6 +200,27 @@ struct Walk {
         pending = node;
         node = sp > 0 ? stk[--sp * kThreads] : kWalkDone;
       }
+#else
+      // Straight-line form of: both children hit -> visit the nearer, push
+      // the farther; one hit -> visit it; none -> pop.  The stack slot sp is
+      // written every step (a push only when both hit; otherwise the slot is
+      // above the stack and dead) and the top is read every step, so the
+      // step has no branch.  sp never exceeds the level of the node being
+      // read, so the slot is within the scene's `stack` levels.
+      const bool both = h0 & h1, any = h0 | h1;
+      const bool first0 = h0 & (!h1 | (tn[0] <= tn[1]));
+      const int c0 = nd.child[0], c1 = nd.child[1];
+      const int top_below = stk[(sp > 0 ? sp - 1 : 0) * kThreads];
+      stk[sp * kThreads] = first0 ? c1 : c0;
+      node = any ? (first0 ? c0 : c1) : (sp > 0 ? top_below : kWalkDone);
+      sp += both ? 1 : ((any | (sp == 0)) ? 0 : -1);
+      // a leaf reached while none is postponed: postpone it and pop
+      const bool park = (node < 0) & (node != kWalkDone) & (pending == 0);
+      const int top2 = stk[(sp > 0 ? sp - 1 : 0) * kThreads];
+      pending = park ? node : pending;
+      node = park ? (sp > 0 ? top2 : kWalkDone) : node;
+      sp -= (park & (sp > 0)) ? 1 : 0;
+#endif
       if (__popcll(__ballot(pending == 0)) <= RTHX_T3_LEAF_LAG) break;
     }
     while (pending < 0) {
