@@ -67,7 +67,10 @@ constexpr int kTrace3dThreads = RTHX_T3_THREADS;  // lanes per workgroup
 constexpr int kTopNodes = 128;
 // static LDS of the 3D kernel: cos table, emitter, counters and (at least)
 // the 64-node cache
-constexpr size_t kTrace3dStaticLds = 16 * kCosTable + 512 + 64 * 64;
+#ifndef RTHX_T3_GTAB
+#define RTHX_T3_GTAB 0
+#endif
+constexpr size_t kTrace3dStaticLds = (RTHX_T3_GTAB ? 0 : 16 * kCosTable) + 512 + 64 * 64;
 // dynamic LDS: the row histogram (`words` = N, or (N + 1) / 2 packed u16,
 // padded to 64), then the stacks
 __host__ __device__ constexpr size_t trace3d_stack_offset(int64_t words) { return (size_t)((words + 63) & ~int64_t(63)); }

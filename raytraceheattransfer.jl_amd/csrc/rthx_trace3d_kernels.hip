@@ -42,17 +42,12 @@ constexpr int kThreads = kTrace3dThreads;
 #define RTHX_T3_BRANCHY 1  // 0: straight-line child selection (config 4 L3 9.5 -> 9.3 Grays/s: slower)
 #endif
 #ifndef RTHX_T3_WAVES
-#define RTHX_T3_WAVES 0  // > 0: amdgpu_waves_per_eu floor (register budget) for variants
+#define RTHX_T3_WAVES 1  // waves per SIMD the LDS-histogram kernels are built for (1 = compiler's choice)
 #endif
 #ifndef RTHX_T3_GH_WAVES
 #define RTHX_T3_GH_WAVES 6  // waves per SIMD the global-histogram kernels are built for (1 = compiler's choice)
 #endif
-constexpr int kGhWaves = RTHX_T3_GH_WAVES;
-#if RTHX_T3_WAVES > 0
-#define RTHX_T3_ATTR __attribute__((amdgpu_waves_per_eu(RTHX_T3_WAVES)))
-#else
-#define RTHX_T3_ATTR
-#endif
+constexpr int kHistWaves = RTHX_T3_WAVES, kGhWaves = RTHX_T3_GH_WAVES;
 
 // Products are fused exactly where the CPU restatement fuses them (fma() in
 // oracle/rthx_oracle.c t3_mt); everything else is built uncontracted.
@@ -88,6 +83,16 @@ __device__ __forceinline__ double moller_trumbore(const Tri3& T, const double* o
   if (!(det > 0.0) || !(U >= 0.0) || !(V >= 0.0) || !(U + V <= det) || !(W > 0.0)) return -1.0;
   return W / det;
 }
+
+#ifndef RTHX_T3_GTAB
+#define RTHX_T3_GTAB 0  // 1: the azimuth table stays in global memory (4 KB less LDS per workgroup)
+#endif
+#if RTHX_T3_GTAB
+__device__ __forceinline__ const double* S_tables_of(const DevScene3D* Sp) { return (const double*)Sp->tables; }
+#define T3_TAB(t) (t)
+#else
+#define T3_TAB(t) ((const double*)lds_opaque(&(t)[0]))
+#endif
 
 constexpr int kWalkDone = INT32_MIN;  // empty stack (leaf references are > INT32_MIN)
 
@@ -284,14 +289,18 @@ __device__ __forceinline__ void emit_ray(const Emit3& E, const double* tab, uint
 // config 4 L4 7.59 -> 7.83 Grays/s), the LDS-histogram ones keep the
 // compiler's 86 (5 waves: a 6-wave budget measured 1 % slower at L3).
 template <bool FAITHFUL, bool PACK16, int TOP, bool GH = false>
-__global__ __launch_bounds__(kThreads) RTHX_T3_ATTR __attribute__((amdgpu_waves_per_eu(GH ? kGhWaves : 1))) void trace_exchange_3d_kernel(const DevScene3D* __restrict__ Sp,
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(GH ? kGhWaves : kHistWaves))) void trace_exchange_3d_kernel(const DevScene3D* __restrict__ Sp,
                                                                                   TraceParams P, TallyParams T) {
   // dynamic LDS: [row histogram][walk stacks] (GH: the stacks only)
   extern __shared__ uint32_t hist[];
   __shared__ Bvh2Node s_top[TOP];
   Bvh2Node RTHX_LDS* top = (Bvh2Node RTHX_LDS*)&s_top[0];
   const int n_top = TOP < Sp->n_nodes ? TOP : Sp->n_nodes;
+#if RTHX_T3_GTAB
+  const double* s_tab = S_tables_of(Sp);  // the azimuth table read from global memory (L1/L2): no LDS
+#else
   __shared__ double s_tab[2 * kCosTable];        // (cos, sin)(2 pi j / 256)
+#endif
   __shared__ Emit3 s_emit;
   __shared__ uint32_t s_tallied;
 #if RTHX_T3_REFILL
@@ -309,8 +318,10 @@ __global__ __launch_bounds__(kThreads) RTHX_T3_ATTR __attribute__((amdgpu_waves_
   const int64_t words = GH ? 0 : PACK16 ? (N + 1) / 2 : N;
   for (int64_t i = tid; i < words; i += kThreads) hist[i] = 0u;
   uint32_t* dense = T.dense + slot * N;
+#if !RTHX_T3_GTAB
   if (!FAITHFUL)
     for (int i = tid; i < 2 * kCosTable; i += kThreads) s_tab[i] = S.tables[i];
+#endif
   // breadth-first top of the BVH (rthx_trace3d.cpp layout_nodes)
   {
     typedef float f4 __attribute__((ext_vector_type(4)));
@@ -355,7 +366,7 @@ __global__ __launch_bounds__(kThreads) RTHX_T3_ATTR __attribute__((amdgpu_waves_
         if (r < (uint32_t)r_end) {
           const Emit3 RTHX_LDS* em = lds_opaque(&s_emit);
           double o[3], d[3];
-          emit_ray<FAITHFUL>(*(const Emit3*)em, (const double*)lds_opaque(&s_tab[0]), (uint32_t)g, r, P.key0, P.key1,
+          emit_ray<FAITHFUL>(*(const Emit3*)em, T3_TAB(s_tab), (uint32_t)g, r, P.key0, P.key1,
                              o, d);
           w.init(o, d);
           live = true;
@@ -372,7 +383,7 @@ __global__ __launch_bounds__(kThreads) RTHX_T3_ATTR __attribute__((amdgpu_waves_
   for (int64_t r = r_begin + tid; r < r_end; r += kThreads) {
     const Emit3 RTHX_LDS* em = lds_opaque(&s_emit);
     double o[3], d[3];
-    emit_ray<FAITHFUL>(*(const Emit3*)em, (const double*)lds_opaque(&s_tab[0]), (uint32_t)g, (uint32_t)r, P.key0,
+    emit_ray<FAITHFUL>(*(const Emit3*)em, T3_TAB(s_tab), (uint32_t)g, (uint32_t)r, P.key0,
                        P.key1, o, d);
     Walk w;
     w.init(o, d);

@@ -170,6 +170,20 @@ def test_coplanar_groups_exact(hip, ndim, level):
     assert np.all(D[same] == 0)
 
 
+@pytest.mark.parametrize("form,faithful", [("0", False), ("1", False), ("1", True)])
+def test_row_count_forms_exact(hip, monkeypatch, form, faithful):
+    """Both row-count forms of the 3D kernel equal the restatement: the LDS
+    row histogram flushed per workgroup (RTHX_T3_GHIST=0) and counts straight
+    to the dense rows (=1; the form large scenes take, built for 6 waves per
+    SIMD).  The host reads the knob at every call."""
+    monkeypatch.setenv("RTHX_T3_GHIST", form)
+    xyz, nv, nrm, nc = H.cube_icosphere_scene(ndim=3, level=2)
+    g = H.cube_icosphere_groups(3, 2)
+    D, info = gpu_dense(xyz, nv, nrm, 3000, seed=13, faithful=faithful, groups=g)
+    C, lost = oracle.trace_exchange_3d(xyz, nv, nrm, 3000, seed=13, nthreads=16, groups=g)
+    assert np.array_equal(D, C) and info["lost_total"] == lost
+
+
 def test_group_validation(hip):
     """Groups must be non-negative and contiguous runs of polygon indices."""
     from rthx._lib import RthxError
