@@ -68,7 +68,7 @@ constexpr int kTopNodes = 128;
 // static LDS of the 3D kernel: cos table, emitter, counters and (at least)
 // the 64-node cache
 #ifndef RTHX_T3_GTAB
-#define RTHX_T3_GTAB 0
+#define RTHX_T3_GTAB 1
 #endif
 constexpr size_t kTrace3dStaticLds = (RTHX_T3_GTAB ? 0 : 16 * kCosTable) + 512 + 64 * 64;
 // dynamic LDS: the row histogram (`words` = N, or (N + 1) / 2 packed u16,

@@ -42,7 +42,7 @@ constexpr int kThreads = kTrace3dThreads;
 #define RTHX_T3_BRANCHY 1  // 0: straight-line child selection (config 4 L3 9.5 -> 9.3 Grays/s: slower)
 #endif
 #ifndef RTHX_T3_WAVES
-#define RTHX_T3_WAVES 1  // waves per SIMD the LDS-histogram kernels are built for (1 = compiler's choice)
+#define RTHX_T3_WAVES 6  // waves per SIMD the LDS-histogram kernels are built for (1 = compiler's choice; 6 with the table in global memory: L3 9.43 -> 9.53 Grays/s)
 #endif
 #ifndef RTHX_T3_GH_WAVES
 #define RTHX_T3_GH_WAVES 6  // waves per SIMD the global-histogram kernels are built for (1 = compiler's choice)
@@ -85,7 +85,7 @@ __device__ __forceinline__ double moller_trumbore(const Tri3& T, const double* o
 }
 
 #ifndef RTHX_T3_GTAB
-#define RTHX_T3_GTAB 0  // 1: the azimuth table stays in global memory (4 KB less LDS per workgroup)
+#define RTHX_T3_GTAB 1  // the azimuth table stays in global memory (4 KB less LDS per workgroup: 6 resident at config 4 L3); 0: staged in LDS
 #endif
 #if RTHX_T3_GTAB
 __device__ __forceinline__ const double* S_tables_of(const DevScene3D* Sp) { return (const double*)Sp->tables; }
