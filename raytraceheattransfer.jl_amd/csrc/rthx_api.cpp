@@ -683,15 +683,12 @@ uint64_t lookback_wait_ticks() {
 // Launch geometry of one trace call (rows, split, LDS histogram layout).
 struct TracePlan {
   int64_t N = 0, R = 0, end = 0, n_rows = 0, split = 1, row_cap = 1, hash_cap = 0, bm_words = 0, part_cap = 0;
-  bool part_lists = false;  // split rows as sorted part lists + part_merge_kernel (else the dense merge)
+  bool part_lists = false;  // split hash rows: sorted part lists + part_merge_kernel (else the last part merges)
   int tally = rthx::kTallyU16;
   int clds = 0;  // rthx_kernels.h LaunchCfg::clds
   bool recording = false, uniform = true;
   size_t lds_bytes = 0, cl_offset = 0;
 };
-
-// Split rows as part lists: staging + merge scratch (16 B per reserved entry) allowed
-constexpr int64_t kPartListBudget = int64_t(24) << 30;
 
 // Hash tallies (large N): the largest table the trace kernel's LDS holds
 // (keys + counts, 8 B per slot); a workgroup traces at most 3/4 as many rays.
@@ -767,20 +764,6 @@ int plan_trace(const rthx_domain* dom, const rthx_trace_args* a, TracePlan& p) {
       p.part_cap = (R + p.split - 1) / p.split;
       p.part_lists = true;
     }
-  } else if (p.split > 1) {
-    // Split rows with LDS histograms: RTHX_PART_LISTS=1 writes each slice's
-    // counts as a sorted list (min(N, chunk) entries reserved per slice)
-    // merged by part_merge_kernel instead of adding them into a dense
-    // [rows][N] buffer that row_compact_kernel compacts.  The lists are ~1/3
-    // of N at C2 shards, but the merge's binary searches in global memory
-    // are latency-bound: 0.62 / 1.60 ms against the dense merge's 0.15 /
-    // 0.09 ms at 4 / 8 emulated ranks, so the dense merge stays the default.
-    const int64_t pc = std::min<int64_t>(N, (R + p.split - 1) / p.split);
-    if (p.n_rows * p.split * pc * 16 <= kPartListBudget && env_flag("RTHX_PART_LISTS")) {
-      p.part_cap = pc;
-      p.row_cap = p.split * pc;
-      p.part_lists = true;
-    }
   }
   // multi-polygon domains: the coarse mesh goes behind the histogram in LDS
   // when it fits (CLDS kernels, rthx_device.h segment_cl)
@@ -854,12 +837,21 @@ int run_trace(rthx_domain* dom, const rthx_trace_args* a, const TracePlan& p, rt
     HIP_TRY(res->stage_cols.reserve((size_t)n_rows * p.row_cap * 4), "hipMalloc stage_cols");
     HIP_TRY(res->stage_cnt.reserve((size_t)n_rows * p.row_cap * 4), "hipMalloc stage_cnt");
   }
-  // split rows: the dense per-row counts, or (part lists) the part merge's
-  // scratch [2][n_rows][row_cap] followed by part_nnz [n_rows][split]
+  // split rows: (hash part lists) the part merge's scratch [2][n_rows][row_cap]
+  // followed by part_nnz [n_rows][split]; (histograms) one slab of the
+  // histogram's words per part, [n_rows][split][words], the arrival counters
+  // [n_rows] (zero between launches: zeroed when allocated) and the parts'
+  // tallied counts [n_rows][split]
+  const int64_t hist_words = p.tally == rthx::kTallyU16 ? (N + 1) / 2 : N;
   const size_t dense_bytes = p.part_lists ? (size_t)n_rows * p.row_cap * 8 + (size_t)n_rows * p.split * 4
-                                          : (size_t)n_rows * N * 4;
+                                          : (size_t)n_rows * p.split * (hist_words + 1) * 4;
   if (p.split > 1) HIP_TRY(res->dense.reserve(dense_bytes), "hipMalloc dense rows");
   else res->dense.release();
+  if (p.split > 1 && !p.part_lists) {
+    const void* before = res->arrive.p;
+    HIP_TRY(res->arrive.reserve((size_t)n_rows * 4), "hipMalloc arrival counters");
+    if (res->arrive.p != before) HIP_TRY(hipMemsetAsync(res->arrive.p, 0, res->arrive.cap, st), "hipMemset arrivals");
+  }
 
   rthx::TraceParams P{};
   P.R = R;
@@ -885,6 +877,8 @@ int run_trace(rthx_domain* dom, const rthx_trace_args* a, const TracePlan& p, rt
   T.row_tallied = res->row_tallied.as<uint32_t>();
   T.dense = p.split > 1 ? res->dense.as<uint32_t>() : nullptr;
   T.part_nnz = p.split > 1 && p.part_lists ? T.dense + 2 * (size_t)n_rows * p.row_cap : nullptr;
+  T.row_arrive = p.split > 1 && !p.part_lists ? res->arrive.as<uint32_t>() : nullptr;
+  T.part_tallied = T.row_arrive ? T.dense + (size_t)n_rows * p.split * hist_words : nullptr;
   T.part_cap = p.part_cap;
   T.hash_cap = (int32_t)p.hash_cap;
   int32_t shift = 32;
@@ -916,10 +910,8 @@ int run_trace(rthx_domain* dom, const rthx_trace_args* a, const TracePlan& p, rt
   } else {
     HIP_TRY(hipMemsetAsync(res->totals.p, 0, 32, st), "hipMemset totals");
   }
-  if (p.split > 1 && n_rows > 0) {
-    if (!p.part_lists) HIP_TRY(hipMemsetAsync(T.dense, 0, (size_t)n_rows * N * 4, st), "hipMemset dense rows");
+  if (p.split > 1 && p.part_lists && n_rows > 0)
     HIP_TRY(hipMemsetAsync(T.row_tallied, 0, (size_t)n_rows * 4, st), "hipMemset row_tallied");
-  }
   HIP_TRY(hipEventRecord(dom->ev[0], st), "hipEventRecord");
   if (n_rows > 0) {
     rthx::LaunchCfg L{};
@@ -950,7 +942,7 @@ int run_trace(rthx_domain* dom, const rthx_trace_args* a, const TracePlan& p, rt
     std::memcpy(totals, res->h_totals.p, 8 * rthx::kLbTotals);
     res->lb_epoch = T.lb_epoch;
   } else {
-    const int merge = p.split == 1 ? rthx::kNoMerge : p.part_lists ? rthx::kMergeParts : rthx::kMergeDense;
+    const int merge = p.part_lists ? rthx::kMergeParts : rthx::kNoMerge;
     int rc = rthx::finish_staged(res, T, merge, st, dom->ev[2], totals);
     if (rc) return rc;
   }
@@ -1023,7 +1015,7 @@ int trace_exchange_one(rthx_domain* dom, const rthx_trace_args* a, rthx_result* 
   // layers), and a row waiting on a slower predecessor idles its CU slot
   // (C5 greenhouse: 15.2 -> 17.6 ms per band with the look-back).  The
   // recorder's kernels stage.
-  const bool lookback = p.split == 1 && n_rows > 0 && dom->single_convex && !p.recording &&
+  const bool lookback = !p.part_lists && n_rows > 0 && dom->single_convex && !p.recording &&
                         (uint64_t)n_rows * (uint64_t)p.row_cap <= rthx::kLbValMax && !env_flag("RTHX_NO_LOOKBACK");
   int64_t totals[rthx::kLbTotals] = {0, 0, 0, 0, 0};
   float ms_trace = 0.f, ms_pack = 0.f;
@@ -1310,6 +1302,7 @@ RTHX_EXPORT int rthx_result_copy_csr_device(const rthx_result* cres, int32_t par
   rthx_result* q = nullptr;
   int rc = device_block(cres, part, &q, nullptr);
   if (rc) return rc;
+  rthx::DeviceGuard keep_device;  // (the caller's current device, e.g. torch's, is restored)
   HIP_TRY(hipSetDevice(q->device), "hipSetDevice");
   hipStream_t st = nullptr;
   HIP_TRY(rthx::device_stream(q->device, &st), "device stream");
@@ -1401,7 +1394,7 @@ RTHX_EXPORT int rthx_multi_trace_exchange(rthx_multi* m, const rthx_trace_args* 
     (void)hipSetDevice(res->device);
     rthx::DevBuf* all[] = {&res->stage_cols, &res->stage_cnt, &res->row_nnz, &res->row_tallied, &res->row_off,
                            &res->totals,     &res->cols,      &res->cnt,     &res->dense,       &res->rec_ids,
-                           &res->rec_ok,     &res->rec_orig,  &res->rec_end, &res->lb_status, &res->lb_totals};
+                           &res->rec_ok,     &res->rec_orig,  &res->rec_end, &res->lb_status, &res->lb_totals, &res->arrive};
     for (rthx::DevBuf* b : all) b->release();
     res->lb_epoch = 0;
     res->device = -1;

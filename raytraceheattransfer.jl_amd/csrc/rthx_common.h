@@ -58,6 +58,20 @@ struct DevBuf {
   T* as() const { return static_cast<T*>(p); }
 };
 
+// Restores the calling thread's current device on scope exit (entry points
+// that switch devices on behalf of a caller who keeps its own, e.g. torch).
+struct DeviceGuard {
+  int prev = -1;
+  DeviceGuard() {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+  }
+  DeviceGuard(const DeviceGuard&) = delete;
+  DeviceGuard& operator=(const DeviceGuard&) = delete;
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
 // Pinned host buffer with grow-only capacity (fast D2H copies).
 struct HostBuf {
   void* p = nullptr;

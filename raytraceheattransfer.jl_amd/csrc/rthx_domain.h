@@ -54,7 +54,8 @@ struct rthx_result {
   bool interleaved = false;
   rthx::DevBuf stage_cols, stage_cnt, row_nnz, row_tallied, row_off, totals, cols, cnt, dense;
   rthx::DevBuf rec_ids, rec_ok, rec_orig, rec_end;
-  rthx::DevBuf lb_status;  // direct-CSR look-back words (unsplit launches)
+  rthx::DevBuf lb_status;  // direct-CSR look-back words
+  rthx::DevBuf arrive;     // split 2D rows: parts arrived per row (zero between launches)
   rthx::DevBuf lb_totals;  // look-back launches' totals, two sets of 4 (launch e uses set e & 1)
   uint32_t lb_epoch = 0;   // epoch of the last look-back launch; 0 = words and totals not yet zeroed
   int64_t lb_nnz_hint = 0; // nnz of the last look-back launch (sizes the next one of the same shape)
@@ -75,7 +76,7 @@ struct rthx_result {
     for (rthx_result* p : parts) delete p;
     if (device >= 0) (void)hipSetDevice(device);
     rthx::DevBuf* all[] = {&stage_cols, &stage_cnt, &row_nnz,  &row_tallied, &row_off,  &totals, &cols,
-                     &cnt,        &dense,     &rec_ids,  &rec_ok,      &rec_orig, &rec_end, &lb_status, &lb_totals, &fvals};
+                     &cnt,        &dense,     &rec_ids,  &rec_ok,      &rec_orig, &rec_end, &lb_status, &lb_totals, &fvals, &arrive};
     for (rthx::DevBuf* b : all) b->release();
     h_cols.release();
     h_cnt.release();

@@ -30,10 +30,16 @@ struct RecordParams {
 enum Tally : int { kTallyU32 = 0, kTallyU16 = 1, kTallyHash = 2 };
 
 // Where the counts go.  Unsplit: each workgroup compacts its row into
-// stage_*[slot*row_cap ..] and writes row_nnz / row_tallied.  Split, dense
-// tallies: the `split` workgroups of a row add into dense[slot*N ..] and
-// row_tallied (both zeroed first); row_compact_kernel then fills stage_* /
-// row_nnz.  Split, hash tallies: part p of a row writes its sorted list to
+// stage_*[slot*row_cap ..] and writes row_nnz / row_tallied (or, with
+// lb_status, straight into the final CSR).  Split 2D rows, histogram
+// tallies: part p of a row stores its LDS histogram whole into the slab
+// dense[(slot*split + p) * words ..] and its tallied count into
+// part_tallied[slot*split + p], then arrives on row_arrive[slot]; the last
+// part to arrive adds the other parts' slabs into its histogram and writes
+// the row like an unsplit one (no merge launch).  Split 3D rows (the
+// trace3d kernels): parts add into dense[slot*N ..] and row_tallied (both
+// zeroed first); row_compact_kernel then fills stage_* / row_nnz.  Split,
+// hash tallies: part p of a row writes its sorted list to
 // stage_*[slot*row_cap + p*chunk ..] (row_cap = R) and part_nnz[slot*split+p];
 // part_merge_kernel merges the parts (scratch: dense) back into the slot.
 struct TallyParams {
@@ -46,8 +52,10 @@ struct TallyParams {
   uint32_t* stage_cnt;
   uint32_t* row_nnz;
   uint32_t* row_tallied;
-  uint32_t* dense;      // split only: [n_rows][N] (dense tallies) or merge scratch [2][n_rows][row_cap] (hash)
-  uint32_t* part_nnz;   // split rows as sorted part lists (hash tallies, or PART_LISTS): [n_rows][split]; null = dense merge
+  uint32_t* dense;      // split only: 2D slabs [n_rows][split][words], 3D [n_rows][N], hash merge scratch [2][n_rows][row_cap]
+  uint32_t* part_nnz;   // split hash tallies: sorted part lists, [n_rows][split]
+  uint32_t* row_arrive;    // split 2D histogram rows: parts arrived, [n_rows]; zero between launches (the last part resets it)
+  uint32_t* part_tallied;  // split 2D histogram rows: rays each part tallied, [n_rows][split]
   int64_t part_cap;     // part lists: entries reserved per part in a row's staging slot
   int32_t hash_cap;     // hash tallies: table slots (power of two; keys then counts in dynamic LDS)
   int32_t hash_shift;   // 32 - log2(hash_cap)

@@ -41,6 +41,12 @@ namespace rthx {
 #endif
 #define RTHX_ML_VIEW mlat_lds_view(lds_opaque(cl_base), D.ml)
 #define RTHX_ML_G D.ml
+#ifndef RTHX_EXP_NOWAIT
+#define RTHX_EXP_NOWAIT 0
+#endif
+#ifndef RTHX_EXP_NOWRITE
+#define RTHX_EXP_NOWRITE 0
+#endif
 #ifndef RTHX_REFILL_Q
 #define RTHX_REFILL_Q 24  // MLAT kernels: idle lanes before the ends are resolved and the queue refills (C5 band 0 / 7 at 1e9 rays: 8 69.7 / 43.3 ms, 16 59.2 / 36.6, 24 57.0 / 34.3, 32 59.5 / 35.5, 40 61.9 / 34.6)
 #endif
@@ -80,7 +86,7 @@ __device__ __forceinline__ uint64_t lookback_offset(unsigned long long* status, 
                                                     uint32_t epoch) {
   constexpr unsigned long long kAgg = 1ull << 62, kInc = 2ull << 62, kVal = kLbValMax;
   const unsigned long long tag = (unsigned long long)epoch << kLbEpochShift;
-  if (slot == 0) {
+  if (slot == 0 || RTHX_EXP_NOWAIT) {
     __hip_atomic_store(&status[0], kInc | tag | nnz, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return 0;
   }
@@ -151,7 +157,7 @@ __device__ __forceinline__ uint32_t compact_row(int64_t n_words, F count2, uint3
   uint32_t* __restrict__ out_n = out_n_ + gbase;
   // (a row that would end past the `cap` entries reserved writes nothing:
   // base_of has flagged the overflow and the host re-traces)
-  for (int64_t w0 = wb; w0 < (gbase + total <= cap ? we : wb); w0 += 64) {
+  for (int64_t w0 = wb; w0 < (gbase + total <= cap && !RTHX_EXP_NOWRITE ? we : wb); w0 += 64) {
     const int64_t w = w0 + lane;
     uint32_t lo = 0u, hi = 0u;
     if (w < we) count2(w, lo, hi);
@@ -741,38 +747,75 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
     return;
   }
 
+  // Split rows: hand this part's histogram to the part of the row that
+  // finishes last, which then writes the whole row as an unsplit row does
+  // (direct CSR by look-back, or its staging slot).  Hand-off (agent scope,
+  // every XCD): the slab and the tallied count are stored write-through
+  // (sc1), every storing wave drains them (vmcnt 0) before the barrier, one
+  // lane arrives on the row's counter, and the part whose arrival returns
+  // split - 1 reads the other slabs with sc1 loads.  It resets the counter,
+  // so the counters are zero between launches.
+  __shared__ uint32_t s_merge;  // bit 0: this part arrived last; bit 1: a packed pair overflowed 16 bits
+  const int64_t split = SPLIT ? T.split : 1;
+  const uint32_t* slabs = SPLIT ? T.dense + (size_t)slot * (size_t)split * (size_t)n_words : nullptr;
+  if constexpr (SPLIT) {
+    uint32_t* mine = T.dense + (size_t)blockIdx.x * (size_t)n_words;
+    for (int64_t w = tid; w < n_words; w += nthr)
+      __hip_atomic_store(&mine[w], hist[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0) __hip_atomic_store(&T.part_tallied[blockIdx.x], s_tallied, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      const uint32_t before =
+          __hip_atomic_fetch_add(&T.row_arrive[slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const bool last = before + 1u == (uint32_t)split;
+      if (last) {
+        __hip_atomic_store(&T.row_arrive[slot], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint32_t t = 0;
+        for (int64_t p = 0; p < split; ++p)
+          t += p == part ? s_tallied
+                         : __hip_atomic_load(&T.part_tallied[slot * split + p], __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+        s_tallied = t;
+      }
+      s_merge = last ? 1u : 0u;
+    }
+    __syncthreads();
+    if (!(s_merge & 1u)) return;
+    // The other parts' counts into this part's histogram.  Packed 16-bit
+    // pairs cannot overflow when R < 65536; otherwise a pair that would
+    // leaves the histogram alone and the row is counted from the slabs.
+    bool ovf = false;
+    for (int64_t w = tid; w < n_words; w += nthr) {
+      const uint32_t own = hist[w];
+      uint32_t lo = PACK16 ? (own & 0xFFFFu) : own, hi = PACK16 ? (own >> 16) : 0u;
+      for (int64_t p = 0; p < split; ++p) {
+        if (p == part) continue;
+        const uint32_t v = __hip_atomic_load(&slabs[p * n_words + w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        lo += PACK16 ? (v & 0xFFFFu) : v;
+        hi += PACK16 ? (v >> 16) : 0u;
+      }
+      if (PACK16 && (lo | hi) > 0xFFFFu) ovf = true;
+      else hist[w] = PACK16 ? (lo | (hi << 16)) : lo;
+    }
+    if (ovf) atomicOr(&s_merge, 2u);
+    __syncthreads();
+  }
+  const bool from_slabs = SPLIT && PACK16 && __builtin_amdgcn_readfirstlane((int)(s_merge & 2u)) != 0;
   auto count2 = [&](int64_t w, uint32_t& lo, uint32_t& hi) {
+    if (SPLIT && PACK16 && from_slabs) {  // (rare: R >= 65536 and one absorber took 65536 of them)
+      lo = hi = 0u;
+      for (int64_t p = 0; p < split; ++p) {
+        const uint32_t v = __hip_atomic_load(&slabs[p * n_words + w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        lo += v & 0xFFFFu;
+        hi += v >> 16;
+      }
+      return;
+    }
     uint32_t v = hist[w];
     lo = PACK16 ? (v & 0xFFFFu) : v;
     hi = PACK16 ? (v >> 16) : 0u;
   };
-  if (SPLIT && T.part_nnz) {
-    // this slice's counts as an ascending list at part * part_cap of the
-    // row's staging slot; part_merge_kernel merges the row's slices
-    const int64_t o = slot * T.row_cap + part * T.part_cap;
-    const uint32_t nnz = compact_row<PACK16>(n_words, count2, T.stage_cols + o, T.stage_cnt + o, wave_sum);
-    if (tid == 0) {
-      T.part_nnz[blockIdx.x] = nnz;
-      atomicAdd(&T.row_tallied[slot], s_tallied);
-    }
-    return;
-  }
-  if (SPLIT) {
-    // add this slice's nonzero counters into the row's dense buffer
-    uint32_t* dense = T.dense + slot * T.n_emitters;
-    for (int64_t w = tid; w < n_words; w += nthr) {
-      uint32_t v = hist[w];
-      if (v == 0u) continue;
-      if (PACK16) {
-        if (v & 0xFFFFu) atomicAdd(&dense[2 * w], v & 0xFFFFu);
-        if (v >> 16) atomicAdd(&dense[2 * w + 1], v >> 16);
-      } else {
-        atomicAdd(&dense[w], v);
-      }
-    }
-    if (tid == 0) atomicAdd(&T.row_tallied[slot], s_tallied);
-    return;
-  }
   if (SINGLE && T.lb_status) {  // (host: single-polygon domains only; keeps the other kernels lean)
     auto base_of = [&](uint32_t nnz) -> uint64_t {
       if (tid == 0) {

@@ -166,7 +166,9 @@ def gather_csr(row_ptr, cols, counts, n: int, group=None, dst: int = 0, as_tenso
     there.  On an NCCL (= RCCL on ROCm) group the tensors travel over xGMI
     from device memory; on gloo through the host.  Returns the merged CSR
     (row_ptr, cols, counts) on the receiving ranks (numpy, or tensors on the
-    group's device with as_tensors), None elsewhere."""
+    group's device with as_tensors: counts are then int32 tensors holding
+    the uint32 bits, so counts >= 2^31 read negative until viewed as
+    uint32), None elsewhere."""
     dev = _device_of(group)
     rp = np.asarray(row_ptr, dtype=np.int64)
     lens = np.diff(rp)
@@ -178,19 +180,37 @@ def gather_csr(row_ptr, cols, counts, n: int, group=None, dst: int = 0, as_tenso
 
 def gather_result(res, n: int, group=None, dst: int = 0, as_tensors: bool = False):
     """gather_csr of a traced rthx result (rthx._lib.DeviceResult).  On an NCCL
-    group the counts never leave device memory before the collective: the
-    block is copied device to device into the tensors RCCL sends
-    (rthx_result_copy_csr_device; its rows are emitter_begin + k *
-    emitter_stride).  On gloo the host CSR is gathered."""
+    group the counts never leave device memory before the collective: each
+    block of the result (one per device of a MultiDeviceDomain trace, rows
+    emitter_begin + k * emitter_stride) is copied device to device
+    (rthx_result_copy_csr_device) and onto this rank's device, and the
+    blocks' rows are put in ascending order before the tensors go to RCCL.
+    On gloo the host CSR is gathered.  With as_tensors the counts come back
+    as int32 tensors holding the uint32 bits (counts >= 2^31 read negative:
+    ``counts.view(torch.int32)`` reinterpreted, ``.cpu().numpy().view(np.uint32)``
+    restores them); the numpy form is uint32."""
     import torch
 
     dev = _device_of(group)
     if dev.type == "cuda":
-        row_off, pairs, d = res.torch_csr()
-        if row_off.device != dev:
-            raise ValueError("the result lives on another device than this rank's")
-        lens = row_off[1:] - row_off[:-1]
-        rows = d["emitter_begin"] + d["emitter_stride"] * torch.arange(d["n_rows"], dtype=torch.int64, device=dev)
+        n_parts = int(res.device_csr(0)["n_parts"])
+        rows_l, lens_l, pairs_l = [], [], []
+        for part in range(n_parts):
+            row_off, pairs, d = res.torch_csr(part)
+            row_off, pairs = row_off.to(dev), pairs.to(dev)
+            rows_l.append(d["emitter_begin"] + d["emitter_stride"]
+                          * torch.arange(d["n_rows"], dtype=torch.int64, device=dev))
+            lens_l.append(row_off[1:] - row_off[:-1])
+            pairs_l.append(pairs)
+        rows, lens, pairs = torch.cat(rows_l), torch.cat(lens_l), torch.cat(pairs_l, dim=1)
+        if n_parts > 1:  # interleaved blocks: entries regrouped by ascending row
+            order = torch.argsort(rows)
+            start = torch.cumsum(lens, 0) - lens
+            lo = lens[order]
+            tot = int(lo.sum().item())
+            first = torch.cumsum(lo, 0) - lo
+            idx = torch.repeat_interleave(start[order] - first, lo) + torch.arange(tot, device=dev)
+            rows, lens, pairs = rows[order], lo, pairs[:, idx]
         keep = lens > 0
         return _gather_blocks(rows[keep], lens[keep], pairs, n, group, dst, as_tensors)
     rp, c, v = res.csr()

@@ -457,6 +457,24 @@ def test_gather_and_broadcast_over_rccl(hip):
         b_rp, b_c, b_v = RD.broadcast_csr(rp, cols, cnt, N, src=0)
         assert np.array_equal(np.asarray(b_rp), rp) and np.array_equal(np.asarray(b_c), cols)
         assert np.array_equal(np.asarray(b_v).view(np.uint32), cnt)
+        # a result of several device blocks (rthx_multi_trace_exchange):
+        # contiguous row blocks on the square, interleaved on the wedges;
+        # every block is gathered, and torch's current device is unchanged
+        for flat2, devices in ((flat, [0, 0]), (H.wedge_domain(8, 3).flat(), [0, 0, 0])):
+            a2 = _args(hip, flat2, 700, seed=10, begin=1, stride=2)[0]
+            md = hip.MultiDeviceDomain(flat2, devices)
+            r2 = hip.DeviceResult()
+            try:
+                r2.trace(md, a2)
+                assert r2.device_csr(0)["n_parts"] == len(devices)
+                m_rp, m_c, m_v = r2.csr()
+                for dst in (0, -1):
+                    g_rp, g_c, g_v = RD.gather_result(r2, flat2.n_emitters, dst=dst)
+                    assert np.array_equal(g_rp, m_rp) and np.array_equal(g_c, m_c) and np.array_equal(g_v, m_v)
+                assert torch.cuda.current_device() == 0
+            finally:
+                r2.close()
+                md.close()
     finally:
         dist.destroy_process_group()
         res.close()

@@ -244,8 +244,9 @@ def test_shards_union_equals_full(hip):
 
 
 def test_split_rows_exact(hip):
-    """Few rows, many rays: every row is split over several workgroups whose
-    histograms meet in a dense row buffer (rthx_api.cpp kSplitTargetBlocks)."""
+    """Few rows, many rays: every row is split over several workgroups; the
+    part that finishes last adds the other parts' histograms to its own and
+    writes the row (rthx_api.cpp kSplitTargetBlocks, rthx_kernels.hip)."""
     dom = H.square_domain(11)
     flat = dom.flat()
     args, _k = _args(hip, flat, 20_000, seed=12)
@@ -256,11 +257,11 @@ def test_split_rows_exact(hip):
 
 
 @pytest.mark.parametrize("case", ["square_pack16", "square_u32", "wedges", "greenhouse"])
-def test_split_part_lists_equal_dense_merge(hip, case, monkeypatch):
-    """Split rows: each slice's counts as a sorted list merged by
-    part_merge_kernel (RTHX_PART_LISTS=1) against the dense row buffer +
-    row_compact_kernel (default), and both against the oracle -- packed and
-    u32 LDS counters, single- and multi-polygon kernels."""
+def test_split_rows_equal_unsplit_rows(hip, case, monkeypatch):
+    """The same launch traced with split rows (default: few rows) and with
+    every row in one workgroup (RTHX_SPLIT_BELOW=1), with and without the
+    direct CSR write, and against the oracle -- packed and u32 LDS counters,
+    single-polygon (look-back) and multi-polygon (staging) kernels."""
     if case == "square_pack16":
         dom, R, kw = H.square_domain(11), 20_000, {}
     elif case == "square_u32":
@@ -272,10 +273,46 @@ def test_split_part_lists_equal_dense_merge(hip, case, monkeypatch):
     flat = dom.flat()
     args, _k = _args(hip, flat, R, seed=41, **kw)
     a = gpu_trace(hip, flat, args)
-    monkeypatch.setenv("RTHX_PART_LISTS", "1")
+    monkeypatch.setenv("RTHX_NO_LOOKBACK", "1")
     b = gpu_trace(hip, flat, args)
+    monkeypatch.delenv("RTHX_NO_LOOKBACK")
+    monkeypatch.setenv("RTHX_SPLIT_BELOW", "1")
+    c = gpu_trace(hip, flat, args)
     assert_same(a, b)
+    assert_same(a, c)
     assert_same(a, oracle.trace_exchange(flat, args, 16))
+
+
+def test_split_rows_sixteen_bit_overflow_counts_from_slabs(hip):
+    """R >= 65536 split into parts of packed 16-bit counters: a row whose
+    summed pair would pass 65535 (one absorber takes > 65535 rays) is counted
+    from the parts' slabs in 32 bits.  On a 1x1 square every row's absorbers
+    take ~1/5 of 1e6 rays each."""
+    dom = H.square_domain(1)
+    flat = dom.flat()
+    args, _k = _args(hip, flat, 1_000_000, seed=43)
+    rp, cols, cnt, info, _ = gpu_trace(hip, flat, args)
+    assert cnt.max() > 65535
+    assert_same((rp, cols, cnt, info), oracle.trace_exchange(flat, args, 16))
+
+
+def test_split_result_reused_across_shapes(hip):
+    """One result object traced split, unsplit, split with other rows and
+    split again: the per-row arrival counters are back at zero after every
+    launch, so each trace equals a fresh result's."""
+    dom = H.square_domain(11)
+    flat = dom.flat()
+    dd = hip.DeviceDomain(flat, 0)
+    res = hip.DeviceResult()
+    try:
+        for R, kw in [(20_000, {}), (300, {}), (9_000, dict(begin=1, stride=3)), (20_000, {}), (20_000, {})]:
+            args, _k = _args(hip, flat, R, seed=44, **kw)
+            res.trace(dd, args)
+            got = res.csr() + (res.info(),)
+            assert_same(got, gpu_trace(hip, flat, args)[:4])
+    finally:
+        res.close()
+        dd.close()
 
 
 def test_edge_cases(hip):

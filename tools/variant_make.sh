@@ -1,11 +1,11 @@
 #!/bin/bash
 # Full librthx.so of git revision REV (or the working tree: REV=.) built by the
-# csrc Makefile into csrc/_variants/<name>/ (A/B timing with RTHX_LIB=...).
+# csrc Makefile into csrc/_ab/<name>/ (git-ignored; it travels to the GPU box, so delete it after the A/B) (A/B timing with RTHX_LIB=...).
 #   tools/variant_make.sh <name> <rev|.> [make VAR=value ...]
 set -e
 name=$1; rev=$2; shift 2
 ROOT=$(cd $(dirname $0)/.. && pwd)
-d=$ROOT/raytraceheattransfer.jl_amd/csrc/_variants/$name
+d=$ROOT/raytraceheattransfer.jl_amd/csrc/_ab/$name
 mkdir -p $d
 if [ "$rev" = "." ]; then
   make -s -j8 -C $ROOT/raytraceheattransfer.jl_amd/csrc BUILD=$d "$@"
