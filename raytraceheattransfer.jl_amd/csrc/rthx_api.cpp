@@ -132,20 +132,23 @@ int check_grid(const rthx_grid_desc& g, int32_t count, const char* what) {
   return RTHX_OK;
 }
 
-// Row splitting: target number of workgroups per launch (>> 256 CUs x ~5
-// resident workgroups) and the fewest rays a split workgroup traces.  4096
-// measured faster than 8192 for every multi-GPU shard of C2 (W = 2: 66.6 ->
-// 77.0 Grays/s per GPU; the dense merge of split rows costs more than the
-// tail of ~4 waves of workgroups), W = 1 unchanged (tools/split_ab.sh).
-#ifndef RTHX_SPLIT_TARGET
-#define RTHX_SPLIT_TARGET 4096
-#endif
-constexpr int64_t kSplitTargetBlocks = RTHX_SPLIT_TARGET;
-// Rows are split only below this many rows: a 4-rank C2 shard (2651 rows)
-// traced unsplit takes 1.058 ms per step against 1.155 ms split in two with
-// the dense merge; an 8-rank shard (1325 rows) keeps its split to ~4096
-// workgroups (1.093 ms; 1.365 unsplit) -- bench.py --emulate-world, round 2.
-constexpr int64_t kSplitBelowRows = 2048;
+// Row splitting, from `slots`: the unsplit kernel's resident workgroups
+// (CUs x workgroups per CU, from the occupancy query).
+// - A launch of fewer rows than half the slots leaves CUs idle for the whole
+//   trace: every row is split into floor(slots / rows) parts, all resident in
+//   one round.
+// - Otherwise rows start as slots free up, and the launch drains while its
+//   last rows finish alone (~half a row's time with idle CUs: most of the
+//   55 us fixed cost of a C2 launch).  The last `slots` rows (one round) are
+//   split into kTailSplit parts, so the drain is in short parts.
+// A split part hands its histogram to the part of its row that finishes
+// last (rthx_kernels.hip), a uint4 slab store and load per lane.
+// RTHX_SPLIT_TARGET=<workgroups> replaces the slot count, RTHX_TAIL_SPLIT /
+// RTHX_TAIL_PCT the tail's parts and its rows in percent of the slots (0:
+// no tail split), RTHX_SPLIT_BELOW=<rows> splits only launches of fewer rows
+// (1: never) -- A/B knobs (profiles/round4/split_ab.log).
+constexpr int64_t kTailSplit = 4;
+constexpr int64_t kTailPct = 100;
 constexpr int64_t kSplitMinRays = 2048;
 
 // Device point-location grids: rthx_grid.cpp.  Cells per mean polygon extent
@@ -683,6 +686,7 @@ uint64_t lookback_wait_ticks() {
 // Launch geometry of one trace call (rows, split, LDS histogram layout).
 struct TracePlan {
   int64_t N = 0, R = 0, end = 0, n_rows = 0, split = 1, row_cap = 1, hash_cap = 0, bm_words = 0, part_cap = 0;
+  int64_t split_begin = 0;  // histogram tallies: rows below are unsplit, rows from here in `split` parts
   bool part_lists = false;  // split hash rows: sorted part lists + part_merge_kernel (else the last part merges)
   int tally = rthx::kTallyU16;
   int clds = 0;  // rthx_kernels.h LaunchCfg::clds
@@ -694,7 +698,9 @@ struct TracePlan {
 // (keys + counts, 8 B per slot); a workgroup traces at most 3/4 as many rays.
 constexpr int64_t kMaxHashCap = 16384;
 
-int plan_trace(const rthx_domain* dom, const rthx_trace_args* a, TracePlan& p) {
+// slots: resident workgroups of the unsplit launch (0: not known yet; rows
+// are then split only where a row's rays need it).
+int plan_trace(const rthx_domain* dom, const rthx_trace_args* a, TracePlan& p, int64_t slots = 0) {
   if (a->bin < 0 || a->bin >= dom->n_bins) return fail(RTHX_EINVAL, "bin out of range");
   if (a->rays_per_emitter < 0 || a->rays_per_emitter > 0xFFFFFFFFll)
     return fail(RTHX_ERANGE, "rays_per_emitter must be in [0, 2^32)");
@@ -712,17 +718,17 @@ int plan_trace(const rthx_domain* dom, const rthx_trace_args* a, TracePlan& p) {
   // counters of a large row); each workgroup then traces R/split rays.
   p.recording = a->n_record > 0 && a->record_bin == a->bin;
   p.split = 1;
-  const int64_t split_target = env_int("RTHX_SPLIT_TARGET", kSplitTargetBlocks, 1, 1 << 20);
-  const int64_t split_below = env_int("RTHX_SPLIT_BELOW", kSplitBelowRows, 1, 1 << 20);
-  if (!p.recording && p.n_rows > 0 && p.n_rows < split_below && R >= 2 * kSplitMinRays)
-    p.split = std::min<int64_t>((split_target + p.n_rows - 1) / p.n_rows, R / kSplitMinRays);
+  const int64_t target = env_int("RTHX_SPLIT_TARGET", slots, 0, 1 << 20);
+  const int64_t split_below = env_int("RTHX_SPLIT_BELOW", 1 << 30, 1, 1 << 30);
+  if (!p.recording && p.n_rows > 0 && p.n_rows < split_below && 2 * p.n_rows <= target && R >= 2 * kSplitMinRays)
+    p.split = std::max<int64_t>(1, std::min<int64_t>(target / p.n_rows, R / kSplitMinRays));
   if (!p.recording && R >= 65536 && ((N + 1) / 2) * 4 + rthx::kStaticLdsBytes <= (int64_t)rthx::kMaxLdsBytes &&
       N * 4 + rthx::kStaticLdsBytes > (int64_t)rthx::kMaxLdsBytes)
     p.split = std::max<int64_t>(p.split, (R + 65534) / 65535);
   int64_t rays_per_block = p.split > 1 ? (R + p.split - 1) / p.split : R;
   p.tally = rays_per_block < 65536 ? rthx::kTallyU16 : rthx::kTallyU32;
   const int64_t words = p.tally == rthx::kTallyU16 ? (N + 1) / 2 : N;
-  p.lds_bytes = (size_t)words * 4;
+  p.lds_bytes = (size_t)((words + 3) & ~int64_t(3)) * 4;  // (whole uint4s: the split rows' slab hand-off)
   p.row_cap = std::max<int64_t>(1, std::min<int64_t>(N, R));
   // Short rows over many emitters (C5 at 1e8 rays per band: R = 2426, N =
   // 41205): a hash table of the row's few distinct absorbers plus an N-bit
@@ -786,8 +792,51 @@ int plan_trace(const rthx_domain* dom, const rthx_trace_args* a, TracePlan& p) {
     p.clds = 1;
     p.lds_bytes = p.cl_offset + (size_t)dom->D.lat.bytes;
   }
+  // the last round of rows in parts (histogram tallies; see kTailSplit)
+  const int64_t tail_split = std::min<int64_t>(env_int("RTHX_TAIL_SPLIT", kTailSplit, 1, 64), R / kSplitMinRays);
+  const int64_t tail_rows = std::min<int64_t>(p.n_rows, target * env_int("RTHX_TAIL_PCT", kTailPct, 0, 1000) / 100);
+  if (p.split == 1 && p.tally != rthx::kTallyHash && !p.recording && tail_split > 1 && tail_rows > 0 &&
+      p.n_rows < split_below) {
+    p.split = tail_split;
+    p.split_begin = p.n_rows - tail_rows;
+  }
+  if (p.split_begin + (p.n_rows - p.split_begin) * p.split >= (1ll << 31))
+    return fail(RTHX_ERANGE, "too many workgroups in one call");
   p.uniform = dom->uniform_beta[a->bin] > -0.1;  // traceRay.jl:4
   return RTHX_OK;
+}
+
+// The kernel choice of a planned trace (launch_trace picks the variant and
+// workgroup size from these); the caller adds the parameters and stream.
+rthx::LaunchCfg launch_of(const rthx_domain* dom, const rthx_trace_args* a, const TracePlan& p) {
+  rthx::LaunchCfg L{};
+  L.D = dom->d_dom;
+  L.lds_bytes = p.lds_bytes;
+  L.uniform = p.uniform;
+  L.tally = p.tally;
+  L.threads = (int)env_int("RTHX_TRACE_THREADS", 0, 0, rthx::kMaxTraceThreads);
+  L.faithful = (a->flags & RTHX_FLAG_FAITHFUL_SAMPLING) != 0;
+  L.single = dom->single_convex;
+  L.clds = p.clds;
+  L.axis = dom->axis_rect && !env_flag("RTHX_NO_AXIS");
+  L.T.split = (int32_t)p.split;
+  L.T.split_begin = p.split_begin;
+  L.T.n_rows = p.n_rows;
+  L.rec.n = p.recording ? 1 : 0;
+  return L;
+}
+
+// Plan of a trace with its rows split to the unsplit launch's resident
+// workgroups (plan_trace): the occupancy of the unsplit plan's kernel, then
+// the plan again with that slot count.
+int plan_trace_split(const rthx_domain* dom, const rthx_trace_args* a, TracePlan& p) {
+  int rc = plan_trace(dom, a, p);
+  if (rc || p.split > 1 || p.recording || p.n_rows == 0 || p.R < 2 * kSplitMinRays) return rc;
+  int64_t slots = 0;
+  rthx::LaunchCfg L = launch_of(dom, a, p);
+  L.slots = &slots;
+  HIP_TRY(rthx::launch_trace(L), "trace kernel occupancy");
+  return plan_trace(dom, a, p, slots);
 }
 
 // One launch sequence of a planned trace.  lookback: the trace kernel writes
@@ -838,18 +887,20 @@ int run_trace(rthx_domain* dom, const rthx_trace_args* a, const TracePlan& p, rt
     HIP_TRY(res->stage_cnt.reserve((size_t)n_rows * p.row_cap * 4), "hipMalloc stage_cnt");
   }
   // split rows: (hash part lists) the part merge's scratch [2][n_rows][row_cap]
-  // followed by part_nnz [n_rows][split]; (histograms) one slab of the
-  // histogram's words per part, [n_rows][split][words], the arrival counters
-  // [n_rows] (zero between launches: zeroed when allocated) and the parts'
-  // tallied counts [n_rows][split]
-  const int64_t hist_words = p.tally == rthx::kTallyU16 ? (N + 1) / 2 : N;
+  // followed by part_nnz [n_rows][split]; (histograms, rows split_begin ..)
+  // one slab of the histogram's words (rounded to uint4s) per part,
+  // [split rows][split][words4], the parts' tallied counts [split rows][split]
+  // and the arrival counters [split rows] (zero between launches: zeroed
+  // when allocated)
+  const int64_t hist_words4 = ((p.tally == rthx::kTallyU16 ? (N + 1) / 2 : N) + 3) & ~int64_t(3);
+  const int64_t split_rows = n_rows - p.split_begin;
   const size_t dense_bytes = p.part_lists ? (size_t)n_rows * p.row_cap * 8 + (size_t)n_rows * p.split * 4
-                                          : (size_t)n_rows * p.split * (hist_words + 1) * 4;
+                                          : (size_t)split_rows * p.split * (hist_words4 + 1) * 4;
   if (p.split > 1) HIP_TRY(res->dense.reserve(dense_bytes), "hipMalloc dense rows");
   else res->dense.release();
   if (p.split > 1 && !p.part_lists) {
     const void* before = res->arrive.p;
-    HIP_TRY(res->arrive.reserve((size_t)n_rows * 4), "hipMalloc arrival counters");
+    HIP_TRY(res->arrive.reserve((size_t)split_rows * 4), "hipMalloc arrival counters");
     if (res->arrive.p != before) HIP_TRY(hipMemsetAsync(res->arrive.p, 0, res->arrive.cap, st), "hipMemset arrivals");
   }
 
@@ -863,13 +914,14 @@ int run_trace(rthx_domain* dom, const rthx_trace_args* a, const TracePlan& p, rt
   P.bin = a->bin;
   P.mixed = p.clds == 2 && !dom->ml_mixed.empty() ? dom->ml_mixed[a->bin] : 1;
   P.beta_uniform = dom->beta_first[a->bin];
-  P.inv_beta_uniform = P.beta_uniform > 0 ? 1.0 / P.beta_uniform : 0.0;
+  P.inv_beta_uniform = P.beta_uniform > 0 ? 1.0 / P.beta_uniform : HUGE_VAL;
 
   rthx::TallyParams T{};
   T.n_emitters = N;
   T.n_rows = n_rows;
   T.row_cap = p.row_cap;
   T.split = (int32_t)p.split;
+  T.split_begin = p.split_begin;
   T.cl_offset = p.clds ? (int32_t)p.cl_offset : 0;
   T.stage_cols = res->stage_cols.as<uint32_t>();
   T.stage_cnt = res->stage_cnt.as<uint32_t>();
@@ -878,7 +930,7 @@ int run_trace(rthx_domain* dom, const rthx_trace_args* a, const TracePlan& p, rt
   T.dense = p.split > 1 ? res->dense.as<uint32_t>() : nullptr;
   T.part_nnz = p.split > 1 && p.part_lists ? T.dense + 2 * (size_t)n_rows * p.row_cap : nullptr;
   T.row_arrive = p.split > 1 && !p.part_lists ? res->arrive.as<uint32_t>() : nullptr;
-  T.part_tallied = T.row_arrive ? T.dense + (size_t)n_rows * p.split * hist_words : nullptr;
+  T.part_tallied = T.row_arrive ? T.dense + (size_t)split_rows * p.split * hist_words4 : nullptr;
   T.part_cap = p.part_cap;
   T.hash_cap = (int32_t)p.hash_cap;
   int32_t shift = 32;
@@ -914,20 +966,11 @@ int run_trace(rthx_domain* dom, const rthx_trace_args* a, const TracePlan& p, rt
     HIP_TRY(hipMemsetAsync(T.row_tallied, 0, (size_t)n_rows * 4, st), "hipMemset row_tallied");
   HIP_TRY(hipEventRecord(dom->ev[0], st), "hipEventRecord");
   if (n_rows > 0) {
-    rthx::LaunchCfg L{};
-    L.D = dom->d_dom;
+    rthx::LaunchCfg L = launch_of(dom, a, p);
     L.P = P;
     L.T = T;
     L.rec = rec;
-    L.lds_bytes = p.lds_bytes;
     L.stream = st;
-    L.uniform = p.uniform;
-    L.tally = p.tally;
-    L.threads = (int)env_int("RTHX_TRACE_THREADS", 0, 0, rthx::kMaxTraceThreads);
-    L.faithful = (a->flags & RTHX_FLAG_FAITHFUL_SAMPLING) != 0;
-    L.single = dom->single_convex;
-    L.clds = p.clds;
-    L.axis = dom->axis_rect && !env_flag("RTHX_NO_AXIS");
     HIP_TRY(rthx::launch_trace(L), "trace_exchange_kernel launch");
   }
   HIP_TRY(hipEventRecord(dom->ev[1], st), "hipEventRecord");
@@ -954,10 +997,10 @@ int run_trace(rthx_domain* dom, const rthx_trace_args* a, const TracePlan& p, rt
 // The whole of one device's trace (validated arguments, any device state).
 int trace_exchange_one(rthx_domain* dom, const rthx_trace_args* a, rthx_result* res) {
   const double t0 = now_ms();
-  TracePlan p;
-  int rc = plan_trace(dom, a, p);
-  if (rc) return rc;
   HIP_TRY(hipSetDevice(dom->device), "hipSetDevice");
+  TracePlan p;
+  int rc = plan_trace_split(dom, a, p);
+  if (rc) return rc;
   if (res->device >= 0 && res->device != dom->device) return fail(RTHX_EINVAL, "result bound to another device");
   for (rthx_result* q : res->parts) delete q;
   res->parts.clear();

@@ -60,6 +60,12 @@ constexpr int kCosTable = 256;  // cos/sin(2 pi j / 256), j < 256
 constexpr int kLogTable = 128;  // neg_log_tab entries
 constexpr int kLogTableOffset = 2 * kCosTable;
 constexpr int kTableDoubles = kLogTableOffset + 4 * kLogTable;
+// The kernels' LDS copy of the tables holds one more double: the launch's
+// TraceParams::inv_beta_uniform, which the free path reads at its point of
+// use (a kernel-argument double kept live across the ray loop is spilled
+// with the SGPRs loaded beside it and reloaded by v_readlane every ray).
+constexpr int kTabInvBeta = kTableDoubles;
+constexpr int kLdsTableDoubles = kTableDoubles + 1;
 
 // Byte layout of the coarse mesh as multi-polygon trace kernels stage it in
 // LDS (CLDS kernels): DevPoly records at 0, then fine grids,
@@ -176,7 +182,7 @@ struct TraceParams {
   int32_t bin;
   int32_t mixed;           // MLAT kernels: some coarse box has no single beta in `bin` (walk_ml)
   double beta_uniform;     // beta of fine face 0 in `bin` (uniform path, traceRay.jl:6-11)
-  double inv_beta_uniform; // 1 / beta_uniform (0 when beta_uniform <= 0)
+  double inv_beta_uniform; // 1 / beta_uniform, +inf when beta_uniform <= 0 (then every free path is inf)
 };
 
 // ---------------------------------------------------------------------------
@@ -1498,9 +1504,10 @@ __device__ __forceinline__ int end_ml(const DevDomain& D, const MLatLds& L, cons
 template <bool UNIFORM, bool FAITHFUL>
 __device__ __forceinline__ double free_path(const TraceParams& P, const double* tabs, double u) {
   if (UNIFORM)
-    return P.beta_uniform > 0 ? (FAITHFUL ? -log(u) / P.beta_uniform
-                                          : neg_log_tab(u, tabs + kLogTableOffset) * P.inv_beta_uniform)
-                              : __builtin_inf();
+    // (u in [0, 1): -ln(u) in (0, inf], so the product with an infinite
+    // inv_beta is inf, as the reference's S for beta = 0)
+    return FAITHFUL ? (P.beta_uniform > 0 ? -log(u) / P.beta_uniform : __builtin_inf())
+                    : neg_log_tab(u, tabs + kLogTableOffset) * tabs[kTabInvBeta];
   return FAITHFUL ? -log(u) : neg_log_tab(u, tabs + kLogTableOffset);
 }
 
@@ -1509,7 +1516,7 @@ template <bool UNIFORM, bool FAITHFUL>
 __device__ __forceinline__ double free_path_u32(const TraceParams& P, const double* tabs, uint32_t w) {
   if (FAITHFUL) return free_path<UNIFORM, true>(P, tabs, u32(w));
   const double l = neg_log_u32(w, tabs + kLogTableOffset);
-  if (UNIFORM) return P.beta_uniform > 0 ? l * P.inv_beta_uniform : __builtin_inf();
+  if (UNIFORM) return l * tabs[kTabInvBeta];  // (P.inv_beta_uniform; l in (0, inf]: inf for beta_uniform <= 0)
   return l;
 }
 

@@ -192,7 +192,7 @@ RTHX_EXPORT int rthx_trace_direct(rthx_domain* dom, const double* weights, const
   Q.P.key1 = (uint32_t)(a->seed >> 32);
   Q.P.bin = a->bin;
   Q.P.beta_uniform = dom->beta_first[a->bin];
-  Q.P.inv_beta_uniform = Q.P.beta_uniform > 0 ? 1.0 / Q.P.beta_uniform : 0.0;
+  Q.P.inv_beta_uniform = Q.P.beta_uniform > 0 ? 1.0 / Q.P.beta_uniform : HUGE_VAL;
   Q.next = Wk.next.as<unsigned long long>();
   Q.alias = Wk.alias.as<uint64_t>();
   Q.el = Wk.el.as<rthx::DirectElem>();

@@ -73,7 +73,7 @@ __global__ __launch_bounds__(FAITHFUL ? kDirectThreads : kDirectMaxThreads) RTHX
   // Q.hist: Q.hist copies of the [3][n_elem] counters; wave v adds into copy
   // v % Q.hist (fewer lanes contend for one LDS address on small domains)
   extern __shared__ uint32_t hist[];
-  __shared__ double s_tab[kTableDoubles];
+  __shared__ double s_tab[kLdsTableDoubles];  // cos and log tables, inv_beta_uniform (rthx_device.h)
   __shared__ SingleCoarse s_single;
   const DevDomain& D = *Dp;
   const int tid = threadIdx.x;
@@ -91,7 +91,7 @@ __global__ __launch_bounds__(FAITHFUL ? kDirectThreads : kDirectMaxThreads) RTHX
     for (int i = tid; i < D.lat.bytes / 16; i += nthr) dst[i] = D.lat_blob[i];
   }
   if (!FAITHFUL)
-    for (int i = tid; i < kTableDoubles; i += nthr) s_tab[i] = D.tables[i];
+    for (int i = tid; i < kLdsTableDoubles; i += nthr) s_tab[i] = i < kTableDoubles ? D.tables[i] : Q.P.inv_beta_uniform;
   if (SINGLE && tid == 0) {
     s_single.poly = D.c_poly[0];
     s_single.grid = D.f_grid[0];

@@ -41,12 +41,10 @@ namespace rthx {
 #endif
 #define RTHX_ML_VIEW mlat_lds_view(lds_opaque(cl_base), D.ml)
 #define RTHX_ML_G D.ml
-#ifndef RTHX_EXP_NOWAIT
-#define RTHX_EXP_NOWAIT 0
-#endif
-#ifndef RTHX_EXP_NOWRITE
-#define RTHX_EXP_NOWRITE 0
-#endif
+// Buffer resource word 3 of a raw (stride 0) buffer on gfx9 and the cache
+// policy of an agent-scope access (sc1: write-through / coherent across XCDs).
+constexpr int kBufferRsrcWord3 = 0x00020000;
+constexpr int kSc1 = 16;
 #ifndef RTHX_REFILL_Q
 #define RTHX_REFILL_Q 24  // MLAT kernels: idle lanes before the ends are resolved and the queue refills (C5 band 0 / 7 at 1e9 rays: 8 69.7 / 43.3 ms, 16 59.2 / 36.6, 24 57.0 / 34.3, 32 59.5 / 35.5, 40 61.9 / 34.6)
 #endif
@@ -86,7 +84,7 @@ __device__ __forceinline__ uint64_t lookback_offset(unsigned long long* status, 
                                                     uint32_t epoch) {
   constexpr unsigned long long kAgg = 1ull << 62, kInc = 2ull << 62, kVal = kLbValMax;
   const unsigned long long tag = (unsigned long long)epoch << kLbEpochShift;
-  if (slot == 0 || RTHX_EXP_NOWAIT) {
+  if (slot == 0) {
     __hip_atomic_store(&status[0], kInc | tag | nnz, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return 0;
   }
@@ -113,6 +111,60 @@ __device__ __forceinline__ uint64_t lookback_offset(unsigned long long* status, 
     if ((v >> 62) == 2) break;
   }
   __hip_atomic_store(&status[slot], kInc | tag | (excl + nnz), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return excl;
+}
+
+// lookback_offset walked by the 64 lanes of one wave: each poll reads the
+// 64 predecessor words below the window's top at once, and the walk ends at
+// the nearest inclusive prefix among them once every word above it is
+// published (otherwise the wave polls the same window again).  Same words,
+// same sums as lookback_offset; called by every lane of the wave, result in
+// every lane.  A row whose predecessors finished together (a round of rows,
+// split parts) sums up to 64 aggregates per poll instead of one.
+#ifndef RTHX_LB_WAVE
+#define RTHX_LB_WAVE 1
+#endif
+__device__ __forceinline__ uint64_t lookback_offset_wave(unsigned long long* status, int64_t slot, uint32_t nnz,
+                                                         unsigned long long* stalled, uint64_t wait_ticks,
+                                                         uint32_t epoch) {
+  constexpr unsigned long long kAgg = 1ull << 62, kInc = 2ull << 62, kVal = kLbValMax;
+  const unsigned long long tag = (unsigned long long)epoch << kLbEpochShift;
+  const uint32_t lane = lane_id();
+  if (slot == 0) {
+    if (lane == 0) __hip_atomic_store(&status[0], kInc | tag | nnz, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return 0;
+  }
+  if (lane == 0) __hip_atomic_store(&status[slot], kAgg | tag | nnz, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  unsigned long long excl = 0;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  uint32_t polls = 0;
+  int64_t top = slot - 1;
+  while (true) {
+    const int64_t j = top - (int64_t)lane;
+    // (below row 0: an inclusive prefix of 0)
+    const unsigned long long v =
+        j >= 0 ? __hip_atomic_load(&status[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : (kInc | tag);
+    const bool pub = ((v >> kLbEpochShift) & kLbEpochMax) == epoch;
+    const uint64_t inc = __ballot(pub && (v >> 62) == 2);
+    const uint64_t unpub = __ballot(!pub);
+    // lanes up to the nearest inclusive prefix (all 64 when none)
+    const uint32_t m = inc ? (uint32_t)__builtin_ctzll(inc) : 63u;
+    const uint64_t upto = m == 63u ? ~0ull : ((2ull << m) - 1ull);
+    if (unpub & upto) {
+      __builtin_amdgcn_s_sleep(1);
+      if ((wait_ticks == 0 || (++polls & 15u) == 0) && __builtin_amdgcn_s_memrealtime() - t0 >= wait_ticks) {
+        if (lane == 0) atomicAdd(stalled, 1ull);
+        break;  // (the host re-traces the launch)
+      }
+      continue;
+    }
+    unsigned long long x = lane <= m ? (v & kVal) : 0ull;
+    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
+    excl += x;
+    if (inc) break;
+    top -= 64;
+  }
+  if (lane == 0) __hip_atomic_store(&status[slot], kInc | tag | (excl + nnz), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return excl;
 }
 
@@ -157,7 +209,7 @@ __device__ __forceinline__ uint32_t compact_row(int64_t n_words, F count2, uint3
   uint32_t* __restrict__ out_n = out_n_ + gbase;
   // (a row that would end past the `cap` entries reserved writes nothing:
   // base_of has flagged the overflow and the host re-traces)
-  for (int64_t w0 = wb; w0 < (gbase + total <= cap && !RTHX_EXP_NOWRITE ? we : wb); w0 += 64) {
+  for (int64_t w0 = wb; w0 < (gbase + total <= cap ? we : wb); w0 += 64) {
     const int64_t w = w0 + lane;
     uint32_t lo = 0u, hi = 0u;
     if (w < we) count2(w, lo, hi);
@@ -333,7 +385,7 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
   // SINGLE: the one coarse polygon and its fine grid, also in LDS, so that
   // its 16 doubles do not occupy SGPRs for the whole loop.
   __shared__ SingleCoarse s_single;
-  __shared__ double s_tab[kTableDoubles];  // cos and log tables (rthx_device.h)
+  __shared__ double s_tab[kLdsTableDoubles];  // cos and log tables, inv_beta_uniform (rthx_device.h)
 
   // CL: what sits in LDS behind the row tally.  SINGLE: 1 = the lattice of
   // the one coarse rectangle (LAT).  Multi-polygon: 1 = the coarse mesh
@@ -341,17 +393,30 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
   constexpr bool CLDS = CL != 0;
   constexpr bool MLAT = CL == 2 && !SINGLE;
   const int tid = threadIdx.x;
-  const int64_t slot = SPLIT ? (int64_t)(blockIdx.x / T.split) : (int64_t)blockIdx.x;
-  const int64_t part = SPLIT ? (int64_t)(blockIdx.x % T.split) : 0;
-  const int64_t chunk = SPLIT ? (P.R + T.split - 1) / T.split : P.R;
-  const int64_t r_begin = part * chunk;
+  // SPLIT: rows [0, split_begin) are one workgroup each, as unsplit; every
+  // later row is `split` workgroups, part p tracing rays [p chunk, (p+1) chunk)
+  // (the last round of rows split, so a launch drains in short parts; or all
+  // rows when there are too few to fill the chip).  32-bit: R < 2^32.
+  const uint32_t bid = blockIdx.x;
+  const uint32_t sb = SPLIT ? (uint32_t)T.split_begin : 0u;
+  const bool tail = SPLIT && bid >= sb;  // (workgroup-uniform)
+  const uint32_t parts = tail ? (uint32_t)T.split : 1u;
+  const uint32_t trow = tail ? (bid - sb) / parts : 0u;  // index among the split rows
+  const uint32_t tpart = tail ? (bid - sb) - trow * parts : 0u;
+  const int64_t slot = tail ? (int64_t)sb + trow : (int64_t)bid;
+  const int64_t part = tpart;
+  const uint32_t chunk = tail ? (uint32_t)((P.R + parts - 1) / parts) : (uint32_t)P.R;
+  const int64_t r_begin = SPLIT ? (int64_t)(tpart * chunk) : 0;
   const int64_t r_end = SPLIT ? (r_begin + chunk < P.R ? r_begin + chunk : P.R) : P.R;
   const int64_t g = P.g_begin + slot * P.g_stride;
   constexpr bool PACK16 = TALLY == kTallyU16, HASH = TALLY == kTallyHash;
   const int64_t n_words = HASH ? 2 * (int64_t)T.hash_cap + T.bm_words : PACK16 ? (T.n_emitters + 1) / 2 : T.n_emitters;
 
   const int nthr = (int)blockDim.x;  // 256, 512 or 1024 (launch_trace_t)
-  for (int64_t w = tid; w < n_words; w += nthr) hist[w] = 0u;
+  // (split histogram kernels: through the 16-byte padding too, which the
+  // slab hand-off moves as whole uint4s; the host sizes LDS for it)
+  const int64_t z_words = SPLIT && !HASH ? (n_words + 3) & ~int64_t(3) : n_words;
+  for (int64_t w = tid; w < z_words; w += nthr) hist[w] = 0u;
   // CLDS: the coarse mesh behind the histogram (T.cl_offset bytes in), and
   // this bin's coarse betas
   char RTHX_LDS* cl_base = (char RTHX_LDS*)hist + T.cl_offset;
@@ -385,7 +450,7 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
     for (int i = tid; i < D.n_coarse; i += nthr) cb[i] = D.c_beta[(size_t)P.bin * D.n_coarse + i];
   }
   if (!FAITHFUL)
-    for (int i = tid; i < kTableDoubles; i += nthr) s_tab[i] = D.tables[i];
+    for (int i = tid; i < kLdsTableDoubles; i += nthr) s_tab[i] = i < kTableDoubles ? D.tables[i] : P.inv_beta_uniform;
   if (tid == 0) {
     s_tallied = 0u;
     s_next = (uint32_t)r_begin;
@@ -750,63 +815,86 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
   // Split rows: hand this part's histogram to the part of the row that
   // finishes last, which then writes the whole row as an unsplit row does
   // (direct CSR by look-back, or its staging slot).  Hand-off (agent scope,
-  // every XCD): the slab and the tallied count are stored write-through
-  // (sc1), every storing wave drains them (vmcnt 0) before the barrier, one
+  // every XCD): part p stores its histogram as uint4s into slab p of the row
+  // and its tallied count, all write-through (sc1, the encoding of an
+  // agent-scope atomic store), drains them (vmcnt 0) before the barrier; one
   // lane arrives on the row's counter, and the part whose arrival returns
-  // split - 1 reads the other slabs with sc1 loads.  It resets the counter,
-  // so the counters are zero between launches.
+  // parts - 1 sums the row's slabs with sc1 loads, a uint4 per lane and up to
+  // four slabs in flight.  It resets the counter, so the counters are zero
+  // between launches.
   __shared__ uint32_t s_merge;  // bit 0: this part arrived last; bit 1: a packed pair overflowed 16 bits
-  const int64_t split = SPLIT ? T.split : 1;
-  const uint32_t* slabs = SPLIT ? T.dense + (size_t)slot * (size_t)split * (size_t)n_words : nullptr;
-  if constexpr (SPLIT) {
-    uint32_t* mine = T.dense + (size_t)blockIdx.x * (size_t)n_words;
-    for (int64_t w = tid; w < n_words; w += nthr)
-      __hip_atomic_store(&mine[w], hist[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (tid == 0) __hip_atomic_store(&T.part_tallied[blockIdx.x], s_tallied, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) {
-      const uint32_t before =
-          __hip_atomic_fetch_add(&T.row_arrive[slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const bool last = before + 1u == (uint32_t)split;
-      if (last) {
-        __hip_atomic_store(&T.row_arrive[slot], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        uint32_t t = 0;
-        for (int64_t p = 0; p < split; ++p)
-          t += p == part ? s_tallied
-                         : __hip_atomic_load(&T.part_tallied[slot * split + p], __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT);
-        s_tallied = t;
+  typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+  const int64_t wstride = (n_words + 3) & ~int64_t(3);  // slab words (whole uint4s)
+  const uint32_t* slabs = tail ? T.dense + (size_t)trow * parts * (size_t)wstride : nullptr;
+  if constexpr (SPLIT && !HASH) {
+    if (tail) {
+      const __amdgpu_buffer_rsrc_t srsrc =
+          __builtin_amdgcn_make_buffer_rsrc((void*)slabs, 0, (int)(parts * wstride * 4), kBufferRsrcWord3);
+      const u4 RTHX_LDS* h4 = (const u4 RTHX_LDS*)(uint32_t RTHX_LDS*)hist;
+      const uint32_t nq = (uint32_t)(wstride / 4);
+      for (uint32_t c = tid; c < nq; c += (uint32_t)nthr)
+        __builtin_amdgcn_raw_buffer_store_b128(h4[c], srsrc, (int)((tpart * wstride + 4 * c) * 4), 0, kSc1);
+      if (tid == 0)
+        __hip_atomic_store(&T.part_tallied[(size_t)trow * parts + tpart], s_tallied, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) {
+        const uint32_t before =
+            __hip_atomic_fetch_add(&T.row_arrive[trow], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const bool last = before + 1u == parts;
+        if (last) {
+          __hip_atomic_store(&T.row_arrive[trow], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          uint32_t t = 0;
+          for (uint32_t p = 0; p < parts; ++p)
+            t += p == tpart ? s_tallied
+                            : __hip_atomic_load(&T.part_tallied[(size_t)trow * parts + p], __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+          s_tallied = t;
+        }
+        s_merge = last ? 1u : 0u;
       }
-      s_merge = last ? 1u : 0u;
-    }
-    __syncthreads();
-    if (!(s_merge & 1u)) return;
-    // The other parts' counts into this part's histogram.  Packed 16-bit
-    // pairs cannot overflow when R < 65536; otherwise a pair that would
-    // leaves the histogram alone and the row is counted from the slabs.
-    bool ovf = false;
-    for (int64_t w = tid; w < n_words; w += nthr) {
-      const uint32_t own = hist[w];
-      uint32_t lo = PACK16 ? (own & 0xFFFFu) : own, hi = PACK16 ? (own >> 16) : 0u;
-      for (int64_t p = 0; p < split; ++p) {
-        if (p == part) continue;
-        const uint32_t v = __hip_atomic_load(&slabs[p * n_words + w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        lo += PACK16 ? (v & 0xFFFFu) : v;
-        hi += PACK16 ? (v >> 16) : 0u;
+      __syncthreads();
+      if (!(s_merge & 1u)) return;
+      // The row's counts: the sum of its slabs (this part's own included).
+      // Packed 16-bit pairs cannot overflow when R < 65536; otherwise a pair
+      // that would leaves the histogram alone and the row is counted from
+      // the slabs.
+      u4 RTHX_LDS* w4 = (u4 RTHX_LDS*)(uint32_t RTHX_LDS*)hist;
+      bool ovf = false;
+      for (uint32_t c = tid; c < nq; c += (uint32_t)nthr) {
+        u4 lo = {0u, 0u, 0u, 0u}, hi = {0u, 0u, 0u, 0u};
+        for (uint32_t p0 = 0; p0 < parts; p0 += 4) {
+          u4 v[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            v[j] = p0 + j < parts
+                       ? __builtin_amdgcn_raw_buffer_load_b128(srsrc, (int)(((p0 + j) * wstride + 4 * c) * 4), 0, kSc1)
+                       : u4{0u, 0u, 0u, 0u};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            lo += PACK16 ? (v[j] & 0xFFFFu) : v[j];
+            if (PACK16) hi += v[j] >> 16;
+          }
+        }
+        if (PACK16) {
+          const u4 o = lo | hi;
+          if ((o.x | o.y | o.z | o.w) > 0xFFFFu) ovf = true;
+          else w4[c] = lo | (hi << 16);
+        } else {
+          w4[c] = lo;
+        }
       }
-      if (PACK16 && (lo | hi) > 0xFFFFu) ovf = true;
-      else hist[w] = PACK16 ? (lo | (hi << 16)) : lo;
+      if (ovf) atomicOr(&s_merge, 2u);
+      __syncthreads();
     }
-    if (ovf) atomicOr(&s_merge, 2u);
-    __syncthreads();
   }
-  const bool from_slabs = SPLIT && PACK16 && __builtin_amdgcn_readfirstlane((int)(s_merge & 2u)) != 0;
+  const bool from_slabs = SPLIT && PACK16 && tail && __builtin_amdgcn_readfirstlane((int)(s_merge & 2u)) != 0;
   auto count2 = [&](int64_t w, uint32_t& lo, uint32_t& hi) {
     if (SPLIT && PACK16 && from_slabs) {  // (rare: R >= 65536 and one absorber took 65536 of them)
       lo = hi = 0u;
-      for (int64_t p = 0; p < split; ++p) {
-        const uint32_t v = __hip_atomic_load(&slabs[p * n_words + w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (uint32_t p = 0; p < parts; ++p) {
+        const uint32_t v = __hip_atomic_load(&slabs[p * wstride + w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         lo += v & 0xFFFFu;
         hi += v >> 16;
       }
@@ -818,9 +906,14 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
   };
   if (SINGLE && T.lb_status) {  // (host: single-polygon domains only; keeps the other kernels lean)
     auto base_of = [&](uint32_t nnz) -> uint64_t {
-      if (tid == 0) {
-        s_base = lookback_offset(T.lb_status, slot, nnz, &T.totals[3], T.lb_wait_ticks, T.lb_epoch);
-        if (s_base + nnz > (uint64_t)T.out_cap) atomicAdd(&T.totals[4], 1ull);  // (the host re-traces)
+      if (RTHX_LB_WAVE ? tid < 64 : tid == 0) {
+        const uint64_t b = RTHX_LB_WAVE
+                               ? lookback_offset_wave(T.lb_status, slot, nnz, &T.totals[3], T.lb_wait_ticks, T.lb_epoch)
+                               : lookback_offset(T.lb_status, slot, nnz, &T.totals[3], T.lb_wait_ticks, T.lb_epoch);
+        if (tid == 0) {
+          s_base = b;
+          if (b + nnz > (uint64_t)T.out_cap) atomicAdd(&T.totals[4], 1ull);  // (the host re-traces)
+        }
       }
       __syncthreads();
       return s_base;
@@ -1058,29 +1151,44 @@ struct OccKey {
     return kern != o.kern ? kern < o.kern : lds != o.lds ? lds < o.lds : device < o.device;
   }
 };
+struct OccVal {
+  int threads, per_cu;
+};
 static std::mutex g_occ_mu;
-static std::map<OccKey, int> g_occ;
+static std::map<OccKey, OccVal> g_occ;
 static int occ_device() {
   int d = 0;
   (void)hipGetDevice(&d);
   return d;
 }
-static int occupancy_cache_get(const void* kern, size_t lds) {
+static OccVal occupancy_cache_get(const void* kern, size_t lds) {
   const OccKey k{kern, lds, occ_device()};
   std::lock_guard<std::mutex> g(g_occ_mu);
   auto it = g_occ.find(k);
-  return it == g_occ.end() ? 0 : it->second;
+  return it == g_occ.end() ? OccVal{0, 0} : it->second;
 }
-static void occupancy_cache_put(const void* kern, size_t lds, int threads) {
+static void occupancy_cache_put(const void* kern, size_t lds, OccVal v) {
   const OccKey k{kern, lds, occ_device()};
   std::lock_guard<std::mutex> g(g_occ_mu);
-  g_occ[k] = threads;
+  g_occ[k] = v;
+}
+static int device_cus() {
+  static std::mutex mu;
+  static std::map<int, int> cus;
+  const int d = occ_device();
+  std::lock_guard<std::mutex> g(mu);
+  auto it = cus.find(d);
+  if (it != cus.end()) return it->second;
+  int n = 0;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess) n = 0;
+  cus[d] = n;
+  return n;
 }
 
 template <bool UNIFORM, int TALLY, bool FAITHFUL, bool SINGLE, bool REC, bool SPLIT, bool AXIS, int CL = 0>
 static hipError_t launch_trace_t(const LaunchCfg& L) {
   auto kern = trace_exchange_kernel<UNIFORM, TALLY, FAITHFUL, SINGLE, REC, SPLIT, AXIS, CL>;
-  const int64_t blocks = L.T.n_rows * (SPLIT ? L.T.split : 1);
+  const int64_t blocks = SPLIT ? L.T.split_begin + (L.T.n_rows - L.T.split_begin) * L.T.split : L.T.n_rows;
   // (MLAT kernels: a 64-slot ray queue per wave behind the lattice)
   auto lds_for = [&](int t) { return L.lds_bytes + (CL == 2 && !SINGLE ? (size_t)t * kRaySlotBytes : 0); };
   // Workgroup size: the one that keeps most waves resident per CU.  With a
@@ -1099,9 +1207,10 @@ static hipError_t launch_trace_t(const LaunchCfg& L) {
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_max);
     if (e != hipSuccess) return e;
   }
-  int threads = occupancy_cache_get((const void*)kern, L.lds_bytes);
+  OccVal occ = occupancy_cache_get((const void*)kern, L.lds_bytes);
+  int threads = occ.threads;
   if (threads == 0) {
-    int best_waves = 0;
+    int best_waves = 0, best_per_cu = 0;
     threads = kTraceThreads;
     bool queried = true;
     for (int t = kTraceThreads; t <= kMaxTraceThreads; t *= 2) {
@@ -1118,13 +1227,24 @@ static hipError_t launch_trace_t(const LaunchCfg& L) {
       const int waves = per_cu * (t / 64);
       if (waves > best_waves || (waves == best_waves && t <= 512)) {
         best_waves = waves;
+        best_per_cu = per_cu;
         threads = t;
       }
     }
-    if (queried) occupancy_cache_put((const void*)kern, L.lds_bytes, threads);
+    occ = OccVal{threads, best_per_cu};
+    if (queried) occupancy_cache_put((const void*)kern, L.lds_bytes, occ);
   }
   if (L.threads == 256 || L.threads == 512 || L.threads == 1024) threads = L.threads;
   const size_t lds = lds_for(threads);
+  if (L.slots) {
+    int per_cu = occ.per_cu;
+    if (threads != occ.threads || per_cu == 0) {
+      hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, threads, lds);
+      if (e != hipSuccess) return e;
+    }
+    *L.slots = (int64_t)per_cu * device_cus();
+    return hipSuccess;
+  }
   hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(threads), lds, L.stream, L.D, L.P, L.T, L.rec);
   return hipGetLastError();
 }

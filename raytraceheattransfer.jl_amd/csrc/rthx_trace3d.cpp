@@ -255,7 +255,9 @@ void layout_nodes(std::vector<rthx::Bvh2Node>& nodes) {
   std::vector<char> taken(n, 0);
   std::vector<int> frontier{0};
   taken[0] = 1;
-  for (size_t h = 0; h < frontier.size() && (int)order.size() < rthx::kTopNodes; ++h) {
+  int bfs_top = rthx::kTopNodes;
+  if (const char* e = getenv("RTHX_T3_BFS_TOP")) bfs_top = std::max(1, atoi(e));  // (A/B: larger LDS tops)
+  for (size_t h = 0; h < frontier.size() && (int)order.size() < bfs_top; ++h) {
     const int i = frontier[h];
     order.push_back(i);
     for (int c = 0; c < 2; ++c) {
@@ -581,6 +583,11 @@ RTHX_EXPORT int rthx_trace_exchange_3d(rthx_scene3d* sc, const rthx_trace_args* 
       L.ghist = sc->ghist_choice[slot_k] == 1;
     }
     if (L.ghist) L.lds_bytes = rthx::trace3d_dynamic_lds(0, sc->S.stack);
+    if (getenv("RTHX_T3_DYNTOP")) {  // (A/B: as many top nodes as the LDS left holds, in dynamic LDS)
+      const int64_t room = (int64_t)rthx::kMaxLdsBytes - (int64_t)L.lds_bytes - 2048;
+      L.n_dyn = (int)std::max<int64_t>(1, std::min<int64_t>(sc->S.n_nodes, room / (int64_t)sizeof(rthx::Bvh2Node)));
+      if (const char* e = getenv("RTHX_T3_DYNTOP_MAX")) L.n_dyn = std::min(L.n_dyn, std::max(1, atoi(e)));
+    }
     HIP_TRY(rthx::launch_trace3d(L), "trace_exchange_3d_kernel launch");
   }
   HIP_TRY(hipEventRecord(sc->ev[1], st), "hipEventRecord");

@@ -88,6 +88,7 @@ struct Trace3dLaunch {
   bool pack16;  // < 65536 rays per workgroup: u16 row-histogram counters
   bool ghist;   // counts straight to the dense rows (no LDS histogram)
   int* top_choice;  // [ghist * 4 + faithful * 2 + pack16]: LDS node-cache size (64 / 128), -1 = not chosen yet
+  int n_dyn = 0;    // > 0: that many top nodes in dynamic LDS behind the stacks (RTHX_T3_DYNTOP)
 };
 
 hipError_t launch_trace3d(const Trace3dLaunch& L);

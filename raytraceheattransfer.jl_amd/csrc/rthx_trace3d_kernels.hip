@@ -288,14 +288,18 @@ __device__ __forceinline__ void emit_ray(const Emit3& E, const double* tab, uint
 // workgroups; they are built for 6 waves per SIMD (80 VGPRs, no spills;
 // config 4 L4 7.59 -> 7.83 Grays/s), the LDS-histogram ones keep the
 // compiler's 86 (5 waves: a 6-wave budget measured 1 % slower at L3).
+// TOP = 0: the top n_dyn nodes (as many as the LDS left by the histogram
+// and the stacks holds) in dynamic LDS behind the stacks.
 template <bool FAITHFUL, bool PACK16, int TOP, bool GH = false>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(GH ? kGhWaves : kHistWaves))) void trace_exchange_3d_kernel(const DevScene3D* __restrict__ Sp,
-                                                                                  TraceParams P, TallyParams T) {
-  // dynamic LDS: [row histogram][walk stacks] (GH: the stacks only)
+                                                                                  TraceParams P, TallyParams T, int n_dyn) {
+  // dynamic LDS: [row histogram][walk stacks][(TOP = 0) top nodes] (GH: no histogram)
   extern __shared__ uint32_t hist[];
-  __shared__ Bvh2Node s_top[TOP];
-  Bvh2Node RTHX_LDS* top = (Bvh2Node RTHX_LDS*)&s_top[0];
-  const int n_top = TOP < Sp->n_nodes ? TOP : Sp->n_nodes;
+  __shared__ Bvh2Node s_top[TOP > 0 ? TOP : 1];
+  const int64_t words_ = GH ? 0 : PACK16 ? (T.n_emitters + 1) / 2 : T.n_emitters;
+  Bvh2Node RTHX_LDS* top = TOP > 0 ? (Bvh2Node RTHX_LDS*)&s_top[0]
+                                   : (Bvh2Node RTHX_LDS*)(hist + trace3d_stack_offset(words_) + (size_t)Sp->stack * kThreads);
+  const int n_top = TOP > 0 ? (TOP < Sp->n_nodes ? TOP : Sp->n_nodes) : n_dyn;
 #if RTHX_T3_GTAB
   const double* s_tab = S_tables_of(Sp);  // the azimuth table read from global memory (L1/L2): no LDS
 #else
@@ -413,6 +417,17 @@ hipError_t launch_variant(const Trace3dLaunch& L) {
   // one (occupancy queries are slow host calls: the choice is kept per scene
   // and kernel variant in L.top_choice).
   int& top = L.top_choice[(GH ? 4 : 0) + (FAITHFUL ? 2 : 0) + (PACK16 ? 1 : 0)];
+  if (L.n_dyn > 0) {  // (RTHX_T3_DYNTOP: the top nodes in dynamic LDS)
+    auto kd = t3::trace_exchange_3d_kernel<FAITHFUL, PACK16, 0, GH>;
+    const size_t lds = L.lds_bytes + (size_t)L.n_dyn * sizeof(Bvh2Node);
+    if (lds > 64 * 1024) {
+      hipError_t e = hipFuncSetAttribute((const void*)kd, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      if (e != hipSuccess) return e;
+    }
+    const int64_t blocks = L.T.n_rows * L.T.split;
+    hipLaunchKernelGGL(kd, dim3((unsigned)blocks), dim3(t3::kThreads), lds, L.stream, L.S, L.P, L.T, L.n_dyn);
+    return hipGetLastError();
+  }
   if (top < 0) {
     int pc64 = 0, pc128 = 0;
     hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
@@ -430,7 +445,7 @@ hipError_t launch_variant(const Trace3dLaunch& L) {
     if (e != hipSuccess) return e;
   }
   const int64_t blocks = L.T.n_rows * L.T.split;
-  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(t3::kThreads), L.lds_bytes, L.stream, L.S, L.P, L.T);
+  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(t3::kThreads), L.lds_bytes, L.stream, L.S, L.P, L.T, 0);
   return hipGetLastError();
 }
 

@@ -202,14 +202,17 @@ def test_group_validation(hip):
 
 
 
-def test_config4_full_size_sampled_rows(hip):
-    """BASELINE config 4 at full size (cube 10x10 per face + icosphere L3,
-    1e8 rays, face groups): every ray is absorbed (closed enclosure), and
-    sampled rows equal the CPU restatement exactly at full R."""
+@pytest.mark.parametrize("ndim,level", [(11, 2), (11, 3), (10, 3)])
+def test_config4_full_size_sampled_rows(hip, ndim, level):
+    """BASELINE config 4 at full size (1e8 rays, face groups): the surveyed
+    cube Ndim = 11 per face (726 quads, reference readme.md:435-466) with
+    icosphere L2 and L3, and the 10x10 + L3 scene of earlier rounds.  Every
+    ray is absorbed (closed enclosure), and sampled rows -- cube faces and a
+    sphere triangle -- equal the CPU restatement exactly at full R."""
     from rthx.trace3d import Scene3D
 
-    xyz, nv, nrm, nc = H.cube_icosphere_scene(ndim=10, level=3)
-    g = H.cube_icosphere_groups(10, 3)
+    xyz, nv, nrm, nc = H.cube_icosphere_scene(ndim=ndim, level=level)
+    g = H.cube_icosphere_groups(ndim, level)
     n = len(nv)
     R = 100_000_000 // n
     s = Scene3D(xyz, nv, nrm, groups=g)
@@ -219,7 +222,7 @@ def test_config4_full_size_sampled_rows(hip):
         s.close()
     assert info["rays_traced"] == n * R and info["lost_total"] == 0
     assert int(cnt.sum()) == n * R
-    stride = n // 4  # rows 0, 470 (cube faces), 940, 1410 (sphere triangles)
+    stride = n // 4  # rows 0, n/4, n/2 (cube faces at 11x11 + L2/L3), 3n/4 (a sphere triangle)
     C, lost = oracle.trace_exchange_3d(xyz, nv, nrm, R, seed=21, begin=0, end=4 * stride, stride=stride,
                                        nthreads=4, groups=g)
     assert lost == 0

@@ -72,6 +72,7 @@ def main():
     ap.add_argument("kernel")
     ap.add_argument("--top", type=int, default=80)
     ap.add_argument("--loops", type=int, default=2, help="full histograms of this many fp64-heaviest loops")
+    ap.add_argument("--dump", default="", help="print instructions FIRST-LAST (the numbering of the loop list)")
     a = ap.parse_args()
     body, name = kernel_lines(a.asm, a.kernel)
     print(f"kernel: {name}")
@@ -95,6 +96,14 @@ def main():
                 j = labels[tgt]
                 loops[j] = max(loops.get(j, i), i)
     spans = sorted(loops.items())
+    if a.dump:
+        first, last = (int(x) for x in a.dump.split("-"))
+        at = {v: k for k, v in labels.items()}
+        for t in range(first, last + 1):
+            if t in at:
+                print(f"{at[t]}:")
+            print(f"  {t:5d}  {insts[t][1]}")
+        return
     print(f"{len(insts)} instructions, {len(spans)} loops")
     rows = []
     for j, i in spans:
