@@ -14,6 +14,9 @@ Tolerances: RMS over all N^2 entries of F_smooth <= 1e-3 (north_star); the
 C&S centreline within the reference's rtol 0.05 (test/test_2d_grey.jl:216)
 and the energy error < 1e-4 W (:220).
 """
+import json
+import os
+
 import numpy as np
 import pytest
 
@@ -48,8 +51,16 @@ def test_f_smooth_rms_vs_1e9_ray_reference(traced):
     rms = float(np.sqrt(np.mean(d * d)))
     nz = Fb > 0
     rms_nz = float(np.sqrt(np.mean(d[nz] ** 2)))
+    rel = float(np.linalg.norm(d) / np.linalg.norm(Fb))
     print(f"F_smooth RMS vs 1e9 rays: all entries {rms:.3e}, nonzero entries {rms_nz:.3e}, "
-          f"max |dF| {np.abs(d).max():.3e}")
+          f"relative (Frobenius) {rel:.3e}, max |dF| {np.abs(d).max():.3e}")
+    rec = os.environ.get("RTHX_ACCURACY_RECORD")  # (measurement runs: the numbers as JSON)
+    if rec:
+        with open(rec, "w") as f:
+            json.dump({"config": "101x101 grey kappa=1, F_smooth of 1e8 rays vs 1e9 rays (independent seeds)",
+                       "n": int(n), "rms_all_entries": rms, "rms_nonzero_entries": rms_nz,
+                       "nonzero_fraction": float(nz.mean()), "relative_frobenius": rel,
+                       "max_abs_dF": float(np.abs(d).max()), "bar": "RMS <= 1e-3 (north_star)"}, f, indent=1)
     assert rms <= 1e-3
     assert rms_nz <= 1e-3
     assert np.allclose(Fa.sum(axis=1), 1.0, atol=1e-9) and np.allclose(Fb.sum(axis=1), 1.0, atol=1e-9)
