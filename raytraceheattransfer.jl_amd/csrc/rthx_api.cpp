@@ -132,23 +132,18 @@ int check_grid(const rthx_grid_desc& g, int32_t count, const char* what) {
   return RTHX_OK;
 }
 
-// Row splitting, from `slots`: the unsplit kernel's resident workgroups
-// (CUs x workgroups per CU, from the occupancy query).
-// - A launch of fewer rows than half the slots leaves CUs idle for the whole
-//   trace: every row is split into floor(slots / rows) parts, all resident in
-//   one round.
-// - Otherwise rows start as slots free up, and the launch drains while its
-//   last rows finish alone (~half a row's time with idle CUs: most of the
-//   55 us fixed cost of a C2 launch).  The last `slots` rows (one round) are
-//   split into kTailSplit parts, so the drain is in short parts.
-// A split part hands its histogram to the part of its row that finishes
-// last (rthx_kernels.hip), a uint4 slab store and load per lane.
-// RTHX_SPLIT_TARGET=<workgroups> replaces the slot count, RTHX_TAIL_SPLIT /
-// RTHX_TAIL_PCT the tail's parts and its rows in percent of the slots (0:
-// no tail split), RTHX_SPLIT_BELOW=<rows> splits only launches of fewer rows
-// (1: never) -- A/B knobs (profiles/round4/split_ab.log).
-constexpr int64_t kTailSplit = 4;
-constexpr int64_t kTailPct = 100;
+// Row splitting.  A launch of fewer rows than half the chip's resident
+// workgroup slots (CUs x workgroups per CU of the unsplit kernel, from the
+// occupancy query) leaves CUs idle for the whole trace, so every row is
+// split into floor(slots / rows) parts, all resident in one round.  A split
+// part hands its histogram to the part of its row that finishes last
+// (rthx_kernels.hip, a uint4 slab store and load per lane).  Larger launches
+// stay unsplit: the emulated 8-rank C2 strong shard (1326 rows, 1024 slots)
+// runs 0.145 ms unsplit against 0.173 / 0.208 / 0.254 ms split into 2 / 3 /
+// 4 parts, and splitting only the last round of rows (the drain) into 2 or
+// 4 parts measured slower at every W (profiles/round4/ab/tail_split_*.log).
+// RTHX_SPLIT_TARGET=<workgroups> replaces the slot count and
+// RTHX_SPLIT_BELOW=<rows> splits only launches of fewer rows (1: never).
 constexpr int64_t kSplitMinRays = 2048;
 
 // Device point-location grids: rthx_grid.cpp.  Cells per mean polygon extent
@@ -686,7 +681,6 @@ uint64_t lookback_wait_ticks() {
 // Launch geometry of one trace call (rows, split, LDS histogram layout).
 struct TracePlan {
   int64_t N = 0, R = 0, end = 0, n_rows = 0, split = 1, row_cap = 1, hash_cap = 0, bm_words = 0, part_cap = 0;
-  int64_t split_begin = 0;  // histogram tallies: rows below are unsplit, rows from here in `split` parts
   bool part_lists = false;  // split hash rows: sorted part lists + part_merge_kernel (else the last part merges)
   int tally = rthx::kTallyU16;
   int clds = 0;  // rthx_kernels.h LaunchCfg::clds
@@ -792,16 +786,7 @@ int plan_trace(const rthx_domain* dom, const rthx_trace_args* a, TracePlan& p, i
     p.clds = 1;
     p.lds_bytes = p.cl_offset + (size_t)dom->D.lat.bytes;
   }
-  // the last round of rows in parts (histogram tallies; see kTailSplit)
-  const int64_t tail_split = std::min<int64_t>(env_int("RTHX_TAIL_SPLIT", kTailSplit, 1, 64), R / kSplitMinRays);
-  const int64_t tail_rows = std::min<int64_t>(p.n_rows, target * env_int("RTHX_TAIL_PCT", kTailPct, 0, 1000) / 100);
-  if (p.split == 1 && p.tally != rthx::kTallyHash && !p.recording && tail_split > 1 && tail_rows > 0 &&
-      p.n_rows < split_below) {
-    p.split = tail_split;
-    p.split_begin = p.n_rows - tail_rows;
-  }
-  if (p.split_begin + (p.n_rows - p.split_begin) * p.split >= (1ll << 31))
-    return fail(RTHX_ERANGE, "too many workgroups in one call");
+  if (p.n_rows * p.split >= (1ll << 31)) return fail(RTHX_ERANGE, "too many workgroups in one call");
   p.uniform = dom->uniform_beta[a->bin] > -0.1;  // traceRay.jl:4
   return RTHX_OK;
 }
@@ -820,7 +805,6 @@ rthx::LaunchCfg launch_of(const rthx_domain* dom, const rthx_trace_args* a, cons
   L.clds = p.clds;
   L.axis = dom->axis_rect && !env_flag("RTHX_NO_AXIS");
   L.T.split = (int32_t)p.split;
-  L.T.split_begin = p.split_begin;
   L.T.n_rows = p.n_rows;
   L.rec.n = p.recording ? 1 : 0;
   return L;
@@ -863,14 +847,18 @@ int run_trace(rthx_domain* dom, const rthx_trace_args* a, const TracePlan& p, rt
     res->stage_cnt.release();
     const int64_t worst = n_rows * p.row_cap;
     const bool same = res->lb_hint_shape[0] == N && res->lb_hint_shape[1] == n_rows && res->lb_hint_shape[2] == R;
+    // (a first launch of a shape reserves the worst case when it is at most
+    // 256 Mi entries -- 2 GiB of columns and counts; C2: 100 M entries, 800
+    // MB -- so it never re-traces; round 3's 2048 entries per row made the
+    // first C2 launch overflow and trace twice, profiles/round4/overflow_cost.json)
+    const int64_t first_guess = worst <= (int64_t(1) << 28) ? worst : std::max<int64_t>(1 << 20, n_rows * std::min<int64_t>(p.row_cap, 4096));
     int64_t want = same && res->lb_nnz_hint > 0
                        ? res->lb_nnz_hint + res->lb_nnz_hint / 8 + 65536
-                       : env_int("RTHX_CSR_CAP", std::max<int64_t>(1 << 20, n_rows * std::min<int64_t>(p.row_cap, 2048)),
-                                 1, worst);  // (tests force a small first guess)
+                       : env_int("RTHX_CSR_CAP", first_guess, 1, worst);  // (tests force a small first guess)
     want = std::min<int64_t>(worst, want);
     want = std::max<int64_t>(want, 1);
     for (rthx::DevBuf* b : {&res->cols, &res->cnt}) {
-      if (b->cap > 2 * (size_t)want * 4 + (64u << 20)) b->release();  // (a much larger earlier trace)
+      if (b->cap > 4 * (size_t)want * 4 + (256u << 20)) b->release();  // (a much larger earlier trace; not the worst-case first guess of this shape)
       HIP_TRY(b->reserve((size_t)want * 4), "hipMalloc direct CSR");
     }
     // fresh words or totals (or a wrapped epoch): zero them once, epoch 1
@@ -887,13 +875,12 @@ int run_trace(rthx_domain* dom, const rthx_trace_args* a, const TracePlan& p, rt
     HIP_TRY(res->stage_cnt.reserve((size_t)n_rows * p.row_cap * 4), "hipMalloc stage_cnt");
   }
   // split rows: (hash part lists) the part merge's scratch [2][n_rows][row_cap]
-  // followed by part_nnz [n_rows][split]; (histograms, rows split_begin ..)
-  // one slab of the histogram's words (rounded to uint4s) per part,
-  // [split rows][split][words4], the parts' tallied counts [split rows][split]
-  // and the arrival counters [split rows] (zero between launches: zeroed
-  // when allocated)
+  // followed by part_nnz [n_rows][split]; (histograms) one slab of the
+  // histogram's words (rounded to uint4s) per part, [n_rows][split][words4],
+  // the parts' tallied counts [n_rows][split] and the arrival counters
+  // [n_rows] (zero between launches: zeroed when allocated)
   const int64_t hist_words4 = ((p.tally == rthx::kTallyU16 ? (N + 1) / 2 : N) + 3) & ~int64_t(3);
-  const int64_t split_rows = n_rows - p.split_begin;
+  const int64_t split_rows = n_rows;
   const size_t dense_bytes = p.part_lists ? (size_t)n_rows * p.row_cap * 8 + (size_t)n_rows * p.split * 4
                                           : (size_t)split_rows * p.split * (hist_words4 + 1) * 4;
   if (p.split > 1) HIP_TRY(res->dense.reserve(dense_bytes), "hipMalloc dense rows");
@@ -921,7 +908,6 @@ int run_trace(rthx_domain* dom, const rthx_trace_args* a, const TracePlan& p, rt
   T.n_rows = n_rows;
   T.row_cap = p.row_cap;
   T.split = (int32_t)p.split;
-  T.split_begin = p.split_begin;
   T.cl_offset = p.clds ? (int32_t)p.cl_offset : 0;
   T.stage_cols = res->stage_cols.as<uint32_t>();
   T.stage_cnt = res->stage_cnt.as<uint32_t>();

@@ -32,10 +32,9 @@ enum Tally : int { kTallyU32 = 0, kTallyU16 = 1, kTallyHash = 2 };
 // Where the counts go.  Unsplit: each workgroup compacts its row into
 // stage_*[slot*row_cap ..] and writes row_nnz / row_tallied (or, with
 // lb_status, straight into the final CSR).  Split 2D rows, histogram
-// tallies (rows split_begin .. n_rows - 1; t = slot - split_begin): part p
-// of a row stores its LDS histogram whole into the slab
-// dense[(t*split + p) * words4 ..] and its tallied count into
-// part_tallied[t*split + p], then arrives on row_arrive[t]; the last
+// tallies: part p of a row stores its LDS histogram whole into the slab
+// dense[(slot*split + p) * words4 ..] and its tallied count into
+// part_tallied[slot*split + p], then arrives on row_arrive[slot]; the last
 // part to arrive sums the slabs into its histogram and writes the row like
 // an unsplit one (no merge launch).  Split 3D rows (the
 // trace3d kernels): parts add into dense[slot*N ..] and row_tallied (both
@@ -47,17 +46,16 @@ struct TallyParams {
   int64_t n_emitters;   // N (histogram length)
   int64_t n_rows;
   int64_t row_cap;      // min(N, R); R for split hash tallies
-  int32_t split;        // workgroups per split row (>= 1)
-  int64_t split_begin;  // 2D histogram kernels: rows below are unsplit, rows from here split (hash: 0)
+  int32_t split;        // workgroups per row (>= 1)
   int32_t cl_offset;    // CLDS kernels: byte offset of the coarse mesh in dynamic LDS
   uint32_t* stage_cols;
   uint32_t* stage_cnt;
   uint32_t* row_nnz;
   uint32_t* row_tallied;
-  uint32_t* dense;      // split only: 2D slabs [split rows][split][words rounded to 4], 3D [n_rows][N], hash merge scratch [2][n_rows][row_cap]
+  uint32_t* dense;      // split only: 2D slabs [n_rows][split][words rounded to 4], 3D [n_rows][N], hash merge scratch [2][n_rows][row_cap]
   uint32_t* part_nnz;   // split hash tallies: sorted part lists, [n_rows][split]
-  uint32_t* row_arrive;    // split 2D histogram rows: parts arrived, [split rows]; zero between launches (the last part resets it)
-  uint32_t* part_tallied;  // split 2D histogram rows: rays each part tallied, [split rows][split]
+  uint32_t* row_arrive;    // split 2D histogram rows: parts arrived, [n_rows]; zero between launches (the last part resets it)
+  uint32_t* part_tallied;  // split 2D histogram rows: rays each part tallied, [n_rows][split]
   int64_t part_cap;     // part lists: entries reserved per part in a row's staging slot
   int32_t hash_cap;     // hash tallies: table slots (power of two; keys then counts in dynamic LDS)
   int32_t hash_shift;   // 32 - log2(hash_cap)

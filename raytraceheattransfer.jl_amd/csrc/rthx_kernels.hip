@@ -393,19 +393,16 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
   constexpr bool CLDS = CL != 0;
   constexpr bool MLAT = CL == 2 && !SINGLE;
   const int tid = threadIdx.x;
-  // SPLIT: rows [0, split_begin) are one workgroup each, as unsplit; every
-  // later row is `split` workgroups, part p tracing rays [p chunk, (p+1) chunk)
-  // (the last round of rows split, so a launch drains in short parts; or all
-  // rows when there are too few to fill the chip).  32-bit: R < 2^32.
+  // SPLIT: every row is `split` workgroups, part p tracing rays
+  // [p chunk, (p+1) chunk).  32-bit: R < 2^32.
   const uint32_t bid = blockIdx.x;
-  const uint32_t sb = SPLIT ? (uint32_t)T.split_begin : 0u;
-  const bool tail = SPLIT && bid >= sb;  // (workgroup-uniform)
-  const uint32_t parts = tail ? (uint32_t)T.split : 1u;
-  const uint32_t trow = tail ? (bid - sb) / parts : 0u;  // index among the split rows
-  const uint32_t tpart = tail ? (bid - sb) - trow * parts : 0u;
-  const int64_t slot = tail ? (int64_t)sb + trow : (int64_t)bid;
+  constexpr bool tail = SPLIT;
+  const uint32_t parts = SPLIT ? (uint32_t)T.split : 1u;
+  const uint32_t trow = SPLIT ? bid / parts : bid;  // the row (slot)
+  const uint32_t tpart = SPLIT ? bid - trow * parts : 0u;
+  const int64_t slot = trow;
   const int64_t part = tpart;
-  const uint32_t chunk = tail ? (uint32_t)((P.R + parts - 1) / parts) : (uint32_t)P.R;
+  const uint32_t chunk = SPLIT ? (uint32_t)((P.R + parts - 1) / parts) : (uint32_t)P.R;
   const int64_t r_begin = SPLIT ? (int64_t)(tpart * chunk) : 0;
   const int64_t r_end = SPLIT ? (r_begin + chunk < P.R ? r_begin + chunk : P.R) : P.R;
   const int64_t g = P.g_begin + slot * P.g_stride;
@@ -1188,7 +1185,7 @@ static int device_cus() {
 template <bool UNIFORM, int TALLY, bool FAITHFUL, bool SINGLE, bool REC, bool SPLIT, bool AXIS, int CL = 0>
 static hipError_t launch_trace_t(const LaunchCfg& L) {
   auto kern = trace_exchange_kernel<UNIFORM, TALLY, FAITHFUL, SINGLE, REC, SPLIT, AXIS, CL>;
-  const int64_t blocks = SPLIT ? L.T.split_begin + (L.T.n_rows - L.T.split_begin) * L.T.split : L.T.n_rows;
+  const int64_t blocks = L.T.n_rows * (SPLIT ? L.T.split : 1);
   // (MLAT kernels: a 64-slot ray queue per wave behind the lattice)
   auto lds_for = [&](int t) { return L.lds_bytes + (CL == 2 && !SINGLE ? (size_t)t * kRaySlotBytes : 0); };
   // Workgroup size: the one that keeps most waves resident per CU.  With a

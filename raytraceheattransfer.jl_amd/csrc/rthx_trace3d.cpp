@@ -15,7 +15,6 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <array>
 #include <cstdio>
 #include <cstdlib>
 #include <cmath>
@@ -38,14 +37,12 @@ struct rthx_scene3d {
   int device = 0;
   hipStream_t stream = nullptr;
   hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
-  DevBuf polys, tris, nodes, tables, scene, nodes4;
+  DevBuf polys, tris, nodes, tables, scene;
   rthx::DevScene3D S{};
   int64_t n_poly = 0;
   int top_choice[8] = {-1, -1, -1, -1, -1, -1, -1, -1};  // LDS node-cache size per kernel variant (launch_trace3d)
   int ghist_choice[4] = {-1, -1, -1, -1};  // per (faithful, pack16, N, R): global-histogram form chosen (1) or not (0)
   int64_t ghist_key[4] = {-1, -1, -1, -1};
-  int w4_threads[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // four-child kernels per (ghist, faithful, pack16): workgroup size
-  int w4_top[8] = {0, 0, 0, 0, 0, 0, 0, 0};      // ... and top nodes in LDS (0 = not chosen yet)
   ~rthx_scene3d() {
     (void)hipSetDevice(device);
     for (auto& e : ev)
@@ -258,9 +255,7 @@ void layout_nodes(std::vector<rthx::Bvh2Node>& nodes) {
   std::vector<char> taken(n, 0);
   std::vector<int> frontier{0};
   taken[0] = 1;
-  int bfs_top = rthx::kTopNodes;
-  if (const char* e = getenv("RTHX_T3_BFS_TOP")) bfs_top = std::max(1, atoi(e));  // (A/B: larger LDS tops)
-  for (size_t h = 0; h < frontier.size() && (int)order.size() < bfs_top; ++h) {
+  for (size_t h = 0; h < frontier.size() && (int)order.size() < rthx::kTopNodes; ++h) {
     const int i = frontier[h];
     order.push_back(i);
     for (int c = 0; c < 2; ++c) {
@@ -300,138 +295,6 @@ void layout_nodes(std::vector<rthx::Bvh2Node>& nodes) {
   }
   nodes.swap(out);
 }
-
-// The four-child tree (Bvh4Node) collapsed from the binary one: each node
-// takes its binary node's two children and, while it has fewer than four,
-// replaces the inner child of largest surface area by that child's two
-// children.  Child boxes are the binary tree's padded fp32 boxes, quantized
-// outward to 8 bits of the node box (power-of-two scale per axis: exact on
-// the host).  Nodes are numbered breadth first (any prefix is the top of the
-// tree: the kernel stages as many as fit in LDS).  group_first maps a
-// binary-node group (the polygons' group id) to its first polygon.
-struct Bvh4Builder {
-  const std::vector<rthx::Bvh2Node>& b2;
-  const std::unordered_map<int32_t, int32_t>& group_first;
-  struct Ch {
-    int32_t ref;  // binary child reference (inner: binary node index)
-    float lo[3], hi[3];
-    int32_t group;
-  };
-  struct Tmp {
-    std::vector<Ch> ch;
-    int axis = 0;
-  };
-  std::vector<Tmp> tmp;  // in creation order (depth first)
-  std::vector<std::array<int32_t, 4>> kids;  // tmp index of inner children (-1: leaf / none)
-  int depth = 0;
-
-  static double area(const Ch& c) {
-    const double x = (double)c.hi[0] - c.lo[0], y = (double)c.hi[1] - c.lo[1], z = (double)c.hi[2] - c.lo[2];
-    return 2.0 * (x * y + y * z + z * x);
-  }
-  Ch child_of(int i, int c) const {
-    Ch h;
-    h.ref = b2[i].child[c];
-    for (int k = 0; k < 3; ++k) {
-      h.lo[k] = b2[i].lo[c][k];
-      h.hi[k] = b2[i].hi[c][k];
-    }
-    h.group = b2[i].group[c];
-    return h;
-  }
-  static bool empty_leaf(const Ch& c) { return c.ref < 0 && ((~c.ref) & ((1 << rthx::kLeafBits) - 1)) == 0; }
-
-  int build(int i, int level) {
-    depth = std::max(depth, level + 1);
-    std::vector<Ch> ch;
-    for (int c = 0; c < 2; ++c)
-      if (!empty_leaf(child_of(i, c))) ch.push_back(child_of(i, c));
-    while (ch.size() < 4) {
-      int best = -1;
-      for (size_t k = 0; k < ch.size(); ++k)
-        if (ch[k].ref >= 0 && (best < 0 || area(ch[k]) > area(ch[best]))) best = (int)k;
-      if (best < 0) break;
-      const int j = ch[best].ref;
-      ch.erase(ch.begin() + best);
-      for (int c = 0; c < 2; ++c)
-        if (!empty_leaf(child_of(j, c))) ch.push_back(child_of(j, c));
-    }
-    // order axis: the widest spread of the child centroids; children ascending along it
-    double cmin[3] = {1e300, 1e300, 1e300}, cmax[3] = {-1e300, -1e300, -1e300};
-    for (const Ch& c : ch)
-      for (int k = 0; k < 3; ++k) {
-        const double m = 0.5 * ((double)c.lo[k] + c.hi[k]);
-        cmin[k] = std::min(cmin[k], m);
-        cmax[k] = std::max(cmax[k], m);
-      }
-    int axis = 0;
-    for (int k = 1; k < 3; ++k)
-      if (cmax[k] - cmin[k] > cmax[axis] - cmin[axis]) axis = k;
-    std::stable_sort(ch.begin(), ch.end(), [&](const Ch& a, const Ch& b) {
-      return (double)a.lo[axis] + a.hi[axis] < (double)b.lo[axis] + b.hi[axis];
-    });
-    const int idx = (int)tmp.size();
-    tmp.push_back(Tmp{ch, axis});
-    kids.push_back({-1, -1, -1, -1});
-    for (size_t k = 0; k < ch.size(); ++k)
-      if (ch[k].ref >= 0) {
-        const int t = build(ch[k].ref, level + 1);
-        kids[idx][k] = t;
-      }
-    return idx;
-  }
-
-  // breadth-first numbering and quantization
-  void emit(std::vector<rthx::Bvh4Node>& out) const {
-    std::vector<int> order{0}, pos(tmp.size(), -1);
-    pos[0] = 0;
-    for (size_t h = 0; h < order.size(); ++h)
-      for (int t : kids[order[h]])
-        if (t >= 0) {
-          pos[t] = (int)order.size();
-          order.push_back(t);
-        }
-    out.assign(order.size(), rthx::Bvh4Node{});
-    for (size_t h = 0; h < order.size(); ++h) {
-      const Tmp& T = tmp[order[h]];
-      rthx::Bvh4Node& nd = out[h];
-      uint32_t meta = ((uint32_t)T.axis << 24) | ((uint32_t)T.ch.size() << 26);
-      for (int k = 0; k < 3; ++k) {
-        float lo = HUGE_VALF, hi = -HUGE_VALF;
-        for (const Ch& c : T.ch) {
-          lo = std::min(lo, c.lo[k]);
-          hi = std::max(hi, c.hi[k]);
-        }
-        const double ext = (double)hi - (double)lo;
-        int e = -126;  // 255 * 2^e >= ext, the smallest such e
-        while (e < 127 && std::ldexp(255.0, e) < ext) ++e;
-        const double sc = std::ldexp(1.0, e);
-        nd.origin[k] = lo;
-        meta |= (uint32_t)(e + 127) << (8 * k);
-        uint32_t ql = 0, qh = 0;
-        for (size_t c = 0; c < T.ch.size(); ++c) {
-          const double a = std::floor(((double)T.ch[c].lo[k] - lo) / sc), b = std::ceil(((double)T.ch[c].hi[k] - lo) / sc);
-          ql |= (uint32_t)std::min(255.0, std::max(0.0, a)) << (8 * c);
-          qh |= (uint32_t)std::min(255.0, std::max(0.0, b)) << (8 * c);
-        }
-        nd.qlo[k] = ql;
-        nd.qhi[k] = qh;
-      }
-      nd.meta = meta;
-      for (size_t c = 0; c < 4; ++c) {
-        if (c >= T.ch.size()) {
-          nd.child[c] = leaf_ref(0, 0);
-          nd.grp[c] = 0xFFFF;
-          continue;
-        }
-        const Ch& C = T.ch[c];
-        nd.child[c] = C.ref >= 0 ? pos[kids[order[h]][c]] : C.ref;
-        auto it = C.group >= 0 ? group_first.find(C.group) : group_first.end();
-        nd.grp[c] = (it != group_first.end() && it->second < 0xFFFF) ? (uint16_t)it->second : (uint16_t)0xFFFF;
-      }
-    }
-  }
-};
 
 }  // namespace
 
@@ -548,14 +411,6 @@ RTHX_EXPORT int rthx_scene3d_create_grouped(const double* xyz, const int32_t* nv
   if (depth > rthx::kBvhStack) depth = build_bvh2(nodes, order, bt, rthx::kBoxPad * scale, true);
   if (depth > rthx::kBvhStack) return fail(RTHX_ERANGE, "BVH too deep for the traversal stack");
   if (tris.size() >= (size_t(1) << (30 - rthx::kLeafBits))) return fail(RTHX_ERANGE, "too many triangles");
-  // the four-child tree, from the binary one before its relayout
-  std::unordered_map<int32_t, int32_t> group_first;
-  for (int64_t k = 0; k < n; ++k) group_first.emplace(polys[k].group, polys[k].glo);
-  std::vector<rthx::Bvh4Node> nodes4;
-  Bvh4Builder B4{nodes, group_first, {}, {}, 0};
-  B4.build(0, 0);
-  B4.emit(nodes4);
-  if (nodes4.size() >= (size_t(1) << 24)) return fail(RTHX_ERANGE, "four-child BVH too large for the walk stack");
   layout_nodes(nodes);
   std::vector<rthx::Tri3> tris_sorted(tris.size());
   for (size_t i = 0; i < order.size(); ++i) tris_sorted[i] = tris[order[i]];
@@ -585,8 +440,7 @@ RTHX_EXPORT int rthx_scene3d_create_grouped(const double* xyz, const int32_t* nv
   if (!up(s->polys, polys.data(), polys.size() * sizeof(rthx::Emit3)) ||
       !up(s->tris, tris_sorted.data(), tris_sorted.size() * sizeof(rthx::Tri3)) ||
       !up(s->nodes, nodes.data(), nodes.size() * sizeof(rthx::Bvh2Node)) ||
-      !up(s->tables, tables.data(), tables.size() * 8) ||
-      !up(s->nodes4, nodes4.data(), nodes4.size() * sizeof(rthx::Bvh4Node)))
+      !up(s->tables, tables.data(), tables.size() * 8))
     return bail(fail(RTHX_ENOMEM, "uploading the 3D scene"));
   s->S.n_poly = (int32_t)n;
   s->S.n_tri = (int32_t)tris.size();
@@ -596,9 +450,6 @@ RTHX_EXPORT int rthx_scene3d_create_grouped(const double* xyz, const int32_t* nv
   s->S.tris = s->tris.as<rthx::Tri3>();
   s->S.nodes = s->nodes.as<rthx::Bvh2Node>();
   s->S.tables = s->tables.as<double>();
-  s->S.nodes4 = s->nodes4.as<rthx::Bvh4Node>();
-  s->S.n_nodes4 = (int32_t)nodes4.size();
-  s->S.stack4 = B4.depth + 1;
   if (!up(s->scene, &s->S, sizeof(s->S))) return bail(fail(RTHX_ENOMEM, "uploading the 3D scene"));
   if (getenv("RTHX_VERBOSE"))
     std::fprintf(stderr, "rthx_scene3d_create: host geometry + BVH %.2f ms, device setup + upload %.2f ms\n",
@@ -613,7 +464,7 @@ RTHX_EXPORT int rthx_scene3d_stats(const rthx_scene3d* sc, int64_t* n_tri, int64
                                    int64_t* lds_bytes) {
   if (!sc) return fail(RTHX_EINVAL, "null scene");
   if (n_tri) *n_tri = sc->S.n_tri;
-  if (n_nodes) *n_nodes = getenv("RTHX_T3_BVH4") && getenv("RTHX_T3_BVH4")[0] == '1' ? sc->S.n_nodes4 : sc->S.n_nodes;
+  if (n_nodes) *n_nodes = sc->S.n_nodes;
   if (depth) *depth = sc->S.stack;
   if (lds_bytes) *lds_bytes = (int64_t)(rthx::trace3d_dynamic_lds(sc->n_poly, sc->S.stack) + rthx::kTrace3dStaticLds);
   return RTHX_OK;
@@ -730,57 +581,6 @@ RTHX_EXPORT int rthx_trace_exchange_3d(rthx_scene3d* sc, const rthx_trace_args* 
       L.ghist = sc->ghist_choice[slot_k] == 1;
     }
     if (L.ghist) L.lds_bytes = rthx::trace3d_dynamic_lds(0, sc->S.stack);
-    const char* w4e = getenv("RTHX_T3_BVH4");
-    L.w4 = w4e && w4e[0] == '1';
-    if (L.w4) {
-      // Four-child tree: the workgroup size whose resident waves per CU (the
-      // register limit) are most, and with it as many top nodes in LDS as
-      // leave that many workgroups resident (ties: more nodes in LDS).
-      const int words = L.ghist ? 0 : (int)(pack16 ? (N + 1) / 2 : N);
-      const int vk = (L.ghist ? 4 : 0) + (L.faithful ? 2 : 0) + (pack16 ? 1 : 0);
-      if (sc->w4_threads[vk] == 0) {
-        int best_t = 256, best_top = 0, best_waves = 0;
-        const int t_env = getenv("RTHX_T3_W4_THREADS") ? atoi(getenv("RTHX_T3_W4_THREADS")) : 0;
-        for (int t = 1024; t >= 256; t -= 256) {
-          if (t_env > 0 && t != t_env) continue;
-          const size_t base = rthx::trace3d_w4_lds(words, sc->S.stack4, t, 0);
-          int k = 0;
-          HIP_TRY(rthx::trace3d_w4_occupancy(L.faithful, pack16, L.ghist, t, base, &k), "3D tracer occupancy");
-          if (k < 1) continue;
-          const int64_t per_wg = (int64_t)rthx::kMaxLdsBytes / k - 2048;  // (static LDS, allocation granularity)
-          int top = (int)std::max<int64_t>(0, std::min<int64_t>(sc->S.n_nodes4, (per_wg - (int64_t)base) / 64));
-          int k2 = 0;
-          while (top > 0) {
-            HIP_TRY(rthx::trace3d_w4_occupancy(L.faithful, pack16, L.ghist, t, rthx::trace3d_w4_lds(words, sc->S.stack4, t, top), &k2),
-                    "3D tracer occupancy");
-            if (k2 >= k) break;
-            top = top * 7 / 8;
-          }
-          const int waves = k * t / 64;
-          if (waves > best_waves || (waves == best_waves && top > best_top)) {
-            best_waves = waves;
-            best_t = t;
-            best_top = top;
-          }
-        }
-        if (const char* e = getenv("RTHX_T3_W4_TOP")) best_top = std::min(best_top, std::max(0, atoi(e)));
-        sc->w4_threads[vk] = best_t;
-        sc->w4_top[vk] = best_top;
-        if (getenv("RTHX_VERBOSE"))
-          std::fprintf(stderr, "rthx 3D four-child walk: %d lanes per workgroup, %d of %d nodes in LDS, %d waves per CU\n",
-                       best_t, best_top, sc->S.n_nodes4, best_waves);
-      }
-      L.threads = sc->w4_threads[vk];
-      L.n_dyn = sc->w4_top[vk];
-      L.lds_bytes = rthx::trace3d_w4_lds(words, sc->S.stack4, L.threads, L.n_dyn);
-      if (L.lds_bytes + 1024 > rthx::kMaxLdsBytes)
-        return fail(RTHX_ERANGE, "N too large for the LDS row histogram and walk stacks of the 3D tracer");
-    }
-    if (!L.w4 && getenv("RTHX_T3_DYNTOP")) {  // (A/B: as many top nodes as the LDS left holds, in dynamic LDS)
-      const int64_t room = (int64_t)rthx::kMaxLdsBytes - (int64_t)L.lds_bytes - 2048;
-      L.n_dyn = (int)std::max<int64_t>(1, std::min<int64_t>(sc->S.n_nodes, room / (int64_t)sizeof(rthx::Bvh2Node)));
-      if (const char* e = getenv("RTHX_T3_DYNTOP_MAX")) L.n_dyn = std::min(L.n_dyn, std::max(1, atoi(e)));
-    }
     HIP_TRY(rthx::launch_trace3d(L), "trace_exchange_3d_kernel launch");
   }
   HIP_TRY(hipEventRecord(sc->ev[1], st), "hipEventRecord");

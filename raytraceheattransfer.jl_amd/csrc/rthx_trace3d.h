@@ -41,23 +41,6 @@ struct alignas(16) Bvh2Node {
 };
 static_assert(sizeof(Bvh2Node) == 64, "Bvh2Node is one 64-byte record");
 
-// Four-child BVH node with quantized child boxes (64 B; Ylitie, Karras and
-// Laine, HPG 2017, at four children).  Child c's bounds on axis k are
-// origin[k] + q * 2^(e_k - 127) for its bytes q of qlo[k] / qhi[k], rounded
-// outward on the host (floor / ceil), so the decoded box contains the
-// child's padded fp32 box exactly.  Children are stored ascending along the
-// node's order axis (their centroids' widest spread); a ray whose direction
-// is negative on that axis visits them in descending order.
-struct alignas(16) Bvh4Node {
-  float origin[3];   // low corner of the union of the child boxes (fp32)
-  uint32_t meta;     // bytes 0-2: biased scale exponents e_k; bits 24-25: order axis; bits 26-28: child count
-  uint32_t qlo[3];   // byte c: child c's quantized low bound on axis k
-  uint32_t qhi[3];   // byte c: child c's quantized high bound
-  int32_t child[4];  // >= 0 an inner node (index into nodes4); < 0 a leaf ~(first << 3 | count)
-  uint16_t grp[4];   // first polygon of the one group the child's triangles belong to; 0xFFFF: several
-};
-static_assert(sizeof(Bvh4Node) == 64, "Bvh4Node is one 64-byte record");
-
 constexpr int kLeafBits = 3;       // up to 7 triangles per leaf reference
 constexpr double kBoxPad = 1e-5;   // fp32 box padding, relative to the scene scale
 
@@ -68,9 +51,6 @@ struct DevScene3D {
   const Tri3 RTHX_GLOBAL* tris;
   const Bvh2Node RTHX_GLOBAL* nodes;
   const double RTHX_GLOBAL* tables;  // kTableDoubles (cos/sin table for the azimuth)
-  const Bvh4Node RTHX_GLOBAL* nodes4;  // the four-child tree collapsed from `nodes`, breadth first (root 0)
-  int32_t n_nodes4;
-  int32_t stack4;  // walk stack entries of the four-child tree (its inner-node depth + 1)
 };
 
 constexpr uint32_t kTrace3dTag = 0x40000000u;  // Philox counter word 3 of the 3D tracer
@@ -105,19 +85,9 @@ struct Trace3dLaunch {
   bool pack16;  // < 65536 rays per workgroup: u16 row-histogram counters
   bool ghist;   // counts straight to the dense rows (no LDS histogram)
   int* top_choice;  // [ghist * 4 + faithful * 2 + pack16]: LDS node-cache size (64 / 128), -1 = not chosen yet
-  int n_dyn = 0;    // > 0: that many top nodes in dynamic LDS behind the stacks (RTHX_T3_DYNTOP; four-child tree: always)
-  bool w4 = false;  // the four-child quantized tree (Bvh4Node)
-  int threads = 0;  // four-child kernels: workgroup size (multiple of 64, <= 1024)
 };
-
-// dynamic LDS of the four-child kernels: [row histogram][stacks: stack4 x threads][n_top nodes]
-__host__ __device__ constexpr size_t trace3d_w4_stack_offset(int64_t words) { return (size_t)((words + 63) & ~int64_t(63)); }
-__host__ __device__ constexpr size_t trace3d_w4_lds(int64_t words, int stack4, int threads, int n_top) {
-  return 4 * (trace3d_w4_stack_offset(words) + (size_t)stack4 * threads) + (size_t)n_top * sizeof(Bvh4Node);
-}
 
 hipError_t launch_trace3d(const Trace3dLaunch& L);
 hipError_t trace3d_occupancy(const Trace3dLaunch& L, size_t lds_hist, size_t lds_gh, int* wg_hist, int* wg_gh);
-hipError_t trace3d_w4_occupancy(bool faithful, bool pack16, bool ghist, int threads, size_t lds, int* per_cu);
 
 }  // namespace rthx

@@ -194,119 +194,6 @@ struct Walk {
   }
 };
 
-// Walk of the four-child quantized tree (Bvh4Node): the same speculative
-// traversal, leaf tests and answers as Walk, over nodes of four children.
-// A node read tests its children's boxes: child c's slab parameters on axis
-// k are fma(q, s_k inv_k, fma(origin_k, inv_k, -o_k inv_k)) for its bounds'
-// bytes q (v_cvt_f32_ubyte), i.e. the decoded bound's parameter with fp32
-// roundings far inside the boxes' kBoxPad padding.  The walk goes on to the
-// first hit child in the node's order (its axis, reversed for a ray going
-// negative on it); the other hit children stay on the lane's stack as one
-// entry (node index, 4-bit mask of children left, direction bit) that a pop
-// advances: one stack entry per level, so the stack is the inner depth + 1.
-// The top n_top nodes (breadth first) are read from LDS, the rest from
-// global memory.
-struct Walk4 : Walk {
-  uint32_t dirbits;  // bit k: the ray goes negative on axis k
-
-  __device__ __forceinline__ void init4(const double* o_, const double* d_) {
-    init(o_, d_);
-    dirbits = (d[0] < 0.0 ? 1u : 0u) | (d[1] < 0.0 ? 2u : 0u) | (d[2] < 0.0 ? 4u : 0u);
-  }
-
-  // the first child of mask m (4 bits) in visiting order (descending when desc)
-  static __device__ __forceinline__ uint32_t first_child(uint32_t m, bool desc) {
-    return desc ? 31u - (uint32_t)__builtin_clz(m) : (uint32_t)__builtin_ctz(m);
-  }
-
-  __device__ __forceinline__ int32_t child_ref(const DevScene3D& S, const Bvh4Node RTHX_LDS* top, int n_top, int n,
-                                               uint32_t c) const {
-    return n < n_top ? top[n].child[c] : S.nodes4[n].child[c];
-  }
-
-  // next node of the stack (kWalkDone when empty); sp and the top entry advance
-  __device__ __forceinline__ int pop4(const DevScene3D& S, const Bvh4Node RTHX_LDS* top, int n_top,
-                                      uint32_t RTHX_LDS* stk, int nthr) {
-    if (sp == 0) return kWalkDone;
-    const uint32_t e = stk[(sp - 1) * nthr];
-    const int n = (int)(e & 0xFFFFFFu);
-    const uint32_t m = (e >> 24) & 15u;
-    const uint32_t c = first_child(m, (e >> 28) & 1u);
-    const uint32_t rest = m & ~(1u << c);
-    if (rest) stk[(sp - 1) * nthr] = (e & ~(15u << 24)) | (rest << 24);
-    else --sp;
-    return child_ref(S, top, n_top, n, c);
-  }
-
-  __device__ __forceinline__ bool step4(const DevScene3D& S, const Bvh4Node RTHX_LDS* top, int n_top, uint32_t gfirst,
-                                        int glo, int glen, uint32_t RTHX_LDS* stk, int nthr) {
-    typedef float f4 __attribute__((ext_vector_type(4)));
-    while (node >= 0) {
-      Bvh4Node nd;
-      if (node < n_top) {
-        const f4 RTHX_LDS* q = (const f4 RTHX_LDS*)(top + node);
-        const f4 w[4] = {q[0], q[1], q[2], q[3]};
-        __builtin_memcpy(&nd, w, sizeof(nd));
-      } else {
-        nd = S.nodes4[node];
-      }
-      float A[3], B[3];
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        const float sc = __builtin_bit_cast(float, ((nd.meta >> (8 * k)) & 0xFFu) << 23);
-        A[k] = sc * inv[k];
-        B[k] = __builtin_fmaf(nd.origin[k], inv[k], -oi[k]);
-      }
-      const uint32_t nch = (nd.meta >> 26) & 7u;
-      uint32_t m = 0;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        float a[3], b[3];
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-          a[k] = __builtin_fmaf((float)((nd.qlo[k] >> (8 * c)) & 0xFFu), A[k], B[k]);
-          b[k] = __builtin_fmaf((float)((nd.qhi[k] >> (8 * c)) & 0xFFu), A[k], B[k]);
-        }
-        // NaN (0 * inf on an axis the ray runs parallel to) drops out of
-        // fminf/fmaxf: that axis then does not prune (conservative)
-        const float tn = fmaxf(fmaxf(fminf(a[0], b[0]), fminf(a[1], b[1])), fmaxf(fminf(a[2], b[2]), 0.0f));
-        const float tf = fminf(fminf(fmaxf(a[0], b[0]), fmaxf(a[1], b[1])), fminf(fmaxf(a[2], b[2]), best_tf));
-        // a child whose triangles all belong to the emitter's group is never entered
-        const bool hit = (tn <= tf) & ((uint32_t)c < nch) & ((uint32_t)nd.grp[c] != gfirst);
-        m |= hit ? (1u << c) : 0u;
-      }
-      if (m == 0u) {
-        node = pop4(S, top, n_top, stk, nthr);
-      } else {
-        const uint32_t axis = (nd.meta >> 24) & 3u;
-        const bool desc = (dirbits >> axis) & 1u;
-        const uint32_t c = first_child(m, desc);
-        const uint32_t rest = m & ~(1u << c);
-        if (rest) {
-          stk[sp * nthr] = (uint32_t)node | (rest << 24) | ((desc ? 1u : 0u) << 28);
-          ++sp;
-        }
-        // (a select chain: nd.child[c] at a lane-varying c would move nd to scratch)
-        node = c == 0u ? nd.child[0] : c == 1u ? nd.child[1] : c == 2u ? nd.child[2] : nd.child[3];
-      }
-      if (node < 0 && node != kWalkDone && pending == 0) {
-        pending = node;
-        node = pop4(S, top, n_top, stk, nthr);
-      }
-      if (__popcll(__ballot(pending == 0)) <= RTHX_T3_LEAF_LAG) break;
-    }
-    while (pending < 0) {
-      leaf(S, glo, glen, pending);
-      pending = 0;
-      if (node < 0 && node != kWalkDone) {
-        pending = node;
-        node = pop4(S, top, n_top, stk, nthr);
-      }
-    }
-    return node != kWalkDone;
-  }
-};
-
 // Emission of ray (g, r): a uniform point on the polygon and a cosine-law
 // direction about its normal.
 template <bool FAITHFUL>
@@ -355,18 +242,14 @@ __device__ __forceinline__ void emit_ray(const Emit3& E, const double* tab, uint
 // workgroups; they are built for 6 waves per SIMD (80 VGPRs, no spills;
 // config 4 L4 7.59 -> 7.83 Grays/s), the LDS-histogram ones keep the
 // compiler's 86 (5 waves: a 6-wave budget measured 1 % slower at L3).
-// TOP = 0: the top n_dyn nodes (as many as the LDS left by the histogram
-// and the stacks holds) in dynamic LDS behind the stacks.
 template <bool FAITHFUL, bool PACK16, int TOP, bool GH = false>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(GH ? kGhWaves : kHistWaves))) void trace_exchange_3d_kernel(const DevScene3D* __restrict__ Sp,
-                                                                                  TraceParams P, TallyParams T, int n_dyn) {
-  // dynamic LDS: [row histogram][walk stacks][(TOP = 0) top nodes] (GH: no histogram)
+                                                                                  TraceParams P, TallyParams T) {
+  // dynamic LDS: [row histogram][walk stacks] (GH: the stacks only)
   extern __shared__ uint32_t hist[];
-  __shared__ Bvh2Node s_top[TOP > 0 ? TOP : 1];
-  const int64_t words_ = GH ? 0 : PACK16 ? (T.n_emitters + 1) / 2 : T.n_emitters;
-  Bvh2Node RTHX_LDS* top = TOP > 0 ? (Bvh2Node RTHX_LDS*)&s_top[0]
-                                   : (Bvh2Node RTHX_LDS*)(hist + trace3d_stack_offset(words_) + (size_t)Sp->stack * kThreads);
-  const int n_top = TOP > 0 ? (TOP < Sp->n_nodes ? TOP : Sp->n_nodes) : n_dyn;
+  __shared__ Bvh2Node s_top[TOP];
+  Bvh2Node RTHX_LDS* top = (Bvh2Node RTHX_LDS*)&s_top[0];
+  const int n_top = TOP < Sp->n_nodes ? TOP : Sp->n_nodes;
   const double* s_tab = (const double*)Sp->tables;  // the azimuth table, read from global memory (L1/L2)
   __shared__ Emit3 s_emit;
   __shared__ uint32_t s_tallied;
@@ -466,111 +349,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(GH ? k
   if (tid == 0) atomicAdd(&T.row_tallied[slot], s_tallied);
 }
 
-// The four-child quantized tree (Walk4): workgroups of any multiple of 64
-// lanes (the host picks the size and how many top nodes fit in LDS);
-// otherwise as trace_exchange_3d_kernel (ray regeneration, LDS or global
-// row histogram).  Dynamic LDS: [row histogram][stacks][top nodes].
-template <bool FAITHFUL, bool PACK16, bool GH>
-__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(GH ? kGhWaves : kHistWaves))) void trace_exchange_3d_w4_kernel(
-    const DevScene3D* __restrict__ Sp, TraceParams P, TallyParams T, int n_top) {
-  extern __shared__ uint32_t hist[];
-  const DevScene3D& S = *Sp;
-  const int tid = threadIdx.x, nthr = (int)blockDim.x;
-  const int64_t N = T.n_emitters;
-  const int64_t words = GH ? 0 : PACK16 ? (N + 1) / 2 : N;
-  uint32_t RTHX_LDS* stk0 = (uint32_t RTHX_LDS*)(hist + trace3d_w4_stack_offset(words));
-  Bvh4Node RTHX_LDS* top = (Bvh4Node RTHX_LDS*)(stk0 + (size_t)S.stack4 * nthr);
-  const double* s_tab = (const double*)S.tables;  // the azimuth table, read from global memory (L1/L2)
-  __shared__ Emit3 s_emit;
-  __shared__ uint32_t s_tallied;
-  __shared__ uint32_t s_next;  // next ray of the slice
-  const int64_t slot = blockIdx.x / T.split, part = blockIdx.x % T.split;
-  const int64_t chunk = (P.R + T.split - 1) / T.split;
-  const int64_t r_begin = part * chunk;
-  const int64_t r_end = r_begin + chunk < P.R ? r_begin + chunk : P.R;
-  const int64_t g = P.g_begin + slot * P.g_stride;
-  for (int64_t i = tid; i < words; i += nthr) hist[i] = 0u;
-  uint32_t* dense = T.dense + slot * N;
-  {
-    typedef float f4 __attribute__((ext_vector_type(4)));
-    const f4 RTHX_GLOBAL* src = (const f4 RTHX_GLOBAL*)S.nodes4;
-    f4 RTHX_LDS* dst = (f4 RTHX_LDS*)top;
-    for (int i = tid; i < 4 * n_top; i += nthr) dst[i] = src[i];
-  }
-  if (tid == 0) {
-    s_emit = S.polys[g];
-    s_tallied = 0u;
-    s_next = (uint32_t)r_begin;
-  }
-  __syncthreads();
-  uint32_t tallied = 0;
-  // the emitter's coplanar group: its triangles are skipped, its subtrees
-  // pruned (nodes name a group by its first polygon, below 0xFFFF)
-  const int glo = s_emit.glo, glen = s_emit.ghi - s_emit.glo;
-  const uint32_t gfirst = glo < 0xFFFF ? (uint32_t)glo : 0x10000u;
-  uint32_t RTHX_LDS* stk = stk0 + tid;
-  auto tally = [&](int a) {
-    if (a >= 0) {
-      if (GH)
-        __hip_atomic_fetch_add(&dense[a], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      else if (PACK16)
-        atomicAdd(&hist[a >> 1], 1u << ((a & 1) * 16));
-      else
-        atomicAdd(&hist[a], 1u);
-      ++tallied;
-    }
-  };
-  const Bvh4Node RTHX_LDS* topo = (const Bvh4Node RTHX_LDS*)lds_opaque((const Bvh4Node*)top);
-  constexpr int kRefill = RTHX_T3_REFILL > 0 ? RTHX_T3_REFILL : 1;
-  Walk4 w;
-  bool live = false;
-  while (true) {
-    if (__popcll(__ballot(!live)) >= kRefill || __ballot(live) == 0ull) {
-      if (!live) {
-        const uint32_t r = atomicAdd(&s_next, 1u);
-        if (r < (uint32_t)r_end) {
-          const Emit3 RTHX_LDS* em = lds_opaque(&s_emit);
-          double o[3], d[3];
-          emit_ray<FAITHFUL>(*(const Emit3*)em, s_tab, (uint32_t)g, r, P.key0, P.key1, o, d);
-          w.init4(o, d);
-          live = true;
-        }
-      }
-    }
-    if (__ballot(live) == 0ull) break;
-    if (live && !w.step4(S, topo, n_top, gfirst, glo, glen, stk, nthr)) {
-      tally(w.best_poly);
-      live = false;
-    }
-  }
-  for (int off = 32; off > 0; off >>= 1) tallied += __shfl_xor(tallied, off);
-  if (lane_id() == 0) atomicAdd(&s_tallied, tallied);
-  __syncthreads();
-  if (!GH)
-    for (int64_t i = tid; i < N; i += nthr) {
-      const uint32_t v = PACK16 ? (hist[i >> 1] >> ((i & 1) * 16)) & 0xFFFFu : hist[i];
-      if (v) atomicAdd(&dense[i], v);
-    }
-  if (tid == 0) atomicAdd(&T.row_tallied[slot], s_tallied);
-}
-
 }  // namespace t3
 
 namespace {
-
-template <bool FAITHFUL, bool PACK16, bool GH>
-hipError_t launch_w4(const Trace3dLaunch& L) {
-  auto kern = t3::trace_exchange_3d_w4_kernel<FAITHFUL, PACK16, GH>;
-  const size_t lds = L.lds_bytes;
-  if (lds > 64 * 1024) {
-    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
-  }
-  const int64_t blocks = L.T.n_rows * L.T.split;
-  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(L.threads), lds, L.stream, L.S, L.P, L.T, L.n_dyn);
-  return hipGetLastError();
-}
-
 
 template <bool FAITHFUL, bool PACK16, bool GH>
 hipError_t launch_variant(const Trace3dLaunch& L) {
@@ -578,17 +359,6 @@ hipError_t launch_variant(const Trace3dLaunch& L) {
   // one (occupancy queries are slow host calls: the choice is kept per scene
   // and kernel variant in L.top_choice).
   int& top = L.top_choice[(GH ? 4 : 0) + (FAITHFUL ? 2 : 0) + (PACK16 ? 1 : 0)];
-  if (L.n_dyn > 0) {  // (RTHX_T3_DYNTOP: the top nodes in dynamic LDS)
-    auto kd = t3::trace_exchange_3d_kernel<FAITHFUL, PACK16, 0, GH>;
-    const size_t lds = L.lds_bytes + (size_t)L.n_dyn * sizeof(Bvh2Node);
-    if (lds > 64 * 1024) {
-      hipError_t e = hipFuncSetAttribute((const void*)kd, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      if (e != hipSuccess) return e;
-    }
-    const int64_t blocks = L.T.n_rows * L.T.split;
-    hipLaunchKernelGGL(kd, dim3((unsigned)blocks), dim3(t3::kThreads), lds, L.stream, L.S, L.P, L.T, L.n_dyn);
-    return hipGetLastError();
-  }
   if (top < 0) {
     int pc64 = 0, pc128 = 0;
     hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
@@ -606,36 +376,16 @@ hipError_t launch_variant(const Trace3dLaunch& L) {
     if (e != hipSuccess) return e;
   }
   const int64_t blocks = L.T.n_rows * L.T.split;
-  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(t3::kThreads), L.lds_bytes, L.stream, L.S, L.P, L.T, 0);
+  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(t3::kThreads), L.lds_bytes, L.stream, L.S, L.P, L.T);
   return hipGetLastError();
 }
 
 }  // namespace
 
 hipError_t launch_trace3d(const Trace3dLaunch& L) {
-  if (L.w4) {
-    if (L.ghist) return L.faithful ? launch_w4<true, false, true>(L) : launch_w4<false, false, true>(L);
-    if (L.faithful) return L.pack16 ? launch_w4<true, true, false>(L) : launch_w4<true, false, false>(L);
-    return L.pack16 ? launch_w4<false, true, false>(L) : launch_w4<false, false, false>(L);
-  }
   if (L.ghist) return L.faithful ? launch_variant<true, false, true>(L) : launch_variant<false, false, true>(L);
   if (L.faithful) return L.pack16 ? launch_variant<true, true, false>(L) : launch_variant<true, false, false>(L);
   return L.pack16 ? launch_variant<false, true, false>(L) : launch_variant<false, false, false>(L);
-}
-
-// Resident workgroups per CU of a four-child kernel at the given workgroup
-// size and dynamic LDS.
-hipError_t trace3d_w4_occupancy(bool faithful, bool pack16, bool ghist, int threads, size_t lds, int* per_cu) {
-  const void* k = ghist ? (faithful ? (const void*)t3::trace_exchange_3d_w4_kernel<true, false, true>
-                                    : (const void*)t3::trace_exchange_3d_w4_kernel<false, false, true>)
-                        : faithful ? (pack16 ? (const void*)t3::trace_exchange_3d_w4_kernel<true, true, false>
-                                             : (const void*)t3::trace_exchange_3d_w4_kernel<true, false, false>)
-                                   : (pack16 ? (const void*)t3::trace_exchange_3d_w4_kernel<false, true, false>
-                                             : (const void*)t3::trace_exchange_3d_w4_kernel<false, false, false>);
-  hipError_t e = hipSuccess;
-  if (lds > 64 * 1024) e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, k, threads, lds);
-  return e;
 }
 
 // Resident workgroups per CU of the LDS-histogram and the global-histogram
