@@ -261,6 +261,10 @@ def main():
     ap.add_argument("--strong", action="store_true",
                     help="strong scaling: --rays-per-gpu is the whole job's ray count, split over the GPUs "
                          "(default: weak scaling, that many rays per GPU)")
+    ap.add_argument("--blocking", action="store_true",
+                    help="time blocking calls (each step waits for its trace and reads its totals back) instead "
+                         "of steps enqueued back to back (RTHX_FLAG_ASYNC; every step's trace still runs in full, "
+                         "its checks run when the result is read)")
     ap.add_argument("--faithful-steps", type=int, default=10,
                     help="steps of the faithful-sampling leg (the reference's acos/sin/cos emission, "
                          "emitVolumeRay2D.jl:26-31), reported beside value; 0 skips it")
@@ -305,6 +309,7 @@ def main():
         dd = _lib.MultiDeviceDomain(flat, devices) if args.gpus > 1 else _lib.DeviceDomain(flat, device)
         targs, _keep = _lib.make_args(0, R, nudge, args.seed, 0, N, 1, device=device,
                                       flags=abi.RTHX_FLAG_DEVICE_ONLY)
+        aargs = targs  # (multi-device traces block)
     else:
         # one process per GPU: rank r drives device LOCAL_RANK (more ranks than
         # devices, e.g. a 2-rank rehearsal on a 1-GPU box, share devices round robin)
@@ -313,6 +318,8 @@ def main():
         dd = _lib.DeviceDomain(flat, device)
         targs, _keep = _lib.make_args(0, R, nudge, args.seed, rank, N, world, device=device,
                                       flags=abi.RTHX_FLAG_DEVICE_ONLY)
+        aargs, _keep_a = _lib.make_args(0, R, nudge, args.seed, rank, N, world, device=device,
+                                        flags=abi.RTHX_FLAG_DEVICE_ONLY | (0 if args.blocking else abi.RTHX_FLAG_ASYNC))
     res = _lib.DeviceResult()
 
     def barrier():
@@ -329,22 +336,37 @@ def main():
         res.trace(dd, targs)
         prewarm_steps += 1
     for _ in range(args.warmup):
-        res.trace(dd, targs)
+        res.trace(dd, aargs)
+    res.info()  # (completes a pending warm-up trace)
     sync_all()
     barrier()
     sync_all()
+    # Timed: K steps, each a whole rthx_trace_exchange of the shard.  By
+    # default they are enqueued back to back (RTHX_FLAG_ASYNC: the call
+    # returns once its trace is on the stream; the result's read-back and
+    # checks happen when it is read), so the host's per-call time overlaps
+    # the previous trace; --blocking waits for every step.
     t0 = time.perf_counter()
-    trace_ms = []
-    pack_ms = []
-    info = None
     for _ in range(args.steps):
-        res.trace(dd, targs)
-        info = res.info()
-        trace_ms.append(info["trace_ms"])
-        pack_ms.append(info["pack_ms"])
+        res.trace(dd, aargs)
     sync_all()
     elapsed = time.perf_counter() - t0
     barrier()
+    info = res.info()  # the last step, completed and checked
+    # Kernel time per launch (HIP events) and the blocking-call rate, from
+    # blocking steps after the timed region (the roofline's avg kernel time)
+    trace_ms = []
+    pack_ms = []
+    n_blk = max(5, min(args.steps, 20))
+    sync_all()
+    tb = time.perf_counter()
+    for _ in range(n_blk):
+        res.trace(dd, targs)
+        ib = res.info()
+        trace_ms.append(ib["trace_ms"])
+        pack_ms.append(ib["pack_ms"])
+    sync_all()
+    blocking_ms = (time.perf_counter() - tb) / n_blk * 1e3
 
     rays_rank = info["rays_traced"]
     nnz_rank = info["nnz"]
@@ -484,6 +506,8 @@ def main():
                 "note": "VALU-issue bound path (roofline_valu); HBM fraction reported as mandated (DESIGN.md §6)",
             },
             "pack_ms": round(float(np.mean(pack_ms)), 4),
+            "step_mode": "blocking calls" if args.blocking else "enqueued back to back (RTHX_FLAG_ASYNC)",
+            "blocking_ms_per_step": round(blocking_ms, 4),
             "roofline_fp64": fp64_roof,
             "roofline_valu": valu_roof,
             "faithful_sampling": faithful,

@@ -57,6 +57,18 @@ extern "C" {
                                             default: algebraic sin(acos(x)) */
 #define RTHX_FLAG_DEVICE_ONLY 0x2u       /* leave the CSR on the device; copy
                                             calls then fetch it on demand */
+#define RTHX_FLAG_ASYNC 0x4u             /* return once the trace is enqueued on
+                                            the domain's stream (single-device,
+                                            single-polygon domains whose result
+                                            was traced at this shape before;
+                                            otherwise the call blocks as usual).
+                                            The first call that reads the result
+                                            (get_info, any copy, the device CSR,
+                                            smoothing) waits for it, checks it and
+                                            fills its info; tracing into the
+                                            result again first drops an unread
+                                            pending trace.  The domain must live
+                                            until then. */
 
 /* Uniform grid over a set of polygons (UniformGrid,
  * src/Domains/domains/DomainStructs.jl:79-86; built by

@@ -828,7 +828,8 @@ int plan_trace_split(const rthx_domain* dom, const rthx_trace_args* a, TracePlan
 // to staging slots, then row_scan + csr_pack.  Fills totals (see
 // finish_staged; totals[3] > 0: a look-back wait gave up).
 int run_trace(rthx_domain* dom, const rthx_trace_args* a, const TracePlan& p, rthx_result* res, bool lookback,
-              const rthx::RecordParams& rec, int64_t totals[rthx::kLbTotals], float* ms_trace, float* ms_pack) {
+              const rthx::RecordParams& rec, int64_t totals[rthx::kLbTotals], float* ms_trace, float* ms_pack,
+              bool async = false) {
   const int64_t n_rows = p.n_rows, N = p.N, R = p.R;
   hipStream_t st = dom->stream;
   HIP_TRY(res->row_nnz.reserve((size_t)n_rows * 4), "hipMalloc row_nnz");
@@ -950,7 +951,9 @@ int run_trace(rthx_domain* dom, const rthx_trace_args* a, const TracePlan& p, rt
   }
   if (p.split > 1 && p.part_lists && n_rows > 0)
     HIP_TRY(hipMemsetAsync(T.row_tallied, 0, (size_t)n_rows * 4, st), "hipMemset row_tallied");
-  HIP_TRY(hipEventRecord(dom->ev[0], st), "hipEventRecord");
+  // (async: the result's own events, read when the result completes)
+  hipEvent_t ev0 = async ? res->pend_ev[0] : dom->ev[0], ev1 = async ? res->pend_ev[1] : dom->ev[1];
+  HIP_TRY(hipEventRecord(ev0, st), "hipEventRecord");
   if (n_rows > 0) {
     rthx::LaunchCfg L = launch_of(dom, a, p);
     L.P = P;
@@ -959,7 +962,12 @@ int run_trace(rthx_domain* dom, const rthx_trace_args* a, const TracePlan& p, rt
     L.stream = st;
     HIP_TRY(rthx::launch_trace(L), "trace_exchange_kernel launch");
   }
-  HIP_TRY(hipEventRecord(dom->ev[1], st), "hipEventRecord");
+  HIP_TRY(hipEventRecord(ev1, st), "hipEventRecord");
+  if (lookback && async) {  // (complete_pending reads the totals back)
+    res->pend_totals = T.totals;
+    res->lb_epoch = T.lb_epoch;
+    return RTHX_OK;
+  }
   if (lookback) {
     HIP_TRY(hipEventRecord(dom->ev[2], st), "hipEventRecord");
     // (a last-row hand-over of the totals into page-locked memory, counting
@@ -980,10 +988,15 @@ int run_trace(rthx_domain* dom, const rthx_trace_args* a, const TracePlan& p, rt
   return RTHX_OK;
 }
 
+int finish_trace(rthx_domain* dom, const rthx_trace_args* a, const TracePlan& p, rthx_result* res, bool lookback,
+                 const rthx::RecordParams& rec, int64_t totals[rthx::kLbTotals], float ms_trace, float ms_pack,
+                 double t0);
+
 // The whole of one device's trace (validated arguments, any device state).
 int trace_exchange_one(rthx_domain* dom, const rthx_trace_args* a, rthx_result* res) {
   const double t0 = now_ms();
   HIP_TRY(hipSetDevice(dom->device), "hipSetDevice");
+  res->pending = false;  // (an unread async trace is superseded: stream order keeps its launch before this one)
   TracePlan p;
   int rc = plan_trace_split(dom, a, p);
   if (rc) return rc;
@@ -1048,8 +1061,39 @@ int trace_exchange_one(rthx_domain* dom, const rthx_trace_args* a, rthx_result* 
                         (uint64_t)n_rows * (uint64_t)p.row_cap <= rthx::kLbValMax && !env_flag("RTHX_NO_LOOKBACK");
   int64_t totals[rthx::kLbTotals] = {0, 0, 0, 0, 0};
   float ms_trace = 0.f, ms_pack = 0.f;
+  // RTHX_FLAG_ASYNC: enqueue only, when the direct CSR is sized from an
+  // earlier launch of this shape (no overflow expected); the checks and the
+  // info wait for the first read (complete_pending)
+  const bool async = (a->flags & RTHX_FLAG_ASYNC) && lookback && n_rec == 0 && res->lb_nnz_hint > 0 &&
+                     res->lb_hint_shape[0] == p.N && res->lb_hint_shape[1] == n_rows && res->lb_hint_shape[2] == R;
+  if (async) {
+    for (auto& e : res->pend_ev)
+      if (!e) HIP_TRY(hipEventCreate(&e), "hipEventCreate");
+    rc = run_trace(dom, a, p, res, true, rec, totals, &ms_trace, &ms_pack, true);
+    if (rc) return rc;
+    res->pending = true;
+    res->pend_dom = dom;
+    res->pend_args = *a;
+    res->pend_args.n_record = 0;
+    res->pend_args.record_ids = nullptr;
+    res->pend_t0 = t0;
+    res->valid = true;
+    return RTHX_OK;
+  }
   rc = run_trace(dom, a, p, res, lookback, rec, totals, &ms_trace, &ms_pack);
   if (rc) return rc;
+  return finish_trace(dom, a, p, res, lookback, rec, totals, ms_trace, ms_pack, t0);
+}
+
+// The checks after a look-back or staged launch (overflow or stall: the same
+// launch traced again), the size hint for the next launch, the info and the
+// row offsets on the host.
+int finish_trace(rthx_domain* dom, const rthx_trace_args* a, const TracePlan& p, rthx_result* res, bool lookback,
+                 const rthx::RecordParams& rec, int64_t totals[rthx::kLbTotals], float ms_trace, float ms_pack,
+                 double t0) {
+  int rc = RTHX_OK;
+  const int64_t R = p.R, n_rows = p.n_rows;
+  const size_t n_rec = res->rec_g.size();
   if (lookback && totals[3] == 0 && totals[4] != 0) {
     // Rows outgrew the reserved direct CSR: the look-back's totals hold the
     // exact nnz, so the same launch -- same draws, same counts -- is traced
@@ -1107,6 +1151,38 @@ int trace_exchange_one(rthx_domain* dom, const rthx_trace_args* a, rthx_result* 
   return RTHX_OK;
 }
 
+// A result traced with RTHX_FLAG_ASYNC, on its first read: its totals back
+// from the device, then the same checks and info as a blocking trace
+// (finish_trace: an overflowed or stalled launch is traced again here).
+int complete_pending(rthx_result* res) {
+  if (!res->pending) return RTHX_OK;
+  res->pending = false;
+  rthx_domain* dom = res->pend_dom;
+  const rthx_trace_args* a = &res->pend_args;
+  HIP_TRY(hipSetDevice(dom->device), "hipSetDevice");
+  HIP_TRY(res->h_totals.reserve(8 * 8), "hipHostMalloc totals");
+  HIP_TRY(hipMemcpyAsync(res->h_totals.p, res->pend_totals, 8 * rthx::kLbTotals, hipMemcpyDeviceToHost, dom->stream),
+          "hipMemcpy totals");
+  HIP_TRY(hipStreamSynchronize(dom->stream), "trace kernel");
+  int64_t totals[rthx::kLbTotals];
+  std::memcpy(totals, res->h_totals.p, 8 * rthx::kLbTotals);
+  float ms_trace = 0.f;
+  HIP_TRY(hipEventElapsedTime(&ms_trace, res->pend_ev[0], res->pend_ev[1]), "hipEventElapsedTime");
+  TracePlan p;
+  int rc = plan_trace_split(dom, a, p);
+  if (rc) return rc;
+  res->valid = false;
+  return finish_trace(dom, a, p, res, true, rthx::RecordParams{}, totals, ms_trace, 0.f, res->pend_t0);
+}
+
+// A result that can be read: traced, and a pending async trace completed.
+int ready(const rthx_result* cres) {
+  if (!cres) return fail(RTHX_EINVAL, "null result");
+  if (!cres->valid) return fail(RTHX_ESTATE, "result holds no trace");
+  rthx::DeviceGuard keep_device;
+  return complete_pending(const_cast<rthx_result*>(cres));
+}
+
 int fetch_row_off(rthx_result* res) {
   if (res->host_row_off) return RTHX_OK;
   HIP_TRY(hipSetDevice(res->device), "hipSetDevice");
@@ -1150,6 +1226,10 @@ int for_each_part(size_t n, F f) {
 
 }  // namespace
 
+namespace rthx {
+int result_ready(const rthx_result* res) { return ready(res); }
+}  // namespace rthx
+
 RTHX_EXPORT int rthx_trace_exchange(rthx_domain* dom, const rthx_trace_args* a, rthx_result* res) {
   if (!dom || !a || !res) return fail(RTHX_EINVAL, "null argument");
   if (a->device != dom->device) return fail(RTHX_EINVAL, "args.device differs from the domain's device");
@@ -1158,7 +1238,7 @@ RTHX_EXPORT int rthx_trace_exchange(rthx_domain* dom, const rthx_trace_args* a, 
 
 RTHX_EXPORT int rthx_result_get_info(const rthx_result* res, rthx_result_info* info) {
   if (!res || !info) return fail(RTHX_EINVAL, "null argument");
-  if (!res->valid) return fail(RTHX_ESTATE, "result holds no trace");
+  if (int rc = ready(res)) return rc;
   *info = res->info;
   return RTHX_OK;
 }
@@ -1282,22 +1362,19 @@ int copy_result(rthx_result* res, int64_t* row_ptr, int32_t* cols, uint32_t* cou
 }  // namespace
 
 RTHX_EXPORT int rthx_result_copy_csr(const rthx_result* cres, int64_t* row_ptr, int32_t* cols, uint32_t* counts) {
-  if (!cres) return fail(RTHX_EINVAL, "null result");
-  if (!cres->valid) return fail(RTHX_ESTATE, "result holds no trace");
+  if (int rc = ready(cres)) return rc;
   return copy_result(const_cast<rthx_result*>(cres), row_ptr, cols, counts, nullptr);
 }
 
 RTHX_EXPORT int rthx_result_copy_F(const rthx_result* cres, int64_t* row_ptr, int32_t* cols, double* vals) {
-  if (!cres) return fail(RTHX_EINVAL, "null result");
-  if (!cres->valid) return fail(RTHX_ESTATE, "result holds no trace");
+  if (int rc = ready(cres)) return rc;
   return copy_result(const_cast<rthx_result*>(cres), row_ptr, cols, nullptr, vals);
 }
 
 namespace {
 // Block `part` of a result (itself for a one-device trace).
 int device_block(const rthx_result* cres, int32_t part, rthx_result** out, int32_t* n_parts) {
-  if (!cres) return fail(RTHX_EINVAL, "null result");
-  if (!cres->valid) return fail(RTHX_ESTATE, "result holds no trace");
+  if (int rc = ready(cres)) return rc;
   rthx_result* res = const_cast<rthx_result*>(cres);
   const int32_t np = res->parts.empty() ? 1 : (int32_t)res->parts.size();
   if (part < 0 || part >= np) return fail(RTHX_EINVAL, "part out of range");
@@ -1348,8 +1425,7 @@ RTHX_EXPORT int rthx_result_copy_csr_device(const rthx_result* cres, int32_t par
 
 RTHX_EXPORT int rthx_result_copy_rays(const rthx_result* cres, double* origins_xy, double* endpoints_xy,
                                       int64_t* emitter, int64_t cap, int64_t* n_out) {
-  if (!cres) return fail(RTHX_EINVAL, "null result");
-  if (!cres->valid) return fail(RTHX_ESTATE, "result holds no trace");
+  if (int rc = ready(cres)) return rc;
   rthx_result* res = const_cast<rthx_result*>(cres);
   // (emitter, part, index in part) of every recorded emitter, ascending emitter
   std::vector<rthx_result*> srcs = res->parts.empty() ? std::vector<rthx_result*>{res} : res->parts;
@@ -1417,6 +1493,11 @@ RTHX_EXPORT int rthx_multi_trace_exchange(rthx_multi* m, const rthx_trace_args* 
   const size_t nd = m->doms.size();
   TracePlan p;
   int rc = plan_trace(m->doms[0], a, p);  // argument checks
+  if (res->pending) {  // (an unread async single-device trace: finished before the buffers go)
+    (void)hipSetDevice(res->device);
+    (void)hipDeviceSynchronize();
+    res->pending = false;
+  }
   if (rc) return rc;
   // a result that held a single-device trace gives up its device buffers
   if (res->device >= 0) {

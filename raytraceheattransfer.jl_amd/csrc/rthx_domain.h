@@ -72,9 +72,20 @@ struct rthx_result {
   std::vector<double> h_orig, h_end;
   bool host_rec = false;
   rthx_result_info info{};
+  // RTHX_FLAG_ASYNC: a look-back launch enqueued and not yet read back; the
+  // first call that reads the result completes it (rthx_api.cpp complete_pending)
+  bool pending = false;
+  rthx_domain* pend_dom = nullptr;
+  rthx_trace_args pend_args{};
+  unsigned long long* pend_totals = nullptr;  // device totals of the pending launch
+  double pend_t0 = 0.0;
+  hipEvent_t pend_ev[2] = {nullptr, nullptr};  // around the pending launch (this result's own events)
   ~rthx_result() {
     for (rthx_result* p : parts) delete p;
     if (device >= 0) (void)hipSetDevice(device);
+    if (pending && device >= 0) (void)hipDeviceSynchronize();  // (a destroyed result's launch must not outlive its buffers)
+    for (auto& e : pend_ev)
+      if (e) (void)hipEventDestroy(e);
     rthx::DevBuf* all[] = {&stage_cols, &stage_cnt, &row_nnz,  &row_tallied, &row_off,  &totals, &cols,
                      &cnt,        &dense,     &rec_ids,  &rec_ok,      &rec_orig, &rec_end, &lb_status, &lb_totals, &fvals, &arrive};
     for (rthx::DevBuf* b : all) b->release();
@@ -94,4 +105,7 @@ enum SplitMerge : int { kNoMerge = 0, kMergeDense = 1, kMergeParts = 2 };
 // recorded after the pack).  Shared by the 2D and 3D tracers.
 int finish_staged(rthx_result* res, const TallyParams& T, int merge, hipStream_t st, hipEvent_t ev_end,
                   int64_t totals[4]);
+// rthx_api.cpp: RTHX_OK when the result holds a trace that can be read (a
+// pending RTHX_FLAG_ASYNC trace is completed first), else the error code.
+int result_ready(const rthx_result* res);
 }  // namespace rthx

@@ -613,7 +613,7 @@ RTHX_EXPORT int rthx_smooth_F_result(const rthx_result* cr, int64_t n, const dou
   if (!out) return fail(RTHX_EINVAL, "null out");
   *out = nullptr;
   if (!cr || !w_in || !args) return fail(RTHX_EINVAL, "bad smoothing arguments");
-  if (!cr->valid) return fail(RTHX_ESTATE, "result holds no trace");
+  if (int rc = rthx::result_ready(cr)) return rc;
   if (!cr->parts.empty() || cr->device < 0)
     return fail(RTHX_EINVAL, "rthx_smooth_F_result needs a single-device result (gather a multi-device CSR first)");
   if (cr->begin != 0 || cr->stride != 1 || cr->n_rows != cr->N)

@@ -500,6 +500,7 @@ RTHX_EXPORT int rthx_trace_exchange_3d(rthx_scene3d* sc, const rthx_trace_args* 
   res->parts.clear();
   res->interleaved = false;
   res->valid = false;
+  res->pending = false;  // (an unread async 2D trace: the device's one stream keeps it before this launch)
   res->host_row_off = false;
   res->host_rec = false;
   res->rec_g.clear();

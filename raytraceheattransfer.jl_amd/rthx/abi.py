@@ -17,6 +17,7 @@ RTHX_ESTATE = -5
 
 RTHX_FLAG_FAITHFUL_SAMPLING = 0x1
 RTHX_FLAG_DEVICE_ONLY = 0x2
+RTHX_FLAG_ASYNC = 0x4  # enqueue only; the first read of the result completes it (include/rthx.h)
 
 _p_i32 = C.POINTER(C.c_int32)
 _p_f64 = C.POINTER(C.c_double)

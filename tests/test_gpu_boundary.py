@@ -478,3 +478,52 @@ def test_gather_and_broadcast_over_rccl(hip):
     finally:
         dist.destroy_process_group()
         res.close()
+
+
+def test_async_traces_equal_blocking_traces(hip):
+    """RTHX_FLAG_ASYNC: traces enqueued back to back into one result (the
+    bench's pipelined steps) read back exactly as blocking traces: the last
+    one's CSR and totals, completed and checked on the first read.  A first
+    trace of a shape blocks (its CSR is sized then); a pending trace that is
+    traced over is superseded; a result destroyed while pending is safe; the
+    device CSR hand-out and F_raw complete a pending trace too."""
+    A = hip.abi
+    dom = H.square_domain(21)
+    flat = dom.flat()
+    dd = hip.DeviceDomain(flat, 0)
+    try:
+        want = {}
+        for seed in (5, 6):
+            args, _k = _args(hip, flat, 4000, seed=seed)
+            want[seed] = _trace(hip, dd, args)
+        res = hip.DeviceResult()
+        try:
+            a5, _k5 = _args(hip, flat, 4000, seed=5, flags=A.RTHX_FLAG_ASYNC | A.RTHX_FLAG_DEVICE_ONLY)
+            a6, _k6 = _args(hip, flat, 4000, seed=6, flags=A.RTHX_FLAG_ASYNC | A.RTHX_FLAG_DEVICE_ONLY)
+            res.trace(dd, a5)  # (first trace of the shape: blocks)
+            for _ in range(4):
+                res.trace(dd, a5)
+            res.trace(dd, a6)  # superseded by the next one
+            res.trace(dd, a5)
+            info = res.info()
+            rp, cols, cnt = res.csr()
+            w = want[5]
+            assert np.array_equal(rp, w[0]) and np.array_equal(cols, w[1]) and np.array_equal(cnt, w[2])
+            for k in ("nnz", "lost_total", "lost_max_row", "rays_traced", "rows_traced"):
+                assert info[k] == w[3][k], k
+            assert info["lookback_fallbacks"] == 0 and info["trace_ms"] > 0
+            # the device CSR of a pending trace
+            res.trace(dd, a6)
+            d = res.device_csr()
+            assert d["nnz"] == want[6][3]["nnz"]
+            rp6, c6, n6 = res.csr()
+            assert np.array_equal(c6, want[6][1]) and np.array_equal(n6, want[6][2])
+            # F_raw of a pending trace
+            res.trace(dd, a5)
+            frp, fc, fv = res.F()
+            assert np.array_equal(fc, w[1]) and np.all(fv > 0)
+            res.trace(dd, a6)  # left pending: closing must be safe
+        finally:
+            res.close()
+    finally:
+        dd.close()

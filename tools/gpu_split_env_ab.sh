@@ -1,17 +1,18 @@
 #!/bin/bash
 # Rank-0 shard of the C2 job at emulated W under environment variants:
-#   bash tools/gpu_split_env_ab.sh "W..." "MODE..." "ENV1;ENV2;..."   (ENV: space-separated VAR=VAL, or "-")
+#   bash tools/gpu_split_env_ab.sh "W..." "MODE..." "ENV1;ENV2;..." [extra bench.py flags]   (ENV: space-separated VAR=VAL, or "-")
 set -o pipefail
 WS=${1:-"4 8"}
 MODES=${2:-"strong weak"}
 IFS=';' read -ra ENVS <<< "${3:--}"
+EXTRA=${4:-}
 for E in "${ENVS[@]}"; do
   for MODE in $MODES; do
     for W in $WS; do
       if [ $W = 1 ]; then extra=""; else extra="--emulate-world $W"; fi
       if [ $MODE = strong ]; then extra="$extra --strong"; fi
       envs=""; [ "$E" != "-" ] && envs="$E"
-      env $envs timeout -k 10 120 python bench.py --no-cpu --faithful-steps 0 --steps 50 --warmup 10 $extra 2>>gpurun_out/split_env.err \
+      env $envs timeout -k 10 120 python bench.py --no-cpu --faithful-steps 0 --steps 50 --warmup 10 $extra $EXTRA 2>>gpurun_out/split_env.err \
         | tail -1 | python -c "
 import json, sys
 d = json.loads(sys.stdin.read())
