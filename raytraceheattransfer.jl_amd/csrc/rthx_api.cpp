@@ -851,7 +851,8 @@ int run_trace(rthx_domain* dom, const rthx_trace_args* a, const TracePlan& p, rt
     // (a first launch of a shape reserves the worst case when it is at most
     // 256 Mi entries -- 2 GiB of columns and counts; C2: 100 M entries, 800
     // MB -- so it never re-traces; round 3's 2048 entries per row made the
-    // first C2 launch overflow and trace twice, profiles/round4/overflow_cost.json)
+    // first C2 launch overflow and trace twice, profiles/round4/overflow_cost.json.
+    // The second launch shrinks the buffers to the measured nnz + 1/8.)
     const int64_t first_guess = worst <= (int64_t(1) << 28) ? worst : std::max<int64_t>(1 << 20, n_rows * std::min<int64_t>(p.row_cap, 4096));
     int64_t want = same && res->lb_nnz_hint > 0
                        ? res->lb_nnz_hint + res->lb_nnz_hint / 8 + 65536
@@ -859,7 +860,7 @@ int run_trace(rthx_domain* dom, const rthx_trace_args* a, const TracePlan& p, rt
     want = std::min<int64_t>(worst, want);
     want = std::max<int64_t>(want, 1);
     for (rthx::DevBuf* b : {&res->cols, &res->cnt}) {
-      if (b->cap > 4 * (size_t)want * 4 + (256u << 20)) b->release();  // (a much larger earlier trace; not the worst-case first guess of this shape)
+      if (b->cap > 2 * (size_t)want * 4 + (64u << 20)) b->release();  // (a much larger earlier trace, or the worst-case first guess of this shape)
       HIP_TRY(b->reserve((size_t)want * 4), "hipMalloc direct CSR");
     }
     // fresh words or totals (or a wrapped epoch): zero them once, epoch 1

@@ -12,7 +12,7 @@ import json, sys
 d = json.loads(sys.stdin.read())
 c = d['config']
 print(f\"W={$W}  rank-0 rows {c['rays_per_step'] // c['rays_per_emitter']:6d}  R={c['rays_per_emitter']}  \"
-      f\"ms/step {d['ms_per_step']:.4f}  kernel {d['roofline']['avg_kernel_ms']:.4f} ms  pack {d['pack_ms']:.4f} ms  \"
+      f\"ms/step {d['ms_per_step']:.4f} (blocking {d['blocking_ms_per_step']:.4f})  kernel {d['roofline']['avg_kernel_ms']:.4f} ms  pack {d['pack_ms']:.4f} ms  \"
       f\"rank-0 {d.get('rank0_mrays_s') or d['value']:.1f} Mrays/s\")
 " || exit 1
 done
