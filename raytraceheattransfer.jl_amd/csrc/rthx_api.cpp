@@ -499,7 +499,7 @@ RTHX_EXPORT int rthx_domain_create(const rthx_domain_desc* desc, int32_t device,
       off = a16(off + 8 * nc);
       if (ncx == 1) {  // layer records (walk_layers), staged per bin
         G.off_lay = (int32_t)off;
-        off = a16(off + sizeof(rthx::LayerRec) * (size_t)ncy);
+        off = a16(off + sizeof(rthx::LayerRec) * (size_t)(ncy + 2));  // (sentinels below and above)
       }
       G.inv_x = (double)nx / (xs[nx] - xs[0]);
       G.inv_y = (double)ny / (ys[ny] - ys[0]);

@@ -116,7 +116,7 @@ struct MLatLayout {
   int32_t blob_bytes;  // staged from ml_blob
   int32_t nx, ny, ncx, ncy;
   int32_t off_ys, off_cxs, off_cys, off_cmap, off_cinfo, off_bsolid, off_beta;
-  int32_t off_lay;     // one coarse column (ncx == 1): LayerRec[ncy] staged per bin after the betas; else 0
+  int32_t off_lay;     // one coarse column (ncx == 1): LayerRec[ncy + 2] (a sentinel, the layers, a sentinel) staged per bin after the betas; else 0
   double inv_x, inv_y, inv_cx, inv_cy;  // first guesses of lattice_index
 };
 
@@ -1164,7 +1164,7 @@ struct MLatLds {
   const MCoarse RTHX_LDS* cinfo;
   const uint32_t RTHX_LDS* bsolid;
   const double RTHX_LDS* beta;
-  const LayerRec RTHX_LDS* lay;  // (one-column lattices)
+  const LayerRec RTHX_LDS* lay;  // (one-column lattices: lay[-1] and lay[ncy] are sentinels)
 };
 
 __device__ __forceinline__ MLatLds mlat_lds_view(const char RTHX_LDS* base, const MLatLayout& G) {
@@ -1177,7 +1177,7 @@ __device__ __forceinline__ MLatLds mlat_lds_view(const char RTHX_LDS* base, cons
   v.cinfo = (const MCoarse RTHX_LDS*)(base + G.off_cinfo);
   v.bsolid = (const uint32_t RTHX_LDS*)(base + G.off_bsolid);
   v.beta = (const double RTHX_LDS*)(base + G.off_beta);
-  v.lay = (const LayerRec RTHX_LDS*)(base + G.off_lay);
+  v.lay = (const LayerRec RTHX_LDS*)(base + G.off_lay) + 1;
   return v;
 }
 
@@ -1358,27 +1358,45 @@ __device__ __forceinline__ int walk_ml(const DevDomain& D, const TraceParams& P,
 // stack of layers j with bounds cys[j], cys[j + 1] (the greenhouse of C5).
 // A ray crosses only layer boundaries (an x wall is the lattice's side:
 // solid, or the ray leaves), so the walker keeps just its layer index and
-// reads the layer's record (bounds, beta, solid walls: LayerRec, two LDS
-// reads) at each segment.  The point is checked against its layer's box at
-// the start of every segment instead of after each crossing: the same test
-// of the neighbouring box (the layer across the crossed boundary; across a
-// side wall or the lattice's top or bottom the layer is kept, which the
-// check then fails).  A point outside it -- a crossing through a corner, a
-// nudge that did not carry the point across, a point outside the lattice --
-// ends the walk with kRayRelocate; the kernel locates it on the lattice
+// reads the layer's record (bounds, beta, solid walls: LayerRec) at each
+// segment.  The point is checked against its layer's box at the start of
+// every segment instead of after each crossing: the same test of the
+// neighbouring box (the layer across the crossed boundary; across a side
+// wall or the lattice's top or bottom the layer is kept, which the check then
+// fails).  A point outside it -- a crossing through a corner, a nudge that
+// did not carry the point across, a point outside the lattice -- ends the
+// walk with kRayRelocate; the kernel locates it on the lattice
 // (relocate_layers: findFace2D's answer, lost when in no box) and the walk
 // goes on.  Same arithmetic, candidates, ties, step count and results as
-// walk_ml.  The loop body is straight-line code: a lane whose ray ends
-// leaves the loop, the wave leaves it when at most `stop` lanes still walk.
-// MIXED: some layer of this bin has no single beta.
+// walk_ml.  MIXED: some layer of this bin has no single beta.
+//
+// Two forms share that arithmetic.  layer_segment is one segment with every
+// case (either wall the nearer, no candidate, the point outside its layer).
+// walk_layers is the loop over the common case only -- the point strictly
+// inside its layer and the y wall the ray points to the nearer candidate --
+// which needs no wall selection: every other segment ends the loop with
+// kRaySlowSeg, before anything is applied, and the kernel runs it through
+// layer_segment.  An x-wall segment is a ray's last (the lattice's side is
+// solid, or the ray leaves it), so the slow path runs about once per ray.
+// The layer records carry a sentinel below the first and above the last
+// layer (NaN bounds: every comparison fails), so a crossing out of the
+// lattice needs no range check in the loop: the sentinel's segment is slow,
+// and layer_segment clamps the layer as walk_ml keeps it.
 constexpr int kRayRelocate = -6;  // walk_layers: p is not in its layer's box
+constexpr int kRaySlowSeg = -7;   // walk_layers: a segment outside the common case (layer_segment finishes it)
+constexpr int kMaxWalkSteps = 10000;  // traceRay.jl:27: no end within 10,000 steps
 
+// One segment of the layered walk from layer cj (the full case analysis;
+// walk_ml's segment on one column): the ray's end (kRayEndGas /
+// kRayEndWall, p at the segment start, u_end its wall parameter),
+// kRayRelocate, -1 (lost), or kRayContinue after the crossing.
 template <bool UNIFORM, bool MIXED>
-__device__ __forceinline__ int walk_layers(const DevDomain& D, const TraceParams& P, const MLatLds& L,
-                                           const MLatLayout& G, MBox& B, double& px, double& py, const MRay& r,
-                                           double& S, double& acc, int& it, double& u_end, uint32_t stop) {
+__device__ __forceinline__ int layer_segment(const DevDomain& D, const TraceParams& P, const MLatLds& L,
+                                             const MLatLayout& G, int& cj, double& px, double& py, const MRay& r,
+                                             double& S, double& acc, int& it, double& u_end) {
   const double eta = P.eta;
   const int ncy = G.ncy;
+  cj = cj < 0 ? 0 : cj >= ncy ? ncy - 1 : cj;  // (walk_layers may stand on a sentinel)
   const bool xdn = r.dx < 0.0, ydn = r.dy < 0.0;
   const double ax = fabs(r.dx), ay = fabs(r.dy);
   const bool vxd = ax >= 1e-10, vyd = ay >= 1e-10;
@@ -1389,23 +1407,86 @@ __device__ __forceinline__ int walk_layers(const DevDomain& D, const TraceParams
   const int sy = ydn ? -1 : 1;
   const double x0 = L.cxs[0], x1 = L.cxs[1];
   const double xf = xdn ? x0 : x1;
+  const LayerRec rec = ld(L.lay + cj);
+  const bool inside = (x0 <= px) & (px < x1) & (rec.y0 <= py) & (py < rec.y1);
+  const double yf = ydn ? rec.y0 : rec.y1;
+  const double nx = fabs(xf - px), ny = fabs(yf - py);
+  // a wall is a candidate when its parameter num / den is > 0: den >= 1e-10
+  // and num > 0 (num / den > 0 exactly then, for den <= 1)
+  const bool vx = vxd & (nx > 0.0), vy = vyd & (ny > 0.0);
+  const double cx = __dmul_rn(nx, ay), cy = __dmul_rn(ny, ax);
+  const bool xw = vx & (!vy | (y_first & (cx < cy)) | (!y_first & (cx <= cy)));
+  const bool any = vx | vy;
+  const double u = any ? div_by_rcp(xw ? nx : ny, xw ? ax : ay, xw ? r.rax : r.ray) : __builtin_inf();
+  const int k = any ? (xw ? kx : ky) : 0;
+  bool gas, lost = false;
+  double accn = 0.0;
+  if (UNIFORM) {
+    gas = S < u;
+  } else {
+    double beta = rec.beta;
+    if (MIXED) {
+      if (beta < 0.0) {
+        const MCoarse m = ld(L.cinfo + L.cmap[cj]);
+        int i, j;
+        const int f0 = ml_fine(L, G, m, px, py, i, j);
+        lost = f0 < 0;  // the segment start lies in no fine cell (traceRay.jl:89-91)
+        beta = lost ? 0.0 : D.beta[(size_t)P.bin * D.n_fine + f0];
+      }
+    }
+    accn = acc + __dmul_rn(beta, u);
+    gas = accn >= S;
+  }
+  const bool wall = !gas & (((rec.solid >> k) & 1u) != 0u);
+  if (!inside | lost | gas | wall) {
+    u_end = u;
+    return !inside ? kRayRelocate : lost ? -1 : gas ? kRayEndGas : kRayEndWall;
+  }
+  const double t = u + eta;
+  px = px + __dmul_rn(t, r.dx);
+  py = py + __dmul_rn(t, r.dy);
+  if (UNIFORM) S -= u; else acc = accn;
+  const int cjn = cj + sy;
+  cj = (!xw & ((unsigned)cjn < (unsigned)ncy)) ? cjn : cj;
+  return ++it >= kMaxWalkSteps ? -1 : kRayContinue;
+}
+
+template <bool UNIFORM, bool MIXED>
+__device__ __forceinline__ int walk_layers(const DevDomain& D, const TraceParams& P, const MLatLds& L,
+                                           const MLatLayout& G, MBox& B, double& px, double& py, const MRay& r,
+                                           double& S, double& acc, int& it, double& u_end, uint32_t stop) {
+  const double eta = P.eta;
+  const bool xdn = r.dx < 0.0, ydn = r.dy < 0.0;
+  const double ax = fabs(r.dx), ay = fabs(r.dy);
+  // (|dy| < 1e-10: the y wall is never a candidate -- every segment is slow)
+  const bool vxd = ax >= 1e-10, vyd = ay >= 1e-10;
+  const bool y_first = ydn | xdn;
+  const uint64_t xinc = y_first ? 0u : 1u;  // the x wall wins ties unless the y wall comes first
+  const uint32_t ybit = ydn ? 1u : 4u;  // solid bit of the y wall the ray points to (wall 0 or 2)
+  const int sy = ydn ? -1 : 1;
+  const double x0 = L.cxs[0], x1 = L.cxs[1];
+  const double xf = xdn ? x0 : x1;
+  const int yoff = ydn ? 0 : 8;  // byte offset of that wall's bound in the LayerRec
   int cj = B.cj;
+  bool fast = true, gas = false, lost = false;
+  double u = 0.0;
   int status = kRayContinue;
 #pragma unroll 1
   while (true) {
-    const LayerRec rec = ld(L.lay + cj);
-    const bool inside = (x0 <= px) & (px < x1) & (rec.y0 <= py) & (py < rec.y1);
-    const double yf = ydn ? rec.y0 : rec.y1;
+    const LayerRec RTHX_LDS* lr = L.lay + cj;
+    const LayerRec rec = ld(lr);
+    const double yf = *(const double RTHX_LDS*)((const char RTHX_LDS*)lr + yoff);
+    // the common case: p strictly inside the layer (y0 < py: then the y wall
+    // is a candidate whichever way the ray points; x0 < px < x1 likewise for
+    // the x wall) and the y wall the nearer candidate.  p == y0 or p == x0,
+    // inside but perhaps without a candidate, is left to layer_segment.
     const double nx = fabs(xf - px), ny = fabs(yf - py);
-    // a wall is a candidate when its parameter num / den is > 0: den >= 1e-10
-    // and num > 0 (num / den > 0 exactly then, for den <= 1)
-    const bool vx = vxd & (nx > 0.0), vy = vyd & (ny > 0.0);
     const double cx = __dmul_rn(nx, ay), cy = __dmul_rn(ny, ax);
-    const bool xw = vx & (!vy | (y_first & (cx < cy)) | (!y_first & (cx <= cy)));
-    const bool any = vx | vy;
-    const double u = any ? div_by_rcp(xw ? nx : ny, xw ? ax : ay, xw ? r.rax : r.ray) : __builtin_inf();
-    const int k = any ? (xw ? kx : ky) : 0;
-    bool gas, lost = false;
+    // (the wall order as one compare: cx <= cy is cx < nextup(cy) for these
+    // finite non-negative products, nextup being the next bit pattern)
+    const bool xw = vxd & (cx < bitsd(dbits(cy) + xinc));
+    fast = vyd & (x0 < px) & (px < x1) & (rec.y0 < py) & (py < rec.y1) & !xw;
+    u = div_by_rcp(ny, ay, r.ray);
     double accn = 0.0;
     if (UNIFORM) {
       gas = S < u;
@@ -1413,34 +1494,30 @@ __device__ __forceinline__ int walk_layers(const DevDomain& D, const TraceParams
       double beta = rec.beta;
       if (MIXED) {
         if (beta < 0.0) {
-          const MCoarse m = ld(L.cinfo + L.cmap[cj]);
+          const MCoarse m = ld(L.cinfo + L.cmap[cj]);  // (a sentinel's beta is 0)
           int i, j;
           const int f0 = ml_fine(L, G, m, px, py, i, j);
-          lost = f0 < 0;  // the segment start lies in no fine cell (traceRay.jl:89-91)
+          lost = f0 < 0;  // (traceRay.jl:89-91)
           beta = lost ? 0.0 : D.beta[(size_t)P.bin * D.n_fine + f0];
         }
       }
       accn = acc + __dmul_rn(beta, u);
       gas = accn >= S;
     }
-    const bool wall = !gas & (((rec.solid >> k) & 1u) != 0u);
-    if (!inside | lost | gas | wall) {
-      status = !inside ? kRayRelocate : lost ? -1 : gas ? kRayEndGas : kRayEndWall;
-      u_end = u;
+    const bool wall = !gas & ((rec.solid & ybit) != 0u);
+    if ((it >= kMaxWalkSteps) | !fast | lost | gas | wall) {
+      status = it >= kMaxWalkSteps ? -1 : !fast ? kRaySlowSeg : lost ? -1 : gas ? kRayEndGas : kRayEndWall;
       break;
     }
     const double t = u + eta;
     px = px + __dmul_rn(t, r.dx);
     py = py + __dmul_rn(t, r.dy);
     if (UNIFORM) S -= u; else acc = accn;
-    const int cjn = cj + sy;
-    cj = (!xw & ((unsigned)cjn < (unsigned)ncy)) ? cjn : cj;
-    if (++it >= 10000) {  // traceRay.jl:27: no end within 10,000 steps
-      status = -1;
-      break;
-    }
+    cj += sy;  // (out of the lattice: a sentinel record, whose segment is slow)
+    ++it;
     if ((uint32_t)__popcll(__ballot(1)) <= stop) break;  // (the lanes still walking)
   }
+  u_end = u;
   B.ci = 0;
   B.cj = cj;
   B.b = cj;

@@ -46,7 +46,7 @@ namespace rthx {
 constexpr int kBufferRsrcWord3 = 0x00020000;
 constexpr int kSc1 = 16;
 #ifndef RTHX_REFILL_Q
-#define RTHX_REFILL_Q 24  // MLAT kernels: idle lanes before the ends are resolved and the queue refills (C5 band 0 / 7 at 1e9 rays: 8 69.7 / 43.3 ms, 16 59.2 / 36.6, 24 57.0 / 34.3, 32 59.5 / 35.5, 40 61.9 / 34.6)
+#define RTHX_REFILL_Q 40  // MLAT kernels: idle lanes before the ends are resolved and the queue refills (C5 at 1e9 rays, band 0 / 4, with walk_layers' fast loop: 24 53.0 / 34.0 ms, 32 49.8 / 32.9, 40 50.2 / 31.2, 48 51.8 / 30.7, 56 59.6 / 32.1; at 1e8: 24 8.65 / 6.45, 40 8.50 / 6.08, 48 9.04 / 6.26)
 #endif
 #ifndef RTHX_REFILL
 #define RTHX_REFILL 32  // refill / end batch of the multi-polygon kernels (lanes; C5: 16 24 32 40 -> 32)
@@ -430,12 +430,14 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
       const char RTHX_GLOBAL* blob = (const char RTHX_GLOBAL*)D.ml_blob;
       const double RTHX_GLOBAL* cys = (const double RTHX_GLOBAL*)(blob + D.ml.off_cys);
       const uint32_t RTHX_GLOBAL* bs = (const uint32_t RTHX_GLOBAL*)(blob + D.ml.off_bsolid);
-      for (int i = tid; i < D.ml.ncy; i += nthr) {
+      // lay[0] and lay[ncy + 1]: sentinels (NaN bounds, beta 0, open walls)
+      for (int i = tid; i < D.ml.ncy + 2; i += nthr) {
+        const bool layer = i >= 1 && i <= D.ml.ncy;
         LayerRec r;
-        r.y0 = cys[i];
-        r.y1 = cys[i + 1];
-        r.beta = D.ml_bbeta[(size_t)P.bin * D.n_coarse + i];
-        r.solid = bs[i];
+        r.y0 = layer ? cys[i - 1] : __builtin_nan("");
+        r.y1 = layer ? cys[i] : __builtin_nan("");
+        r.beta = layer ? D.ml_bbeta[(size_t)P.bin * D.n_coarse + i - 1] : 0.0;
+        r.solid = layer ? bs[i - 1] : 0u;
         r.pad = 0u;
         lay[i] = r;
       }
@@ -586,6 +588,14 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
     int state = -1;
     while (true) {
       // Resolve the ended rays, then hand the queue's rays to the idle lanes.
+      if (state == kRaySlowSeg) {  // (walk_layers: a segment outside its common case; first, as it may end the ray)
+        int cj = box.cj;
+        state = P.mixed ? layer_segment<UNIFORM, true>(D, P, RTHX_ML_VIEW, RTHX_ML_G, cj, px, py, ry, S, acc, it, u_end)
+                        : layer_segment<UNIFORM, false>(D, P, RTHX_ML_VIEW, RTHX_ML_G, cj, px, py, ry, S, acc, it, u_end);
+        box.ci = 0;
+        box.cj = cj;
+        box.b = cj;
+      }
       if (state == kRayEndGas || state == kRayEndWall) {
         const bool gas = state == kRayEndGas;
         end_move_ml<UNIFORM>(D, P, RTHX_ML_VIEW, RTHX_ML_G, box, px, py, ry, S, acc, u_end, gas);
