@@ -4,7 +4,7 @@
 #                                          traffic, per-config table (C5 per band
 #                                          and total), 3D tracer, mesh() pipeline,
 #                                          SQ counters of the headline kernel
-#   bash tools/gpu_round3_final.sh TAG b   SQ counters of C5 band 0, strong-scaling
+#   bash tools/gpu_round3_final.sh TAG b   SQ counters of C5 band 0, C5's 8-rank emulation, strong-scaling
 #                                          emulation of C2, the direct-method cases
 #                                          and D2's SQ counters, the 3D tracer's SQ
 #                                          counters, smoke()
@@ -25,6 +25,8 @@ else
   bash tools/gpu_sq_any.sh c5b0_$TAG trace_exchange_kernel 999956940 python3 $PWD/tools/bench_configs.py --only C5 \
     --rays 1e9 --steps 1 --bins 0 --no-ramp > $OUT/sq_c5b0_$TAG.log 2>&1 || exit 1
   grep -v "^  SQ_" $OUT/sq_c5b0_$TAG.log
+  timeout -k 10 300 python tools/bench_c5_bands.py --emulate-world 8 --rays 1e9 --steps 2 > $OUT/c5_emulated.log 2>&1 || exit 1
+  grep -v amdgpu $OUT/c5_emulated.log
   bash tools/gpu_strong.sh > $OUT/strong_emulated.log 2>&1 || exit 1
   cat $OUT/strong_emulated.log
   timeout -k 10 300 python tools/bench_direct.py > $OUT/direct.log 2>&1 || exit 1
