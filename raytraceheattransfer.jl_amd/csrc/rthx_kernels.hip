@@ -121,9 +121,6 @@ __device__ __forceinline__ uint64_t lookback_offset(unsigned long long* status, 
 // same sums as lookback_offset; called by every lane of the wave, result in
 // every lane.  A row whose predecessors finished together (a round of rows,
 // split parts) sums up to 64 aggregates per poll instead of one.
-#ifndef RTHX_LB_WAVE
-#define RTHX_LB_WAVE 1
-#endif
 __device__ __forceinline__ uint64_t lookback_offset_wave(unsigned long long* status, int64_t slot, uint32_t nnz,
                                                          unsigned long long* stalled, uint64_t wait_ticks,
                                                          uint32_t epoch) {
@@ -913,10 +910,10 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
   };
   if (SINGLE && T.lb_status) {  // (host: single-polygon domains only; keeps the other kernels lean)
     auto base_of = [&](uint32_t nnz) -> uint64_t {
-      if (RTHX_LB_WAVE ? tid < 64 : tid == 0) {
-        const uint64_t b = RTHX_LB_WAVE
-                               ? lookback_offset_wave(T.lb_status, slot, nnz, &T.totals[3], T.lb_wait_ticks, T.lb_epoch)
-                               : lookback_offset(T.lb_status, slot, nnz, &T.totals[3], T.lb_wait_ticks, T.lb_epoch);
+      // (the wave-wide walk: 0.8-1.5 % faster than one lane's,
+      // profiles/round4/ab/lookback_wave_vs_one_lane.log)
+      if (tid < 64) {
+        const uint64_t b = lookback_offset_wave(T.lb_status, slot, nnz, &T.totals[3], T.lb_wait_ticks, T.lb_epoch);
         if (tid == 0) {
           s_base = b;
           if (b + nnz > (uint64_t)T.out_cap) atomicAdd(&T.totals[4], 1ull);  // (the host re-traces)
