@@ -250,36 +250,94 @@ function flatten(rtm)
     return Flat(keep, grids, Ref(desc))
 end
 
-# one uploaded domain per rtm: an rthx_domain (one device) or an rthx_multi
-# (DEVICES, rows split over them)
-const DOMAINS = IdDict{Any, Tuple{Flat, Ptr{Cvoid}, Bool}}()
-
-function device_domain(rtm)
-    haskey(DOMAINS, rtm) && return DOMAINS[rtm][2]
-    flat = flatten(rtm)
-    h = Ref{Ptr{Cvoid}}(C_NULL)
-    GC.@preserve flat begin
-        check(ccall((:rthx_domain_create, LIB[]), Cint, (Ptr{DomainDesc}, Int32, Ptr{Ptr{Cvoid}}),
-                    flat.desc, DEVICE[], h))
-    end
-    DOMAINS[rtm] = (flat, h[], false)
-    return h[]
+# --- uploaded domains -------------------------------------------------------
+# One upload per (rtm, kind): an rthx_domain (one device) or an rthx_multi
+# (DEVICES, rows split over them).  The reference reads the domain live at
+# every trace (traceRay.jl:87-100 reads kappa_g / sigma_s_g per segment, and
+# its tests set n_spectral_bins after construction, test/test_2d_spectral.jl:79),
+# so every call flattens rtm again and compares the flattened geometry,
+# beta[fine, bin] and uniform_across_bin with the upload's (same_domain): a
+# mutated domain, another device list or another library is uploaded again.
+# Uploads are held in a WeakKeyDict (rtm is a mutable struct): when rtm is
+# collected the entry goes, and the Uploaded's finalizer frees the device
+# copy.  `invalidate!(rtm)` and `release_all!()` free them explicitly.
+mutable struct Uploaded
+    flat::Flat
+    handle::Ptr{Cvoid}
+    multi::Bool
+    devices::Vector{Int32}
+    lib::String
 end
 
-const MULTI = IdDict{Any, Tuple{Flat, Ptr{Cvoid}}}()
+function release!(u::Uploaded)
+    if u.handle != C_NULL
+        ccall((u.multi ? :rthx_multi_destroy : :rthx_domain_destroy, u.lib), Cvoid, (Ptr{Cvoid},), u.handle)
+        u.handle = C_NULL
+    end
+    return nothing
+end
 
-function multi_domain(rtm)
-    haskey(MULTI, rtm) && return MULTI[rtm][2]
+const UPLOADS = WeakKeyDict{Any, Dict{Bool, Uploaded}}()
+
+"""
+    same_domain(a::Flat, b::Flat)
+
+Element-wise equality of two flattenings' numeric arrays (geometry, grids,
+LUTs, beta[fine, bin], uniform_across_bin), not of their descriptors, whose
+pointers differ per flatten.  (Base's `hash` of a large array samples only
+some elements, so a changed kappa could hash alike: compare them all.)
+"""
+same_domain(a::Flat, b::Flat) =
+    length(a.arrays) == length(b.arrays) &&
+    all(x isa Vector{GridDesc} || isequal(x, y) for (x, y) in zip(a.arrays, b.arrays))
+
+"""
+    invalidate!(rtm)
+
+Free rtm's uploaded device copies (both kinds); the next trace uploads it
+again.  Mutations are also caught by the per-call comparison.
+"""
+function invalidate!(rtm)
+    ups = pop!(UPLOADS, rtm, nothing)
+    ups === nothing || foreach(release!, values(ups))
+    return nothing
+end
+
+"Free every uploaded domain (e.g. before `enable!` with another library)."
+function release_all!()
+    for k in collect(keys(UPLOADS))
+        invalidate!(k)
+    end
+    return nothing
+end
+
+function uploaded(rtm, multi::Bool)
     flat = flatten(rtm)
+    devs = multi ? copy(DEVICES[]) : Int32[DEVICE[]]
+    ups = get!(() -> Dict{Bool, Uploaded}(), UPLOADS, rtm)
+    u = get(ups, multi, nothing)
+    if u !== nothing && u.handle != C_NULL && same_domain(u.flat, flat) && u.devices == devs && u.lib == LIB[]
+        return u.handle
+    end
+    u === nothing || release!(u)
     h = Ref{Ptr{Cvoid}}(C_NULL)
-    devs = DEVICES[]
     GC.@preserve flat devs begin
-        check(ccall((:rthx_multi_create, LIB[]), Cint, (Ptr{DomainDesc}, Ptr{Int32}, Int32, Ptr{Ptr{Cvoid}}),
-                    flat.desc, devs, Int32(length(devs)), h))
+        if multi
+            check(ccall((:rthx_multi_create, LIB[]), Cint, (Ptr{DomainDesc}, Ptr{Int32}, Int32, Ptr{Ptr{Cvoid}}),
+                        flat.desc, devs, Int32(length(devs)), h))
+        else
+            check(ccall((:rthx_domain_create, LIB[]), Cint, (Ptr{DomainDesc}, Int32, Ptr{Ptr{Cvoid}}),
+                        flat.desc, devs[1], h))
+        end
     end
-    MULTI[rtm] = (flat, h[])
-    return h[]
+    u = Uploaded(flat, h[], multi, devs, LIB[])
+    finalizer(release!, u)
+    ups[multi] = u
+    return u.handle
 end
+
+device_domain(rtm) = uploaded(rtm, false)
+multi_domain(rtm) = uploaded(rtm, true)
 
 # Page-locked cols / counts buffers reused across traces (rthx_host_register):
 # the library DMAs the device CSR straight into them.
@@ -582,6 +640,7 @@ the other calls run on the first.
 """
 function enable!(; lib::AbstractString, device::Integer = 0, devices = [device], seed::Integer = 1,
                  faithful::Bool = false, smoothing::Bool = false, direct::Bool = true, viewfactors3d::Bool = true)
+    lib == LIB[] || release_all!()  # (uploads belong to the library that made them)
     LIB[] = lib
     DEVICES[] = Int32[d for d in devices]
     isempty(DEVICES[]) && error("enable!: empty device list")

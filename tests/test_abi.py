@@ -148,3 +148,25 @@ def test_julia_shim_mirrors_header():
     called = set(re.findall(r"ccall\(\(:(rthx_\w+)", jl))
     assert called and called <= set(declared_functions())
     assert f"RTHX_ABI_VERSION = Int32({abi.RTHX_ABI_VERSION})" in jl
+
+
+def test_julia_shim_domain_cache_invalidates():
+    """The shim's upload cache (RTHX.jl `uploaded`) must not serve a stale
+    device copy: the reference reads kappa/sigma live at every trace
+    (traceRay.jl:87-100) and its tests mutate a domain after construction
+    (test/test_2d_spectral.jl:79).  Not executable here (no Julia): checked
+    as text -- uploads compared element-wise with a fresh flattening every
+    call, keyed on the device list and library, weakly keyed on rtm with a
+    finalizer that destroys the device copy, and an explicit invalidate!."""
+    jl = open(os.path.join(H.ROOT, "raytraceheattransfer.jl_amd", "julia", "RTHX.jl")).read()
+    up = re.search(r"\nfunction uploaded\(rtm, multi::Bool\)\n(.*?)\nend\n", jl, re.S).group(1)
+    assert "flatten(rtm)" in up and "same_domain(u.flat, flat)" in up
+    assert "u.devices == devs" in up and "u.lib == LIB[]" in up
+    assert "release!(u)" in up and "finalizer(release!, u)" in up
+    assert "WeakKeyDict" in jl and "IdDict" not in jl
+    assert re.search(r"\nfunction invalidate!\(rtm\)\n", jl)
+    rel = re.search(r"\nfunction release!\(u::Uploaded\)\n(.*?)\nend\n", jl, re.S).group(1)
+    assert ":rthx_multi_destroy" in rel and ":rthx_domain_destroy" in rel and "C_NULL" in rel
+    # every trace call site goes through the checked cache
+    assert "device_domain(rtm) = uploaded(rtm, false)" in jl and "multi_domain(rtm) = uploaded(rtm, true)" in jl
+    assert "release_all!()" in re.search(r"\nfunction enable!\((.*?)\nend\n", jl, re.S).group(1)
