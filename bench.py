@@ -353,6 +353,15 @@ def main():
     elapsed = time.perf_counter() - t0
     barrier()
     info = res.info()  # the last step, completed and checked
+    # Every timed step is checked, not only the last: a step that a later
+    # one replaced before any read (RTHX_FLAG_ASYNC) had its look-back stall
+    # and CSR-overflow flags carried into the next step's totals by the
+    # device (rthx_result_info superseded / superseded_faults).
+    if info["superseded_faults"] != 0:
+        raise SystemExit(f"bench: {info['superseded_faults']} timed step(s) stalled or overflowed their CSR")
+    steps_checked = info["superseded"] + 1
+    if not args.blocking and args.mode != "threads" and steps_checked != args.steps:
+        raise SystemExit(f"bench: {steps_checked} of {args.steps} timed steps accounted for")
     # Kernel time per launch (HIP events) and the blocking-call rate, from
     # blocking steps after the timed region (the roofline's avg kernel time)
     trace_ms = []
@@ -507,6 +516,7 @@ def main():
             },
             "pack_ms": round(float(np.mean(pack_ms)), 4),
             "step_mode": "blocking calls" if args.blocking else "enqueued back to back (RTHX_FLAG_ASYNC)",
+            "steps_checked": steps_checked,
             "blocking_ms_per_step": round(blocking_ms, 4),
             "roofline_fp64": fp64_roof,
             "roofline_valu": valu_roof,

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define RTHX_ABI_VERSION 2
+#define RTHX_ABI_VERSION 3  /* 3: rthx_result_info.superseded / superseded_faults */
 
 /* status codes */
 #define RTHX_OK 0
@@ -162,6 +162,11 @@ typedef struct rthx_result_info {
                               on a predecessor row (re-traced on the staging path), or the
                               rows outgrew the CSR reserved from the previous launch's nnz
                               (re-traced into buffers of the exact size) */
+  int32_t superseded;      /* RTHX_FLAG_ASYNC traces on this result that a later trace replaced
+                              before anything read them (their counts were never read) */
+  int32_t superseded_faults; /* of those, traces whose look-back stalled or whose rows
+                              outgrew the CSR: a result is never re-traced for them, but a
+                              benchmark of back-to-back async steps checks that this is 0 */
 } rthx_result_info;
 
 typedef struct rthx_domain rthx_domain;

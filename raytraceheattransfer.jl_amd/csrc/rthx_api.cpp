@@ -85,17 +85,29 @@ hipError_t device_stream(int device, hipStream_t* out) {
 }
 }  // namespace rthx
 
+namespace rthx {
+bool knobs_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("RTHX_DEV_KNOBS");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
+const char* knob(const char* name) { return knobs_enabled() ? getenv(name) : nullptr; }
+}  // namespace rthx
+
 namespace {
 
-// Integer tuning knob from the environment, clamped to [lo, hi].
+// Integer tuning knob (rthx::knob), clamped to [lo, hi].
 int64_t env_int(const char* name, int64_t dflt, int64_t lo, int64_t hi) {
-  const char* e = getenv(name);
+  const char* e = rthx::knob(name);
   if (!e || !*e) return dflt;
   return std::min<int64_t>(hi, std::max<int64_t>(lo, std::strtoll(e, nullptr, 10)));
 }
 
 bool env_flag(const char* name) {
-  const char* e = getenv(name);
+  const char* e = rthx::knob(name);
   return e && e[0] == '1';
 }
 
@@ -673,20 +685,13 @@ namespace {
 constexpr uint64_t kLookbackWaitTicks = 25'000'000;
 
 uint64_t lookback_wait_ticks() {
-  const char* e = getenv("RTHX_LB_WAIT_US");
+  const char* e = rthx::knob("RTHX_LB_WAIT_US");
   if (e && *e) return (uint64_t)std::strtoull(e, nullptr, 10) * 100;  // 100 ticks per microsecond
   return kLookbackWaitTicks;
 }
 
-// Launch geometry of one trace call (rows, split, LDS histogram layout).
-struct TracePlan {
-  int64_t N = 0, R = 0, end = 0, n_rows = 0, split = 1, row_cap = 1, hash_cap = 0, bm_words = 0, part_cap = 0;
-  bool part_lists = false;  // split hash rows: sorted part lists + part_merge_kernel (else the last part merges)
-  int tally = rthx::kTallyU16;
-  int clds = 0;  // rthx_kernels.h LaunchCfg::clds
-  bool recording = false, uniform = true;
-  size_t lds_bytes = 0, cl_offset = 0;
-};
+using rthx::TracePlan;  // (rthx_domain.h: a pending async trace keeps its plan)
+static_assert(rthx::kTallyU16 == 1, "TracePlan::tally default");
 
 // Hash tallies (large N): the largest table the trace kernel's LDS holds
 // (keys + counts, 8 B per slot); a workgroup traces at most 3/4 as many rays.
@@ -819,7 +824,10 @@ int plan_trace_split(const rthx_domain* dom, const rthx_trace_args* a, TracePlan
   int64_t slots = 0;
   rthx::LaunchCfg L = launch_of(dom, a, p);
   L.slots = &slots;
-  HIP_TRY(rthx::launch_trace(L), "trace kernel occupancy");
+  if (rthx::launch_trace(L) != hipSuccess || slots <= 0) {  // (occupancy unknown: the plan without a slot split)
+    (void)hipGetLastError();
+    return RTHX_OK;
+  }
   return plan_trace(dom, a, p, slots);
 }
 
@@ -829,7 +837,7 @@ int plan_trace_split(const rthx_domain* dom, const rthx_trace_args* a, TracePlan
 // finish_staged; totals[3] > 0: a look-back wait gave up).
 int run_trace(rthx_domain* dom, const rthx_trace_args* a, const TracePlan& p, rthx_result* res, bool lookback,
               const rthx::RecordParams& rec, int64_t totals[rthx::kLbTotals], float* ms_trace, float* ms_pack,
-              bool async = false) {
+              bool async = false, bool check_prev = false) {
   const int64_t n_rows = p.n_rows, N = p.N, R = p.R;
   hipStream_t st = dom->stream;
   HIP_TRY(res->row_nnz.reserve((size_t)n_rows * 4), "hipMalloc row_nnz");
@@ -888,9 +896,11 @@ int run_trace(rthx_domain* dom, const rthx_trace_args* a, const TracePlan& p, rt
   if (p.split > 1) HIP_TRY(res->dense.reserve(dense_bytes), "hipMalloc dense rows");
   else res->dense.release();
   if (p.split > 1 && !p.part_lists) {
-    const void* before = res->arrive.p;
-    HIP_TRY(res->arrive.reserve((size_t)split_rows * 4), "hipMalloc arrival counters");
-    if (res->arrive.p != before) HIP_TRY(hipMemsetAsync(res->arrive.p, 0, res->arrive.cap, st), "hipMemset arrivals");
+    // (zeroed whenever reserve allocates: a grown buffer may come back at the
+    // same address, so the pointer alone does not tell)
+    bool fresh = false;
+    HIP_TRY(res->arrive.reserve((size_t)split_rows * 4, &fresh), "hipMalloc arrival counters");
+    if (fresh) HIP_TRY(hipMemsetAsync(res->arrive.p, 0, res->arrive.cap, st), "hipMemset arrivals");
   }
 
   rthx::TraceParams P{};
@@ -941,7 +951,9 @@ int run_trace(rthx_domain* dom, const rthx_trace_args* a, const TracePlan& p, rt
       HIP_TRY(hipMemsetAsync(T.lb_status, 0, res->lb_status.cap, st), "hipMemset look-back words");
       HIP_TRY(hipMemsetAsync(res->lb_totals.p, 0, 2 * 8 * 8, st), "hipMemset look-back totals");
       e = 0;
+      check_prev = false;  // (trace_exchange_one absorbed a replaced launch on the host: lb_chain_ok)
     }
+    T.check_prev = check_prev ? 1u : 0u;
     ++e;
     res->lb_epoch = 0;  // set again once the launch has completed
     T.lb_epoch = e;
@@ -989,6 +1001,13 @@ int run_trace(rthx_domain* dom, const rthx_trace_args* a, const TracePlan& p, rt
   return RTHX_OK;
 }
 
+// The look-back words and totals of `res` serve a launch of n_rows without
+// being zeroed first (run_trace's epoch test, reserve sizes).
+bool lb_chain_ok(const rthx_result* res, int64_t n_rows) {
+  return res->lb_status.p && (size_t)n_rows * 8 <= res->lb_status.cap && res->lb_totals.p && res->lb_epoch != 0 &&
+         res->lb_epoch < rthx::kLbEpochMax;
+}
+
 int finish_trace(rthx_domain* dom, const rthx_trace_args* a, const TracePlan& p, rthx_result* res, bool lookback,
                  const rthx::RecordParams& rec, int64_t totals[rthx::kLbTotals], float ms_trace, float ms_pack,
                  double t0);
@@ -997,7 +1016,11 @@ int finish_trace(rthx_domain* dom, const rthx_trace_args* a, const TracePlan& p,
 int trace_exchange_one(rthx_domain* dom, const rthx_trace_args* a, rthx_result* res) {
   const double t0 = now_ms();
   HIP_TRY(hipSetDevice(dom->device), "hipSetDevice");
-  res->pending = false;  // (an unread async trace is superseded: stream order keeps its launch before this one)
+  // An unread async trace on this result is replaced by this one (stream
+  // order keeps its launch before this one).  The result reads as empty
+  // until this trace is done, whatever happens below.
+  const bool superseding = res->pending;
+  res->valid = false;
   TracePlan p;
   int rc = plan_trace_split(dom, a, p);
   if (rc) return rc;
@@ -1060,6 +1083,20 @@ int trace_exchange_one(rthx_domain* dom, const rthx_trace_args* a, rthx_result* 
   // recorder's kernels stage.
   const bool lookback = !p.part_lists && n_rows > 0 && dom->single_convex && !p.recording &&
                         (uint64_t)n_rows * (uint64_t)p.row_cap <= rthx::kLbValMax && !env_flag("RTHX_NO_LOOKBACK");
+  // The replaced launch's stall / overflow flags: read by this launch's row 0
+  // when it uses the same look-back totals without zeroing them (run_trace),
+  // else on the host now, before its buffers are reused.
+  bool check_prev = false;
+  if (superseding) {
+    if (lookback && lb_chain_ok(res, n_rows)) {
+      res->pending = false;
+      res->sup_count += 1;
+      check_prev = true;
+    } else {
+      rc = rthx::absorb_superseded(res);
+      if (rc) return rc;
+    }
+  }
   int64_t totals[rthx::kLbTotals] = {0, 0, 0, 0, 0};
   float ms_trace = 0.f, ms_pack = 0.f;
   // RTHX_FLAG_ASYNC: enqueue only, when the direct CSR is sized from an
@@ -1070,9 +1107,10 @@ int trace_exchange_one(rthx_domain* dom, const rthx_trace_args* a, rthx_result* 
   if (async) {
     for (auto& e : res->pend_ev)
       if (!e) HIP_TRY(hipEventCreate(&e), "hipEventCreate");
-    rc = run_trace(dom, a, p, res, true, rec, totals, &ms_trace, &ms_pack, true);
+    rc = run_trace(dom, a, p, res, true, rec, totals, &ms_trace, &ms_pack, true, check_prev);
     if (rc) return rc;
     res->pending = true;
+    res->pend_plan = p;
     res->pend_dom = dom;
     res->pend_args = *a;
     res->pend_args.n_record = 0;
@@ -1081,7 +1119,7 @@ int trace_exchange_one(rthx_domain* dom, const rthx_trace_args* a, rthx_result* 
     res->valid = true;
     return RTHX_OK;
   }
-  rc = run_trace(dom, a, p, res, lookback, rec, totals, &ms_trace, &ms_pack);
+  rc = run_trace(dom, a, p, res, lookback, rec, totals, &ms_trace, &ms_pack, false, check_prev);
   if (rc) return rc;
   return finish_trace(dom, a, p, res, lookback, rec, totals, ms_trace, ms_pack, t0);
 }
@@ -1095,6 +1133,7 @@ int finish_trace(rthx_domain* dom, const rthx_trace_args* a, const TracePlan& p,
   int rc = RTHX_OK;
   const int64_t R = p.R, n_rows = p.n_rows;
   const size_t n_rec = res->rec_g.size();
+  const int64_t chained_faults = lookback ? totals[5] : 0;  // (replaced async launches, TallyParams::check_prev)
   if (lookback && totals[3] == 0 && totals[4] != 0) {
     // Rows outgrew the reserved direct CSR: the look-back's totals hold the
     // exact nnz, so the same launch -- same draws, same counts -- is traced
@@ -1133,6 +1172,7 @@ int finish_trace(rthx_domain* dom, const rthx_trace_args* a, const TracePlan& p,
   res->info.lost_max_row = totals[2];
   res->info.trace_ms = ms_trace;
   res->info.pack_ms = ms_pack;
+  rthx::take_superseded(res, chained_faults);
 
   if (!(a->flags & RTHX_FLAG_DEVICE_ONLY)) {
     res->h_row_off.resize(n_rows + 1);
@@ -1169,11 +1209,10 @@ int complete_pending(rthx_result* res) {
   std::memcpy(totals, res->h_totals.p, 8 * rthx::kLbTotals);
   float ms_trace = 0.f;
   HIP_TRY(hipEventElapsedTime(&ms_trace, res->pend_ev[0], res->pend_ev[1]), "hipEventElapsedTime");
-  TracePlan p;
-  int rc = plan_trace_split(dom, a, p);
-  if (rc) return rc;
   res->valid = false;
-  return finish_trace(dom, a, p, res, true, rthx::RecordParams{}, totals, ms_trace, 0.f, res->pend_t0);
+  // (the launched plan, not a new one: environment knobs or the occupancy
+  // query must not change what finish_trace checks or re-traces)
+  return finish_trace(dom, a, res->pend_plan, res, true, rthx::RecordParams{}, totals, ms_trace, 0.f, res->pend_t0);
 }
 
 // A result that can be read: traced, and a pending async trace completed.
@@ -1229,6 +1268,28 @@ int for_each_part(size_t n, F f) {
 
 namespace rthx {
 int result_ready(const rthx_result* res) { return ready(res); }
+
+int absorb_superseded(rthx_result* res) {
+  if (!res->pending) return RTHX_OK;
+  res->pending = false;
+  res->valid = false;
+  rthx_domain* dom = res->pend_dom;
+  HIP_TRY(hipSetDevice(dom->device), "hipSetDevice");
+  HIP_TRY(res->h_totals.reserve(8 * 8), "hipHostMalloc totals");
+  HIP_TRY(hipMemcpyAsync(res->h_totals.p, res->pend_totals, 8 * kLbTotals, hipMemcpyDeviceToHost, dom->stream),
+          "hipMemcpy totals");
+  HIP_TRY(hipStreamSynchronize(dom->stream), "replaced trace");
+  const int64_t* t = static_cast<const int64_t*>(res->h_totals.p);
+  res->sup_count += 1;
+  res->sup_faults += (int32_t)(((t[3] | t[4]) != 0 ? 1 : 0) + t[5]);
+  return RTHX_OK;
+}
+
+void take_superseded(rthx_result* res, int64_t chained_faults) {
+  res->info.superseded = res->sup_count;
+  res->info.superseded_faults = res->sup_faults + (int32_t)chained_faults;
+  res->sup_count = res->sup_faults = 0;
+}
 }  // namespace rthx
 
 RTHX_EXPORT int rthx_trace_exchange(rthx_domain* dom, const rthx_trace_args* a, rthx_result* res) {
@@ -1494,10 +1555,10 @@ RTHX_EXPORT int rthx_multi_trace_exchange(rthx_multi* m, const rthx_trace_args* 
   const size_t nd = m->doms.size();
   TracePlan p;
   int rc = plan_trace(m->doms[0], a, p);  // argument checks
-  if (res->pending) {  // (an unread async single-device trace: finished before the buffers go)
-    (void)hipSetDevice(res->device);
-    (void)hipDeviceSynchronize();
-    res->pending = false;
+  if (res->pending) {  // (an unread async single-device trace: counted and finished before its buffers go)
+    rthx::DeviceGuard keep_device;
+    const int rc2 = rthx::absorb_superseded(res);
+    if (rc2) return rc2;
   }
   if (rc) return rc;
   // a result that held a single-device trace gives up its device buffers
@@ -1564,7 +1625,12 @@ RTHX_EXPORT int rthx_multi_trace_exchange(rthx_multi* m, const rthx_trace_args* 
     I.trace_ms = std::max(I.trace_ms, J.trace_ms);
     I.pack_ms = std::max(I.pack_ms, J.pack_ms);
     I.lookback_fallbacks += J.lookback_fallbacks;
+    I.superseded += J.superseded;
+    I.superseded_faults += J.superseded_faults;
   }
+  I.superseded += res->sup_count;  // (a replaced single-device trace of this result)
+  I.superseded_faults += res->sup_faults;
+  res->sup_count = res->sup_faults = 0;
   res->valid = true;
   I.total_ms = now_ms() - t0;
   return RTHX_OK;

@@ -32,6 +32,14 @@ inline int hip_fail(hipError_t e, const char* what) {
   } while (0)
 
 // Device buffer with grow-only capacity.
+// Tuning and test knobs from the environment (RTHX_NO_AXIS, RTHX_FORCE_HASH,
+// RTHX_LB_WAIT_US, ...: the tests' and A/B tools' switches) are honoured only
+// when RTHX_DEV_KNOBS=1 was set when the library first looked (read once, at
+// the first knob): a user's environment cannot change the kernel path.
+// knob(name) is getenv(name) then, else nullptr.
+bool knobs_enabled();
+const char* knob(const char* name);
+
 struct DevBuf {
   void* p = nullptr;
   size_t cap = 0;
@@ -39,8 +47,12 @@ struct DevBuf {
   DevBuf(const DevBuf&) = delete;
   DevBuf& operator=(const DevBuf&) = delete;
   ~DevBuf() { release(); }
-  hipError_t reserve(size_t bytes) {
+  // fresh (optional): set when this call allocated (the contents are then
+  // undefined -- a grown buffer can come back at its old address)
+  hipError_t reserve(size_t bytes, bool* fresh = nullptr) {
+    if (fresh) *fresh = false;
     if (bytes <= cap && p) return hipSuccess;
+    if (fresh) *fresh = true;
     if (p) (void)hipFree(p);
     p = nullptr;
     cap = 0;
@@ -80,8 +92,12 @@ struct HostBuf {
   HostBuf(const HostBuf&) = delete;
   HostBuf& operator=(const HostBuf&) = delete;
   ~HostBuf() { release(); }
-  hipError_t reserve(size_t bytes) {
+  // fresh (optional): set when this call allocated (the contents are then
+  // undefined -- a grown buffer can come back at its old address)
+  hipError_t reserve(size_t bytes, bool* fresh = nullptr) {
+    if (fresh) *fresh = false;
     if (bytes <= cap && p) return hipSuccess;
+    if (fresh) *fresh = true;
     if (p) (void)hipHostFree(p);
     p = nullptr;
     cap = 0;

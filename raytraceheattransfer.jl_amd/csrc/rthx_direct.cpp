@@ -181,9 +181,9 @@ RTHX_EXPORT int rthx_trace_direct(rthx_domain* dom, const double* weights, const
   L.uniform = dom->uniform_beta[a->bin] > -0.1;  // traceRay.jl:4
   L.faithful = (a->flags & RTHX_FLAG_FAITHFUL_SAMPLING) != 0;
   L.single = dom->single_convex;
-  L.axis = dom->axis_rect && !(getenv("RTHX_NO_AXIS") && getenv("RTHX_NO_AXIS")[0] == '1');
+  L.axis = dom->axis_rect && !(rthx::knob("RTHX_NO_AXIS") && rthx::knob("RTHX_NO_AXIS")[0] == '1');
   // the lattice in LDS behind the counters (the exchange kernels' LAT locate)
-  L.lat = L.single && L.axis && dom->D.lat.bytes > 0 && !(getenv("RTHX_NO_LAT") && getenv("RTHX_NO_LAT")[0] == '1') &&
+  L.lat = L.single && L.axis && dom->D.lat.bytes > 0 && !(rthx::knob("RTHX_NO_LAT") && rthx::knob("RTHX_NO_LAT")[0] == '1') &&
           (3 * n * 4 > rthx::kHistBytes || 3 * n * 4 + 16 + dom->D.lat.bytes <= rthx::kHistBytes);
   L.lat_bytes = L.lat ? dom->D.lat.bytes : 0;
   rthx::DirectParams& Q = L.Q;

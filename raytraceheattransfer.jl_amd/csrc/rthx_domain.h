@@ -17,6 +17,16 @@
 #include "rthx_device.h"
 
 namespace rthx {
+// Launch geometry of one 2D trace call (rthx_api.cpp plan_trace: rows,
+// split, LDS histogram layout).
+struct TracePlan {
+  int64_t N = 0, R = 0, end = 0, n_rows = 0, split = 1, row_cap = 1, hash_cap = 0, bm_words = 0, part_cap = 0;
+  bool part_lists = false;  // split hash rows: sorted part lists + part_merge_kernel (else the last part merges)
+  int tally = 1;            // rthx_kernels.h Tally (kTallyU16)
+  int clds = 0;             // rthx_kernels.h LaunchCfg::clds
+  bool recording = false, uniform = true;
+  size_t lds_bytes = 0, cl_offset = 0;
+};
 struct DirectWork;                   // rthx_direct.cpp: device buffers of rthx_trace_direct
 void destroy_direct_work(DirectWork* w);
 }  // namespace rthx
@@ -80,6 +90,13 @@ struct rthx_result {
   unsigned long long* pend_totals = nullptr;  // device totals of the pending launch
   double pend_t0 = 0.0;
   hipEvent_t pend_ev[2] = {nullptr, nullptr};  // around the pending launch (this result's own events)
+  rthx::TracePlan pend_plan{};                 // the pending launch's plan (reused when it completes)
+  // Async traces replaced by a later trace before any read (rthx_result_info
+  // superseded / superseded_faults of the next trace): counted on the host,
+  // and the faults of a replaced look-back launch read back either by the
+  // replacing launch's row 0 (TallyParams::check_prev, totals[5]) or, when
+  // that launch cannot, by the host before it starts (absorb_superseded).
+  int32_t sup_count = 0, sup_faults = 0;
   ~rthx_result() {
     for (rthx_result* p : parts) delete p;
     if (device >= 0) (void)hipSetDevice(device);
@@ -108,4 +125,10 @@ int finish_staged(rthx_result* res, const TallyParams& T, int merge, hipStream_t
 // rthx_api.cpp: RTHX_OK when the result holds a trace that can be read (a
 // pending RTHX_FLAG_ASYNC trace is completed first), else the error code.
 int result_ready(const rthx_result* res);
+// rthx_api.cpp: a pending RTHX_FLAG_ASYNC trace that a new trace replaces:
+// waits for it, counts it (and whether it stalled or overflowed) in
+// res->sup_count / sup_faults, and marks the result empty.
+int absorb_superseded(rthx_result* res);
+// Moves sup_count / sup_faults into res->info (the trace that replaced them).
+void take_superseded(rthx_result* res, int64_t chained_faults);
 }  // namespace rthx

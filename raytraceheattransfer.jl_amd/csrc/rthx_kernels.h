@@ -69,18 +69,23 @@ struct TallyParams {
   uint32_t* out_cnt;
   int64_t out_cap;               // entries out_cols / out_cnt hold (rows past it flag totals[4])
   int64_t* row_off;              // [n_rows + 1]
-  unsigned long long* totals;    // nnz, lost rays, max lost per row, look-back stalls, CSR overflows (zeroed)
+  unsigned long long* totals;    // kLbTotals words (zeroed)
   unsigned long long* totals_next;  // look-back launches: the next launch's totals, zeroed by row 0
   int64_t R;
   uint64_t lb_wait_ticks;        // longest look-back wait (s_memrealtime ticks, 100 MHz) before giving up
   uint32_t lb_epoch;             // 1 .. kLbEpochMax: tag of this launch's look-back words
+  uint32_t check_prev;           // 1: the previous launch on these totals was never read back (a superseded
+                                 // RTHX_FLAG_ASYNC trace): row 0 folds its stall / overflow flags into totals[5]
 };
 
 // Look-back word: flag (1 aggregate, 2 inclusive prefix) in bits 62-63, the
 // launch epoch in bits 46-61, the value below.  A word of another epoch
 // (or a zeroed one: epochs start at 1) is not yet published.
 constexpr int kLbEpochShift = 46;
-constexpr int kLbTotals = 5;  // totals words of a look-back launch (TallyParams::totals)
+// Totals words of a look-back launch (TallyParams::totals): nnz, lost rays,
+// max lost per row, look-back stalls, CSR overflows, and [5] superseded
+// launches before this one that stalled or overflowed (check_prev).
+constexpr int kLbTotals = 6;
 constexpr uint32_t kLbEpochMax = 0xFFFF;
 constexpr unsigned long long kLbValMax = (1ull << kLbEpochShift) - 1;
 

@@ -43,6 +43,10 @@ namespace rthx {
 #define RTHX_ML_G D.ml
 // Buffer resource word 3 of a raw (stride 0) buffer on gfx9 and the cache
 // policy of an agent-scope access (sc1: write-through / coherent across XCDs).
+// Both encodings are gfx94x/gfx950 ones: no other target is built.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "rthx_kernels.hip targets gfx950 only (buffer resource word 3 and sc1 encodings)"
+#endif
 constexpr int kBufferRsrcWord3 = 0x00020000;
 constexpr int kSc1 = 16;
 #ifndef RTHX_REFILL_Q
@@ -761,8 +765,13 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
         T.row_off[T.n_rows] = (int64_t)(b + nnz);
         T.totals[0] = b + nnz;
       }
-      if (slot == 0)  // the next look-back launch's totals (rthx_api.cpp run_trace)
+      if (slot == 0) {  // the next look-back launch's totals (rthx_api.cpp run_trace) -- which still hold
+                        // the previous launch's: when nobody read them back (a superseded async trace), its
+                        // stall / overflow flags carry over into this launch's totals[5] first
+        if (T.check_prev)
+          T.totals[5] = T.totals_next[5] + ((T.totals_next[3] | T.totals_next[4]) != 0ull ? 1ull : 0ull);
         for (int i = 0; i < kLbTotals; ++i) T.totals_next[i] = 0ull;
+      }
     }
   };
   if constexpr (HASH) {

@@ -451,7 +451,7 @@ RTHX_EXPORT int rthx_scene3d_create_grouped(const double* xyz, const int32_t* nv
   s->S.nodes = s->nodes.as<rthx::Bvh2Node>();
   s->S.tables = s->tables.as<double>();
   if (!up(s->scene, &s->S, sizeof(s->S))) return bail(fail(RTHX_ENOMEM, "uploading the 3D scene"));
-  if (getenv("RTHX_VERBOSE"))
+  if (rthx::knob("RTHX_VERBOSE"))
     std::fprintf(stderr, "rthx_scene3d_create: host geometry + BVH %.2f ms, device setup + upload %.2f ms\n",
                  t_bvh - t_start, now_ms() - t_bvh);
   *out = s;
@@ -481,13 +481,17 @@ RTHX_EXPORT int rthx_trace_exchange_3d(rthx_scene3d* sc, const rthx_trace_args* 
   if (a->device != sc->device) return fail(RTHX_EINVAL, "args.device differs from the scene's device");
   HIP_TRY(hipSetDevice(sc->device), "hipSetDevice");
   if (res->device >= 0 && res->device != sc->device) return fail(RTHX_EINVAL, "result bound to another device");
+  {  // (an unread async 2D trace on this result: counted and finished before its buffers go)
+    const int rc0 = rthx::absorb_superseded(res);
+    if (rc0) return rc0;
+  }
   res->device = sc->device;
   const int64_t N = sc->n_poly, R = a->rays_per_emitter;
   const int64_t end = std::min<int64_t>(a->emitter_end, N);
   const int64_t n_rows = end > a->emitter_begin ? (end - a->emitter_begin + a->emitter_stride - 1) / a->emitter_stride : 0;
   int64_t split = 1;
   int64_t split_target = kSplitTargetBlocks;
-  if (const char* e = getenv("RTHX_T3_SPLIT_TARGET")) split_target = std::max<int64_t>(1, std::atoll(e));
+  if (const char* e = rthx::knob("RTHX_T3_SPLIT_TARGET")) split_target = std::max<int64_t>(1, std::atoll(e));
   if (n_rows > 0 && R >= 2 * kSplitMinRays)
     split = std::max<int64_t>(1, std::min<int64_t>((split_target + n_rows - 1) / n_rows, R / kSplitMinRays));
   const bool pack16 = (R + split - 1) / split < 65536;
@@ -500,7 +504,6 @@ RTHX_EXPORT int rthx_trace_exchange_3d(rthx_scene3d* sc, const rthx_trace_args* 
   res->parts.clear();
   res->interleaved = false;
   res->valid = false;
-  res->pending = false;  // (an unread async 2D trace: the device's one stream keeps it before this launch)
   res->host_row_off = false;
   res->host_rec = false;
   res->rec_g.clear();
@@ -563,7 +566,7 @@ RTHX_EXPORT int rthx_trace_exchange_3d(rthx_scene3d* sc, const rthx_trace_args* 
     L.top_choice = sc->top_choice;
     // The global-histogram form when its LDS (the stacks alone) keeps more
     // workgroups resident than the LDS histogram's (RTHX_T3_GHIST=0/1 forces).
-    const char* gh = getenv("RTHX_T3_GHIST");
+    const char* gh = rthx::knob("RTHX_T3_GHIST");
     if (gh && (gh[0] == '0' || gh[0] == '1')) {
       L.ghist = gh[0] == '1';
     } else {
@@ -599,6 +602,7 @@ RTHX_EXPORT int rthx_trace_exchange_3d(rthx_scene3d* sc, const rthx_trace_args* 
             "hipMemcpy row_off");
     res->host_row_off = true;
   }
+  rthx::take_superseded(res, 0);
   res->info.nnz = totals[0];
   res->info.lost_total = totals[1];
   res->info.lost_max_row = totals[2];

@@ -23,7 +23,7 @@ module RTHX
 
 using SparseArrays
 
-const RTHX_ABI_VERSION = Int32(2)
+const RTHX_ABI_VERSION = Int32(3)
 const RTHX_FLAG_FAITHFUL_SAMPLING = UInt32(0x1)
 
 const LIB = Ref{String}("")
@@ -99,6 +99,8 @@ struct ResultInfo
     total_ms::Float64
     n_devices::Int32
     lookback_fallbacks::Int32
+    superseded::Int32
+    superseded_faults::Int32
 end
 
 struct SmoothArgs

@@ -6,7 +6,7 @@ from __future__ import annotations
 
 import ctypes as C
 
-RTHX_ABI_VERSION = 2
+RTHX_ABI_VERSION = 3
 
 RTHX_OK = 0
 RTHX_EINVAL = -1
@@ -98,6 +98,8 @@ class ResultInfo(C.Structure):
         ("total_ms", C.c_double),
         ("n_devices", C.c_int32),
         ("lookback_fallbacks", C.c_int32),
+        ("superseded", C.c_int32),
+        ("superseded_faults", C.c_int32),
     ]
 
     def as_dict(self) -> dict:

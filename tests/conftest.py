@@ -5,6 +5,11 @@ import sys
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# The tests switch kernel paths through librthx's environment knobs
+# (RTHX_NO_AXIS, RTHX_FORCE_HASH, RTHX_LB_WAIT_US, ...), which the library
+# honours only with RTHX_DEV_KNOBS=1 set before it first reads one
+# (rthx_common.h knob).
+os.environ["RTHX_DEV_KNOBS"] = "1"
 for p in (os.path.join(ROOT, "raytraceheattransfer.jl_amd"), ROOT, os.path.join(ROOT, "tests")):
     if p not in sys.path:
         sys.path.insert(0, p)

@@ -45,7 +45,7 @@ def test_struct_sizes_match_header():
     # offsets fixed by the header's field order (x86-64 SysV)
     assert C.sizeof(abi.GridDesc) == 48
     assert C.sizeof(abi.TraceArgs) == 80
-    assert C.sizeof(abi.ResultInfo) == 96
+    assert C.sizeof(abi.ResultInfo) == 104
     assert C.sizeof(abi.SmoothArgs) == 32
     assert C.sizeof(abi.SmoothInfo) == 88
     assert C.sizeof(abi.SolveArgs) == 32

@@ -512,6 +512,8 @@ def test_async_traces_equal_blocking_traces(hip):
             for k in ("nnz", "lost_total", "lost_max_row", "rays_traced", "rows_traced"):
                 assert info[k] == w[3][k], k
             assert info["lookback_fallbacks"] == 0 and info["trace_ms"] > 0
+            # four async a5 and the a6 were replaced unread; none faulted
+            assert info["superseded"] == 5 and info["superseded_faults"] == 0
             # the device CSR of a pending trace
             res.trace(dd, a6)
             d = res.device_csr()
@@ -523,6 +525,57 @@ def test_async_traces_equal_blocking_traces(hip):
             frp, fc, fv = res.F()
             assert np.array_equal(fc, w[1]) and np.all(fv > 0)
             res.trace(dd, a6)  # left pending: closing must be safe
+        finally:
+            res.close()
+    finally:
+        dd.close()
+
+
+def test_superseded_async_faults_are_counted(hip, monkeypatch):
+    """async steps that a later step replaces unread are
+    checked too.  With a zero look-back wait bound (RTHX_LB_WAIT_US=0) a step
+    stalls as soon as a row has to wait; its stall flag is carried by the
+    next launch's row 0 into that launch's totals (TallyParams::check_prev)
+    and reported as superseded_faults, while the last step -- traced with the
+    default bound -- still equals the blocking trace.  A replaced step that
+    the next trace cannot chain (a staged launch, which frees the look-back
+    totals) is read back on the host first.  Each replaced step is counted
+    exactly once."""
+    A = hip.abi
+    dom = H.square_domain(31)
+    flat = dom.flat()
+    dd = hip.DeviceDomain(flat, 0)
+    try:
+        b, _kb = _args(hip, flat, 3000, seed=5)
+        ref = _trace(hip, dd, b)
+        a, _ka = _args(hip, flat, 3000, seed=5, flags=A.RTHX_FLAG_ASYNC | A.RTHX_FLAG_DEVICE_ONLY)
+        res = hip.DeviceResult()
+        try:
+            res.trace(dd, b)  # (sizes the shape: later async calls enqueue)
+            k = 8
+            faults = 0
+            for form in ("chained", "absorbed"):
+                monkeypatch.setenv("RTHX_LB_WAIT_US", "0")
+                for _ in range(k):
+                    res.trace(dd, a)
+                monkeypatch.delenv("RTHX_LB_WAIT_US")
+                if form == "chained":
+                    res.trace(dd, a)  # same shape: row 0 folds in the replaced step's flags
+                    info = res.info()
+                    rp, cols, cnt = res.csr()
+                    assert np.array_equal(rp, ref[0]) and np.array_equal(cols, ref[1]) and np.array_equal(cnt, ref[2])
+                else:
+                    other, _ko = _args(hip, flat, 2000, seed=5)
+                    monkeypatch.setenv("RTHX_NO_LOOKBACK", "1")
+                    res.trace(dd, other)  # the staging path: the replaced step is read back on the host first
+                    monkeypatch.delenv("RTHX_NO_LOOKBACK")
+                    info = res.info()
+                    res.trace(dd, b)
+                    assert res.info()["superseded"] == 0
+                assert info["superseded"] == k, (form, info["superseded"])
+                assert 0 <= info["superseded_faults"] <= k
+                faults += info["superseded_faults"]
+            assert faults >= 1, "a zero wait bound never stalled a replaced step"
         finally:
             res.close()
     finally:

@@ -473,3 +473,27 @@ def test_host_path_crosbie_schrenker_on_gpu(hip):
     assert np.allclose(np.asarray(F.sum(axis=1)).ravel(), 1.0)
     sf = H.centerline_source_function(dom, nd)
     assert np.linalg.norm(sf - ana) <= 0.02 * np.linalg.norm(ana)
+
+
+def test_split_arrival_counters_grow(hip):
+    """a result first traced split over a few rows, then split
+    over more rows than its arrival-counter buffer held (6 -> 272 rows, both
+    under the resident-slot target so both launches split): the grown
+    buffer is zeroed whenever it is allocated (DevBuf::reserve's fresh flag),
+    even when it comes back at the same address, so both traces equal fresh
+    results.  Then back to few rows and to the first shape."""
+    dom = H.square_domain(31)
+    flat = dom.flat()
+    dd = hip.DeviceDomain(flat, 0)
+    res = hip.DeviceResult()
+    try:
+        for R, stride in [(20_000, 200), (20_000, 4), (20_000, 3), (9_000, 200), (20_000, 4)]:
+            args, _k = _args(hip, flat, R, seed=45, begin=0, stride=stride)
+            res.trace(dd, args)
+            got = res.csr() + (res.info(),)
+            want = gpu_trace(hip, flat, args)
+            assert_same(got, want[:4])
+        assert got[3]["rows_traced"] == len(range(0, flat.n_emitters, 4)) and got[3]["rows_traced"] > 64
+    finally:
+        res.close()
+        dd.close()

@@ -1,6 +1,7 @@
 #!/bin/bash
 # C5 bands under environment variants (one process per variant):
 #   bash tools/gpu_c5_env.sh TAG "BINS" RAYS "ENV1" "ENV2" ...   ("-" = defaults)
+export RTHX_DEV_KNOBS=1  # (librthx honours RTHX_* knobs only with this set: rthx_common.h knob)
 set -o pipefail
 TAG=$1; BINS=$2; RAYS=$3; shift 3
 mkdir -p gpurun_out

@@ -2,6 +2,7 @@
 # A/B of librthx.so variants on the direct-method cases (RTHX_LIB per run),
 # then the SQ counters of the in-tree build on one case.
 #   bash tools/gpu_direct_ab.sh TAG CASES SQ_CASE lib1.so lib2.so ...
+export RTHX_DEV_KNOBS=1  # (librthx honours RTHX_* knobs only with this set: rthx_common.h knob)
 set -o pipefail
 TAG=$1; CASES=$2; SQC=$3; shift 3
 mkdir -p gpurun_out

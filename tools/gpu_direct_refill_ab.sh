@@ -1,3 +1,4 @@
+export RTHX_DEV_KNOBS=1  # (librthx honours RTHX_* knobs only with this set: rthx_common.h knob)
 set -o pipefail
 A=raytraceheattransfer.jl_amd/csrc
 for r in 1 2; do

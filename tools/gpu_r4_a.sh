@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round 4: split / workgroup-size A/B at the emulated W=8 strong shard and at
 # W=1, then config 4 at the surveyed size (cube 11x11 + icosphere L2 / L3).
+export RTHX_DEV_KNOBS=1  # (librthx honours RTHX_* knobs only with this set: rthx_common.h knob)
 set -o pipefail
 mkdir -p gpurun_out
 bash tools/gpu_split_env_ab.sh "8" "strong" "RTHX_SPLIT_BELOW=1 RTHX_TRACE_THREADS=256;RTHX_SPLIT_BELOW=1 RTHX_TRACE_THREADS=512;RTHX_SPLIT_BELOW=1 RTHX_TRACE_THREADS=1024;RTHX_SPLIT_TARGET=2652 RTHX_TRACE_THREADS=256;RTHX_SPLIT_TARGET=3978 RTHX_TRACE_THREADS=256;RTHX_SPLIT_TARGET=2652 RTHX_TRACE_THREADS=1024" > gpurun_out/ab_w8b.log 2>&1 || exit 1

@@ -2,6 +2,7 @@
 # Round 4: parity subset (with the async boundary test), wave-wide vs
 # one-lane look-back A/B on the C2 rank-0 shards (blocking steps), the bench
 # line pipelined and blocking, the CSR overflow cost.
+export RTHX_DEV_KNOBS=1  # (librthx honours RTHX_* knobs only with this set: rthx_common.h knob)
 set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_boundary.py tests/test_gpu_large_n.py tests/test_gpu_trace3d.py -m gpu -x -q \

@@ -3,6 +3,7 @@
 # per job) and weak (1e8 rays per GPU) C2 jobs at emulated W = 1..8, under
 # the split settings given as "BELOW:TARGET" pairs.
 #   bash tools/gpu_split_ab.sh TAG "2048:4096 4096:4096 4096:8192"
+export RTHX_DEV_KNOBS=1  # (librthx honours RTHX_* knobs only with this set: rthx_common.h knob)
 set -o pipefail
 TAG=${1:-split}
 SETS=${2:-"2048:4096"}

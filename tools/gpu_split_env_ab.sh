@@ -1,6 +1,7 @@
 #!/bin/bash
 # Rank-0 shard of the C2 job at emulated W under environment variants:
 #   bash tools/gpu_split_env_ab.sh "W..." "MODE..." "ENV1;ENV2;..." [extra bench.py flags]   (ENV: space-separated VAR=VAL, or "-")
+export RTHX_DEV_KNOBS=1  # (librthx honours RTHX_* knobs only with this set: rthx_common.h knob)
 set -o pipefail
 WS=${1:-"4 8"}
 MODES=${2:-"strong weak"}

@@ -1,6 +1,7 @@
 #!/bin/bash
 # 3D tracer: its GPU tests on the in-tree build, then config 4 (L3, L4) per library.
 #   bash tools/gpu_t3_ab.sh TAG lib1.so lib2.so ...
+export RTHX_DEV_KNOBS=1  # (librthx honours RTHX_* knobs only with this set: rthx_common.h knob)
 set -o pipefail
 TAG=$1; shift
 mkdir -p gpurun_out

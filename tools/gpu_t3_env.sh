@@ -2,6 +2,7 @@
 # 3D tracer: GPU tests, then config 4 (L3, L4) under each setting of one
 # environment knob (e.g. RTHX_T3_GHIST, RTHX_T3_SPLIT_TARGET; "auto" = unset).
 #   bash tools/gpu_t3_env.sh TAG VAR "auto 0 1"
+export RTHX_DEV_KNOBS=1  # (librthx honours RTHX_* knobs only with this set: rthx_common.h knob)
 set -o pipefail
 TAG=$1; VAR=$2; SETS=$3
 mkdir -p gpurun_out

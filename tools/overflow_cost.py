@@ -12,6 +12,8 @@ result objects with the default first guess and with a tiny one
 """
 import json
 import os
+
+os.environ.setdefault("RTHX_DEV_KNOBS", "1")  # (RTHX_CSR_CAP is a knob: rthx_common.h)
 import sys
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))

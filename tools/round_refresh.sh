@@ -3,6 +3,7 @@
 #   GPU test suite, bench line + rocprof stats + PMC traffic (gpu_profile.sh),
 #   per-config throughput table and the config-4 3D tracer.
 #   bash tools/round_refresh.sh [tag]
+export RTHX_DEV_KNOBS=1  # (librthx honours RTHX_* knobs only with this set: rthx_common.h knob)
 set -o pipefail
 TAG=${1:-r1}
 OUT=gpurun_out
