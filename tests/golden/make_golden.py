@@ -15,6 +15,10 @@ oracle_c1_seed1.npz — CPU-restatement absorber counts for README Ex.1
 (11x11, kappa=1, 1e6 rays, seed 1): a regression fixture that the HIP path
 must reproduce exactly.
 
+reference_known_answers.json (`python tests/golden/make_golden.py known`) --
+the diffusion limit, reflecting-wall energy and parallel-plate tests of the
+reference and its icosphere-enclosure readme example (main_known_answers).
+
 reference_3d.json (`python tests/golden/make_golden.py 3d`) — the 3D view
 factor known answers of test/test_3d_viewfactors.jl (Narayanaswamy 2015
 examples :31-75 and the EES unit-cube table :101-143, tolerance VF_TOLERANCE
@@ -134,8 +138,98 @@ def main_3d():
     print("wrote reference_3d.json:", len(cases), "Narayanaswamy cases,", len(rot), "rotations")
 
 
+def _num(txt, pattern):
+    return float(re.search(pattern, txt, re.S).group(1).replace("_", ""))
+
+
+def main_known_answers():
+    """reference_known_answers.json (`python tests/golden/make_golden.py known`):
+    the remaining known answers of the reference's own tests and readme, parsed
+    from the files (constants, tolerances, geometry); the tests restate the
+    reference's formulas around them.
+      * diffusion limit: test/test_2d_diffusion.jl:15-77;
+      * reflecting-wall energy conservation: test/test_2d_grey_reflecting.jl:42-69;
+      * parallel plates vs the textbook flux: test/test_2d_grey_reflecting.jl:85-137;
+      * the icosphere enclosure's equator limit: readme.md:532-704 (icosahedron
+        vertices and faces of icosphere_mesh, n_cap, Ndim, the level table)."""
+    ref = "/root/reference"
+    dif = open(os.path.join(ref, "test/test_2d_diffusion.jl")).read()
+    refl = open(os.path.join(ref, "test/test_2d_grey_reflecting.jl")).read()
+    readme = open(os.path.join(ref, "readme.md")).read()
+    out = {"source": "test/test_2d_diffusion.jl, test/test_2d_grey_reflecting.jl, readme.md:532-704"}
+    n_side = int(re.search(r'\("sparse", (\d+), true\)', dif).group(1))
+    out["diffusion"] = {
+        "source": "test/test_2d_diffusion.jl:15-77",
+        "T_hot": _num(dif, r"T_HOT_DIFF\s*=\s*([0-9.]+)"),
+        "beta": _num(dif, r"BETA_DIFF\s*=\s*([0-9.]+)"),
+        "aspect": _num(dif, r"ASPECT_DIFF\s*=\s*([0-9.]+)"),
+        "N_side": n_side,
+        "rays_per_element": int(_num(dif, r"N_rays = \(4 \* N_side \+ N_side\^2\) \* ([0-9_]+)")),
+        "rms_tol": _num(dif, r"RMS_TOL\s*=\s*([0-9.]+)"),
+        "ratio_tol": _num(dif, r"RATIO_TOL\s*=\s*([0-9.]+)"),
+        "energy_tol": _num(dif, r"abs\(sum\(mesh.energy_error\)\) < ([0-9.eE+-]+)"),
+        "expect_sparse": True,
+        "formula": "diffusion_S(z) = E_b1 - (3 beta z / 4) q_z, q_z = (E_bw1 - E_bw2) / (3 beta D / 4 + 1/eps1 "
+                   "+ 1/eps2 - 1), E_b1 = E_bw1 + q_z (1/2 - 1/eps1); D = eps = E_bw1 = 1, E_bw2 = 0 (:19-23,:46)",
+    }
+    t1 = refl.split("TEST 2")[0]
+    t2 = refl.split("TEST 2")[1]
+    out["reflecting_energy"] = {
+        "source": "test/test_2d_grey_reflecting.jl:42-69",
+        "T_hot": _num(t1, r"T_hot\s*=\s*([0-9.]+)"),
+        "Ndim": int(_num(t1, r"Ndim\s*=\s*([0-9]+)")),
+        "rays": int(_num(t1, r"N_rays_total = ([0-9_]+)")),
+        "kappa": 1.0,
+        "T_in_w": [1000.0, -1.0, -1.0, -1.0],
+        "epsilon": [float(x) for x in re.search(r"face.epsilon = \[([^\]]+)\]", t1).group(1).split(",")],
+        "energy_tol": _num(refl, r"ENERGY_TOLERANCE = ([0-9.eE+-]+)"),
+    }
+    out["parallel_plates"] = {
+        "source": "test/test_2d_grey_reflecting.jl:85-137",
+        "eps": _num(t2, r"eps_plates = ([0-9.]+)"),
+        "T_hot": _num(t2, r"T_hot\s*=\s*([0-9.]+)"),
+        "T_cold": _num(t2, r"T_cold\s*=\s*([0-9.]+)"),
+        "W": _num(t2, r"W = ([0-9.]+)"),
+        "H": _num(t2, r"H = ([0-9.]+)"),
+        "Nx": int(_num(t2, r"Nx = ([0-9]+)")),
+        "Ny": int(_num(t2, r"Ny = ([0-9]+)")),
+        "rays": int(_num(t2, r"N_rays_total = ([0-9_]+)")),
+        "kappa": _num(t2, r"PolyVolume2D\{Float64\}\(vertices, solidWalls, 1, ([0-9.eE+-]+), 0.0\)"),
+        "k_dykstra": int(_num(t2, r"k_dykstra=([0-9]+)")),
+        "rel_tol": _num(refl, r"ANALYTICAL_TOLERANCE = ([0-9.]+)"),
+        "energy_tol": _num(refl, r"ENERGY_TOLERANCE = ([0-9.eE+-]+)"),
+        "formula": "q = sigma (T_hot^4 - T_cold^4) / (1/eps + 1/eps - 1), mean over the central Nx div 5 "
+                   "bottom-wall elements (:118-136)",
+    }
+    ico = readme[readme.index("function icosphere_mesh"):]
+    raw = re.search(r"ico_points_raw = \[(.*?)\]", ico, re.S).group(1)
+    vals = [x for x in re.split(r"[\s;]+", raw.strip()) if x]
+    phi = (1 + math.sqrt(5)) / 2
+    nums = [phi if v == "φ" else -phi if v == "-φ" else float(v) for v in vals]
+    faces = re.search(r"faces = \[(.*?)\]", ico, re.S).group(1)
+    fnums = [int(x) for x in re.split(r"[\s;]+", faces.strip()) if x]
+    table = re.findall(r"\|\s*(\d)\s*\|\s*(\d+)\s*\|\s*([0-9.eE+-]+)\s*\|", readme[readme.index("T_equator"):])
+    out["icosphere"] = {
+        "source": "readme.md:532-704",
+        "ico_points_raw": [nums[i:i + 3] for i in range(0, len(nums), 3)],
+        "faces": [fnums[i:i + 3] for i in range(0, len(fnums), 3)],
+        "n_cap": int(_num(ico, r"n_cap\s*=\s*([0-9]+)")),
+        "Ndim": 1,
+        "T_hot": _num(ico, r"T_hot\s*=\s*([0-9.]+)"),
+        "T_cold": _num(ico, r"T_cold\s*=\s*([0-9.]+)"),
+        "T_limit": ((1000.0 ** 4 + 0.0 ** 4) / 2) ** 0.25,
+        "analytic_error_K": {lvl: float(err) for lvl, _ntri, err in table},
+    }
+    assert len(out["icosphere"]["ico_points_raw"]) == 12 and len(out["icosphere"]["faces"]) == 20
+    with open(os.path.join(HERE, "reference_known_answers.json"), "w") as fh:
+        json.dump(out, fh, indent=1)
+    print("wrote reference_known_answers.json")
+
+
 if __name__ == "__main__":
     if sys.argv[1:] == ["3d"]:
         main_3d()
+    elif sys.argv[1:] == ["known"]:
+        main_known_answers()
     else:
         main()

@@ -354,3 +354,156 @@ def cube_icosphere_groups(ndim=10, level=3):
     n_sph = 20 * 4 ** level
     return np.concatenate([np.arange(n_cube) // (ndim * ndim), 6 + np.arange(n_sph)]).astype(np.int32)
 
+
+
+# --------------------------------------------------------------------------
+# the reference's remaining known answers (tests/golden/reference_known_answers.json)
+# --------------------------------------------------------------------------
+def known_answers():
+    return golden("reference_known_answers.json")
+
+
+def rect_domain(W, H, nx, ny, kappa, T_in_w, epsilon, q_in_w=(0.0, 0.0, 0.0, 0.0), sigma_s=0.0):
+    """One W x H rectangle meshed nx x ny, all walls solid (walls: 1 bottom,
+    2 right, 3 top, 4 left), as the reference's diffusion and reflecting-wall
+    tests build it (test/test_2d_diffusion.jl:29-40,
+    test/test_2d_grey_reflecting.jl:51-68,:102-113)."""
+    face = PolyVolume2D([(0.0, 0.0), (W, 0.0), (W, H), (0.0, H)], [True] * 4, 1, kappa, sigma_s)
+    face.T_in_w = [float(t) for t in T_in_w]
+    face.q_in_w = [float(q) for q in q_in_w]
+    face.epsilon = [float(e) for e in epsilon]
+    face.T_in_g = -1.0
+    face.q_in_g = 0.0
+    return RayTracingDomain2D([face], [(nx, ny)])
+
+
+def diffusion_domain():
+    d = known_answers()["diffusion"]
+    n = d["N_side"]
+    return rect_domain(d["aspect"], 1.0, n, n, d["beta"], [d["T_hot"], 0.0, 0.0, 0.0], [1.0] * 4)
+
+
+def diffusion_S(z, beta, D, eps1, eps2, E1, E2):
+    """diffusion_S (test/test_2d_diffusion.jl:19-23)."""
+    q = (E1 - E2) / (3 * beta * D / 4 + 1 / eps1 + 1 / eps2 - 1)
+    Eb1 = E1 + q * (0.5 - 1 / eps1)
+    return Eb1 - (3 * beta * z / 4) * q
+
+
+def diffusion_centerline_rms(dom, T_gas):
+    """centerline_rms_S (test/test_2d_diffusion.jl:43-49): the column of cells
+    at x index (N-1) div 2 + 1 (fine faces x fastest), S = (T/T_hot)^4
+    against diffusion_S at the cell-centre taus."""
+    d = known_answers()["diffusion"]
+    n = d["N_side"]
+    grid = np.asarray(T_gas).reshape(n, n)  # [y][x]
+    Tc = grid[:, (n - 1) // 2]
+    S = (Tc / d["T_hot"]) ** 4
+    taus = np.linspace(1 / (2 * n), 1 - 1 / (2 * n), n)
+    Sref = diffusion_S(taus, d["beta"], 1.0, 1.0, 1.0, 1.0, 0.0)
+    return float(np.sqrt(np.mean((S - Sref) ** 2)))
+
+
+def reflecting_domain():
+    d = known_answers()["reflecting_energy"]
+    return rect_domain(1.0, 1.0, d["Ndim"], d["Ndim"], d["kappa"], d["T_in_w"], d["epsilon"])
+
+
+def plates_domain():
+    d = known_answers()["parallel_plates"]
+    return rect_domain(d["W"], d["H"], d["Nx"], d["Ny"], d["kappa"], [d["T_hot"], d["T_cold"], d["T_cold"], d["T_cold"]],
+                       [d["eps"], 1.0, d["eps"], 1.0])
+
+
+def plates_flux(dom, q_surf):
+    """(mean q_w / area over the central bottom-wall elements, textbook q)
+    (test/test_2d_grey_reflecting.jl:115-136): fine faces 1..Nx are the
+    bottom row, wall 1 their hot wall."""
+    d = known_answers()["parallel_plates"]
+    nx = d["Nx"]
+    q_text = STEFAN_BOLTZMANN * (d["T_hot"] ** 4 - d["T_cold"] ** 4) / (2 / d["eps"] - 1)
+    n_central = max(1, nx // 5)
+    lo = (nx - n_central) // 2 + 1
+    vals = []
+    for col in range(lo, lo + n_central):
+        s = dom.surface_mapping[(1, col, 1)] - 1
+        face = dom.fine_mesh[0][col - 1]
+        vals.append(q_surf[s] / face.area[0])
+    return float(np.mean(vals)), q_text
+
+
+def solve_grey_full(dom, F):
+    """solve_grey plus the per-element powers writeResultsToDomainGrey! stores
+    (equilibriumGrey2D.jl:176-211): returns (T, q, energy_error) in global
+    element order, q = e - Abs (net emitted power)."""
+    a = element_arrays(dom)
+    ns, nv = dom.num_surfaces, dom.num_volumes
+    n = ns + nv
+    F = sp.csr_matrix(F)[:n, :n]
+    q_known = np.concatenate([(a["Tw"] < 0).astype(int), (a["Tg"] < 0).astype(int)])
+    E = np.zeros(n); Q = np.zeros(n)
+    E[:ns] = np.where(q_known[:ns] == 0, a["eps"] * STEFAN_BOLTZMANN * a["area"] * np.maximum(a["Tw"], 0) ** 4, 0)
+    Q[:ns] = np.where(q_known[:ns] == 1, a["qw"], 0)
+    E[ns:] = np.where(q_known[ns:] == 0, 4 * a["kappa"] * STEFAN_BOLTZMANN * a["vol"] * np.maximum(a["Tg"], 0) ** 4, 0)
+    Q[ns:] = np.where(q_known[ns:] == 1, a["qg"], 0)
+    b = np.zeros(n)
+    if np.any(a["omega"] > 1e-6) or np.sum(a["eps"]) < n:
+        b[:ns] = 1.0 - a["eps"]
+        b[ns:] = a["omega"]
+    h = np.where(q_known == 1, Q, E)
+    coeff = np.where(q_known == 1, 1.0, b)
+    M = sp.identity(n, format="csr") - sp.diags(coeff) @ F.T.tocsr()
+    j = spla.spsolve(M.tocsc(), h)
+    g = F.T @ j
+    r = b * g
+    Abs = (1.0 - b) * g
+    e = np.maximum(j - r, 0.0)
+    T = np.zeros(n)
+    T[:ns] = np.where(a["eps"] > 0, (e[:ns] / (np.maximum(a["eps"], 1e-300) * STEFAN_BOLTZMANN * a["area"])) ** 0.25, 0)
+    kv = a["kappa"] * a["vol"]
+    T[ns:] = np.where(kv > 0, (e[ns:] / (4 * np.maximum(kv, 1e-300) * STEFAN_BOLTZMANN)) ** 0.25, 0)
+    return T, e - Abs, float(np.sum(j - r - Abs))
+
+
+def icosphere_mesh(level):
+    """icosphere_mesh (readme.md:532-589): the readme's icosahedron (vertices
+    normalised, its 20 faces in its order) subdivided `level` times, midpoints
+    shared through a cache keyed on the sorted vertex pair and appended in
+    first-use order; each face -> (a, ab, ca), (ab, b, bc), (ca, bc, c),
+    (ab, bc, ca).  Returns (points[n][3], faces[m][3] 1-based)."""
+    ico = known_answers()["icosphere"]
+    pts = [np.asarray(p, dtype=float) / np.linalg.norm(p) for p in ico["ico_points_raw"]]
+    faces = [tuple(f) for f in ico["faces"]]
+    for _ in range(level):
+        cache = {}
+        new = list(pts)
+
+        def mid(i, j):
+            key = (min(i, j), max(i, j))
+            if key in cache:
+                return cache[key]
+            m = (pts[i - 1] + pts[j - 1]) / 2
+            new.append(m / np.linalg.norm(m))
+            cache[key] = len(new)
+            return len(new)
+
+        nf = []
+        for a, b, c in faces:
+            ab, bc, ca = mid(a, b), mid(b, c), mid(c, a)
+            nf += [(a, ab, ca), (ab, b, bc), (ca, bc, c), (ab, bc, ca)]
+        pts, faces = new, nf
+    return np.array(pts), np.array(faces, dtype=np.int64)
+
+
+def icosphere_caps(points, faces, n_cap):
+    """The readme's hot / cold caps and equator (readme.md:663-697): the n_cap
+    triangles with the highest / lowest centroid z (partialsortperm: stable,
+    ties by index), and the equilibrium triangle with the smallest |z|
+    (argmin: first)."""
+    zc = np.array([points[f - 1].mean(axis=0)[2] for f in faces])
+    order = np.argsort(-zc, kind="stable")
+    hot = order[:n_cap]
+    cold = np.argsort(zc, kind="stable")[:n_cap]
+    eq_ids = np.setdiff1d(np.arange(len(faces)), np.concatenate([hot, cold]))
+    equator = int(eq_ids[np.argmin(np.abs(zc[eq_ids]))])
+    return hot, cold, equator

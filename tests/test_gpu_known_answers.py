@@ -1,0 +1,214 @@
+"""The reference's remaining known answers through the product path on the
+MI355X: mesh() traced and smoothed on the device (rthx_trace_exchange,
+rthx_smooth_F_result), then the device GERT solve (rthx_solve_grey*), and the
+3D icosphere enclosure of the reference's readme, analytic and Monte Carlo.
+
+Sources (tests/golden/reference_known_answers.json, parsed from the reference
+by tests/golden/make_golden.py):
+  * diffusion limit, test/test_2d_diffusion.jl:15-77 (1000:1 cells, beta 25);
+  * reflecting-wall energy conservation, test/test_2d_grey_reflecting.jl:42-69;
+  * parallel plates vs the textbook flux, test/test_2d_grey_reflecting.jl:85-137
+    (a 100:1 nearly transparent gap, eps 0.5 walls, 500 Dykstra rounds);
+  * the icosphere enclosure's equator limit ((T_hot^4 + T_cold^4)/2)^(1/4),
+    readme.md:532-704 (hot / cold caps of 6 triangles, Ndim = 1).
+Tolerances are the reference's own unless the docstring says otherwise.  The
+same geometries' counts equal the CPU restatement exactly at reduced R.
+"""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+import helpers as H
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _gas_T(dom):
+    return np.array([f.T_g for f in dom.fine_mesh[0]])
+
+
+@pytest.mark.parametrize("case", ["diffusion", "reflecting", "plates"])
+def test_known_answer_geometries_exact_counts(hip, case):
+    """Each geometry's counts from the device equal the CPU restatement's
+    exactly (reduced R; the same seeded draws): the diffusion slab's 1000:1
+    cells (lattice locate), the plates' 100:1 gap, reflecting walls (the
+    tracer ignores epsilon: exchange factors are geometric)."""
+    dom = {"diffusion": H.diffusion_domain, "reflecting": H.reflecting_domain, "plates": H.plates_domain}[case]()
+    flat = dom.flat()
+    R = {"diffusion": 300, "reflecting": 2000, "plates": 20_000}[case]
+    args, _k = hip.make_args(0, R, H.NUDGE, 17, 0, flat.n_emitters, 1)
+    dd = hip.DeviceDomain(flat, 0)
+    res = hip.DeviceResult()
+    try:
+        res.trace(dd, args)
+        info = res.info()
+        rp, cols, cnt = res.csr()
+    finally:
+        res.close()
+        dd.close()
+    orp, ocols, ocnt, oinfo, _ = oracle.trace_exchange(flat, args, 16)
+    assert np.array_equal(rp, orp) and np.array_equal(cols, ocols) and np.array_equal(cnt, ocnt)
+    assert info["lost_total"] == oinfo["lost_total"]
+
+
+def test_diffusion_limit(hip):
+    """test/test_2d_diffusion.jl:15-77 through trace -> smooth -> solve on
+    the device: F_smooth comes out sparse with no negative entry, the
+    smoothed solve's centreline S(tau) is within RMS 0.02 of the diffusion
+    solution and below half the raw solve's error, |energy error| < 1e-6."""
+    from rthx.equilibrium import solve_equilibrium
+
+    d = H.known_answers()["diffusion"]
+    n = d["N_side"]
+    dom = H.diffusion_domain()
+    dom((4 * n + n * n) * d["rays_per_element"], seed=3, verbose=False)
+    Fs = dom.F_smooth
+    assert sp.issparse(Fs) == d["expect_sparse"]
+    assert (Fs.data < 0).sum() == 0
+    solve_equilibrium(dom, dom.F_raw)
+    e_raw = H.diffusion_centerline_rms(dom, _gas_T(dom))
+    solve_equilibrium(dom)
+    e_ap = H.diffusion_centerline_rms(dom, _gas_T(dom))
+    assert e_ap < d["rms_tol"], e_ap
+    assert e_ap < d["ratio_tol"] * e_raw, (e_ap, e_raw)
+    assert abs(dom.energy_error) < d["energy_tol"]
+
+
+def test_reflecting_walls_conserve_energy(hip):
+    """test/test_2d_grey_reflecting.jl:42-69: |energy error| < 1e-4 W with
+    F_smooth, reflecting (eps 0.5) radiative-equilibrium walls."""
+    from rthx.equilibrium import solve_equilibrium
+
+    d = H.known_answers()["reflecting_energy"]
+    dom = H.reflecting_domain()
+    dom(d["rays"], seed=4, verbose=False)
+    T, _, _, _ = solve_equilibrium(dom)
+    assert abs(dom.energy_error) < d["energy_tol"]
+    assert np.all(np.isfinite(T)) and 0.0 < T.max() <= d["T_hot"] + 1e-6
+
+
+def test_parallel_plates_textbook_flux(hip):
+    """test/test_2d_grey_reflecting.jl:85-137: mesh(1e7; k_dykstra = 500),
+    solve with F_smooth; the central hot elements' q_w / area within 5 % of
+    sigma (T1^4 - T2^4) / (2/eps - 1), |energy error| < 1e-4 W."""
+    from rthx.equilibrium import solve_equilibrium
+
+    d = H.known_answers()["parallel_plates"]
+    dom = H.plates_domain()
+    dom(d["rays"], k_dykstra=d["k_dykstra"], seed=5, verbose=False)
+    assert dom.last_smooth_info["k_dykstra"] == d["k_dykstra"]
+    solve_equilibrium(dom)
+    q = np.zeros(dom.num_surfaces)
+    for (c, f, w), s in dom.surface_mapping.items():
+        q[s - 1] = dom.fine_mesh[c - 1][f - 1].q_w[w - 1]
+    q_mean, q_text = H.plates_flux(dom, q)
+    assert abs(q_mean - q_text) / q_text < d["rel_tol"], (q_mean, q_text)
+    assert abs(dom.energy_error) < d["energy_tol"]
+
+
+# --- the icosphere enclosure (readme.md:532-704) ---------------------------
+def _icosphere_domain(level):
+    from rthx import ViewFactorDomain3D
+
+    ico = H.known_answers()["icosphere"]
+    pts, faces = H.icosphere_mesh(level)
+    n_tri = len(faces)
+    hot, cold, eq = H.icosphere_caps(pts, faces, min(ico["n_cap"], n_tri // 4))
+    T_in = np.full(n_tri, -1.0)
+    T_in[hot] = ico["T_hot"]
+    T_in[cold] = ico["T_cold"]
+    dom = ViewFactorDomain3D(pts, faces, ico["Ndim"], np.zeros(n_tri), T_in, np.ones(n_tri))
+    return dom, eq
+
+
+@pytest.mark.parametrize("level", [0, 1, 2, 3])
+def test_icosphere_equator_limit_analytic(hip, level):
+    """readme.md:649-704 on the analytic path (rthx_view_factors_3d ->
+    smoothing -> solve on the device): |T_equator - T_limit| matches the
+    readme's table -- 6.8e-2 K at level 0 (caps over half the sphere), and
+    at machine-precision level from level 1 (the readme's 1e-13 .. 6e-11 K;
+    bound here 1e-8 K: GMRES to rtol 1e-12 instead of a dense LU)."""
+    from rthx.equilibrium import solve_equilibrium
+
+    ico = H.known_answers()["icosphere"]
+    dom, eq = _icosphere_domain(level)
+    dom()
+    solve_equilibrium(dom)
+    err = abs(dom.facesMesh[eq].subFaces[0].T_w - ico["T_limit"])
+    if level == 0:
+        assert abs(err - ico["analytic_error_K"]["0"]) < 5e-3, err
+    else:
+        assert err < 1e-8, err
+
+
+def _binomial_z(counts, R, F):
+    """Two-sided exact binomial tail of each count against F, as the
+    equivalent Gaussian |z| (norm.isf(p / 2)): Monte Carlo counts of small
+    F are skewed, so a plain (c - RF) / sigma overstates their tails."""
+    from scipy import stats
+
+    c = np.asarray(counts, dtype=np.float64)
+    p = np.clip(np.asarray(F, dtype=np.float64), 1e-300, 1.0)
+    lo = stats.binom.cdf(c, R, p)
+    hi = stats.binom.sf(c - 1, R, p)
+    tail = np.minimum(1.0, 2.0 * np.minimum(lo, hi))
+    return stats.norm.isf(np.maximum(tail, 1e-300) / 2.0)
+
+
+@pytest.mark.parametrize("level", [2, 3])
+def test_icosphere_enclosure_montecarlo(hip, level):
+    """BASELINE config 4's second enclosure on the 3D Monte Carlo tracer:
+    the inside of the readme's icosphere (concave: every triangle sees every
+    other), rays leaving along the inward normals, 1e8 rays in total.
+      * Sampled rows (four, spread over the sphere) equal the brute-force
+        CPU restatement exactly at full R.
+      * Every F_ij agrees with the analytic view factor (rthx_view_factors_3d,
+        pinned by F_EES / Narayanaswamy): the exact binomial tail of each
+        count, as an equivalent Gaussian |z|, stays below the family-wise
+        bound for all n^2 entries at alpha = 1e-3 (Bonferroni: 5.8 at level 2,
+        6.3 at level 3), and the share beyond 5 sigma is near its expectation
+        (5.7e-7 per entry; at most 10 entries at level 3's 1.6e6).
+      * After smoothing and the device solve, the equator triangle is within
+        2 K of 840.896 K with the readme's hot / cold caps.
+    """
+    from scipy import stats
+
+    from rthx.domain3d import view_factors_3d
+    from rthx.equilibrium import solve_equilibrium
+    from rthx.trace3d import Scene3D
+
+    ico = H.known_answers()["icosphere"]
+    dom, eq = _icosphere_domain(level)
+    xyz, nv = dom.polygon_arrays()
+    normals = np.array([s.inwardNormal for s in dom.subfaces()])
+    n = len(nv)
+    R = 100_000_000 // n
+    s = Scene3D(xyz, nv, normals)
+    try:
+        rp, cols, cnt, info = s.trace(R, seed=31)
+    finally:
+        s.close()
+    assert info["rays_traced"] == n * R and info["lost_total"] == 0
+    D = np.zeros((n, n), dtype=np.int64)
+    for i in range(n):
+        D[i, cols[rp[i]:rp[i + 1]]] = cnt[rp[i]:rp[i + 1]]
+    assert np.all(np.diag(D) == 0) and np.all(D.sum(axis=1) == R)
+    stride = n // 4
+    C, lost = oracle.trace_exchange_3d(xyz, nv, normals, R, seed=31, begin=1, end=1 + 4 * stride, stride=stride,
+                                       nthreads=16)
+    assert lost == 0
+    for k in range(4):
+        assert np.array_equal(D[1 + k * stride], C[k]), 1 + k * stride
+    Fa, _, _ = view_factors_3d(xyz, nv)
+    off = ~np.eye(n, dtype=bool)
+    z = _binomial_z(D[off], R, Fa[off])
+    bound = stats.norm.isf(1e-3 / (2 * off.sum()))
+    assert z.max() < bound, (z.max(), bound)
+    assert np.count_nonzero(z > 5.0) <= max(10, 20 * 5.7e-7 * off.sum())
+    dom(method="montecarlo", rays_tot=n * R, seed=31)
+    assert dom.last_vf_info["rays_per_emitter"] == R
+    solve_equilibrium(dom)
+    T_eq = dom.facesMesh[eq].subFaces[0].T_w
+    assert abs(T_eq - ico["T_limit"]) < 2.0, T_eq
+    assert abs(dom.energy_error) < H.golden("reference_3d.json")["energy_tolerance_W"] * 100

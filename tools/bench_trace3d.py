@@ -4,6 +4,8 @@ restatement on a bounded row sample (diagnostic; bench.py's headline is the
 2D tracer).
 
   python tools/bench_trace3d.py [--rays 1e8] [--ndim 10] [--level 3] [--steps 5]
+  python tools/bench_trace3d.py --interior --level 3   # config 4's other enclosure:
+      the inside of the readme's icosphere (readme.md:532-704), no cube
 """
 import argparse
 import os
@@ -31,8 +33,20 @@ def main():
     ap.add_argument("--cpu-rows", type=int, default=8)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-groups", action="store_true", help="every polygon its own group (no coplanar faces)")
+    ap.add_argument("--interior", action="store_true", help="the inside of the readme's unit icosphere alone")
     args = ap.parse_args()
-    xyz, nv, nrm, nc = H.cube_icosphere_scene(args.ndim, args.level, args.radius)
+    if args.interior:  # rays leave the triangles toward the centre; every triangle sees every other
+        pts, faces = H.icosphere_mesh(args.level)
+        xyz = np.zeros((len(faces), 4, 3))
+        for i, f in enumerate(faces):
+            xyz[i, :3] = pts[f - 1]
+            xyz[i, 3] = pts[f[2] - 1]
+        nv = np.full(len(faces), 3, dtype=np.int32)
+        nrm = -xyz[:, :3].mean(axis=1)
+        nc = 0
+        args.no_groups = True
+    else:
+        xyz, nv, nrm, nc = H.cube_icosphere_scene(args.ndim, args.level, args.radius)
     n = len(nv)
     R = int(args.rays) // n
     from rthx import _lib
@@ -57,7 +71,9 @@ def main():
     k = float(np.median(ks))
     c = float(np.median(cs)) * 1e3
     rays = n * R
-    line = (f"config4 cube {args.ndim}x{args.ndim}/face + icosphere L{args.level} (n={n}, {n - nc} triangles, "
+    what = (f"config4 icosphere interior L{args.level}" if args.interior else
+            f"config4 cube {args.ndim}x{args.ndim}/face + icosphere L{args.level}")
+    line = (f"{what} (n={n}, {n - nc} triangles, "
             f"{int(np.sum(np.where(nv == 4, 2, 1)))} MT triangles, {'polygon' if args.no_groups else 'face'} groups)  R={R} rays={rays:.3e}  scene build {t_build * 1e3:.0f} ms (groups {t_groups * 1e3:.0f} ms)  "
             f"BVH {stats}  kernel {k:.2f} ms ({rays / k / 1e6:.2f} Grays/s)  call {c:.2f} ms  lost {info['lost_total']}  nnz {info['nnz']}")
     if args.cpu_rows > 0:
