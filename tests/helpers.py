@@ -507,3 +507,73 @@ def icosphere_caps(points, faces, n_cap):
     eq_ids = np.setdiff1d(np.arange(len(faces)), np.concatenate([hot, cold]))
     equator = int(eq_ids[np.argmin(np.abs(zc[eq_ids]))])
     return hot, cold, equator
+
+
+def vf3d_clamp_affected(xyz, nv):
+    """Pairs whose analytic view factor (viewFactor3D.jl:133-190, restated by
+    oracle_view_factors_3d and rthx_view_factors_3d) passes through the
+    reference's cos(alpha) clamp: some edge pair counts as skew
+    (edgePairParameters3D.jl: 1 - cos^2 > 10 eps) with |cos alpha| > 0.999,
+    which viewFactor3D.jl:157 clamps to 0.999 -- alpha 2.56 deg instead of
+    the true, smaller angle.  Nearly parallel edges of nearby triangles of a
+    refined sphere fall there, and their terms come out far off (icosphere
+    level 3: a row of F sums to 10).  Returns an n x n bool mask."""
+    n = len(nv)
+    E = np.zeros((n, 4, 3))
+    valid = np.zeros((n, 4), dtype=bool)
+    for k in range(n):
+        m = int(nv[k])
+        P = xyz[k, :m]
+        e = np.roll(P, -1, axis=0) - P
+        E[k, :m] = e / np.linalg.norm(e, axis=1)[:, None]
+        valid[k, :m] = True
+    c = np.einsum("aik,bjk->abij", E, E)
+    skew = (1.0 - c * c) > 10 * np.finfo(np.float64).eps
+    hit = skew & (np.abs(c) > 0.999) & valid[:, None, :, None] & valid[None, :, None, :]
+    aff = np.any(hit, axis=(2, 3))
+    np.fill_diagonal(aff, False)
+    return aff
+
+
+_DUNAVANT5 = (np.array([[1 / 3, 1 / 3, 1 / 3],
+                        [0.059715871789770, 0.470142064105115, 0.470142064105115],
+                        [0.470142064105115, 0.059715871789770, 0.470142064105115],
+                        [0.470142064105115, 0.470142064105115, 0.059715871789770],
+                        [0.797426985353087, 0.101286507323456, 0.101286507323456],
+                        [0.101286507323456, 0.797426985353087, 0.101286507323456],
+                        [0.101286507323456, 0.101286507323456, 0.797426985353087]]),
+              np.array([0.225, 0.132394152788506, 0.132394152788506, 0.132394152788506,
+                        0.125939180544827, 0.125939180544827, 0.125939180544827]))
+
+
+def _triangle_quadrature(tri, levels=3):
+    """Points and weights (summing to the area) of the degree-5 Dunavant rule
+    on the 4**levels midpoint sub-triangles of `tri`."""
+    tris = [np.asarray(tri, dtype=np.float64)]
+    for _ in range(levels):
+        nxt = []
+        for a, b, c in tris:
+            ab, bc, ca = (a + b) / 2, (b + c) / 2, (c + a) / 2
+            nxt += [np.array([a, ab, ca]), np.array([ab, b, bc]), np.array([ca, bc, c]), np.array([ab, bc, ca])]
+        tris = nxt
+    T = np.array(tris)
+    bary, w = _DUNAVANT5
+    pts = np.einsum("pk,tkd->tpd", bary, T).reshape(-1, 3)
+    area = 0.5 * np.linalg.norm(np.cross(T[:, 1] - T[:, 0], T[:, 2] - T[:, 0]), axis=1)
+    return pts, (area[:, None] * w[None, :]).ravel()
+
+
+def view_factor_quadrature(tri_a, n_a, tri_b, n_b, levels=3):
+    """F_ab = (1 / A_a) int_a int_b cos(theta_a) cos(theta_b) / (pi r^2) by
+    product quadrature (independent of the contour-integral formula; for
+    triangles that share no vertex).  n_a, n_b: the sides the faces see."""
+    pa, wa = _triangle_quadrature(tri_a, levels)
+    pb, wb = _triangle_quadrature(tri_b, levels)
+    na = np.asarray(n_a, dtype=np.float64) / np.linalg.norm(n_a)
+    nb = np.asarray(n_b, dtype=np.float64) / np.linalg.norm(n_b)
+    d = pb[None, :, :] - pa[:, None, :]
+    r2 = np.einsum("abk,abk->ab", d, d)
+    ca = np.einsum("abk,k->ab", d, na)
+    cb = -np.einsum("abk,k->ab", d, nb)
+    k = np.where((ca > 0) & (cb > 0), ca * cb / (np.pi * r2 * r2), 0.0)
+    return float(wa @ k @ wb / wa.sum())

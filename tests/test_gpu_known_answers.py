@@ -97,7 +97,9 @@ def test_parallel_plates_textbook_flux(hip):
     d = H.known_answers()["parallel_plates"]
     dom = H.plates_domain()
     dom(d["rays"], k_dykstra=d["k_dykstra"], seed=5, verbose=False)
-    assert dom.last_smooth_info["k_dykstra"] == d["k_dykstra"]
+    # prescribed rounds (the default would be 0 or 1); DkAP stops once the
+    # Dykstra iterates have converged (smoothExchangeFactors.jl:299-318)
+    assert 1 < dom.last_smooth_info["k_dykstra"] <= d["k_dykstra"]
     solve_equilibrium(dom)
     q = np.zeros(dom.num_surfaces)
     for (c, f, w), s in dom.surface_mapping.items():
@@ -163,12 +165,22 @@ def test_icosphere_enclosure_montecarlo(hip, level):
     other), rays leaving along the inward normals, 1e8 rays in total.
       * Sampled rows (four, spread over the sphere) equal the brute-force
         CPU restatement exactly at full R.
-      * Every F_ij agrees with the analytic view factor (rthx_view_factors_3d,
-        pinned by F_EES / Narayanaswamy): the exact binomial tail of each
-        count, as an equivalent Gaussian |z|, stays below the family-wise
-        bound for all n^2 entries at alpha = 1e-3 (Bonferroni: 5.8 at level 2,
-        6.3 at level 3), and the share beyond 5 sigma is near its expectation
-        (5.7e-7 per entry; at most 10 entries at level 3's 1.6e6).
+      * F agrees with exact view factors.  The analytic path
+        (rthx_view_factors_3d, the reference's viewFactor3D restated, pinned
+        by F_EES / Narayanaswamy) is exact except where viewFactor3D.jl:157
+        clamps cos(alpha) of a nearly parallel skew edge pair to 0.999
+        (helpers.vf3d_clamp_affected: 2,880 pairs at level 2, 37,440 at
+        level 3, where its rows then sum to 2.09 and 10.08).  So:
+          - every other pair: the exact binomial tail of its count, as an
+            equivalent Gaussian |z|, stays below the family-wise bound at
+            alpha = 1e-3 (Bonferroni over the pairs tested: ~5.8 / 6.2),
+            and the share beyond 5 sigma is near its expectation;
+          - the clamped pairs of each row together carry the closure
+            remainder 1 - sum(other F) within the same bound;
+          - 48 clamped pairs that share no vertex agree with product
+            quadrature of the view-factor integral (helpers.
+            view_factor_quadrature, independent of the contour formula),
+            where the clamped analytic values do not.
       * After smoothing and the device solve, the equator triangle is within
         2 K of 840.896 K with the readme's hot / cold caps.
     """
@@ -202,10 +214,27 @@ def test_icosphere_enclosure_montecarlo(hip, level):
         assert np.array_equal(D[1 + k * stride], C[k]), 1 + k * stride
     Fa, _, _ = view_factors_3d(xyz, nv)
     off = ~np.eye(n, dtype=bool)
-    z = _binomial_z(D[off], R, Fa[off])
-    bound = stats.norm.isf(1e-3 / (2 * off.sum()))
+    aff = H.vf3d_clamp_affected(xyz, nv)
+    exact = off & ~aff
+    z = _binomial_z(D[exact], R, Fa[exact])
+    bound = stats.norm.isf(1e-3 / (2 * exact.sum()))
     assert z.max() < bound, (z.max(), bound)
-    assert np.count_nonzero(z > 5.0) <= max(10, 20 * 5.7e-7 * off.sum())
+    assert np.count_nonzero(z > 5.0) <= max(10, 20 * 5.7e-7 * exact.sum())
+    # closure: the clamped pairs of a row carry the rest of the row
+    rest = np.clip(1.0 - np.where(exact, Fa, 0.0).sum(axis=1), 0.0, 1.0)
+    rows = aff.any(axis=1)
+    zc = _binomial_z(np.where(aff, D, 0).sum(axis=1)[rows], R, rest[rows])
+    assert zc.max() < stats.norm.isf(1e-3 / (2 * rows.sum())), zc.max()
+    # clamped pairs sharing no vertex against quadrature of the integral
+    shares = lambda a, b: any(np.min(np.linalg.norm(xyz[b, :3] - p, axis=1)) < 1e-12 for p in xyz[a, :3])
+    cand = [tuple(ab) for ab in np.argwhere(aff)[::97] if not shares(*ab)][:48]
+    assert len(cand) >= 24
+    Fq = np.array([H.view_factor_quadrature(xyz[a, :3], normals[a], xyz[b, :3], normals[b]) for a, b in cand])
+    Dc = np.array([D[a, b] for a, b in cand])
+    zq = _binomial_z(Dc, R, Fq)
+    assert zq.max() < stats.norm.isf(1e-3 / (2 * len(cand))), zq.max()
+    Fc = np.array([Fa[a, b] for a, b in cand])
+    assert np.max(np.abs(Fc - Fq) / Fq) > 0.5  # (the clamp's error, which the Monte Carlo counts do not share)
     dom(method="montecarlo", rays_tot=n * R, seed=31)
     assert dom.last_vf_info["rays_per_emitter"] == R
     solve_equilibrium(dom)
