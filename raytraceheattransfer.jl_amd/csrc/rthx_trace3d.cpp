@@ -37,10 +37,11 @@ struct rthx_scene3d {
   int device = 0;
   hipStream_t stream = nullptr;
   hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
-  DevBuf polys, tris, nodes, tables, scene;
+  DevBuf polys, tris, nodes, tables, scene, faces, lines, hull_tris;
   rthx::DevScene3D S{};
   int64_t n_poly = 0;
-  int top_choice[8] = {-1, -1, -1, -1, -1, -1, -1, -1};  // LDS node-cache size per kernel variant (launch_trace3d)
+  int64_t n_hull_tris = 0, n_in_tris = 0;  // box hull: hull / interior triangles
+  int top_choice[16] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};  // LDS node-cache size per kernel variant (launch_trace3d)
   int ghist_choice[4] = {-1, -1, -1, -1};  // per (faithful, pack16, N, R): global-histogram form chosen (1) or not (0)
   int64_t ghist_key[4] = {-1, -1, -1, -1};
   ~rthx_scene3d() {
@@ -296,6 +297,143 @@ void layout_nodes(std::vector<rthx::Bvh2Node>& nodes) {
   nodes.swap(out);
 }
 
+// Box hull (rthx_trace3d.h HullFace): six coplanar groups that are the six
+// faces of the scene's bounding box, each a lattice of quads whose corners
+// lie within 1e-12 of the box's extent of the lattice lines.  Faces are
+// stored in the order 2 axis + side.
+struct HullBuild {
+  std::vector<rthx::HullFace> faces;
+  std::vector<float> lines;
+  std::vector<int64_t> cell_poly;  // polygon of every hull cell, in face / cell order
+  std::vector<char> in_hull;       // per polygon
+  double margin = 0.0;
+};
+
+// Sorted distinct values of v, those within tol of the previous one merged.
+std::vector<double> cluster_lines(std::vector<double> v, double tol) {
+  std::sort(v.begin(), v.end());
+  std::vector<double> out;
+  for (double x : v)
+    if (out.empty() || x - out.back() > tol) out.push_back(x);
+  return out;
+}
+
+// Index of x among the lines (within tol), or -1.
+int64_t line_index(const std::vector<double>& L, double x, double tol) {
+  const auto it = std::lower_bound(L.begin(), L.end(), x - tol);
+  return (it != L.end() && std::fabs(*it - x) <= tol) ? (int64_t)(it - L.begin()) : -1;
+}
+
+bool detect_box_hull(const std::vector<rthx::Emit3>& P, int64_t n, const double* slo, const double* shi,
+                     HullBuild& hb) {
+  double L[3], Lmax = 0.0;
+  for (int k = 0; k < 3; ++k) {
+    L[k] = shi[k] - slo[k];
+    if (!(L[k] > 0.0)) return false;
+    Lmax = std::max(Lmax, L[k]);
+  }
+  const double tol = 1e-12 * Lmax;
+  hb.margin = (double)rthx::kHullMargin * Lmax;
+  int64_t run_b[6], run_e[6];
+  for (int f = 0; f < 6; ++f) run_b[f] = run_e[f] = -1;
+  // which box plane each group lies on (all its polygons quads)
+  for (int64_t b = 0; b < n; b = P[b].ghi) {
+    const int64_t e = P[b].ghi;
+    int face = -1;
+    for (int f = 0; f < 6 && face < 0; ++f) {
+      const int k = f >> 1;
+      const double plane = (f & 1) ? shi[k] : slo[k];
+      bool on = true;
+      for (int64_t p = b; p < e && on; ++p) {
+        on = P[p].nv == 4;
+        for (int i = 0; i < 4 && on; ++i) on = std::fabs(P[p].v[i][k] - plane) <= tol;
+      }
+      if (on) face = f;
+    }
+    if (face < 0) continue;  // an interior group
+    if (run_b[face] >= 0) return false;  // (two groups on one face plane)
+    run_b[face] = b;
+    run_e[face] = e;
+  }
+  hb.faces.clear();
+  hb.lines.clear();
+  hb.cell_poly.clear();
+  hb.in_hull.assign((size_t)n, 0);
+  for (int f = 0; f < 6; ++f) {
+    if (run_b[f] < 0) return false;
+    const int k = f >> 1, u = (k + 1) % 3, v = (k + 2) % 3;
+    std::vector<double> cu, cv;
+    for (int64_t p = run_b[f]; p < run_e[f]; ++p)
+      for (int i = 0; i < 4; ++i) {
+        cu.push_back(P[p].v[i][u] - slo[u]);
+        cv.push_back(P[p].v[i][v] - slo[v]);
+      }
+    const std::vector<double> lu = cluster_lines(cu, tol), lv = cluster_lines(cv, tol);
+    const int64_t nu = (int64_t)lu.size() - 1, nv = (int64_t)lv.size() - 1;
+    if (nu < 1 || nv < 1 || nu * nv != run_e[f] - run_b[f]) return false;
+    if (std::fabs(lu.front()) > tol || std::fabs(lu.back() - L[u]) > tol || std::fabs(lv.front()) > tol ||
+        std::fabs(lv.back() - L[v]) > tol)
+      return false;  // (the face must cover the box face)
+    for (int64_t i = 0; i < nu; ++i)
+      if (lu[i + 1] - lu[i] < 8.0 * hb.margin) return false;  // (one neighbour cell covers the margin)
+    for (int64_t j = 0; j < nv; ++j)
+      if (lv[j + 1] - lv[j] < 8.0 * hb.margin) return false;
+    std::vector<int64_t> cell((size_t)(nu * nv), -1);
+    for (int64_t p = run_b[f]; p < run_e[f]; ++p) {
+      int64_t iu[4], iv[4];
+      for (int i = 0; i < 4; ++i) {
+        iu[i] = line_index(lu, P[p].v[i][u] - slo[u], tol);
+        iv[i] = line_index(lv, P[p].v[i][v] - slo[v], tol);
+        if (iu[i] < 0 || iv[i] < 0) return false;
+      }
+      const int64_t i0 = *std::min_element(iu, iu + 4), j0 = *std::min_element(iv, iv + 4);
+      int seen = 0;  // the four corners of cell (i0, j0), each once
+      for (int i = 0; i < 4; ++i) {
+        const int64_t di = iu[i] - i0, dj = iv[i] - j0;
+        if (di < 0 || di > 1 || dj < 0 || dj > 1) return false;
+        seen |= 1 << (di + 2 * dj);
+      }
+      if (seen != 15 || cell[(size_t)(j0 * nu + i0)] >= 0) return false;
+      cell[(size_t)(j0 * nu + i0)] = p;
+    }
+    rthx::HullFace F{};
+    F.axis = k;
+    F.side = f & 1;
+    F.group = P[run_b[f]].group;
+    F.nu = (int32_t)nu;
+    F.nv = (int32_t)nv;
+    F.lu = (int32_t)hb.lines.size();
+    for (double x : lu) hb.lines.push_back((float)x);
+    F.lv = (int32_t)hb.lines.size();
+    for (double x : lv) hb.lines.push_back((float)x);
+    F.cell0 = (int32_t)hb.cell_poly.size();
+    F.plane = (f & 1) ? (float)L[k] : 0.0f;
+    F.inv_du = (float)((double)nu / L[u]);
+    F.inv_dv = (float)((double)nv / L[v]);
+    for (int64_t c : cell) {
+      hb.cell_poly.push_back(c);
+      hb.in_hull[(size_t)c] = 1;
+    }
+    hb.faces.push_back(F);
+  }
+  return true;
+}
+
+// Leaf references of `nodes` shifted by `tri_off` triangles and inner
+// references by `node_off` nodes (a BVH appended behind another).
+void shift_bvh(std::vector<rthx::Bvh2Node>& nodes, int32_t node_off, int32_t tri_off) {
+  for (auto& nd : nodes)
+    for (int c = 0; c < 2; ++c) {
+      const int32_t r = nd.child[c];
+      if (r >= 0) {
+        nd.child[c] = r + node_off;
+      } else {
+        const int32_t ref = ~r;
+        nd.child[c] = leaf_ref((ref >> rthx::kLeafBits) + tri_off, ref & ((1 << rthx::kLeafBits) - 1));
+      }
+    }
+}
+
 }  // namespace
 
 RTHX_EXPORT int rthx_scene3d_create(const double* xyz, const int32_t* nv, const double* normal, int64_t n,
@@ -330,6 +468,7 @@ RTHX_EXPORT int rthx_scene3d_create_grouped(const double* xyz, const int32_t* nv
   std::vector<rthx::Emit3> polys(n);
   std::vector<rthx::Tri3> tris;
   std::vector<BuildTri> bt;
+  std::vector<int64_t> tri0((size_t)n);  // first triangle of each polygon
   double slo[3] = {1e300, 1e300, 1e300}, shi[3] = {-1e300, -1e300, -1e300};
   for (int64_t k = 0; k < n; ++k) {
     const int m = nv[k];
@@ -377,6 +516,7 @@ RTHX_EXPORT int rthx_scene3d_create_grouped(const double* xyz, const int32_t* nv
     E.group = group ? group[k] : (int32_t)k;
     E.glo = glo[k];
     E.ghi = ghi[k];
+    tri0[(size_t)k] = (int64_t)tris.size();
     const int corners[2][3] = {{0, 1, 2}, {2, 3, 0}};
     for (int h = 0; h < (m == 4 ? 2 : 1); ++h) {
       const V a = v[corners[h][0]], b = v[corners[h][1]], c = v[corners[h][2]];
@@ -404,16 +544,55 @@ RTHX_EXPORT int rthx_scene3d_create_grouped(const double* xyz, const int32_t* nv
   // that stays within the scene scale
   double scale = 0.0;
   for (int k = 0; k < 3; ++k) scale = std::max({scale, std::fabs(slo[k]), std::fabs(shi[k]), shi[k] - slo[k]});
+  // the whole scene's BVH (without a box hull: the only one)
   std::vector<int> order(tris.size());
   std::vector<rthx::Bvh2Node> nodes;
   nodes.reserve(tris.size());
   int depth = build_bvh2(nodes, order, bt, rthx::kBoxPad * scale, false);
   if (depth > rthx::kBvhStack) depth = build_bvh2(nodes, order, bt, rthx::kBoxPad * scale, true);
   if (depth > rthx::kBvhStack) return fail(RTHX_ERANGE, "BVH too deep for the traversal stack");
-  if (tris.size() >= (size_t(1) << (30 - rthx::kLeafBits))) return fail(RTHX_ERANGE, "too many triangles");
+  if (2 * tris.size() >= (size_t(1) << (30 - rthx::kLeafBits))) return fail(RTHX_ERANGE, "too many triangles");
   layout_nodes(nodes);
   std::vector<rthx::Tri3> tris_sorted(tris.size());
   for (size_t i = 0; i < order.size(); ++i) tris_sorted[i] = tris[order[i]];
+  // Box hull: the interior triangles' BVH first (its top is what the kernel
+  // caches in LDS), the whole scene's appended as the fallback walk.
+  HullBuild hb;
+  const char* no_hull = rthx::knob("RTHX_T3_NO_HULL");
+  const bool hull = group && !(no_hull && no_hull[0] == '1') && detect_box_hull(polys, n, slo, shi, hb);
+  std::vector<rthx::Tri3> hull_tris;
+  int32_t full_root = 0, n_in_nodes = (int32_t)nodes.size();
+  int64_t n_in_tris = (int64_t)tris.size();
+  if (hull) {
+    for (int64_t c : hb.cell_poly)
+      for (int h = 0; h < 2; ++h) hull_tris.push_back(tris[(size_t)(tri0[(size_t)c] + h)]);
+    std::vector<BuildTri> bt_in;
+    std::vector<int64_t> in_idx;
+    for (size_t t = 0; t < tris.size(); ++t)
+      if (!hb.in_hull[(size_t)tris[t].poly]) {
+        bt_in.push_back(bt[t]);
+        in_idx.push_back((int64_t)t);
+      }
+    std::vector<rthx::Bvh2Node> nodes_in;
+    std::vector<rthx::Tri3> all_tris;
+    if (!bt_in.empty()) {
+      std::vector<int> order_in(bt_in.size());
+      int d_in = build_bvh2(nodes_in, order_in, bt_in, rthx::kBoxPad * scale, false);
+      if (d_in > rthx::kBvhStack) d_in = build_bvh2(nodes_in, order_in, bt_in, rthx::kBoxPad * scale, true);
+      if (d_in > rthx::kBvhStack) return fail(RTHX_ERANGE, "BVH too deep for the traversal stack");
+      depth = std::max(depth, d_in);
+      layout_nodes(nodes_in);
+      for (int i : order_in) all_tris.push_back(tris[(size_t)in_idx[(size_t)i]]);
+    }
+    n_in_tris = (int64_t)all_tris.size();
+    n_in_nodes = (int32_t)nodes_in.size();
+    full_root = n_in_nodes;
+    shift_bvh(nodes, full_root, (int32_t)n_in_tris);
+    nodes_in.insert(nodes_in.end(), nodes.begin(), nodes.end());
+    nodes.swap(nodes_in);
+    all_tris.insert(all_tris.end(), tris_sorted.begin(), tris_sorted.end());
+    tris_sorted.swap(all_tris);
+  }
   std::vector<double> tables(rthx::kTableDoubles);
   rthx::fill_tables(tables.data());
 
@@ -426,6 +605,8 @@ RTHX_EXPORT int rthx_scene3d_create_grouped(const double* xyz, const int32_t* nv
   if (!s) return fail(RTHX_ENOMEM, "host allocation failed");
   s->device = device;
   s->n_poly = n;
+  s->n_hull_tris = (int64_t)hull_tris.size();
+  s->n_in_tris = n_in_tris;
   auto bail = [&](int code) {
     delete s;
     return code;
@@ -442,6 +623,10 @@ RTHX_EXPORT int rthx_scene3d_create_grouped(const double* xyz, const int32_t* nv
       !up(s->nodes, nodes.data(), nodes.size() * sizeof(rthx::Bvh2Node)) ||
       !up(s->tables, tables.data(), tables.size() * 8))
     return bail(fail(RTHX_ENOMEM, "uploading the 3D scene"));
+  if (hull && (!up(s->faces, hb.faces.data(), hb.faces.size() * sizeof(rthx::HullFace)) ||
+               !up(s->lines, hb.lines.data(), hb.lines.size() * sizeof(float)) ||
+               !up(s->hull_tris, hull_tris.data(), hull_tris.size() * sizeof(rthx::Tri3))))
+    return bail(fail(RTHX_ENOMEM, "uploading the 3D scene's box hull"));
   s->S.n_poly = (int32_t)n;
   s->S.n_tri = (int32_t)tris.size();
   s->S.n_nodes = (int32_t)nodes.size();
@@ -450,6 +635,17 @@ RTHX_EXPORT int rthx_scene3d_create_grouped(const double* xyz, const int32_t* nv
   s->S.tris = s->tris.as<rthx::Tri3>();
   s->S.nodes = s->nodes.as<rthx::Bvh2Node>();
   s->S.tables = s->tables.as<double>();
+  s->S.hull = hull ? 1 : 0;
+  s->S.full_root = full_root;
+  s->S.n_in_nodes = n_in_nodes;
+  for (int k = 0; k < 3; ++k) {
+    s->S.box_lo[k] = slo[k];
+    s->S.box_len[k] = (float)(shi[k] - slo[k]);
+  }
+  s->S.margin = (float)hb.margin;
+  s->S.faces = hull ? s->faces.as<rthx::HullFace>() : nullptr;
+  s->S.hull_lines = hull ? s->lines.as<float>() : nullptr;
+  s->S.hull_tris = hull ? s->hull_tris.as<rthx::Tri3>() : nullptr;
   if (!up(s->scene, &s->S, sizeof(s->S))) return bail(fail(RTHX_ENOMEM, "uploading the 3D scene"));
   if (rthx::knob("RTHX_VERBOSE"))
     std::fprintf(stderr, "rthx_scene3d_create: host geometry + BVH %.2f ms, device setup + upload %.2f ms\n",
@@ -467,6 +663,14 @@ RTHX_EXPORT int rthx_scene3d_stats(const rthx_scene3d* sc, int64_t* n_tri, int64
   if (n_nodes) *n_nodes = sc->S.n_nodes;
   if (depth) *depth = sc->S.stack;
   if (lds_bytes) *lds_bytes = (int64_t)(rthx::trace3d_dynamic_lds(sc->n_poly, sc->S.stack) + rthx::kTrace3dStaticLds);
+  return RTHX_OK;
+}
+
+RTHX_EXPORT int rthx_scene3d_hull(const rthx_scene3d* sc, int32_t* hull, int64_t* hull_tris, int64_t* interior_tris) {
+  if (!sc) return fail(RTHX_EINVAL, "null scene");
+  if (hull) *hull = sc->S.hull;
+  if (hull_tris) *hull_tris = sc->n_hull_tris;
+  if (interior_tris) *interior_tris = sc->n_in_tris;
   return RTHX_OK;
 }
 
@@ -564,6 +768,7 @@ RTHX_EXPORT int rthx_trace_exchange_3d(rthx_scene3d* sc, const rthx_trace_args* 
     L.faithful = (a->flags & RTHX_FLAG_FAITHFUL_SAMPLING) != 0;
     L.pack16 = pack16;
     L.top_choice = sc->top_choice;
+    L.hull = sc->S.hull != 0;
     // The global-histogram form when its LDS (the stacks alone) keeps more
     // workgroups resident than the LDS histogram's (RTHX_T3_GHIST=0/1 forces).
     const char* gh = rthx::knob("RTHX_T3_GHIST");

@@ -44,13 +44,52 @@ static_assert(sizeof(Bvh2Node) == 64, "Bvh2Node is one 64-byte record");
 constexpr int kLeafBits = 3;       // up to 7 triangles per leaf reference
 constexpr double kBoxPad = 1e-5;   // fp32 box padding, relative to the scene scale
 
+// Box hull (rthx_trace3d.cpp detect_box_hull): the scene's outer boundary is
+// an axis-aligned box whose six faces are six coplanar groups, each a
+// lattice of quads.  A ray's hull hit is then found without the BVH: for
+// every face plane the ray can reach (fp32, coordinates relative to the box
+// corner) the lattice cells within kHullMargin of the plane hit are the
+// candidates, and their triangles get the same fp64 Moeller-Trumbore test and
+// (t, id) tie rule as in the walk; the walk then covers the other
+// ("interior") triangles only, starting from that hit.  A triangle that is
+// not a candidate cannot pass Moeller-Trumbore (its cell lies more than the
+// margin from where the ray meets its plane, and the quads lie within 1e-12
+// of the box of the lattice), so the result is the brute-force one.  Rays
+// with a direction component below kHullMinDir, or that hit no candidate
+// (a crack between two triangles), walk the whole scene's BVH instead.
+struct HullFace {
+  int32_t axis, side;        // plane x_axis = box lo (side 0) or hi (side 1)
+  int32_t group;             // its coplanar group (the emitter's own group is skipped)
+  int32_t nu, nv;            // lattice cells along u = (axis + 1) % 3 and v = (axis + 2) % 3
+  int32_t lu, lv;            // offsets of the nu + 1 / nv + 1 lattice lines in DevScene3D::hull_lines
+  int32_t cell0;             // first cell: triangles hull_tris[2 (cell0 + j nu + i) + h], h = 0, 1
+  float plane;               // plane coordinate relative to the box corner
+  float inv_du, inv_dv;      // nu / extent_u, nv / extent_v (first guess of the cell)
+  float pad;
+};
+constexpr float kHullMargin = 1e-4f;  // candidate margin, relative to the box's largest extent
+constexpr float kHullMinDir = 1e-6f;  // smallest |direction component| the hull path takes
+
 struct DevScene3D {
   int32_t n_poly, n_tri, n_nodes;
-  int32_t stack;  // walk stack entries a lane needs (inner-node depth of the BVH)
+  int32_t stack;  // walk stack entries a lane needs (inner-node depth of the BVHs)
   const Emit3 RTHX_GLOBAL* polys;
   const Tri3 RTHX_GLOBAL* tris;
   const Bvh2Node RTHX_GLOBAL* nodes;
   const double RTHX_GLOBAL* tables;  // kTableDoubles (cos/sin table for the azimuth)
+  // nodes / tris hold one BVH -- the whole scene's, root 0 -- or, with a box
+  // hull, two: the interior triangles' (root 0, its top first: the LDS cache)
+  // and, from full_root on, the whole scene's (the fallback walk).
+  int32_t hull;         // 1: box hull fast path (HullFace x 6)
+  int32_t full_root;    // root node of the whole scene's BVH
+  int32_t n_in_nodes;   // nodes of the interior BVH (0: no interior triangles)
+  int32_t pad0;
+  double box_lo[3];     // box corner (hull coordinates are relative to it)
+  float box_len[3];     // box extents
+  float margin;         // kHullMargin x the largest extent
+  const HullFace RTHX_GLOBAL* faces;       // [6]
+  const float RTHX_GLOBAL* hull_lines;     // lattice lines relative to the box corner
+  const Tri3 RTHX_GLOBAL* hull_tris;       // [2 x cells], cell order, (v0 v1 v2), (v2 v3 v0)
 };
 
 constexpr uint32_t kTrace3dTag = 0x40000000u;  // Philox counter word 3 of the 3D tracer
@@ -84,7 +123,8 @@ struct Trace3dLaunch {
   bool faithful;
   bool pack16;  // < 65536 rays per workgroup: u16 row-histogram counters
   bool ghist;   // counts straight to the dense rows (no LDS histogram)
-  int* top_choice;  // [ghist * 4 + faithful * 2 + pack16]: LDS node-cache size (64 / 128), -1 = not chosen yet
+  bool hull;    // box hull fast path (DevScene3D::hull)
+  int* top_choice;  // [hull * 8 + ghist * 4 + faithful * 2 + pack16]: LDS node-cache size (64 / 128), -1 = not chosen yet
 };
 
 hipError_t launch_trace3d(const Trace3dLaunch& L);

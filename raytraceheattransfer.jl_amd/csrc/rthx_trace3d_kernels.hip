@@ -129,14 +129,69 @@ struct Walk {
     for (int k = first; k < last; ++k) {
       const Tri3 T = S.tris[k];
       if ((unsigned)(T.poly - glo) < (unsigned)glen) continue;  // the emitter's group
-      const double t = moller_trumbore(T, o, d);
-      if (t > 0.0 && (t < best_t || (t == best_t && T.id < best_id))) {
-        best_t = t;
-        best_id = T.id;
-        best_poly = T.poly;
-        best_tf = (float)(best_t * (1.0 + 1e-6));
-      }
+      consider(T);
     }
+  }
+
+  void __device__ __forceinline__ consider(const Tri3& T) {
+    const double t = moller_trumbore(T, o, d);
+    if (t > 0.0 && (t < best_t || (t == best_t && T.id < best_id))) {
+      best_t = t;
+      best_id = T.id;
+      best_poly = T.poly;
+      best_tf = (float)(best_t * (1.0 + 1e-6));
+    }
+  }
+
+  // Box hull (rthx_trace3d.h HullFace): the nearest hull triangle hit, from
+  // the lattice cells within the margin of where the ray meets each face
+  // plane it can reach, into best_*; false when the hull path does not
+  // apply (a direction component below kHullMinDir) or no candidate is hit
+  // (the ray then walks the whole scene's BVH).
+  __device__ __forceinline__ bool hull_hit(const DevScene3D& S, int group) {
+    float of[3], df[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      of[k] = (float)(o[k] - S.box_lo[k]);
+      df[k] = (float)d[k];
+    }
+    if (!(fminf(fminf(fabsf(df[0]), fabsf(df[1])), fabsf(df[2])) >= kHullMinDir)) return false;
+    const float m = S.margin;
+#pragma unroll
+    for (int f = 0; f < 6; ++f) {
+      constexpr int kU[3] = {1, 2, 0}, kV[3] = {2, 0, 1};
+      const int k = f >> 1, u = kU[f >> 1], v = kV[f >> 1];
+      const HullFace RTHX_GLOBAL& F = S.faces[f];
+      if (F.group == group) continue;  // (the emitter's own face)
+      const float t = (F.plane - of[k]) * inv[k];
+      if (!(t >= -m)) continue;  // behind the ray by more than the margin (or NaN)
+      const float tp = fmaxf(t, 0.0f);
+      const float pu = __builtin_fmaf(tp, df[u], of[u]), pv = __builtin_fmaf(tp, df[v], of[v]);
+      if (!(pu >= -m && pu <= S.box_len[u] + m && pv >= -m && pv <= S.box_len[v] + m)) continue;
+      int i0, i1, j0, j1;
+      cell_range(S.hull_lines + F.lu, F.nu, F.inv_du, pu, m, i0, i1);
+      cell_range(S.hull_lines + F.lv, F.nv, F.inv_dv, pv, m, j0, j1);
+      for (int j = j0; j <= j1; ++j)
+        for (int i = i0; i <= i1; ++i) {
+          const int c = F.cell0 + j * F.nu + i;
+          const Tri3 A = S.hull_tris[2 * c], B = S.hull_tris[2 * c + 1];
+          consider(A);
+          consider(B);
+        }
+    }
+    return best_poly >= 0;
+  }
+
+  // Lattice cells [lo, hi] of the lines [0, n] within margin m of p
+  // (first guess from the uniform spacing, then corrected).
+  static __device__ __forceinline__ void cell_range(const float RTHX_GLOBAL* L, int n, float inv, float p, float m,
+                                                    int& lo, int& hi) {
+    int i = (int)(p * inv);
+    i = i < 0 ? 0 : i > n - 1 ? n - 1 : i;
+    while (i > 0 && p < L[i]) --i;
+    while (i < n - 1 && p >= L[i + 1]) ++i;
+    lo = (i > 0 && p - L[i] < m) ? i - 1 : i;
+    hi = (i < n - 1 && L[i + 1] - p < m) ? i + 1 : i;
   }
 
   // One round of the walk: descend (speculatively) until all but
@@ -242,14 +297,19 @@ __device__ __forceinline__ void emit_ray(const Emit3& E, const double* tab, uint
 // workgroups; they are built for 6 waves per SIMD (80 VGPRs, no spills;
 // config 4 L4 7.59 -> 7.83 Grays/s), the LDS-histogram ones keep the
 // compiler's 86 (5 waves: a 6-wave budget measured 1 % slower at L3).
-template <bool FAITHFUL, bool PACK16, int TOP, bool GH = false>
+// HULL: the scene has a box hull (DevScene3D::hull): a ray's hull hit comes
+// from the face lattices and the walk covers the interior BVH (root 0; its
+// top is the LDS cache), or the whole scene's (full_root) when the hull path
+// does not apply.
+template <bool FAITHFUL, bool PACK16, int TOP, bool GH = false, bool HULL = false>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(GH ? kGhWaves : kHistWaves))) void trace_exchange_3d_kernel(const DevScene3D* __restrict__ Sp,
                                                                                   TraceParams P, TallyParams T) {
   // dynamic LDS: [row histogram][walk stacks] (GH: the stacks only)
   extern __shared__ uint32_t hist[];
   __shared__ Bvh2Node s_top[TOP];
   Bvh2Node RTHX_LDS* top = (Bvh2Node RTHX_LDS*)&s_top[0];
-  const int n_top = TOP < Sp->n_nodes ? TOP : Sp->n_nodes;
+  const int n_cached = HULL ? Sp->n_in_nodes : Sp->n_nodes;
+  const int n_top = TOP < n_cached ? TOP : n_cached;
   const double* s_tab = (const double*)Sp->tables;  // the azimuth table, read from global memory (L1/L2)
   __shared__ Emit3 s_emit;
   __shared__ uint32_t s_tallied;
@@ -315,6 +375,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(GH ? k
           emit_ray<FAITHFUL>(*(const Emit3*)em, s_tab, (uint32_t)g, r, P.key0, P.key1,
                              o, d);
           w.init(o, d);
+          if (HULL)
+            w.node = w.hull_hit(S, grp) ? (S.n_in_nodes > 0 ? 0 : kWalkDone) : S.full_root;
           live = true;
         }
       }
@@ -333,6 +395,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(GH ? k
                        P.key1, o, d);
     Walk w;
     w.init(o, d);
+    if (HULL) w.node = w.hull_hit(S, grp) ? (S.n_in_nodes > 0 ? 0 : kWalkDone) : S.full_root;
     while (w.step(S, topo, n_top, grp, glo, glen, stk)) {
     }
     tally(w.best_poly);
@@ -353,24 +416,24 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(GH ? k
 
 namespace {
 
-template <bool FAITHFUL, bool PACK16, bool GH>
+template <bool FAITHFUL, bool PACK16, bool GH, bool HULL>
 hipError_t launch_variant(const Trace3dLaunch& L) {
   // The 128-node cache when it costs no workgroup per CU against the 64-node
   // one (occupancy queries are slow host calls: the choice is kept per scene
   // and kernel variant in L.top_choice).
-  int& top = L.top_choice[(GH ? 4 : 0) + (FAITHFUL ? 2 : 0) + (PACK16 ? 1 : 0)];
+  int& top = L.top_choice[(HULL ? 8 : 0) + (GH ? 4 : 0) + (FAITHFUL ? 2 : 0) + (PACK16 ? 1 : 0)];
   if (top < 0) {
     int pc64 = 0, pc128 = 0;
     hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &pc64, (const void*)t3::trace_exchange_3d_kernel<FAITHFUL, PACK16, 64, GH>, t3::kThreads, L.lds_bytes);
+        &pc64, (const void*)t3::trace_exchange_3d_kernel<FAITHFUL, PACK16, 64, GH, HULL>, t3::kThreads, L.lds_bytes);
     if (e != hipSuccess) return e;
     e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &pc128, (const void*)t3::trace_exchange_3d_kernel<FAITHFUL, PACK16, 128, GH>, t3::kThreads, L.lds_bytes);
+        &pc128, (const void*)t3::trace_exchange_3d_kernel<FAITHFUL, PACK16, 128, GH, HULL>, t3::kThreads, L.lds_bytes);
     if (e != hipSuccess) return e;
     top = pc128 > 0 && pc128 >= pc64 ? 128 : 64;
   }
-  auto kern = top == 128 ? t3::trace_exchange_3d_kernel<FAITHFUL, PACK16, 128, GH>
-                         : t3::trace_exchange_3d_kernel<FAITHFUL, PACK16, 64, GH>;
+  auto kern = top == 128 ? t3::trace_exchange_3d_kernel<FAITHFUL, PACK16, 128, GH, HULL>
+                         : t3::trace_exchange_3d_kernel<FAITHFUL, PACK16, 64, GH, HULL>;
   if (L.lds_bytes > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.lds_bytes);
     if (e != hipSuccess) return e;
@@ -382,21 +445,32 @@ hipError_t launch_variant(const Trace3dLaunch& L) {
 
 }  // namespace
 
+template <bool HULL>
+hipError_t launch_trace3d_h(const Trace3dLaunch& L) {
+  if (L.ghist) return L.faithful ? launch_variant<true, false, true, HULL>(L) : launch_variant<false, false, true, HULL>(L);
+  if (L.faithful) return L.pack16 ? launch_variant<true, true, false, HULL>(L) : launch_variant<true, false, false, HULL>(L);
+  return L.pack16 ? launch_variant<false, true, false, HULL>(L) : launch_variant<false, false, false, HULL>(L);
+}
+
 hipError_t launch_trace3d(const Trace3dLaunch& L) {
-  if (L.ghist) return L.faithful ? launch_variant<true, false, true>(L) : launch_variant<false, false, true>(L);
-  if (L.faithful) return L.pack16 ? launch_variant<true, true, false>(L) : launch_variant<true, false, false>(L);
-  return L.pack16 ? launch_variant<false, true, false>(L) : launch_variant<false, false, false>(L);
+  return L.hull ? launch_trace3d_h<true>(L) : launch_trace3d_h<false>(L);
 }
 
 // Resident workgroups per CU of the LDS-histogram and the global-histogram
 // forms (the host keeps the global one when it fits more).
 hipError_t trace3d_occupancy(const Trace3dLaunch& L, size_t lds_hist, size_t lds_gh, int* wg_hist, int* wg_gh) {
-  const void* kh = L.faithful ? (L.pack16 ? (const void*)t3::trace_exchange_3d_kernel<true, true, 64, false>
-                                          : (const void*)t3::trace_exchange_3d_kernel<true, false, 64, false>)
-                              : (L.pack16 ? (const void*)t3::trace_exchange_3d_kernel<false, true, 64, false>
-                                          : (const void*)t3::trace_exchange_3d_kernel<false, false, 64, false>);
-  const void* kg = L.faithful ? (const void*)t3::trace_exchange_3d_kernel<true, false, 64, true>
-                              : (const void*)t3::trace_exchange_3d_kernel<false, false, 64, true>;
+  const void* kh = L.hull ? (L.faithful ? (L.pack16 ? (const void*)t3::trace_exchange_3d_kernel<true, true, 64, false, true>
+                                                     : (const void*)t3::trace_exchange_3d_kernel<true, false, 64, false, true>)
+                                         : (L.pack16 ? (const void*)t3::trace_exchange_3d_kernel<false, true, 64, false, true>
+                                                     : (const void*)t3::trace_exchange_3d_kernel<false, false, 64, false, true>))
+                          : (L.faithful ? (L.pack16 ? (const void*)t3::trace_exchange_3d_kernel<true, true, 64, false>
+                                                     : (const void*)t3::trace_exchange_3d_kernel<true, false, 64, false>)
+                                         : (L.pack16 ? (const void*)t3::trace_exchange_3d_kernel<false, true, 64, false>
+                                                     : (const void*)t3::trace_exchange_3d_kernel<false, false, 64, false>));
+  const void* kg = L.hull ? (L.faithful ? (const void*)t3::trace_exchange_3d_kernel<true, false, 64, true, true>
+                                         : (const void*)t3::trace_exchange_3d_kernel<false, false, 64, true, true>)
+                          : (L.faithful ? (const void*)t3::trace_exchange_3d_kernel<true, false, 64, true>
+                                         : (const void*)t3::trace_exchange_3d_kernel<false, false, 64, true>);
   hipError_t e = hipSuccess;
   if (lds_hist > 64 * 1024) e = hipFuncSetAttribute(kh, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_hist);
   if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(wg_hist, kh, t3::kThreads, lds_hist);

@@ -100,6 +100,9 @@ def load(path: Optional[str] = None) -> C.CDLL:
     if hasattr(lib, "rthx_scene3d_stats"):  # (older A/B variant libraries lack it)
         lib.rthx_scene3d_stats.argtypes = [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int64),
                                            C.POINTER(C.c_int32), C.POINTER(C.c_int64)]
+    if hasattr(lib, "rthx_scene3d_hull"):  # (older A/B variant libraries lack it)
+        lib.rthx_scene3d_hull.argtypes = [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_int64),
+                                          C.POINTER(C.c_int64)]
     lib.rthx_trace_exchange_3d.argtypes = [C.c_void_p, C.POINTER(abi.TraceArgs), C.c_void_p]
     lib.rthx_view_factors_3d.argtypes = [dp, C.POINTER(C.c_int32), C.c_int64, C.POINTER(abi.Vf3dArgs), dp, dp,
                                          C.POINTER(abi.Vf3dInfo)]

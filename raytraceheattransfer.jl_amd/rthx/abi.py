@@ -275,6 +275,7 @@ EXPORTED_SYMBOLS = (
     "rthx_scene3d_create_grouped",
     "rthx_scene3d_destroy",
     "rthx_scene3d_stats",
+    "rthx_scene3d_hull",
     "rthx_trace_exchange_3d",
 )
 

@@ -70,7 +70,12 @@ class Scene3D:
         nt, nn, ln = C.c_int64(), C.c_int64(), C.c_int64()
         dp = C.c_int32()
         check(self._lib.rthx_scene3d_stats(self.handle, C.byref(nt), C.byref(nn), C.byref(dp), C.byref(ln)))
-        return {"n_tri": nt.value, "n_nodes": nn.value, "depth": dp.value, "lds_bytes": ln.value}
+        out = {"n_tri": nt.value, "n_nodes": nn.value, "depth": dp.value, "lds_bytes": ln.value}
+        if hasattr(self._lib, "rthx_scene3d_hull"):  # rthx_scene3d_hull: the box-hull fast path
+            h, ht, it = C.c_int32(), C.c_int64(), C.c_int64()
+            check(self._lib.rthx_scene3d_hull(self.handle, C.byref(h), C.byref(ht), C.byref(it)))
+            out.update(hull=bool(h.value), hull_tris=ht.value, interior_tris=it.value)
+        return out
 
     def close(self) -> None:
         if getattr(self, "handle", None):

@@ -577,3 +577,54 @@ def view_factor_quadrature(tri_a, n_a, tri_b, n_b, levels=3):
     cb = -np.einsum("abk,k->ab", d, nb)
     k = np.where((ca > 0) & (cb > 0), ca * cb / (np.pi * r2 * r2), 0.0)
     return float(wa @ k @ wb / wa.sum())
+
+
+def box_scene(lines, level=None, radius=0.25, center=None, perturb=0.0, seed=0):
+    """A closed box whose six faces are lattices of quads over the given
+    lattice lines (lines[k]: sorted coordinates along axis k, first and last
+    = the box), every face one coplanar group (rays leave inward), optionally
+    an icosphere of `level` inside (each triangle its own group, rays leave
+    outward).  `perturb` moves the interior lattice lines by up to that
+    fraction of a cell (a non-uniform lattice).  Returns (xyz, nv, normals,
+    groups, n_hull_polygons); faces in the order of rthx_trace3d's hull
+    detection does not matter."""
+    rng = np.random.default_rng(seed)
+    L = [np.array(l, dtype=np.float64) for l in lines]
+    if perturb:
+        for k in range(3):
+            d = np.diff(L[k])
+            L[k][1:-1] += perturb * rng.uniform(-0.5, 0.5, len(L[k]) - 2) * np.minimum(d[:-1], d[1:])
+    lo = np.array([l[0] for l in L])
+    hi = np.array([l[-1] for l in L])
+    c = (lo + hi) / 2 if center is None else np.asarray(center, dtype=np.float64)
+    polys, normals, groups = [], [], []
+    gid = 0
+    for k in range(3):
+        u, v = (k + 1) % 3, (k + 2) % 3
+        for side in (0, 1):
+            plane = hi[k] if side else lo[k]
+            for j in range(len(L[v]) - 1):
+                for i in range(len(L[u]) - 1):
+                    q = np.zeros((4, 3))
+                    for m, (a, b) in enumerate([(i, j), (i + 1, j), (i + 1, j + 1), (i, j + 1)]):
+                        q[m, k] = plane
+                        q[m, u] = L[u][a]
+                        q[m, v] = L[v][b]
+                    polys.append(q)
+                    nrm = np.zeros(3)
+                    nrm[k] = -1.0 if side else 1.0
+                    normals.append(nrm)
+                    groups.append(gid)
+            gid += 1
+    n_hull = len(polys)
+    if level is not None:
+        for tri in icosphere(level, radius, c):
+            q = np.zeros((4, 3))
+            q[:3] = tri
+            q[3] = tri[2]
+            polys.append(q)
+            normals.append(tri.mean(axis=0) - c)
+            groups.append(gid)
+            gid += 1
+    nv = np.array([4] * n_hull + [3] * (len(polys) - n_hull), dtype=np.int32)
+    return np.array(polys), nv, np.array(normals), np.array(groups, dtype=np.int32), n_hull

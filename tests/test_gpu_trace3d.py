@@ -231,3 +231,81 @@ def test_config4_full_size_sampled_rows(hip, ndim, level):
         row = np.zeros(n, dtype=np.uint32)
         row[cols[rp[g0]:rp[g0 + 1]]] = cnt[rp[g0]:rp[g0 + 1]]
         assert np.array_equal(row, C[k]), g0
+
+
+def _hull_dense(xyz, nv, nrm, R, seed, groups, monkeypatch=None, no_hull=False, faithful=False):
+    from rthx.trace3d import Scene3D
+
+    if monkeypatch is not None:
+        monkeypatch.setenv("RTHX_T3_NO_HULL", "1" if no_hull else "0")
+    s = Scene3D(xyz, nv, nrm, groups=groups)
+    try:
+        st = s.stats()
+        rp, cols, cnt, info = s.trace(R, seed=seed, faithful=faithful)
+    finally:
+        s.close()
+    n = len(nv)
+    D = np.zeros((n, n), dtype=np.uint32)
+    for i in range(n):
+        D[i, cols[rp[i]:rp[i + 1]]] = cnt[rp[i]:rp[i + 1]]
+    return D, info, st
+
+
+@pytest.mark.parametrize("ndim,level,faithful", [(3, 1, False), (6, 2, False), (4, 2, True), (11, 0, False)])
+def test_box_hull_exact(hip, monkeypatch, ndim, level, faithful):
+    """Box-hull fast path (rthx_trace3d.h HullFace): config 4's cube faces are
+    found as the scene box's six face lattices; hull hits come from the
+    lattice and the walk covers the sphere only.  Counts equal the
+    brute-force restatement exactly, and the plain walk (RTHX_T3_NO_HULL=1)."""
+    xyz, nv, nrm, nc = H.cube_icosphere_scene(ndim=ndim, level=level)
+    g = H.cube_icosphere_groups(ndim, level)
+    D, info, st = _hull_dense(xyz, nv, nrm, 4000, 14, g, monkeypatch, faithful=faithful)
+    assert st["hull"] and st["hull_tris"] == 12 * ndim * ndim and st["interior_tris"] == 20 * 4 ** level
+    C, lost = oracle.trace_exchange_3d(xyz, nv, nrm, 4000, seed=14, nthreads=16, groups=g)
+    assert np.array_equal(D, C) and info["lost_total"] == lost
+    D0, info0, st0 = _hull_dense(xyz, nv, nrm, 4000, 14, g, monkeypatch, no_hull=True, faithful=faithful)
+    assert not st0["hull"] and np.array_equal(D, D0)
+
+
+@pytest.mark.parametrize("case", ["nonuniform", "empty", "far", "flat"])
+def test_box_hull_scenes_exact(hip, monkeypatch, case):
+    """Hull scenes beyond config 4: perturbed (non-uniform) lattices with
+    different cell counts per axis around an icosphere; a box with nothing
+    inside (no interior BVH); a box far from the origin and shrunk (fp32
+    coordinates relative to the box corner); a flat 10:1:0.2 box."""
+    if case == "nonuniform":
+        lines = [np.linspace(0, 2, 9), np.linspace(0, 1, 5), np.linspace(0, 1.5, 7)]
+        xyz, nv, nrm, g, nh = H.box_scene(lines, level=2, radius=0.3, perturb=0.6, seed=3)
+    elif case == "empty":
+        xyz, nv, nrm, g, nh = H.box_scene([np.linspace(0, 1, 6)] * 3)
+    elif case == "far":
+        xyz, nv, nrm, g, nh = H.box_scene([np.linspace(0, 1, 5)] * 3, level=1, radius=0.3)
+        xyz = np.ascontiguousarray(xyz * 1e-3 + np.array([250.0, -1000.0, 37.5]))
+    else:
+        lines = [np.linspace(0, 10, 21), np.linspace(0, 1, 3), np.linspace(0, 0.2, 2)]
+        xyz, nv, nrm, g, nh = H.box_scene(lines, level=1, radius=0.08)
+    D, info, st = _hull_dense(xyz, nv, nrm, 3000, 15, g, monkeypatch)
+    assert st["hull"] and st["hull_tris"] == 2 * nh
+    C, lost = oracle.trace_exchange_3d(xyz, nv, nrm, 3000, seed=15, nthreads=16, groups=g)
+    assert np.array_equal(D, C) and info["lost_total"] == lost
+    assert lost == 0
+
+
+def test_box_hull_not_taken(hip, monkeypatch):
+    """The fast path needs six face groups that are lattices on the box:
+    without groups, or with one face's quads split into two groups, the scene
+    walks its BVH as before (and still equals the restatement)."""
+    from rthx.trace3d import Scene3D
+
+    xyz, nv, nrm, nc = H.cube_icosphere_scene(ndim=3, level=1)
+    s = Scene3D(xyz, nv, nrm)
+    try:
+        assert not s.stats()["hull"]
+    finally:
+        s.close()
+    g = H.cube_icosphere_groups(3, 1).copy()
+    g[5:9] = 10_000  # (face 0's last 4 quads: a group of their own)
+    D, info, st = _hull_dense(xyz, nv, nrm, 2000, 16, g, monkeypatch)
+    assert not st["hull"]
+    C, lost = oracle.trace_exchange_3d(xyz, nv, nrm, 2000, seed=16, nthreads=16, groups=g)
+    assert np.array_equal(D, C)
