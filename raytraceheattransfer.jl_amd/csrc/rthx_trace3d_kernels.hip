@@ -41,7 +41,10 @@ constexpr int kThreads = kTrace3dThreads;
 #ifndef RTHX_T3_GH_WAVES
 #define RTHX_T3_GH_WAVES 6  // waves per SIMD the global-histogram kernels are built for (1 = compiler's choice)
 #endif
-constexpr int kHistWaves = RTHX_T3_WAVES, kGhWaves = RTHX_T3_GH_WAVES;
+#ifndef RTHX_T3_HULL_WAVES
+#define RTHX_T3_HULL_WAVES 6  // waves per SIMD of the box-hull kernels (80 VGPRs, 2 spilled as in the plain kernels)
+#endif
+constexpr int kHistWaves = RTHX_T3_WAVES, kGhWaves = RTHX_T3_GH_WAVES, kHullWaves = RTHX_T3_HULL_WAVES;
 
 // Products are fused exactly where the CPU restatement fuses them (fma() in
 // oracle/rthx_oracle.c t3_mt); everything else is built uncontracted.
@@ -133,7 +136,7 @@ struct Walk {
     }
   }
 
-  void __device__ __forceinline__ consider(const Tri3& T) {
+  __device__ __forceinline__ void consider(const Tri3& T) {
     const double t = moller_trumbore(T, o, d);
     if (t > 0.0 && (t < best_t || (t == best_t && T.id < best_id))) {
       best_t = t;
@@ -149,34 +152,36 @@ struct Walk {
   // apply (a direction component below kHullMinDir) or no candidate is hit
   // (the ray then walks the whole scene's BVH).
   __device__ __forceinline__ bool hull_hit(const DevScene3D& S, int group) {
-    float of[3], df[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      of[k] = (float)(o[k] - S.box_lo[k]);
-      df[k] = (float)d[k];
-    }
-    if (!(fminf(fminf(fabsf(df[0]), fabsf(df[1])), fabsf(df[2])) >= kHullMinDir)) return false;
+    // Per-axis values as separate registers: selects over array elements
+    // were folded into a dynamic index, which put this Walk in scratch.
+    float o0 = (float)(o[0] - S.box_lo[0]), o1 = (float)(o[1] - S.box_lo[1]), o2 = (float)(o[2] - S.box_lo[2]);
+    float d0 = (float)d[0], d1 = (float)d[1], d2 = (float)d[2];
+    float i0 = inv[0], i1 = inv[1], i2 = inv[2];
+    __asm__("" : "+v"(o0), "+v"(o1), "+v"(o2), "+v"(d0), "+v"(d1), "+v"(d2), "+v"(i0), "+v"(i1), "+v"(i2));
+    if (!(fminf(fminf(fabsf(d0), fabsf(d1)), fabsf(d2)) >= kHullMinDir)) return false;
     const float m = S.margin;
-#pragma unroll
+    // one loop body for the six faces (the unrolled form spilled ~100 VGPRs)
+#pragma nounroll
     for (int f = 0; f < 6; ++f) {
-      constexpr int kU[3] = {1, 2, 0}, kV[3] = {2, 0, 1};
-      const int k = f >> 1, u = kU[f >> 1], v = kV[f >> 1];
       const HullFace RTHX_GLOBAL& F = S.faces[f];
       if (F.group == group) continue;  // (the emitter's own face)
-      const float t = (F.plane - of[k]) * inv[k];
+      const int k = f >> 1;  // axis; u = (k + 1) % 3, v = (k + 2) % 3
+      const bool a0 = k == 0, a1 = k == 1;
+      const float t = (F.plane - (a0 ? o0 : a1 ? o1 : o2)) * (a0 ? i0 : a1 ? i1 : i2);
       if (!(t >= -m)) continue;  // behind the ray by more than the margin (or NaN)
       const float tp = fmaxf(t, 0.0f);
-      const float pu = __builtin_fmaf(tp, df[u], of[u]), pv = __builtin_fmaf(tp, df[v], of[v]);
-      if (!(pu >= -m && pu <= S.box_len[u] + m && pv >= -m && pv <= S.box_len[v] + m)) continue;
-      int i0, i1, j0, j1;
-      cell_range(S.hull_lines + F.lu, F.nu, F.inv_du, pu, m, i0, i1);
-      cell_range(S.hull_lines + F.lv, F.nv, F.inv_dv, pv, m, j0, j1);
-      for (int j = j0; j <= j1; ++j)
-        for (int i = i0; i <= i1; ++i) {
+      const float pu = __builtin_fmaf(tp, a0 ? d1 : a1 ? d2 : d0, a0 ? o1 : a1 ? o2 : o0);
+      const float pv = __builtin_fmaf(tp, a0 ? d2 : a1 ? d0 : d1, a0 ? o2 : a1 ? o0 : o1);
+      const float lu = S.box_len[a0 ? 1 : a1 ? 2 : 0], lv = S.box_len[a0 ? 2 : a1 ? 0 : 1];
+      if (!(pu >= -m && pu <= lu + m && pv >= -m && pv <= lv + m)) continue;
+      int c0, c1, r0, r1;
+      cell_range(S.hull_lines + F.lu, F.nu, F.inv_du, pu, m, c0, c1);
+      cell_range(S.hull_lines + F.lv, F.nv, F.inv_dv, pv, m, r0, r1);
+      for (int j = r0; j <= r1; ++j)
+        for (int i = c0; i <= c1; ++i) {
           const int c = F.cell0 + j * F.nu + i;
-          const Tri3 A = S.hull_tris[2 * c], B = S.hull_tris[2 * c + 1];
-          consider(A);
-          consider(B);
+#pragma nounroll
+          for (int h = 0; h < 2; ++h) consider(S.hull_tris[2 * c + h]);
         }
     }
     return best_poly >= 0;
@@ -302,7 +307,7 @@ __device__ __forceinline__ void emit_ray(const Emit3& E, const double* tab, uint
 // top is the LDS cache), or the whole scene's (full_root) when the hull path
 // does not apply.
 template <bool FAITHFUL, bool PACK16, int TOP, bool GH = false, bool HULL = false>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(GH ? kGhWaves : kHistWaves))) void trace_exchange_3d_kernel(const DevScene3D* __restrict__ Sp,
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(HULL ? kHullWaves : GH ? kGhWaves : kHistWaves))) void trace_exchange_3d_kernel(const DevScene3D* __restrict__ Sp,
                                                                                   TraceParams P, TallyParams T) {
   // dynamic LDS: [row histogram][walk stacks] (GH: the stacks only)
   extern __shared__ uint32_t hist[];
