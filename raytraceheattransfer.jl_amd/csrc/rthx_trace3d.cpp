@@ -416,7 +416,7 @@ bool detect_box_hull(const std::vector<rthx::Emit3>& P, int64_t n, const double*
     }
     hb.faces.push_back(F);
   }
-  return true;
+  return hb.lines.size() <= 4096;  // (the kernel stages the lines in LDS: at most 16 KB)
 }
 
 // Leaf references of `nodes` shifted by `tri_off` triangles and inner
@@ -638,6 +638,7 @@ RTHX_EXPORT int rthx_scene3d_create_grouped(const double* xyz, const int32_t* nv
   s->S.hull = hull ? 1 : 0;
   s->S.full_root = full_root;
   s->S.n_in_nodes = n_in_nodes;
+  s->S.n_hull_lines = hull ? (int32_t)hb.lines.size() : -1;
   for (int k = 0; k < 3; ++k) {
     s->S.box_lo[k] = slo[k];
     s->S.box_len[k] = (float)(shi[k] - slo[k]);
@@ -662,7 +663,7 @@ RTHX_EXPORT int rthx_scene3d_stats(const rthx_scene3d* sc, int64_t* n_tri, int64
   if (n_tri) *n_tri = sc->S.n_tri;
   if (n_nodes) *n_nodes = sc->S.n_nodes;
   if (depth) *depth = sc->S.stack;
-  if (lds_bytes) *lds_bytes = (int64_t)(rthx::trace3d_dynamic_lds(sc->n_poly, sc->S.stack) + rthx::kTrace3dStaticLds);
+  if (lds_bytes) *lds_bytes = (int64_t)(rthx::trace3d_dynamic_lds(sc->n_poly, sc->S.stack, sc->S.n_hull_lines) + rthx::kTrace3dStaticLds);
   return RTHX_OK;
 }
 
@@ -699,7 +700,7 @@ RTHX_EXPORT int rthx_trace_exchange_3d(rthx_scene3d* sc, const rthx_trace_args* 
   if (n_rows > 0 && R >= 2 * kSplitMinRays)
     split = std::max<int64_t>(1, std::min<int64_t>((split_target + n_rows - 1) / n_rows, R / kSplitMinRays));
   const bool pack16 = (R + split - 1) / split < 65536;
-  const size_t lds_bytes = rthx::trace3d_dynamic_lds(pack16 ? (N + 1) / 2 : N, sc->S.stack);
+  const size_t lds_bytes = rthx::trace3d_dynamic_lds(pack16 ? (N + 1) / 2 : N, sc->S.stack, sc->S.n_hull_lines);
   if (lds_bytes + rthx::kTrace3dStaticLds > rthx::kMaxLdsBytes)
     return fail(RTHX_ERANGE, "N too large for the LDS row histogram and walk stacks of the 3D tracer");
   if (n_rows * split >= (int64_t(1) << 31)) return fail(RTHX_ERANGE, "too many rows in one call");
@@ -779,7 +780,7 @@ RTHX_EXPORT int rthx_trace_exchange_3d(rthx_scene3d* sc, const rthx_trace_args* 
       const int64_t key = N * 2 + (pack16 ? 1 : 0);
       if (sc->ghist_key[slot_k] != key) {
         int wh = 0, wg = 0;
-        HIP_TRY(rthx::trace3d_occupancy(L, lds_bytes, rthx::trace3d_dynamic_lds(0, sc->S.stack), &wh, &wg),
+        HIP_TRY(rthx::trace3d_occupancy(L, lds_bytes, rthx::trace3d_dynamic_lds(0, sc->S.stack, sc->S.n_hull_lines), &wh, &wg),
                 "3D tracer occupancy");
         // (more than a quarter more workgroups: at config 4 L3 the GH form's
         // 6 against the histogram's 5 measured 4 % slower -- a returnless
@@ -789,7 +790,7 @@ RTHX_EXPORT int rthx_trace_exchange_3d(rthx_scene3d* sc, const rthx_trace_args* 
       }
       L.ghist = sc->ghist_choice[slot_k] == 1;
     }
-    if (L.ghist) L.lds_bytes = rthx::trace3d_dynamic_lds(0, sc->S.stack);
+    if (L.ghist) L.lds_bytes = rthx::trace3d_dynamic_lds(0, sc->S.stack, sc->S.n_hull_lines);
     HIP_TRY(rthx::launch_trace3d(L), "trace_exchange_3d_kernel launch");
   }
   HIP_TRY(hipEventRecord(sc->ev[1], st), "hipEventRecord");

@@ -67,6 +67,8 @@ struct HullFace {
   float inv_du, inv_dv;      // nu / extent_u, nv / extent_v (first guess of the cell)
   float pad;
 };
+static_assert(sizeof(HullFace) == 48, "HullFace is 12 words");
+constexpr int kHullFaceWords = 6 * 12;  // the six face records, as the kernel stages them in LDS
 constexpr float kHullMargin = 1e-4f;  // candidate margin, relative to the box's largest extent
 constexpr float kHullMinDir = 1e-6f;  // smallest |direction component| the hull path takes
 
@@ -83,7 +85,7 @@ struct DevScene3D {
   int32_t hull;         // 1: box hull fast path (HullFace x 6)
   int32_t full_root;    // root node of the whole scene's BVH
   int32_t n_in_nodes;   // nodes of the interior BVH (0: no interior triangles)
-  int32_t pad0;
+  int32_t n_hull_lines; // lattice lines of all faces (staged in LDS behind the face records)
   double box_lo[3];     // box corner (hull coordinates are relative to it)
   float box_len[3];     // box extents
   float margin;         // kHullMargin x the largest extent
@@ -108,10 +110,12 @@ constexpr int kTopNodes = 128;
 // cache
 constexpr size_t kTrace3dStaticLds = 512 + 64 * 64;
 // dynamic LDS: the row histogram (`words` = N, or (N + 1) / 2 packed u16,
-// padded to 64), then the stacks
+// padded to 64), then the stacks, then (box hull) the face records and lines
 __host__ __device__ constexpr size_t trace3d_stack_offset(int64_t words) { return (size_t)((words + 63) & ~int64_t(63)); }
-__host__ __device__ constexpr size_t trace3d_dynamic_lds(int64_t words, int stack) {
-  return 4 * (trace3d_stack_offset(words) + (size_t)stack * kTrace3dThreads);
+// (box hull: the face records and lattice lines follow the stacks)
+__host__ __device__ constexpr size_t trace3d_dynamic_lds(int64_t words, int stack, int hull_lines = -1) {
+  return 4 * (trace3d_stack_offset(words) + (size_t)stack * kTrace3dThreads +
+              (hull_lines >= 0 ? (size_t)(kHullFaceWords + hull_lines) : 0));
 }
 
 struct Trace3dLaunch {

@@ -150,8 +150,14 @@ struct Walk {
   // the lattice cells within the margin of where the ray meets each face
   // plane it can reach, into best_*; false when the hull path does not
   // apply (a direction component below kHullMinDir) or no candidate is hit
-  // (the ray then walks the whole scene's BVH).
-  __device__ __forceinline__ bool hull_hit(const DevScene3D& S, int group) {
+  // (the ray then walks the whole scene's BVH).  Two passes: first the
+  // faces a lane's ray can meet (a bit mask, fp32, face constants only),
+  // then the candidate faces one at a time per lane -- each lane its own
+  // face, so the Moeller-Trumbore tests run for the whole wave at once
+  // rather than once per face.  Face records and lattice lines are read
+  // from LDS (hf, hl).
+  __device__ __forceinline__ bool hull_hit(const DevScene3D& S, int group, const HullFace RTHX_LDS* hf,
+                                           const float RTHX_LDS* hl) {
     // Per-axis values as separate registers: selects over array elements
     // were folded into a dynamic index, which put this Walk in scratch.
     float o0 = (float)(o[0] - S.box_lo[0]), o1 = (float)(o[1] - S.box_lo[1]), o2 = (float)(o[2] - S.box_lo[2]);
@@ -160,23 +166,34 @@ struct Walk {
     __asm__("" : "+v"(o0), "+v"(o1), "+v"(o2), "+v"(d0), "+v"(d1), "+v"(d2), "+v"(i0), "+v"(i1), "+v"(i2));
     if (!(fminf(fminf(fabsf(d0), fabsf(d1)), fabsf(d2)) >= kHullMinDir)) return false;
     const float m = S.margin;
-    // one loop body for the six faces (the unrolled form spilled ~100 VGPRs)
-#pragma nounroll
+    const float L0 = S.box_len[0], L1 = S.box_len[1], L2 = S.box_len[2];
+    uint32_t cand = 0;
+#pragma unroll
     for (int f = 0; f < 6; ++f) {
-      const HullFace RTHX_GLOBAL& F = S.faces[f];
-      if (F.group == group) continue;  // (the emitter's own face)
+      if (S.faces[f].group == group) continue;  // (the emitter's own face)
       const int k = f >> 1;  // axis; u = (k + 1) % 3, v = (k + 2) % 3
-      const bool a0 = k == 0, a1 = k == 1;
+      const float ok_ = k == 0 ? o0 : k == 1 ? o1 : o2, ik = k == 0 ? i0 : k == 1 ? i1 : i2;
+      const float plane = (f & 1) ? (k == 0 ? L0 : k == 1 ? L1 : L2) : 0.0f;
+      const float t = (plane - ok_) * ik;
+      const float tp = fmaxf(t, 0.0f);
+      const float pu = __builtin_fmaf(tp, k == 0 ? d1 : k == 1 ? d2 : d0, k == 0 ? o1 : k == 1 ? o2 : o0);
+      const float pv = __builtin_fmaf(tp, k == 0 ? d2 : k == 1 ? d0 : d1, k == 0 ? o2 : k == 1 ? o0 : o1);
+      const float lu = k == 0 ? L1 : k == 1 ? L2 : L0, lv = k == 0 ? L2 : k == 1 ? L0 : L1;
+      // (t below -m: the plane lies behind the ray by more than the margin; NaN fails too)
+      if (t >= -m && pu >= -m && pu <= lu + m && pv >= -m && pv <= lv + m) cand |= 1u << f;
+    }
+    while (cand) {
+      const int f = __builtin_ctz(cand);
+      cand &= cand - 1u;
+      const HullFace RTHX_LDS& F = hf[f];
+      const bool a0 = F.axis == 0, a1 = F.axis == 1;
       const float t = (F.plane - (a0 ? o0 : a1 ? o1 : o2)) * (a0 ? i0 : a1 ? i1 : i2);
-      if (!(t >= -m)) continue;  // behind the ray by more than the margin (or NaN)
       const float tp = fmaxf(t, 0.0f);
       const float pu = __builtin_fmaf(tp, a0 ? d1 : a1 ? d2 : d0, a0 ? o1 : a1 ? o2 : o0);
       const float pv = __builtin_fmaf(tp, a0 ? d2 : a1 ? d0 : d1, a0 ? o2 : a1 ? o0 : o1);
-      const float lu = S.box_len[a0 ? 1 : a1 ? 2 : 0], lv = S.box_len[a0 ? 2 : a1 ? 0 : 1];
-      if (!(pu >= -m && pu <= lu + m && pv >= -m && pv <= lv + m)) continue;
       int c0, c1, r0, r1;
-      cell_range(S.hull_lines + F.lu, F.nu, F.inv_du, pu, m, c0, c1);
-      cell_range(S.hull_lines + F.lv, F.nv, F.inv_dv, pv, m, r0, r1);
+      cell_range(hl + F.lu, F.nu, F.inv_du, pu, m, c0, c1);
+      cell_range(hl + F.lv, F.nv, F.inv_dv, pv, m, r0, r1);
       for (int j = r0; j <= r1; ++j)
         for (int i = c0; i <= c1; ++i) {
           const int c = F.cell0 + j * F.nu + i;
@@ -189,7 +206,7 @@ struct Walk {
 
   // Lattice cells [lo, hi] of the lines [0, n] within margin m of p
   // (first guess from the uniform spacing, then corrected).
-  static __device__ __forceinline__ void cell_range(const float RTHX_GLOBAL* L, int n, float inv, float p, float m,
+  static __device__ __forceinline__ void cell_range(const float RTHX_LDS* L, int n, float inv, float p, float m,
                                                     int& lo, int& hi) {
     int i = (int)(p * inv);
     i = i < 0 ? 0 : i > n - 1 ? n - 1 : i;
@@ -352,6 +369,17 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(HULL ?
   // the emitter's coplanar group: its triangles are skipped, its subtrees pruned
   const int grp = s_emit.group, glo = s_emit.glo, glen = s_emit.ghi - s_emit.glo;
   int RTHX_LDS* stk = (int RTHX_LDS*)(hist + trace3d_stack_offset(words)) + tid;
+  // HULL: the six face records and the lattice lines behind the stacks
+  uint32_t RTHX_LDS* hull_lds = (uint32_t RTHX_LDS*)(hist + trace3d_stack_offset(words) + (size_t)S.stack * kThreads);
+  const HullFace RTHX_LDS* hf = (const HullFace RTHX_LDS*)hull_lds;
+  const float RTHX_LDS* hl = (const float RTHX_LDS*)(hull_lds + kHullFaceWords);
+  if (HULL) {
+    const uint32_t RTHX_GLOBAL* fsrc = (const uint32_t RTHX_GLOBAL*)S.faces;
+    const uint32_t RTHX_GLOBAL* lsrc = (const uint32_t RTHX_GLOBAL*)S.hull_lines;
+    for (int i = tid; i < kHullFaceWords + S.n_hull_lines; i += kThreads)
+      hull_lds[i] = i < kHullFaceWords ? fsrc[i] : lsrc[i - kHullFaceWords];
+    __syncthreads();
+  }
   auto tally = [&](int a) {
     if (a >= 0) {
       if (GH)
@@ -381,7 +409,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(HULL ?
                              o, d);
           w.init(o, d);
           if (HULL)
-            w.node = w.hull_hit(S, grp) ? (S.n_in_nodes > 0 ? 0 : kWalkDone) : S.full_root;
+            w.node = w.hull_hit(S, grp, hf, hl) ? (S.n_in_nodes > 0 ? 0 : kWalkDone) : S.full_root;
           live = true;
         }
       }
@@ -400,7 +428,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(HULL ?
                        P.key1, o, d);
     Walk w;
     w.init(o, d);
-    if (HULL) w.node = w.hull_hit(S, grp) ? (S.n_in_nodes > 0 ? 0 : kWalkDone) : S.full_root;
+    if (HULL) w.node = w.hull_hit(S, grp, hf, hl) ? (S.n_in_nodes > 0 ? 0 : kWalkDone) : S.full_root;
     while (w.step(S, topo, n_top, grp, glo, glen, stk)) {
     }
     tally(w.best_poly);
