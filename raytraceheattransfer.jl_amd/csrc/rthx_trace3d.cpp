@@ -586,6 +586,41 @@ RTHX_EXPORT int rthx_scene3d_create_grouped(const double* xyz, const int32_t* nv
     }
     n_in_tris = (int64_t)all_tris.size();
     n_in_nodes = (int32_t)nodes_in.size();
+    // Is the interior one convex set, seen from the sides its rays leave?
+    // Every interior vertex must lie on or behind every interior polygon's
+    // emitting plane (within 1e-12 of the scene scale).  Then a ray leaving
+    // an interior polygon away from its edges meets no interior triangle:
+    // the points it reaches are beyond that plane, and every other interior
+    // triangle is behind it but for the edges and vertices it shares
+    // (DESIGN.md §7e).
+    if (!bt_in.empty()) {
+      std::vector<V> verts;
+      for (int64_t k = 0; k < n; ++k)
+        if (!hb.in_hull[(size_t)k])
+          for (int i = 0; i < polys[(size_t)k].nv; ++i)
+            verts.push_back({polys[(size_t)k].v[i][0], polys[(size_t)k].v[i][1], polys[(size_t)k].v[i][2]});
+      std::sort(verts.begin(), verts.end(), [](const V& a, const V& b) {
+        return a.x < b.x || (a.x == b.x && (a.y < b.y || (a.y == b.y && a.z < b.z)));
+      });
+      verts.erase(std::unique(verts.begin(), verts.end(),
+                              [](const V& a, const V& b) { return a.x == b.x && a.y == b.y && a.z == b.z; }),
+                  verts.end());
+      const double tol = 1e-12 * scale;
+      bool convex = true;
+      for (int64_t k = 0; k < n && convex; ++k) {
+        if (hb.in_hull[(size_t)k]) continue;
+        const rthx::Emit3& E = polys[(size_t)k];
+        const V nn{E.n[0], E.n[1], E.n[2]}, p0{E.v[0][0], E.v[0][1], E.v[0][2]};
+        for (const V& q : verts)
+          if (dot(nn, sub(q, p0)) > tol) {
+            convex = false;
+            break;
+          }
+      }
+      if (convex)
+        for (int64_t k = 0; k < n; ++k)
+          if (!hb.in_hull[(size_t)k]) polys[(size_t)k].convex = 1;
+    }
     full_root = n_in_nodes;
     shift_bvh(nodes, full_root, (int32_t)n_in_tris);
     nodes_in.insert(nodes_in.end(), nodes.begin(), nodes.end());

@@ -19,7 +19,20 @@ struct alignas(16) Emit3 {
   int32_t nv;
   int32_t group;      // coplanar group (rthx_scene3d_create_grouped): rays never hit their own group
   int32_t glo, ghi;   // the group's polygons are [glo, ghi) (one contiguous run)
+  // 1: a polygon of a box-hull scene's interior, and the interior triangles
+  // form one convex set seen from the sides rays leave (every interior
+  // vertex on or behind every interior emitting plane).  A ray that leaves
+  // such a polygon away from its edges cannot meet another interior
+  // triangle, so after its hull hit it walks nothing (rthx_trace3d_kernels.hip).
+  int32_t convex;
+  int32_t pad0, pad1, pad2;
 };
+static_assert(sizeof(Emit3) == 208, "Emit3 layout");
+// A ray leaving a convex interior polygon skips the interior walk only when
+// its emission point lies at least this barycentric weight inside the
+// emitting triangle and its direction this far off the polygon's plane.
+constexpr double kConvexMinWeight = 1e-6;
+constexpr double kConvexMinCos = 1e-6;
 
 // Triangle for the Moeller-Trumbore test: v0, e1 = v1 - v0, e2 = v2 - v0.
 struct alignas(16) Tri3 {

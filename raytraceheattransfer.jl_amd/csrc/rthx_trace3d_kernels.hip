@@ -273,9 +273,11 @@ struct Walk {
 
 // Emission of ray (g, r): a uniform point on the polygon and a cosine-law
 // direction about its normal.
+// deep: the point lies at least kConvexMinWeight (barycentric) inside its
+// triangle and the direction at least kConvexMinCos off the plane (Emit3::convex).
 template <bool FAITHFUL>
 __device__ __forceinline__ void emit_ray(const Emit3& E, const double* tab, uint32_t g, uint32_t r, uint32_t k0,
-                                         uint32_t k1, double* o, double* d) {
+                                         uint32_t k1, double* o, double* d, bool& deep) {
   const RayDraws rd(r, g, 0u, kTrace3dTag, k0, k1);
   const double R1 = rd.R1(), R2 = rd.R2();
   const double s1 = sqrt(R1);
@@ -290,6 +292,7 @@ __device__ __forceinline__ void emit_ray(const Emit3& E, const double* tab, uint
   for (int k = 0; k < 3; ++k) o[k] = wa * E.v[ia][k] + wb * E.v[ib][k] + wc * E.v[ic][k];
   const double u3 = rd.path();
   const double st = sqrt(u3), ct = sqrt(1.0 - u3);
+  deep = fmin(fmin(wa, wb), wc) >= kConvexMinWeight && ct >= kConvexMinCos;
   const uint32_t w = rd.c[3];
   double cphi, sphi;
   if (FAITHFUL) {
@@ -368,6 +371,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(HULL ?
   uint32_t tallied = 0;
   // the emitter's coplanar group: its triangles are skipped, its subtrees pruned
   const int grp = s_emit.group, glo = s_emit.glo, glen = s_emit.ghi - s_emit.glo;
+  const bool convex = HULL && s_emit.convex != 0;
   int RTHX_LDS* stk = (int RTHX_LDS*)(hist + trace3d_stack_offset(words)) + tid;
   // HULL: the six face records and the lattice lines behind the stacks
   uint32_t RTHX_LDS* hull_lds = (uint32_t RTHX_LDS*)(hist + trace3d_stack_offset(words) + (size_t)S.stack * kThreads);
@@ -405,11 +409,13 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(HULL ?
         if (r < (uint32_t)r_end) {
           const Emit3 RTHX_LDS* em = lds_opaque(&s_emit);
           double o[3], d[3];
+          bool deep;
           emit_ray<FAITHFUL>(*(const Emit3*)em, s_tab, (uint32_t)g, r, P.key0, P.key1,
-                             o, d);
+                             o, d, deep);
           w.init(o, d);
-          if (HULL)
-            w.node = w.hull_hit(S, grp, hf, hl) ? (S.n_in_nodes > 0 ? 0 : kWalkDone) : S.full_root;
+          if (HULL)  // (a convex interior emitter's deep ray meets no interior triangle: no walk)
+            w.node = w.hull_hit(S, grp, hf, hl) ? (S.n_in_nodes > 0 && !(convex && deep) ? 0 : kWalkDone)
+                                                : S.full_root;
           live = true;
         }
       }
@@ -424,11 +430,13 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(HULL ?
   for (int64_t r = r_begin + tid; r < r_end; r += kThreads) {
     const Emit3 RTHX_LDS* em = lds_opaque(&s_emit);
     double o[3], d[3];
+    bool deep;
     emit_ray<FAITHFUL>(*(const Emit3*)em, s_tab, (uint32_t)g, (uint32_t)r, P.key0,
-                       P.key1, o, d);
+                       P.key1, o, d, deep);
     Walk w;
     w.init(o, d);
-    if (HULL) w.node = w.hull_hit(S, grp, hf, hl) ? (S.n_in_nodes > 0 ? 0 : kWalkDone) : S.full_root;
+    if (HULL)
+      w.node = w.hull_hit(S, grp, hf, hl) ? (S.n_in_nodes > 0 && !(convex && deep) ? 0 : kWalkDone) : S.full_root;
     while (w.step(S, topo, n_top, grp, glo, glen, stk)) {
     }
     tally(w.best_poly);
