@@ -504,10 +504,13 @@ int rthx_scene3d_stats(const rthx_scene3d* scene, int64_t* n_tri, int64_t* n_nod
                        int64_t* lds_bytes);
 /* Box hull of a grouped scene (any pointer may be NULL): *hull = 1 when six
  * of its coplanar groups are the faces of its bounding box, each a lattice of
- * quads (rthx_trace3d.h HullFace).  Their hull hits are then found from the
- * lattice (the same Moeller-Trumbore test on the candidate cells) and the BVH
- * walk covers the other -- interior -- triangles only; the counts are those
- * of the plain walk.  hull_tris / interior_tris: the triangles of each kind. */
+ * quads (rthx_trace3d.h HullFace), 2 when in addition the other (interior)
+ * triangles form one convex set seen from the sides their rays leave.  Hull
+ * hits are then found from the lattice (the same Moeller-Trumbore test on the
+ * candidate cells), the BVH walk covers the interior triangles only, and
+ * with 2 a ray leaving an interior polygon away from its edges walks nothing;
+ * the counts are those of the plain walk.  hull_tris / interior_tris: the
+ * triangles of each kind. */
 int rthx_scene3d_hull(const rthx_scene3d* scene, int32_t* hull, int64_t* hull_tris, int64_t* interior_tris);
 int rthx_trace_exchange_3d(rthx_scene3d* scene, const rthx_trace_args* args, rthx_result* res);
 

@@ -41,6 +41,7 @@ struct rthx_scene3d {
   rthx::DevScene3D S{};
   int64_t n_poly = 0;
   int64_t n_hull_tris = 0, n_in_tris = 0;  // box hull: hull / interior triangles
+  bool convex_interior = false;             // box hull: the interior is one convex set (Emit3::convex)
   int top_choice[16] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};  // LDS node-cache size per kernel variant (launch_trace3d)
   int ghist_choice[4] = {-1, -1, -1, -1};  // per (faithful, pack16, N, R): global-histogram form chosen (1) or not (0)
   int64_t ghist_key[4] = {-1, -1, -1, -1};
@@ -641,6 +642,7 @@ RTHX_EXPORT int rthx_scene3d_create_grouped(const double* xyz, const int32_t* nv
   s->device = device;
   s->n_poly = n;
   s->n_hull_tris = (int64_t)hull_tris.size();
+  s->convex_interior = hull && n_in_tris > 0 && polys[(size_t)(n - 1)].convex == 1;
   s->n_in_tris = n_in_tris;
   auto bail = [&](int code) {
     delete s;
@@ -704,7 +706,7 @@ RTHX_EXPORT int rthx_scene3d_stats(const rthx_scene3d* sc, int64_t* n_tri, int64
 
 RTHX_EXPORT int rthx_scene3d_hull(const rthx_scene3d* sc, int32_t* hull, int64_t* hull_tris, int64_t* interior_tris) {
   if (!sc) return fail(RTHX_EINVAL, "null scene");
-  if (hull) *hull = sc->S.hull;
+  if (hull) *hull = sc->S.hull ? (sc->convex_interior ? 2 : 1) : 0;
   if (hull_tris) *hull_tris = sc->n_hull_tris;
   if (interior_tris) *interior_tris = sc->n_in_tris;
   return RTHX_OK;

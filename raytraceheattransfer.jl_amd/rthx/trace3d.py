@@ -74,7 +74,7 @@ class Scene3D:
         if hasattr(self._lib, "rthx_scene3d_hull"):  # rthx_scene3d_hull: the box-hull fast path
             h, ht, it = C.c_int32(), C.c_int64(), C.c_int64()
             check(self._lib.rthx_scene3d_hull(self.handle, C.byref(h), C.byref(ht), C.byref(it)))
-            out.update(hull=bool(h.value), hull_tris=ht.value, interior_tris=it.value)
+            out.update(hull=h.value > 0, convex_interior=h.value == 2, hull_tris=ht.value, interior_tris=it.value)
         return out
 
     def close(self) -> None:

@@ -579,15 +579,15 @@ def view_factor_quadrature(tri_a, n_a, tri_b, n_b, levels=3):
     return float(wa @ k @ wb / wa.sum())
 
 
-def box_scene(lines, level=None, radius=0.25, center=None, perturb=0.0, seed=0):
+def box_scene(lines, level=None, radius=0.25, center=None, perturb=0.0, seed=0, spheres=None):
     """A closed box whose six faces are lattices of quads over the given
     lattice lines (lines[k]: sorted coordinates along axis k, first and last
     = the box), every face one coplanar group (rays leave inward), optionally
     an icosphere of `level` inside (each triangle its own group, rays leave
     outward).  `perturb` moves the interior lattice lines by up to that
-    fraction of a cell (a non-uniform lattice).  Returns (xyz, nv, normals,
-    groups, n_hull_polygons); faces in the order of rthx_trace3d's hull
-    detection does not matter."""
+    fraction of a cell (a non-uniform lattice); `spheres`: more icospheres,
+    (level, radius, centre) each.  Returns (xyz, nv, normals, groups,
+    n_hull_polygons)."""
     rng = np.random.default_rng(seed)
     L = [np.array(l, dtype=np.float64) for l in lines]
     if perturb:
@@ -617,13 +617,15 @@ def box_scene(lines, level=None, radius=0.25, center=None, perturb=0.0, seed=0):
                     groups.append(gid)
             gid += 1
     n_hull = len(polys)
-    if level is not None:
-        for tri in icosphere(level, radius, c):
+    objs = list(spheres or []) + ([(level, radius, c)] if level is not None else [])
+    for lvl, rad, cen in objs:
+        cen = np.asarray(cen, dtype=np.float64)
+        for tri in icosphere(lvl, rad, cen):
             q = np.zeros((4, 3))
             q[:3] = tri
             q[3] = tri[2]
             polys.append(q)
-            normals.append(tri.mean(axis=0) - c)
+            normals.append(tri.mean(axis=0) - cen)
             groups.append(gid)
             gid += 1
     nv = np.array([4] * n_hull + [3] * (len(polys) - n_hull), dtype=np.int32)

@@ -261,13 +261,14 @@ def test_box_hull_exact(hip, monkeypatch, ndim, level, faithful):
     g = H.cube_icosphere_groups(ndim, level)
     D, info, st = _hull_dense(xyz, nv, nrm, 4000, 14, g, monkeypatch, faithful=faithful)
     assert st["hull"] and st["hull_tris"] == 12 * ndim * ndim and st["interior_tris"] == 20 * 4 ** level
+    assert st["convex_interior"]  # (one sphere: its deep rays walk nothing after the hull hit)
     C, lost = oracle.trace_exchange_3d(xyz, nv, nrm, 4000, seed=14, nthreads=16, groups=g)
     assert np.array_equal(D, C) and info["lost_total"] == lost
     D0, info0, st0 = _hull_dense(xyz, nv, nrm, 4000, 14, g, monkeypatch, no_hull=True, faithful=faithful)
     assert not st0["hull"] and np.array_equal(D, D0)
 
 
-@pytest.mark.parametrize("case", ["nonuniform", "empty", "far", "flat"])
+@pytest.mark.parametrize("case", ["nonuniform", "empty", "far", "flat", "two_spheres", "concave"])
 def test_box_hull_scenes_exact(hip, monkeypatch, case):
     """Hull scenes beyond config 4: perturbed (non-uniform) lattices with
     different cell counts per axis around an icosphere; a box with nothing
@@ -281,14 +282,21 @@ def test_box_hull_scenes_exact(hip, monkeypatch, case):
     elif case == "far":
         xyz, nv, nrm, g, nh = H.box_scene([np.linspace(0, 1, 5)] * 3, level=1, radius=0.3)
         xyz = np.ascontiguousarray(xyz * 1e-3 + np.array([250.0, -1000.0, 37.5]))
-    else:
+    elif case == "flat":
         lines = [np.linspace(0, 10, 21), np.linspace(0, 1, 3), np.linspace(0, 0.2, 2)]
         xyz, nv, nrm, g, nh = H.box_scene(lines, level=1, radius=0.08)
+    elif case == "two_spheres":  # (not one convex set: the interior walk runs for every ray)
+        xyz, nv, nrm, g, nh = H.box_scene([np.linspace(0, 2, 9), np.linspace(0, 1, 5), np.linspace(0, 1, 5)],
+                                          spheres=[(2, 0.3, (0.5, 0.5, 0.5)), (1, 0.25, (1.45, 0.5, 0.55))])
+    else:  # a sphere seen from inside (rays leave inward): concave, not convex
+        xyz, nv, nrm, g, nh = H.box_scene([np.linspace(0, 1, 4)] * 3, level=1, radius=0.4)
+        nrm[nh:] = -nrm[nh:]
     D, info, st = _hull_dense(xyz, nv, nrm, 3000, 15, g, monkeypatch)
     assert st["hull"] and st["hull_tris"] == 2 * nh
+    assert st["convex_interior"] == (case in ("nonuniform", "far", "flat"))
     C, lost = oracle.trace_exchange_3d(xyz, nv, nrm, 3000, seed=15, nthreads=16, groups=g)
     assert np.array_equal(D, C) and info["lost_total"] == lost
-    assert lost == 0
+    assert lost == 0 or case == "concave"
 
 
 def test_box_hull_not_taken(hip, monkeypatch):
