@@ -61,7 +61,11 @@ __device__ __forceinline__ void cross3(const double* a, const double* b, double*
 // deferred, as in the paper's culling branch: U = s.p, V = d.q, T = e2.q are
 // compared against det (signs normalised to det > 0) and t = T / det is
 // formed only for a hit.  Returns t, or -1 for a miss.
-__device__ __forceinline__ double moller_trumbore(const Tri3& T, const double* o, const double* d) {
+// deep (optional): set when the hit lies at least 1 % of the triangle's
+// barycentric range from its edge v0-v2 (U >= det / 100): a quad's other
+// triangle, across that diagonal, cannot then be hit (Walk::hull_hit).
+__device__ __forceinline__ double moller_trumbore(const Tri3& T, const double* o, const double* d,
+                                                  bool* deep = nullptr) {
   double p[3], q[3], s[3];
   cross3(d, T.e2, p);
   double det = dot3(T.e1, p);
@@ -78,6 +82,7 @@ __device__ __forceinline__ double moller_trumbore(const Tri3& T, const double* o
     W = -W;
   }
   if (!(det > 0.0) || !(U >= 0.0) || !(V >= 0.0) || !(U + V <= det) || !(W > 0.0)) return -1.0;
+  if (deep) *deep = U >= 0.01 * det;
   return W / det;
 }
 
@@ -136,8 +141,10 @@ struct Walk {
     }
   }
 
-  __device__ __forceinline__ void consider(const Tri3& T) {
-    const double t = moller_trumbore(T, o, d);
+  // (deep: as moller_trumbore's, false on a miss)
+  __device__ __forceinline__ void consider(const Tri3& T, bool* deep = nullptr) {
+    if (deep) *deep = false;
+    const double t = moller_trumbore(T, o, d, deep);
     if (t > 0.0 && (t < best_t || (t == best_t && T.id < best_id))) {
       best_t = t;
       best_id = T.id;
@@ -194,11 +201,21 @@ struct Walk {
       int c0, c1, r0, r1;
       cell_range(hl + F.lu, F.nu, F.inv_du, pu, m, c0, c1);
       cell_range(hl + F.lv, F.nv, F.inv_dv, pv, m, r0, r1);
+      // A quad cell's triangles (v0 v1 v2), (v2 v3 v0) share the diagonal
+      // v0-v2.  A hit well inside the first (deep: 1 % of its barycentric
+      // range from that edge, which is far more than the quad's 1e-12
+      // non-planarity can move a hit point, given kHullMinDir) rules out the
+      // second, so a lone candidate cell tests it only when needed.
+      const bool one = (c0 == c1) & (r0 == r1);
       for (int j = r0; j <= r1; ++j)
         for (int i = c0; i <= c1; ++i) {
           const int c = F.cell0 + j * F.nu + i;
 #pragma nounroll
-          for (int h = 0; h < 2; ++h) consider(S.hull_tris[2 * c + h]);
+          for (int h = 0; h < 2; ++h) {
+            bool deep_h;
+            consider(S.hull_tris[2 * c + h], &deep_h);
+            if (one & deep_h) break;  // (h = 0: the second cannot be hit; h = 1: the last anyway)
+          }
         }
     }
     return best_poly >= 0;
