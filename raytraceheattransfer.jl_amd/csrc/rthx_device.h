@@ -193,14 +193,15 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);  // gfx950 v_bitop3_b32: a ^ b ^ c
 }
 
-__device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
+template <int ROUNDS = 10>
+__device__ __forceinline__ void philox4x32(uint32_t c[4], uint32_t k0, uint32_t k1) {
 #if RTHX_PHILOX_OPAQUE_KEY
   // Opaque key: the 20 round keys are formed in each block (scalar adds)
   // instead of being hoisted into 20 SGPRs held across the whole ray loop.
   __asm__ volatile("" : "+s"(k0), "+s"(k1));
 #endif
 #pragma unroll
-  for (int i = 0; i < 10; ++i) {
+  for (int i = 0; i < ROUNDS; ++i) {
     // one 32x32->64 multiply per product (v_mad_u64_u32) instead of mul_lo + mul_hi
     uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
     uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
@@ -211,6 +212,11 @@ __device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32
     k1 += 0xBB67AE85u;
   }
 }
+__device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) { philox4x32<10>(c, k0, k1); }
+// Rounds of the 2D emission words (philox_words; A/B builds only)
+#ifndef RTHX_PHILOX_ROUNDS
+#define RTHX_PHILOX_ROUNDS 10
+#endif
 
 // Uniform in [0, 1) with 52 random bits, built like Julia's rand(): the top
 // 52 bits of (hi:lo) as the mantissa of a double in [1, 2), minus 1.
@@ -266,7 +272,7 @@ struct RayWords {
 __device__ __forceinline__ void philox_words(uint32_t w0, uint32_t w1, uint32_t blk, uint32_t w3, uint32_t k0,
                                              uint32_t k1, uint32_t out[4]) {
   out[0] = w0; out[1] = w1; out[2] = blk; out[3] = w3;
-  philox4x32_10(out, k0, k1);
+  philox4x32<RTHX_PHILOX_ROUNDS>(out, k0, k1);
 }
 
 #define RTHX_TWO_PI 6.283185307179586
