@@ -559,6 +559,7 @@ RTHX_EXPORT int rthx_scene3d_create_grouped(const double* xyz, const int32_t* nv
   // Box hull: the interior triangles' BVH first (its top is what the kernel
   // caches in LDS), the whole scene's appended as the fallback walk.
   HullBuild hb;
+  double ball[4] = {0.0, 0.0, 0.0, 0.0};
   const char* no_hull = rthx::knob("RTHX_T3_NO_HULL");
   const bool hull = group && !(no_hull && no_hull[0] == '1') && detect_box_hull(polys, n, slo, shi, hb);
   std::vector<rthx::Tri3> hull_tris;
@@ -621,6 +622,19 @@ RTHX_EXPORT int rthx_scene3d_create_grouped(const double* xyz, const int32_t* nv
       if (convex)
         for (int64_t k = 0; k < n; ++k)
           if (!hb.in_hull[(size_t)k]) polys[(size_t)k].convex = 1;
+      // the interior's bounding ball: centre the vertices' mean, radius the
+      // farthest vertex, padded by 1e-9 relative plus 1e-12 of the scene
+      // (every interior triangle lies within it: convex combinations)
+      V cen{0.0, 0.0, 0.0};
+      for (const V& q : verts) cen = {cen.x + q.x, cen.y + q.y, cen.z + q.z};
+      const double inv_nv = 1.0 / (double)verts.size();
+      cen = {cen.x * inv_nv, cen.y * inv_nv, cen.z * inv_nv};
+      double r = 0.0;
+      for (const V& q : verts) r = std::max(r, norm(sub(q, cen)));
+      ball[0] = cen.x;
+      ball[1] = cen.y;
+      ball[2] = cen.z;
+      ball[3] = r * (1.0 + 1e-9) + 1e-12 * scale;
     }
     full_root = n_in_nodes;
     shift_bvh(nodes, full_root, (int32_t)n_in_tris);
@@ -681,6 +695,7 @@ RTHX_EXPORT int rthx_scene3d_create_grouped(const double* xyz, const int32_t* nv
     s->S.box_len[k] = (float)(shi[k] - slo[k]);
   }
   s->S.margin = (float)hb.margin;
+  for (int k = 0; k < 4; ++k) s->S.ball[k] = ball[k];
   s->S.faces = hull ? s->faces.as<rthx::HullFace>() : nullptr;
   s->S.hull_lines = hull ? s->lines.as<float>() : nullptr;
   s->S.hull_tris = hull ? s->hull_tris.as<rthx::Tri3>() : nullptr;

@@ -100,6 +100,8 @@ struct DevScene3D {
   int32_t n_in_nodes;   // nodes of the interior BVH (0: no interior triangles)
   int32_t n_hull_lines; // lattice lines of all faces (staged in LDS behind the face records)
   double box_lo[3];     // box corner (hull coordinates are relative to it)
+  double ball[4];       // box hull: a ball (centre, radius) around every interior triangle, padded
+                        // (radius 0: no interior); a ray that misses it meets no interior triangle
   float box_len[3];     // box extents
   float margin;         // kHullMargin x the largest extent
   const HullFace RTHX_GLOBAL* faces;       // [6]

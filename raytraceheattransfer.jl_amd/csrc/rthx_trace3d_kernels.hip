@@ -221,6 +221,19 @@ struct Walk {
     return best_poly >= 0;
   }
 
+  // Does the ray (t > 0) pass through the interior's bounding ball?  (The
+  // ball's radius carries a relative pad of 1e-9, far above this test's
+  // rounding: a ray that misses it by rounding cannot reach an interior
+  // triangle, which lies within the unpadded ball.)
+  __device__ __forceinline__ bool meets_ball(const DevScene3D& S) const {
+    const double q0 = o[0] - S.ball[0], q1 = o[1] - S.ball[1], q2 = o[2] - S.ball[2];
+    const double b = __builtin_fma(q0, d[0], __builtin_fma(q1, d[1], q2 * d[2]));        // q . d
+    const double c = __builtin_fma(q0, q0, __builtin_fma(q1, q1, q2 * q2)) - S.ball[3] * S.ball[3];
+    // roots of t^2 + 2 b t + c (|d| = 1): some t > 0 inside the ball iff
+    // c < 0 (the origin inside) or b < 0 with b^2 > c
+    return c < 0.0 || (b < 0.0 && b * b > c);
+  }
+
   // Lattice cells [lo, hi] of the lines [0, n] within margin m of p
   // (first guess from the uniform spacing, then corrected).
   static __device__ __forceinline__ void cell_range(const float RTHX_LDS* L, int n, float inv, float p, float m,
@@ -430,9 +443,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(HULL ?
           emit_ray<FAITHFUL>(*(const Emit3*)em, s_tab, (uint32_t)g, r, P.key0, P.key1,
                              o, d, deep);
           w.init(o, d);
-          if (HULL)  // (a convex interior emitter's deep ray meets no interior triangle: no walk)
-            w.node = w.hull_hit(S, grp, hf, hl) ? (S.n_in_nodes > 0 && !(convex && deep) ? 0 : kWalkDone)
-                                                : S.full_root;
+          if (HULL)  // (a convex interior emitter's deep ray, or one that misses the interior's ball, meets no interior triangle: no walk)
+            w.node = w.hull_hit(S, grp, hf, hl)
+                         ? (S.n_in_nodes > 0 && !(convex && deep) && w.meets_ball(S) ? 0 : kWalkDone)
+                         : S.full_root;
           live = true;
         }
       }
@@ -453,7 +467,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(HULL ?
     Walk w;
     w.init(o, d);
     if (HULL)
-      w.node = w.hull_hit(S, grp, hf, hl) ? (S.n_in_nodes > 0 && !(convex && deep) ? 0 : kWalkDone) : S.full_root;
+      w.node = w.hull_hit(S, grp, hf, hl)
+                   ? (S.n_in_nodes > 0 && !(convex && deep) && w.meets_ball(S) ? 0 : kWalkDone)
+                   : S.full_root;
     while (w.step(S, topo, n_top, grp, glo, glen, stk)) {
     }
     tally(w.best_poly);
