@@ -39,6 +39,8 @@ def load() -> C.CDLL:
     lib = C.CDLL(LIB_PATH)
     lib.oracle_philox4x32_10.argtypes = [C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
     lib.oracle_philox4x32_10.restype = None
+    lib.oracle_philox4x32_emit.argtypes = lib.oracle_philox4x32_10.argtypes
+    lib.oracle_philox4x32_emit.restype = None
     lib.oracle_ray_draws.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(C.c_double)]
     lib.oracle_ray_draws.restype = None
     lib.oracle_trace_exchange.argtypes = [C.POINTER(abi.DomainDesc), C.POINTER(abi.TraceArgs), C.c_int,
@@ -69,12 +71,13 @@ def load() -> C.CDLL:
     return lib
 
 
-def philox(ctr, key):
+def philox(ctr, key, emit=False):
+    """Philox-4x32-10 block (emit: the 2D emission words' 7-round block)."""
     lib = load()
     c = (C.c_uint32 * 4)(*ctr)
     k = (C.c_uint32 * 2)(*key)
     o = (C.c_uint32 * 4)()
-    lib.oracle_philox4x32_10(c, k, o)
+    (lib.oracle_philox4x32_emit if emit else lib.oracle_philox4x32_10)(c, k, o)
     return list(o)
 
 

@@ -39,7 +39,10 @@
 #define ORACLE_API __attribute__((visibility("default")))
 
 /* ------------------------------------------------------------------------ */
-/* Philox-4x32-10 (Salmon et al., SC'11; Random123 reference constants).     */
+/* Philox-4x32 (Salmon et al., SC'11; Random123 reference constants): 10      */
+/* rounds for the 3D tracer and the direct method, 7 for the 2D exchange     */
+/* tracer's emission words (ray_words; DESIGN.md §5 "Random numbers").  The  */
+/* round function is pinned by the Random123 10-round known answers.        */
 /* The Julia reference uses the unseeded task-local Xoshiro `rand()`         */
 /* (traceRay.jl:25, emitSurfaceRay2D.jl:5 ...), which no test pins.          */
 /* ------------------------------------------------------------------------ */
@@ -47,12 +50,12 @@
 #define PHILOX_M1 0xCD9E8D57u
 #define PHILOX_W0 0x9E3779B9u
 #define PHILOX_W1 0xBB67AE85u
+#define EMIT_ROUNDS 7 /* the device's RTHX_PHILOX_ROUNDS (csrc/rthx_device.h) */
 
-ORACLE_API void oracle_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2],
-                                     uint32_t out[4]) {
+static void philox4x32(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4], int rounds) {
   uint32_t c0 = ctr[0], c1 = ctr[1], c2 = ctr[2], c3 = ctr[3];
   uint32_t k0 = key[0], k1 = key[1];
-  for (int round = 0; round < 10; ++round) {
+  for (int round = 0; round < rounds; ++round) {
     uint64_t p0 = (uint64_t)PHILOX_M0 * c0;
     uint64_t p1 = (uint64_t)PHILOX_M1 * c2;
     uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
@@ -64,6 +67,15 @@ ORACLE_API void oracle_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2
     k1 += PHILOX_W1;
   }
   out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+ORACLE_API void oracle_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
+  philox4x32(ctr, key, out, 10);
+}
+
+/* The emission words' block function (EMIT_ROUNDS rounds). */
+ORACLE_API void oracle_philox4x32_emit(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
+  philox4x32(ctr, key, out, EMIT_ROUNDS);
 }
 
 /* Uniform in [0, 1) with 52 random bits, built like Julia's rand() (a
@@ -87,7 +99,8 @@ static inline double u32(uint32_t w) { return (double)w * 0x1.0p-32; }
  *   volume emitter:  u1 = u32(a0), u2 = u32(a1), theta draw u32(a2), phi
  *                    draw u32(a3), free path u32(pw), quad triangle
  *                    selection u32(sw)
- * 32 random bits per draw.  Exchange ray (g, r) in bin b: a = Philox(r, g,
+ * 32 random bits per draw, from Philox-4x32-7 blocks (emit_words).  Exchange
+ * ray (g, r) in bin b: a = Philox(r, g,
  * 0, b), pw = word r & 3 of Philox(r >> 2, g, 1, b) (one block for four
  * consecutive rays), sw = word 0 of Philox(r, g, 2, b), drawn only by quads
  * that are not axis-aligned rectangles (and by every quad in faithful
@@ -103,16 +116,23 @@ static void block_words(uint64_t seed, uint32_t w0, uint32_t w1, uint32_t blk, u
   oracle_philox4x32_10(ctr, key, out);
 }
 
+/* A block of the exchange tracer's emission words (EMIT_ROUNDS rounds). */
+static void emit_words(uint64_t seed, uint32_t w0, uint32_t w1, uint32_t blk, uint32_t w3, uint32_t out[4]) {
+  uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+  uint32_t ctr[4] = {w0, w1, blk, w3};
+  oracle_philox4x32_emit(ctr, key, out);
+}
+
 static void ray_words(uint64_t seed, uint32_t bin, uint32_t g, uint32_t r, int volume, int need_sel, words_t* w) {
-  block_words(seed, r, g, 0u, bin, w->a);
+  emit_words(seed, r, g, 0u, bin, w->a);
   w->pw = w->sw = 0u;
   if (volume) {
     uint32_t b[4];
-    block_words(seed, r >> 2, g, 1u, bin, b);
+    emit_words(seed, r >> 2, g, 1u, bin, b);
     w->pw = b[r & 3u];
     if (need_sel) {
       uint32_t c[4];
-      block_words(seed, r, g, 2u, bin, c);
+      emit_words(seed, r, g, 2u, bin, c);
       w->sw = c[0];
     }
   }
