@@ -371,8 +371,16 @@ RTHX_EXPORT int rthx_domain_create(const rthx_domain_desc* desc, int32_t device,
   for (size_t f = 0; f < nf && d->axis_rect; ++f) d->axis_rect = canonical_rect(s.fine_nv[f], fpoly[f]);
   // (cos, sin)(2 pi j / 256) for the emission azimuth (cos_2pi_u32) and the
   // free-path log table (neg_log_tab)
-  std::vector<double> tables(rthx::kTableDoubles);
-  rthx::fill_tables(tables.data());
+  // One copy per bin, each followed by the bin's 1 / beta_uniform (the
+  // kernels' kTabInvBeta slot; +inf when beta_uniform <= 0), so that a
+  // kernel reading the tables from global memory finds a whole
+  // kLdsTableDoubles block at bin * kLdsTableDoubles.
+  std::vector<double> tables((size_t)s.n_bins * rthx::kLdsTableDoubles);
+  for (int b = 0; b < s.n_bins; ++b) {
+    double* t = tables.data() + (size_t)b * rthx::kLdsTableDoubles;
+    rthx::fill_tables(t);
+    t[rthx::kTabInvBeta] = d->beta_first[b] > 0 ? 1.0 / d->beta_first[b] : HUGE_VAL;
+  }
   UP(cpoly.data(), nc, D.c_poly);
   UP(csolid.data(), nc, D.c_solid);
   UP(s.coarse_bbox, 4 * nc, D.c_bbox);

@@ -49,6 +49,13 @@ namespace rthx {
 #endif
 constexpr int kBufferRsrcWord3 = 0x00020000;
 constexpr int kSc1 = 16;
+#ifndef RTHX_GTAB
+// 1: the cos / log tables (and 1 / beta_uniform) read from the domain's
+// per-bin copy in global memory (L1 / L2) instead of LDS: 8 KB less LDS per
+// workgroup; C5 bands -1.2 %, C2 and C3 unchanged, the emulated strong
+// shards unchanged (profiles/round5/ab/tables_global.log).  0: LDS (A/B).
+#define RTHX_GTAB 1
+#endif
 #ifndef RTHX_REFILL_Q
 #define RTHX_REFILL_Q 40  // MLAT kernels: idle lanes before the ends are resolved and the queue refills (C5 at 1e9 rays, band 0 / 4, with walk_layers' fast loop: 24 53.0 / 34.0 ms, 32 49.8 / 32.9, 40 50.2 / 31.2, 48 51.8 / 30.7, 56 59.6 / 32.1; at 1e8: 24 8.65 / 6.45, 40 8.50 / 6.08, 48 9.04 / 6.26)
 #endif
@@ -386,7 +393,15 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
   // SINGLE: the one coarse polygon and its fine grid, also in LDS, so that
   // its 16 doubles do not occupy SGPRs for the whole loop.
   __shared__ SingleCoarse s_single;
+#if RTHX_GTAB
+  // cos and log tables and inv_beta_uniform read from global memory (L1 / L2;
+  // the domain's per-bin copy): 8 KB less LDS per workgroup
+  const double* const g_tab = (const double*)((const double RTHX_GLOBAL*)D.tables + (size_t)P.bin * kLdsTableDoubles);
+#define RTHX_TAB_PTR g_tab
+#else
   __shared__ double s_tab[kLdsTableDoubles];  // cos and log tables, inv_beta_uniform (rthx_device.h)
+#define RTHX_TAB_PTR ((const double*)lds_opaque(&s_tab[0]))
+#endif
 
   // CL: what sits in LDS behind the row tally.  SINGLE: 1 = the lattice of
   // the one coarse rectangle (LAT).  Multi-polygon: 1 = the coarse mesh
@@ -449,8 +464,10 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
     double RTHX_LDS* cb = (double RTHX_LDS*)(cl_base + D.cl.off_beta);
     for (int i = tid; i < D.n_coarse; i += nthr) cb[i] = D.c_beta[(size_t)P.bin * D.n_coarse + i];
   }
+#if !RTHX_GTAB
   if (!FAITHFUL)
     for (int i = tid; i < kLdsTableDoubles; i += nthr) s_tab[i] = i < kTableDoubles ? D.tables[i] : P.inv_beta_uniform;
+#endif
   if (tid == 0) {
     s_tallied = 0u;
     s_next = (uint32_t)r_begin;
@@ -505,7 +522,7 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
       // Opaque LDS addresses: re-read the loop-invariant coarse record and cos
       // table at their point of use instead of hoisting ~40 values into VGPRs.
       const SingleCoarse RTHX_LDS* sc = lds_opaque(&s_single);
-      const double RTHX_LDS* tab = lds_opaque(&s_tab[0]);
+      const double* tab = RTHX_TAB_PTR;
       const Emitter RTHX_LDS* em = lds_opaque(&s_emit);
       const Emitter& e = *(const Emitter*)em;
       const RayWords rw = ray_words<EK>(P, e, (uint32_t)g, r, have_pw, pw, FAITHFUL);
@@ -616,7 +633,7 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
         const uint32_t rr = base + lane;
         const bool valid = lane < want && rr < (uint32_t)r_end;
         if (valid) {
-          const double RTHX_LDS* tab = lds_opaque(&s_tab[0]);
+          const double* tab = RTHX_TAB_PTR;
           const Emitter RTHX_LDS* em = lds_opaque(&s_emit);
           const Emitter& e = *(const Emitter*)em;
           double v[kRaySlotDoubles];
@@ -705,7 +722,7 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
           if (!live) {
             r = atomicAdd(&s_next, 1u);
             if (r < (uint32_t)r_end) {
-              const double RTHX_LDS* tab = lds_opaque(&s_tab[0]);
+              const double* tab = RTHX_TAB_PTR;
               const Emitter RTHX_LDS* em = lds_opaque(&s_emit);
               const Emitter& e = *(const Emitter*)em;
               start_ray<UNIFORM, FAITHFUL>(P, e, (const double*)tab, (uint32_t)g, r, px, py, dx, dy, S);
