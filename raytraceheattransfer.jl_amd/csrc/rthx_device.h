@@ -233,29 +233,6 @@ __device__ __forceinline__ double u52(uint32_t hi, uint32_t lo) {
 
 __device__ __forceinline__ double u32(uint32_t w) { return (double)w * 0x1.0p-32; }
 
-// Two-block draws (the 3D tracer, rthx_trace3d_kernels.hip): counters
-// (w0, w1, blk, w3) -> a and (w0, w1, blk + 1, w3) -> c;
-//   R1 = u52(a0,a1)  R2 = u52(a2,a3)  path = u52(c0,c1)  sel = u32(c2)
-//   th = u32(c3)     ph = u32(a1[11:0]<<20 | a3[11:0]<<8 | c1[11:4])
-struct RayDraws {
-  uint32_t a[4], c[4];
-  __device__ __forceinline__ RayDraws(uint32_t w0, uint32_t w1, uint32_t blk, uint32_t w3, uint32_t k0, uint32_t k1) {
-    a[0] = w0; a[1] = w1; a[2] = blk; a[3] = w3;
-    c[0] = w0; c[1] = w1; c[2] = blk + 1u; c[3] = w3;
-    philox4x32_10(a, k0, k1);
-    philox4x32_10(c, k0, k1);
-  }
-  __device__ __forceinline__ double R1() const { return u52(a[0], a[1]); }
-  __device__ __forceinline__ double R2() const { return u52(a[2], a[3]); }
-  __device__ __forceinline__ double path() const { return u52(c[0], c[1]); }
-  __device__ __forceinline__ double sel() const { return u32(c[2]); }
-  __device__ __forceinline__ double th() const { return u32(c[3]); }
-  __device__ __forceinline__ uint32_t ph_bits() const {
-    return ((a[1] & 0xFFFu) << 20) | ((a[3] & 0xFFFu) << 8) | ((c[1] & 0xFFFu) >> 4);
-  }
-  __device__ __forceinline__ double ph() const { return u32(ph_bits()); }
-};
-
 // The random words of one 2D emission (exchange tracer and the direct
 // method's emission; the CPU restatement's emit_words has the same layout):
 //   surface emitter: pos = u32(a0), Lambert draws l1 = u32(a1), l2 = u32(a2)
@@ -274,11 +251,60 @@ struct RayWords {
   uint32_t pw, sw;
 };
 
+// Philox block of counter (w0, w1, blk, w3) with w1, blk and w3
+// wave-uniform (the row, the block number, the bin): the first rounds are
+// written out, because round 1's product M1 blk and word 0 and round 2's
+// product M0 c0 and word 3 are then uniform too and go to scalar
+// instructions (plain xors and multiplies; the v_bitop3 form would put them
+// on the VALU).  The same arithmetic as philox4x32, so the same words.
+template <int ROUNDS>
+__device__ __forceinline__ void philox_block_u(uint32_t w0, uint32_t w1, uint32_t blk, uint32_t w3, uint32_t k0,
+                                               uint32_t k1, uint32_t out[4]) {
+  constexpr uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+  static_assert(ROUNDS >= 3, "rounds 1-3 are written out");
+  // round 1: c = (w0, w1, blk, w3)
+  const uint64_t a0 = (uint64_t)M0 * w0, a1 = (uint64_t)M1 * blk;
+  const uint32_t u0 = (uint32_t)(a1 >> 32) ^ w1 ^ k0, u1 = (uint32_t)a1;  // (uniform)
+  const uint32_t v2 = (uint32_t)(a0 >> 32) ^ (w3 ^ k1), v3 = (uint32_t)a0;
+  // round 2: c = (u0, u1, v2, v3)
+  const uint64_t b0 = (uint64_t)M0 * u0, b1 = (uint64_t)M1 * v2;  // (b0 uniform)
+  const uint32_t x0 = (uint32_t)(b1 >> 32) ^ (u1 ^ (k0 + W0)), x1 = (uint32_t)b1;
+  const uint32_t x2 = ((uint32_t)(b0 >> 32) ^ (k1 + W1)) ^ v3, x3 = (uint32_t)b0;  // (x3 uniform)
+  // round 3: c = (x0, x1, x2, x3)
+  const uint64_t d0 = (uint64_t)M0 * x0, d1 = (uint64_t)M1 * x2;
+  out[0] = xor3((uint32_t)(d1 >> 32), x1, k0 + 2u * W0);
+  out[1] = (uint32_t)d1;
+  out[2] = (uint32_t)(d0 >> 32) ^ (x3 ^ (k1 + 2u * W1));
+  out[3] = (uint32_t)d0;
+  philox4x32<ROUNDS - 3>(out, k0 + 3u * W0, k1 + 3u * W1);
+}
+
 __device__ __forceinline__ void philox_words(uint32_t w0, uint32_t w1, uint32_t blk, uint32_t w3, uint32_t k0,
                                              uint32_t k1, uint32_t out[4]) {
-  out[0] = w0; out[1] = w1; out[2] = blk; out[3] = w3;
-  philox4x32<RTHX_PHILOX_ROUNDS>(out, k0, k1);
+  philox_block_u<RTHX_PHILOX_ROUNDS>(w0, w1, blk, w3, k0, k1, out);
 }
+
+// Two-block draws (the 3D tracer, rthx_trace3d_kernels.hip): counters
+// (w0, w1, blk, w3) -> a and (w0, w1, blk + 1, w3) -> c;
+//   R1 = u52(a0,a1)  R2 = u52(a2,a3)  path = u52(c0,c1)  sel = u32(c2)
+//   th = u32(c3)     ph = u32(a1[11:0]<<20 | a3[11:0]<<8 | c1[11:4])
+struct RayDraws {
+  uint32_t a[4], c[4];
+  // (w1, blk, w3 wave-uniform: philox_block_u)
+  __device__ __forceinline__ RayDraws(uint32_t w0, uint32_t w1, uint32_t blk, uint32_t w3, uint32_t k0, uint32_t k1) {
+    philox_block_u<10>(w0, w1, blk, w3, k0, k1, a);
+    philox_block_u<10>(w0, w1, blk + 1u, w3, k0, k1, c);
+  }
+  __device__ __forceinline__ double R1() const { return u52(a[0], a[1]); }
+  __device__ __forceinline__ double R2() const { return u52(a[2], a[3]); }
+  __device__ __forceinline__ double path() const { return u52(c[0], c[1]); }
+  __device__ __forceinline__ double sel() const { return u32(c[2]); }
+  __device__ __forceinline__ double th() const { return u32(c[3]); }
+  __device__ __forceinline__ uint32_t ph_bits() const {
+    return ((a[1] & 0xFFFu) << 20) | ((a[3] & 0xFFFu) << 8) | ((c[1] & 0xFFFu) >> 4);
+  }
+  __device__ __forceinline__ double ph() const { return u32(ph_bits()); }
+};
 
 #define RTHX_TWO_PI 6.283185307179586
 
