@@ -52,7 +52,8 @@ constexpr int kSc1 = 16;
 #ifndef RTHX_GTAB
 // 1: the cos / log tables (and 1 / beta_uniform) read from the domain's
 // per-bin copy in global memory (L1 / L2) instead of LDS: 8 KB less LDS per
-// workgroup; C5 bands -1.2 %, C2 and C3 unchanged, the emulated strong
+// workgroup; C5 bands -1.2 % at 1e9 rays and -27 % at 1e8 (more of its
+// short-row workgroups fit a CU), C2 and C3 unchanged, the emulated strong
 // shards unchanged (profiles/round5/ab/tables_global.log).  0: LDS (A/B).
 #define RTHX_GTAB 1
 #endif
