@@ -40,8 +40,8 @@
 
 /* ------------------------------------------------------------------------ */
 /* Philox-4x32 (Salmon et al., SC'11; Random123 reference constants): 10      */
-/* rounds for the 3D tracer and the direct method, 7 for the 2D exchange     */
-/* tracer's emission words (ray_words; DESIGN.md §5 "Random numbers").  The  */
+/* rounds for the 3D tracer, 7 for the 2D tracers' words (the exchange       */
+/* tracer's ray_words, the direct method's block_at).  The     */
 /* round function is pinned by the Random123 10-round known answers.        */
 /* The Julia reference uses the unseeded task-local Xoshiro `rand()`         */
 /* (traceRay.jl:25, emitSurfaceRay2D.jl:5 ...), which no test pins.          */
@@ -992,7 +992,7 @@ typedef struct {
 static void block_at(uint64_t seed, uint32_t r0, uint32_t r1, uint32_t blk, uint32_t tag, uint32_t out[4]) {
   uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
   uint32_t ctr[4] = {r0, r1, blk, tag};
-  oracle_philox4x32_10(ctr, key, out);
+  oracle_philox4x32_emit(ctr, key, out);  /* (EMIT_ROUNDS, as the device's philox_block) */
 }
 
 static hit_t trace_leg(const dom_t* D, const rthx_direct_args* a, const double* p, const double* dir, int c,
@@ -1023,7 +1023,7 @@ static void direct_ray(dworker_t* W, uint64_t ray) {
   uint32_t col = (uint32_t)(((uint64_t)w[2] * (uint64_t)n) >> 32);
   uint64_t at = W->alias[col];
   int64_t g = (w[3] < (uint32_t)at) ? (int64_t)col : (int64_t)(at >> 32);
-  block_words(a->seed, r0, r1, 1u, tag, rw.a);
+  emit_words(a->seed, r0, r1, 1u, tag, rw.a);
   double p[2], dir[2];
   int f;
   double u_path;

@@ -213,11 +213,12 @@ __device__ __forceinline__ void philox4x32(uint32_t c[4], uint32_t k0, uint32_t 
   }
 }
 __device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) { philox4x32<10>(c, k0, k1); }
-// Rounds of the 2D exchange tracer's emission words (philox_words): 7, the
+// Rounds of the 2D tracers' words (philox_words; the direct method's
+// philox_block, rthx_direct_kernels.hip): 7, the
 // fewest rounds at which Salmon et al. (SC'11) found Philox4x32 passing
 // TestU01's BigCrush (their default of 10 adds a safety margin).  7
 // rounds take 4.7 % off the headline kernel (profiles/round5/ab_philox.log).
-// The 3D tracer (RayDraws) and the direct method keep 10.  The CPU
+// The 3D tracer (RayDraws) keeps 10.  The CPU
 // restatement's EMIT_ROUNDS (oracle/rthx_oracle.c) must match.
 #ifndef RTHX_PHILOX_ROUNDS
 #define RTHX_PHILOX_ROUNDS 7

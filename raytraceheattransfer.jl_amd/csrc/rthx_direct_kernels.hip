@@ -17,7 +17,7 @@
 //   blk 2i+2, i >= 1 interaction of iteration i: choice u32(w0), direction draws w1, w2,
 //                    free path of iteration i + 1 u32(w3)
 //   blk 2i+1, i >= 1 roulette of iteration i, u52(w0,w1) -- drawn only past roulette_after
-// One Philox block per leg (32-bit draws, as the exchange tracer's).
+// One Philox block per leg (32-bit draws and 7 rounds, as the exchange tracer's).
 // oracle/rthx_oracle.c (oracle_trace_direct) draws the same blocks.
 //
 // Bookkeeping (directRayTracing.jl:72-128): the emission count is added when
@@ -47,7 +47,7 @@ constexpr int kDirectRefill = RTHX_DIRECT_REFILL;  // refill once this many lane
 __device__ __forceinline__ void philox_block(uint32_t w[4], uint32_t r0, uint32_t r1, uint32_t blk, uint32_t tag,
                                              uint32_t k0, uint32_t k1) {
   w[0] = r0; w[1] = r1; w[2] = blk; w[3] = tag;
-  philox4x32_10(w, k0, k1);
+  philox4x32<RTHX_PHILOX_ROUNDS>(w, k0, k1);  // (the 2D words' rounds, rthx_device.h)
 }
 
 #ifndef RTHX_DIRECT_WAVES
