@@ -14,7 +14,7 @@
  * (test/test_2d_grey.jl:25-33), the 840.896 K wedge limit
  * (test/test_triangle_mesh.jl:48-74).  Bit-for-bit stream parity with the
  * Julia reference is impossible (it calls the unseeded global rand(),
- * SURVEY.md §0.6); this restatement uses a counter-based Philox-4x32-10
+ * SURVEY.md §0.6); this restatement uses a counter-based Philox-4x32
  * stream that the HIP kernel shares, so GPU and CPU counts can be compared
  * exactly.
  *

@@ -1,6 +1,6 @@
 """HIP path (librthx through the C ABI) against the CPU restatement.
 
-Both sides draw every ray from the same Philox-4x32-10 stream, so absorber
+Both sides draw every ray from the same Philox-4x32 stream (7-round blocks), so absorber
 counts are compared exactly (row pointers, columns, counts).  At sizes the
 oracle finishes in seconds the comparison covers every row; at BASELINE's
 full sizes it covers a strided sample of rows plus size-independent
