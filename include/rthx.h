@@ -132,7 +132,7 @@ typedef struct rthx_trace_args {
   int64_t rays_per_emitter;  /* R = div(rays_total, N), parallelRayTracing.jl:6 */
   double nudge;              /* eta; reference default 1e4*eps(Float64),
                                 multiDispatchRayTrace2D.jl:10 */
-  uint64_t seed;             /* Philox-4x32 key (7 rounds: 2D tracers; 10: 3D) */
+  uint64_t seed;             /* Philox-4x32-7 key */
   int64_t emitter_begin;     /* trace emitters g = begin + k*stride < end */
   int64_t emitter_end;
   int64_t emitter_stride;    /* >= 1 (1 = contiguous block) */

@@ -39,9 +39,8 @@
 #define ORACLE_API __attribute__((visibility("default")))
 
 /* ------------------------------------------------------------------------ */
-/* Philox-4x32 (Salmon et al., SC'11; Random123 reference constants): 10      */
-/* rounds for the 3D tracer, 7 for the 2D tracers' words (the exchange       */
-/* tracer's ray_words, the direct method's block_at).  The     */
+/* Philox-4x32 (Salmon et al., SC'11; Random123 reference constants): every  */
+/* tracer draws from 7-round blocks (EMIT_ROUNDS).  The        */
 /* round function is pinned by the Random123 10-round known answers.        */
 /* The Julia reference uses the unseeded task-local Xoshiro `rand()`         */
 /* (traceRay.jl:25, emitSurfaceRay2D.jl:5 ...), which no test pins.          */
@@ -113,7 +112,7 @@ typedef struct {
 static void block_words(uint64_t seed, uint32_t w0, uint32_t w1, uint32_t blk, uint32_t w3, uint32_t out[4]) {
   uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
   uint32_t ctr[4] = {w0, w1, blk, w3};
-  oracle_philox4x32_10(ctr, key, out);
+  oracle_philox4x32_emit(ctr, key, out);
 }
 
 /* A block of the exchange tracer's emission words (EMIT_ROUNDS rounds). */
@@ -1440,7 +1439,7 @@ static void* t3_worker(void* arg) {
       draws3_t rd;
       draws3_at(W->seed, (uint32_t)r, (uint32_t)g, 0u, 0x40000000u, &rd);
       uint32_t cc[4] = {(uint32_t)r, (uint32_t)g, 1u, 0x40000000u}, c[4];
-      oracle_philox4x32_10(cc, key, c);
+      oracle_philox4x32_emit(cc, key, c);
       double s1 = sqrt(rd.R1);
       double wa = 1.0 - s1, wb = s1 * (1.0 - rd.R2), wc = s1 * rd.R2;
       int ia = 0, ib = 1, ic = 2;

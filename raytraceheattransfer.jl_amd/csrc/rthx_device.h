@@ -186,7 +186,8 @@ struct TraceParams {
 };
 
 // ---------------------------------------------------------------------------
-// Philox-4x32 counter RNG (Salmon et al. SC'11), 10 rounds unless stated.
+// Philox-4x32 counter RNG (Salmon et al. SC'11); the tracers run
+// RTHX_PHILOX_ROUNDS (7) rounds.
 // Counter (r, g, block, bin), key (seed lo, seed hi).
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
@@ -212,14 +213,12 @@ __device__ __forceinline__ void philox4x32(uint32_t c[4], uint32_t k0, uint32_t 
     k1 += 0xBB67AE85u;
   }
 }
-__device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) { philox4x32<10>(c, k0, k1); }
-// Rounds of the 2D tracers' words (philox_words; the direct method's
-// philox_block, rthx_direct_kernels.hip): 7, the
+// Rounds of every tracer's blocks (philox_words, RayDraws; the direct
+// method's philox_block, rthx_direct_kernels.hip): 7, the
 // fewest rounds at which Salmon et al. (SC'11) found Philox4x32 passing
 // TestU01's BigCrush (their default of 10 adds a safety margin).  7
 // rounds take 4.7 % off the headline kernel (profiles/round5/ab_philox.log).
-// The 3D tracer (RayDraws) keeps 10.  The CPU
-// restatement's EMIT_ROUNDS (oracle/rthx_oracle.c) must match.
+// The CPU restatement's EMIT_ROUNDS (oracle/rthx_oracle.c) must match.
 #ifndef RTHX_PHILOX_ROUNDS
 #define RTHX_PHILOX_ROUNDS 7
 #endif
@@ -293,8 +292,8 @@ struct RayDraws {
   uint32_t a[4], c[4];
   // (w1, blk, w3 wave-uniform: philox_block_u)
   __device__ __forceinline__ RayDraws(uint32_t w0, uint32_t w1, uint32_t blk, uint32_t w3, uint32_t k0, uint32_t k1) {
-    philox_block_u<10>(w0, w1, blk, w3, k0, k1, a);
-    philox_block_u<10>(w0, w1, blk + 1u, w3, k0, k1, c);
+    philox_block_u<RTHX_PHILOX_ROUNDS>(w0, w1, blk, w3, k0, k1, a);
+    philox_block_u<RTHX_PHILOX_ROUNDS>(w0, w1, blk + 1u, w3, k0, k1, c);
   }
   __device__ __forceinline__ double R1() const { return u52(a[0], a[1]); }
   __device__ __forceinline__ double R2() const { return u52(a[2], a[3]); }

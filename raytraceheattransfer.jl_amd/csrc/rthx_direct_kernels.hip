@@ -47,7 +47,7 @@ constexpr int kDirectRefill = RTHX_DIRECT_REFILL;  // refill once this many lane
 __device__ __forceinline__ void philox_block(uint32_t w[4], uint32_t r0, uint32_t r1, uint32_t blk, uint32_t tag,
                                              uint32_t k0, uint32_t k1) {
   w[0] = r0; w[1] = r1; w[2] = blk; w[3] = tag;
-  philox4x32<RTHX_PHILOX_ROUNDS>(w, k0, k1);  // (the 2D words' rounds, rthx_device.h)
+  philox4x32<RTHX_PHILOX_ROUNDS>(w, k0, k1);  // (every tracer's rounds, rthx_device.h)
 }
 
 #ifndef RTHX_DIRECT_WAVES
