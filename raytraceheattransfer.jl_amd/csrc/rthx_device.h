@@ -1013,7 +1013,10 @@ __device__ __forceinline__ LatticeLds lattice_lds_view(const char RTHX_LDS* base
 // INSIDE: the caller knows p lies in the rectangle's half-open box (a ray
 // of an axis-aligned rectangle volume emitter: its uniform point, nudged
 // toward the cell's midpoint, lies in the cell, and the cell in the box).
-template <bool UNIFORM, bool INSIDE = false>
+// FOUR: the four-wall test for every point (no branch on the point's
+// position: the direct method's rays start on walls and inside alike; for a
+// point in the half-open box it gives dist_in_box's answer).
+template <bool UNIFORM, bool INSIDE = false, bool FOUR = false>
 __device__ __forceinline__ int segment_lat(const DevDomain& D, const TraceParams& P, const SingleCoarse& sc,
                                            const LatticeLds& L, const LatticeLayout& G, double& px, double& py,
                                            double dx, double dy, double& S, double& acc) {
@@ -1023,7 +1026,7 @@ __device__ __forceinline__ int segment_lat(const DevDomain& D, const TraceParams
   // walls, dist_in_box; any other point takes the four-wall test)
   const double cx0 = sc.poly.x[0], cx1 = sc.poly.x[1], cy0 = sc.poly.y[0], cy1 = sc.poly.y[2];
   double u;
-  if (INSIDE || (cx0 <= px && px < cx1 && cy0 <= py && py < cy1))
+  if (!FOUR && (INSIDE || (cx0 <= px && px < cx1 && cy0 <= py && py < cy1)))
     u = dist_in_box(px, py, dx, dy, dx < 0.0 ? cx0 : cx1, dy < 0.0 ? cy0 : cy1, k);
   else
     u = dist_to_box(px, py, dx, dy, cx0, cx1, cy0, cy1, k);

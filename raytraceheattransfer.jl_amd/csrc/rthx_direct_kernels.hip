@@ -50,6 +50,9 @@ __device__ __forceinline__ void philox_block(uint32_t w[4], uint32_t r0, uint32_
   philox4x32<RTHX_PHILOX_ROUNDS>(w, k0, k1);  // (every tracer's rounds, rthx_device.h)
 }
 
+#ifndef RTHX_DIRECT_FOUR
+#define RTHX_DIRECT_FOUR 1  // LAT legs: the four-wall distance test for every start point (A/B: 0 branches on it)
+#endif
 #ifndef RTHX_DIRECT_WAVES
 #define RTHX_DIRECT_WAVES 0  // > 0: amdgpu_waves_per_eu floor (register budget) for variants
 #endif
@@ -195,7 +198,7 @@ __global__ __launch_bounds__(FAITHFUL ? kDirectThreads : kDirectMaxThreads) RTHX
       int a;
       if (LAT) {
         const SingleCoarse RTHX_LDS* sc = lds_opaque(&s_single);
-        a = seg < 10000 ? segment_lat<UNIFORM>(D, Q.P, *(const SingleCoarse*)sc,
+        a = seg < 10000 ? segment_lat<UNIFORM, false, RTHX_DIRECT_FOUR>(D, Q.P, *(const SingleCoarse*)sc,
                                                lattice_lds_view(lds_opaque(lat_base), D.lat), D.lat, px, py, dx, dy,
                                                S, acc)
                         : -1;
