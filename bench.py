@@ -361,6 +361,8 @@ def main():
     step_faults = int(info["superseded_faults"])
     bad = step_faults != 0 or (not args.blocking and args.mode != "threads" and steps_checked != args.steps)
     if dist is not None:  # (one decision for every rank: the fallback below has its own barriers)
+        import torch
+
         fb = torch.tensor([1.0 if bad else 0.0], dtype=torch.float64)
         dist.all_reduce(fb, op=dist.ReduceOp.MAX)
         bad = fb.item() > 0
