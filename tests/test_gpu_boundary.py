@@ -326,6 +326,22 @@ def test_bench_two_gpus_as_a_plain_command(hip, mode):
     assert d["config"]["rays_per_step"] == (40_000_000 // 10605) * 10605
 
 
+def test_bench_falls_back_to_blocking_steps_when_pipelined_steps_fault(hip, monkeypatch):
+    """With a zero look-back wait bound (RTHX_LB_WAIT_US=0) the pipelined
+    timed steps stall and are superseded unread, so bench.py times the steps
+    again as blocking calls (each re-traced when needed) and says so in its
+    line; two ranks decide together.  A normal run reports no faults."""
+    monkeypatch.setenv("RTHX_LB_WAIT_US", "0")
+    for extra in ([], ["--gpus", "2", "--rays-per-gpu", "20000000"]):
+        d = _bench_line(["--steps", "4", "--warmup", "1", "--prewarm-s", "0", "--no-cpu", "--faithful-steps", "0"] + extra)
+        assert d["pipelined_step_faults"] > 0 and d["step_mode"].startswith("blocking calls (fallback")
+        assert d["steps_checked"] == 4 and d["value"] > 0
+    monkeypatch.delenv("RTHX_LB_WAIT_US")
+    d = _bench_line(["--steps", "4", "--warmup", "1", "--prewarm-s", "0", "--no-cpu", "--faithful-steps", "0"])
+    assert d["pipelined_step_faults"] == 0 and d["steps_checked"] == 4
+    assert d["step_mode"] == "enqueued back to back (RTHX_FLAG_ASYNC)"
+
+
 @pytest.mark.parametrize("case", ["square", "greenhouse", "shard"])
 def test_device_csr_equals_host_csr(hip, case):
     """rthx_result_get_device_csr / rthx_result_copy_csr_device: the block a
