@@ -174,6 +174,10 @@ typedef struct rthx_result rthx_result;
 
 /* Library / device queries. */
 int rthx_abi_version(void);
+/* First 16 hex digits of sha256 over the library's sources (csrc/ *.cpp, *.h, *.hip
+ * sorted, csrc/Makefile, include/rthx.h) at build time: tells a prebuilt
+ * library from one built out of the sources beside it. */
+const char* rthx_build_id(void);
 const char* rthx_last_error(void);
 int rthx_device_count(int32_t* count);
 int rthx_device_synchronize(int32_t device);
@@ -256,6 +260,24 @@ int rthx_result_get_device_csr(const rthx_result* res, int32_t part, rthx_device
  * complete. */
 int rthx_result_copy_csr_device(const rthx_result* res, int32_t part, int64_t* row_off, uint32_t* cols,
                                 uint32_t* counts);
+
+/* Assembly of a row-sharded count matrix on one device (BASELINE config C5
+ * over W GPUs: rank k traces rows g = k, k + W, k + 2W, ... of a band with
+ * emitter_begin = k, emitter_stride = W, and the band's owner merges the W
+ * blocks its gather received).  Block k (0 <= k < n_shards <= 64) is a CSR
+ * over its own n_k = ceil((n_rows - k) / n_shards) rows: shard_row_off[k]
+ * (n_k + 1 offsets into its arrays), shard_cols[k], shard_counts[k] -- the
+ * layout rthx_result_copy_csr_device writes.  Output: row_ptr[n_rows + 1]
+ * (from 0), cols and counts in row order.  Every data pointer is device
+ * memory that `device` can read; the three pointer arrays are host arrays.
+ * stream: a hipStream_t on `device` to enqueue on (the call returns once the
+ * merge is enqueued), or NULL (the library's stream; returns when done).
+ * Takes the place of the reference's merge of per-thread COO triplets into
+ * one matrix (parallelRayTracing.jl:128-145) for blocks from several GPUs. */
+int rthx_merge_row_shards(int32_t device, int32_t n_shards, int64_t n_rows,
+                          const int64_t* const* shard_row_off, const uint32_t* const* shard_cols,
+                          const uint32_t* const* shard_counts, int64_t* row_ptr, uint32_t* cols,
+                          uint32_t* counts, void* stream);
 
 /* ------------------------------------------------------------------------
  * Several devices: the GPU counterpart of the reference's

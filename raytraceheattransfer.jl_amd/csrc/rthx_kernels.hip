@@ -871,8 +871,14 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
       __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (tid == 0) {
+        // Memory-model ordering of the hand-off (not only the cache policy's):
+        // the barrier orders every wave's slab stores before this lane's
+        // agent-scope release, and the arrival is acquire as well, so the part
+        // that arrives last sees every other part's slab and tallied count;
+        // its barrier below hands that on to the lanes that read the slabs.
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         const uint32_t before =
-            __hip_atomic_fetch_add(&T.row_arrive[trow], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(&T.row_arrive[trow], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
         const bool last = before + 1u == parts;
         if (last) {
           __hip_atomic_store(&T.row_arrive[trow], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

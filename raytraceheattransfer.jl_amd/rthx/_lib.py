@@ -46,6 +46,8 @@ def load(path: Optional[str] = None) -> C.CDLL:
     _prefer_single_hip_runtime()
     lib = C.CDLL(p, mode=C.RTLD_GLOBAL)
     lib.rthx_abi_version.restype = C.c_int
+    if hasattr(lib, "rthx_build_id"):  # (older A/B variant libraries lack it)
+        lib.rthx_build_id.restype = C.c_char_p
     lib.rthx_last_error.restype = C.c_char_p
     lib.rthx_device_count.argtypes = [C.POINTER(C.c_int32)]
     lib.rthx_device_synchronize.argtypes = [C.c_int32]
@@ -65,6 +67,10 @@ def load(path: Optional[str] = None) -> C.CDLL:
                                           C.POINTER(C.c_int64), C.c_int64, C.POINTER(C.c_int64)]
     lib.rthx_result_get_device_csr.argtypes = [C.c_void_p, C.c_int32, C.POINTER(abi.DeviceCsr)]
     lib.rthx_result_copy_csr_device.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p]
+    if hasattr(lib, "rthx_merge_row_shards"):  # (older A/B variant libraries lack it)
+        pp = C.POINTER(C.c_void_p)
+        lib.rthx_merge_row_shards.argtypes = [C.c_int32, C.c_int32, C.c_int64, pp, pp, pp, C.c_void_p, C.c_void_p,
+                                              C.c_void_p, C.c_void_p]
     lib.rthx_host_register.argtypes = [C.c_void_p, C.c_size_t]
     lib.rthx_host_unregister.argtypes = [C.c_void_p]
     lib.rthx_multi_create.argtypes = [C.POINTER(abi.DomainDesc), C.POINTER(C.c_int32), C.c_int32,
@@ -110,6 +116,40 @@ def load(path: Optional[str] = None) -> C.CDLL:
         raise RthxError("librthx ABI version mismatch")
     _lib = lib
     return lib
+
+
+def source_build_id() -> str:
+    """The build id that a librthx.so built from the sources in this tree
+    carries: sha256 over csrc/*.{cpp,h,hip} (sorted by name), csrc/Makefile
+    and include/rthx.h, first 16 hex digits (csrc/Makefile BUILD_ID)."""
+    import glob
+    import hashlib
+
+    csrc = os.path.join(os.path.dirname(_PKG_DIR), "csrc")
+    names = sorted(os.path.basename(p) for ext in ("hip", "cpp", "h") for p in glob.glob(os.path.join(csrc, "*." + ext)))
+    files = [os.path.join(csrc, n) for n in names] + [os.path.join(csrc, "Makefile"),
+                                                       os.path.join(os.path.dirname(os.path.dirname(_PKG_DIR)),
+                                                                    "include", "rthx.h")]
+    h = hashlib.sha256()
+    for f in files:
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def build_id() -> str:
+    """rthx_build_id() of the loaded library."""
+    return load().rthx_build_id().decode()
+
+
+def check_build_id() -> str:
+    """Raise RthxError unless the loaded librthx.so was built from the sources
+    in this tree (a stale prebuilt library fails loudly); returns the id."""
+    got, want = build_id(), source_build_id()
+    if got != want:
+        raise RthxError(f"librthx.so build id {got} does not match its sources ({want}): rebuild it "
+                        "(python __graft_entry__.py build)")
+    return got
 
 
 def check(rc: int) -> None:

@@ -242,6 +242,7 @@ class Vf3dInfo(C.Structure):
 # Every symbol include/rthx.h declares (checked by tests/test_abi_symbols.py).
 EXPORTED_SYMBOLS = (
     "rthx_abi_version",
+    "rthx_build_id",
     "rthx_last_error",
     "rthx_device_count",
     "rthx_device_synchronize",
@@ -256,6 +257,7 @@ EXPORTED_SYMBOLS = (
     "rthx_result_copy_F",
     "rthx_result_get_device_csr",
     "rthx_result_copy_csr_device",
+    "rthx_merge_row_shards",
     "rthx_host_register",
     "rthx_host_unregister",
     "rthx_multi_create",

@@ -31,5 +31,8 @@ def hip():
     from rthx import _lib
 
     lib = _lib.load()
+    # the library under test was built from the sources in this tree (a stale
+    # prebuilt librthx.so fails here, loudly)
+    print(f"librthx build id {_lib.check_build_id()}")
     assert _lib.device_count() >= 1, "no HIP device visible"
     return _lib

@@ -41,6 +41,15 @@ def test_every_declared_symbol_is_exported(lib):
         getattr(lib, s)
 
 
+def test_build_id_matches_sources(lib):
+    """The library carries the hash of the sources it was built from
+    (csrc/Makefile BUILD_ID), and it is the hash of this tree's sources."""
+    got = lib.rthx_build_id().decode()
+    assert len(got) == 16 and int(got, 16) >= 0
+    assert got == _lib.source_build_id()
+    assert _lib.check_build_id() == got
+
+
 def test_struct_sizes_match_header():
     # offsets fixed by the header's field order (x86-64 SysV)
     assert C.sizeof(abi.GridDesc) == 48

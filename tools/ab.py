@@ -41,6 +41,11 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--ndim", type=int, default=101)
     ap.add_argument("--c5-bin", type=int, default=-1, help="time one band of the C5 greenhouse instead of C2")
+    ap.add_argument("--stride", type=int, default=1,
+                    help="rank 0's rows of a W-way row shard (rows 0, W, 2W, ...; --rays stays the whole job's)")
+    ap.add_argument("--env", default="",
+                    help="NAME=v1,v2,...: every library is also timed with each value of that knob "
+                         "(RTHX_DEV_KNOBS is set; 'auto' leaves the knob unset)")
     args = ap.parse_args()
     import bench
 
@@ -55,27 +60,43 @@ def main():
     N = flat.n_emitters
     R = args.rays // N
     nudge = 10_000 * np.finfo(np.float64).eps
-    targs, _k = _lib.make_args(max(args.c5_bin, 0), R, nudge, 1, 0, N, 1, flags=abi.RTHX_FLAG_DEVICE_ONLY)
+    targs, _k = _lib.make_args(max(args.c5_bin, 0), R, nudge, 1, 0, N, args.stride, flags=abi.RTHX_FLAG_DEVICE_ONLY)
+    os.environ["RTHX_DEV_KNOBS"] = "1"
+    knob, vals = (args.env.split("=", 1)[0], args.env.split("=", 1)[1].split(",")) if args.env else (None, [None])
+
+    def set_knob(v):
+        if knob is None:
+            return
+        if v in (None, "auto"):
+            os.environ.pop(knob, None)
+        else:
+            os.environ[knob] = v
+
     runs = []
     for p in args.libs:
         lib = open_lib(p)
-        h, r = C.c_void_p(), C.c_void_p()
-        assert lib.rthx_domain_create(C.byref(flat.desc), 0, C.byref(h)) == 0, lib.rthx_last_error()
-        assert lib.rthx_result_create(C.byref(r)) == 0
-        for _ in range(2):
-            assert lib.rthx_trace_exchange(h, C.byref(targs), r) == 0, lib.rthx_last_error()
-        runs.append((p, lib, h, r, []))
+        for v in vals:
+            set_knob(v)
+            h, r = C.c_void_p(), C.c_void_p()
+            assert lib.rthx_domain_create(C.byref(flat.desc), 0, C.byref(h)) == 0, lib.rthx_last_error()
+            assert lib.rthx_result_create(C.byref(r)) == 0
+            for _ in range(2):
+                assert lib.rthx_trace_exchange(h, C.byref(targs), r) == 0, lib.rthx_last_error()
+            tag = os.path.basename(os.path.dirname(p)) or p
+            runs.append((tag + (f" {knob}={v}" if knob else ""), lib, h, r, [], v))
     for _ in range(args.rounds):
-        for p, lib, h, r, ts in runs:
+        for p, lib, h, r, ts, v in runs:
+            set_knob(v)
             for _ in range(args.steps):
                 assert lib.rthx_trace_exchange(h, C.byref(targs), r) == 0
                 inf = abi.ResultInfo()
                 lib.rthx_result_get_info(r, C.byref(inf))
                 ts.append(inf.trace_ms)
-    for p, lib, h, r, ts in runs:
+    rays = len(range(0, N, args.stride)) * R
+    for p, lib, h, r, ts, v in runs:
         t = np.array(ts)
-        print(f"{os.path.basename(os.path.dirname(p)) or p:12s} median {np.median(t):.4f} ms  min {t.min():.4f}  "
-              f"p90 {np.percentile(t, 90):.4f}  {N * R / np.median(t) / 1e6:.1f} Mrays/s (R={R})", flush=True)
+        print(f"{p:12s} median {np.median(t):.4f} ms  min {t.min():.4f}  "
+              f"p90 {np.percentile(t, 90):.4f}  {rays / np.median(t) / 1e6:.1f} Mrays/s (R={R}, {rays // R} rows)", flush=True)
 
 
 if __name__ == "__main__":
