@@ -156,6 +156,72 @@ def cpu_baseline(dom, R, nudge, seed, budget_s=12.0):
     }
 
 
+PHILOX10_LIB = os.path.join(ROOT, "raytraceheattransfer.jl_amd", "csrc", "_build", "philox10", "librthx.so")
+
+
+def philox10_leg(flat, R, nudge, seed, begin, stride, steps, device):
+    """The same shard traced by the 10-round-Philox build of the exchange
+    tracer (csrc/Makefile philox10: Random123's default rounds, BASELINE.md
+    §2's RNG; the product draws from 7-round blocks), timed
+    like `value` (steps enqueued back to back) and blocking (kernel time).
+    Loaded with RTLD_LOCAL beside the product library; reported beside
+    `value`, never as it."""
+    import ctypes as C
+
+    from rthx import _lib, abi
+
+    if not os.path.exists(PHILOX10_LIB):
+        return None
+    lib = C.CDLL(PHILOX10_LIB, mode=os.RTLD_LOCAL)
+    lib.rthx_last_error.restype = C.c_char_p
+    lib.rthx_domain_create.argtypes = [C.POINTER(abi.DomainDesc), C.c_int32, C.POINTER(C.c_void_p)]
+    lib.rthx_domain_destroy.argtypes = [C.c_void_p]
+    lib.rthx_result_create.argtypes = [C.POINTER(C.c_void_p)]
+    lib.rthx_result_destroy.argtypes = [C.c_void_p]
+    lib.rthx_trace_exchange.argtypes = [C.c_void_p, C.POINTER(abi.TraceArgs), C.c_void_p]
+    lib.rthx_result_get_info.argtypes = [C.c_void_p, C.POINTER(abi.ResultInfo)]
+    lib.rthx_device_synchronize.argtypes = [C.c_int32]
+
+    def ok(rc):
+        if rc != 0:
+            raise RuntimeError(f"philox10 library: {lib.rthx_last_error().decode()}")
+
+    h, r = C.c_void_p(), C.c_void_p()
+    ok(lib.rthx_domain_create(C.byref(flat.desc), device, C.byref(h)))
+    ok(lib.rthx_result_create(C.byref(r)))
+    try:
+        targs, _k1 = _lib.make_args(0, R, nudge, seed, begin, flat.n_emitters, stride, device=device,
+                                    flags=abi.RTHX_FLAG_DEVICE_ONLY)
+        aargs, _k2 = _lib.make_args(0, R, nudge, seed, begin, flat.n_emitters, stride, device=device,
+                                    flags=abi.RTHX_FLAG_DEVICE_ONLY | abi.RTHX_FLAG_ASYNC)
+        inf = abi.ResultInfo()
+        for _ in range(5):
+            ok(lib.rthx_trace_exchange(h, C.byref(targs), r))
+        for _ in range(5):
+            ok(lib.rthx_trace_exchange(h, C.byref(aargs), r))
+        ok(lib.rthx_result_get_info(r, C.byref(inf)))
+        ok(lib.rthx_device_synchronize(device))
+        t = time.perf_counter()
+        for _ in range(steps):
+            ok(lib.rthx_trace_exchange(h, C.byref(aargs), r))
+        ok(lib.rthx_device_synchronize(device))
+        el = time.perf_counter() - t
+        ok(lib.rthx_result_get_info(r, C.byref(inf)))
+        faults = int(inf.superseded_faults)
+        rays = int(inf.rays_traced)
+        kms = []
+        for _ in range(10):
+            ok(lib.rthx_trace_exchange(h, C.byref(targs), r))
+            ok(lib.rthx_result_get_info(r, C.byref(inf)))
+            kms.append(inf.trace_ms)
+    finally:
+        lib.rthx_result_destroy(r)
+        lib.rthx_domain_destroy(h)
+    return {"value": round(rays * steps / el / 1e6, 3), "unit": "Mrays/s", "ms_per_step": round(el / steps * 1e3, 4),
+            "avg_kernel_ms": round(float(np.mean(kms)), 4), "steps": steps, "pipelined_step_faults": faults,
+            "note": "Philox4x32-10 draws (csrc/_build/philox10/librthx.so), rank 0's launch, same workload"}
+
+
 def read_pmc_traffic():
     """HBM bytes per trace launch from the committed rocprofv3 --pmc summary
     (profiles/roundN/pmc_traffic.json, newest round, written by tools/pmc_summary.py from
@@ -265,6 +331,9 @@ def main():
                     help="time blocking calls (each step waits for its trace and reads its totals back) instead "
                          "of steps enqueued back to back (RTHX_FLAG_ASYNC; every step's trace still runs in full, "
                          "its checks run when the result is read)")
+    ap.add_argument("--philox10-steps", type=int, default=20,
+                    help="steps of the Philox4x32-10 leg (the 10-round build of the tracer), reported beside value; "
+                         "0 skips it")
     ap.add_argument("--faithful-steps", type=int, default=10,
                     help="steps of the faithful-sampling leg (the reference's acos/sin/cos emission, "
                          "emitVolumeRay2D.jl:26-31), reported beside value; 0 skips it")
@@ -437,6 +506,11 @@ def main():
                     "avg_kernel_ms": round(float(np.mean(f_ms)), 4), "steps": args.faithful_steps,
                     "gpus": 1, "note": "faithful sampling (RTHX_FLAG_FAITHFUL_SAMPLING), rank 0's launch"}
 
+    p10 = None
+    if rank == 0 and args.philox10_steps > 0:
+        p10 = philox10_leg(flat, R, nudge, args.seed, targs.emitter_begin, targs.emitter_stride,
+                           args.philox10_steps, device)
+
     # PCIe-inclusive end-to-end passes, reported aside (never `value`): the
     # trace plus the CSR of counts DMA'd into page-locked caller arrays that a
     # caller reuses across traces (rthx_host_register), and the same with F_raw
@@ -524,6 +598,8 @@ def main():
                                 if args.mode == "threads" else "one process per GPU)")),
                 "devices_visible": ndev,
                 "seed": args.seed,
+                "rng": ("Philox4x32-7 blocks, counter (emitter, ray, draw), key (seed, bin); 32-bit uniform draws "
+                        "(DESIGN.md §5); the 10-round build is timed in `philox10`"),
             },
             "roofline": {
                 "bound": "hbm",
@@ -545,6 +621,7 @@ def main():
             "roofline_fp64": fp64_roof,
             "roofline_valu": valu_roof,
             "faithful_sampling": faithful,
+            "philox10": p10,
             "e2e_with_d2h_mrays_s": round(e2e, 3) if e2e else None,
             "e2e_F_with_d2h_mrays_s": round(e2e_F, 3) if e2e_F else None,
         }

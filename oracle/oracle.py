@@ -30,13 +30,24 @@ def build() -> str:
     return LIB_PATH
 
 
+def use_emit_rounds(rounds: int) -> None:
+    """Switch the restatement to the build whose emission blocks take
+    `rounds` Philox rounds (7: the product's, 10: librthx_oracle_p10.so, the
+    counterpart of csrc/_build/philox10/librthx.so)."""
+    global _lib, LIB_PATH
+    want = os.path.join(_HERE, "_build", "librthx_oracle.so" if rounds == 7 else f"librthx_oracle_p{rounds}.so")
+    if want != LIB_PATH:
+        LIB_PATH = want
+        _lib = None
+
+
 def load() -> C.CDLL:
     global _lib
     if _lib is not None:
         return _lib
     if not os.path.exists(LIB_PATH):
         build()
-    lib = C.CDLL(LIB_PATH)
+    lib = C.CDLL(LIB_PATH, mode=os.RTLD_LOCAL)
     lib.oracle_philox4x32_10.argtypes = [C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
     lib.oracle_philox4x32_10.restype = None
     lib.oracle_philox4x32_emit.argtypes = lib.oracle_philox4x32_10.argtypes

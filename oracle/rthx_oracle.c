@@ -49,7 +49,9 @@
 #define PHILOX_M1 0xCD9E8D57u
 #define PHILOX_W0 0x9E3779B9u
 #define PHILOX_W1 0xBB67AE85u
+#ifndef EMIT_ROUNDS
 #define EMIT_ROUNDS 7 /* the device's RTHX_PHILOX_ROUNDS (csrc/rthx_device.h) */
+#endif
 
 static void philox4x32(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4], int rounds) {
   uint32_t c0 = ctr[0], c1 = ctr[1], c2 = ctr[2], c3 = ctr[3];

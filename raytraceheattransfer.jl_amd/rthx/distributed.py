@@ -258,3 +258,382 @@ def broadcast_csr(row_ptr, cols, counts, n: int, src: int, group=None):
     dist.broadcast(pairs, src, group=group)
     p = pairs.cpu().numpy()
     return rp.cpu().numpy(), p[0].copy(), p[1].view(np.uint32).copy()
+
+
+# ---------------------------------------------------------------------------
+# C5 over W GPUs, row-sharded and pipelined (BASELINE configs[4]).
+#
+# Every rank traces its rows g = rank, rank + W, ... of EVERY traced band (the
+# row stride balances the ranks, which band per GPU cannot: the C5 bands do
+# not cost alike), and band i is assembled on its owner rank i mod W: the
+# ranks' blocks are gathered there (RCCL over xGMI on an NCCL group) and
+# merged in row order on the owner's GPU (rthx_merge_row_shards).  Band i's
+# copy-out, gather and merge run on a second host thread and HIP stream while
+# band i + 1 traces, so only the last band's assembly is exposed.  The
+# reference traces its bins one after another on one host
+# (parallelRayTracing.jl:20-42); the counts are the same whoever traces a row
+# (counter-based RNG keyed by seed, bin, emitter, ray).
+# ---------------------------------------------------------------------------
+
+
+class TorchBandComm:
+    """The pipeline's two collectives on a torch.distributed group: every
+    rank's block size (all_gather) and the blocks to the band's owner
+    (gather).  Tensors live on the group's device (cuda on NCCL = RCCL,
+    cpu on gloo)."""
+
+    def __init__(self, group=None):
+        import torch.distributed as dist
+
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self.device = _device_of(group)
+
+    def all_sizes(self, band: int, n: int) -> List[int]:
+        import torch
+        import torch.distributed as dist
+
+        out = [torch.zeros(1, dtype=torch.int64, device=self.device) for _ in range(self.world)]
+        dist.all_gather(out, torch.tensor([n], dtype=torch.int64, device=self.device), group=self.group)
+        return [int(x.item()) for x in out]
+
+    def gather(self, band: int, t, dst: int):
+        import torch
+        import torch.distributed as dist
+
+        out = [torch.empty_like(t) for _ in range(self.world)] if self.rank == dst else None
+        dist.gather(t, out, dst=dst, group=self.group)
+        return out
+
+
+class EmulatedBandComm:
+    """One GPU standing in for rank `rank` of W (diagnostic: the one-GPU
+    projection of tools/bench_c5_bands.py --pipeline, and the GPU tests):
+    the other ranks' blocks of the bands this rank owns were traced
+    beforehand on this GPU (`peers[band][k]` = (row_off, pairs) tensors of
+    rank k), and the gather copies them into fresh buffers on this GPU -- the
+    receive's HBM writes, without the xGMI transfer itself."""
+
+    def __init__(self, rank: int, world: int, device: int, peers):
+        import torch
+
+        self.rank, self.world = rank, world
+        self.device = torch.device("cuda", device)
+        self.peers = peers
+
+    @classmethod
+    def for_rank(cls, dom, rays: int, rank: int, world: int, device: int = 0, seed: int = 1, nudge: float = None,
+                 faithful: bool = False):
+        """The stand-in for `rank`, its peers' blocks of the bands it owns
+        (traced band i is owned by rank i mod W) traced now, on `device`."""
+        import torch
+
+        if nudge is None:
+            nudge = 10_000 * np.finfo(np.float64).eps
+        traced = traced_bands(dom)
+        N = dom.flat().n_emitters
+        R = rays // N
+        tracer = HipShardTracer(dom, device, n_results=1)
+        peers = {}
+        try:
+            for i, (b, _bins) in enumerate(traced):
+                if i % world != rank:
+                    continue
+                blocks = []
+                for k in range(world):
+                    if k == rank:
+                        blocks.append(None)
+                        continue
+                    sh = tracer(b - 1, R, nudge, seed, k, world, faithful)
+                    ro = torch.empty(sh.n_rows + 1, dtype=torch.int64, device=torch.device("cuda", device))
+                    pr = torch.empty((2, max(sh.nnz, 1)), dtype=torch.int32, device=ro.device)
+                    sh.fill(ro, pr[0], pr[1])
+                    sh.done()
+                    blocks.append((ro, pr[:, :sh.nnz]))
+                peers[i] = blocks
+        finally:
+            tracer.close()
+        return cls(rank, world, device, peers)
+
+    def all_sizes(self, band: int, n: int) -> List[int]:
+        p = self.peers.get(band)
+        if p is None:
+            return [n] * self.world
+        return [n if k == self.rank else int(p[k][1].shape[1]) for k in range(self.world)]
+
+    def gather(self, band: int, t, dst: int):
+        import torch
+
+        if self.rank != dst:
+            return None
+        out = []
+        for k in range(self.world):
+            if k == self.rank:
+                out.append(t)
+                continue
+            src = self.peers[band][k][0 if t.dtype == torch.int64 else 1]
+            o = torch.zeros_like(t)
+            if t.dim() == 1:
+                o[:src.shape[0]].copy_(src)
+            else:
+                o[:, :src.shape[1]].copy_(src)
+            out.append(o)
+        return out
+
+
+class HipShardTracer:
+    """One rank's row shard of a band traced on its GPU (rthx_trace_exchange,
+    emitter_begin = rank, emitter_stride = W, counts left on the device).
+    Two results alternate: band i + 1 traces into one while band i's counts
+    are still being copied out of the other."""
+
+    def __init__(self, dom, device: int = 0, n_results: int = 2):
+        import queue
+
+        from ._lib import DeviceResult, device_domain
+
+        self.dd = device_domain(dom, device)
+        self.device = device
+        self.n = dom.flat().n_emitters
+        self._free = queue.Queue()
+        self._all = [DeviceResult() for _ in range(n_results)]
+        for r in self._all:
+            self._free.put(r)
+
+    def __call__(self, bin0: int, R: int, nudge: float, seed: int, begin: int, stride: int, faithful: bool):
+        from . import abi
+        from ._lib import make_args
+
+        flags = abi.RTHX_FLAG_DEVICE_ONLY | (abi.RTHX_FLAG_FAITHFUL_SAMPLING if faithful else 0)
+        args, keep = make_args(bin0, R, nudge, seed, begin, self.n, stride, self.device, flags)
+        res = self._free.get()  # (waits until the worker has copied a result out)
+        try:
+            res.trace(self.dd, args)
+        except Exception:
+            self._free.put(res)
+            raise
+        del keep
+        return _HipShard(res, self._free, begin, stride)
+
+    def close(self):
+        for r in self._all:
+            r.close()
+
+
+class _HipShard:
+    def __init__(self, res, free, begin: int, stride: int):
+        self.res, self._free = res, free
+        self.begin, self.stride = begin, stride
+        self.info = res.info()
+        self.nnz = int(self.info["nnz"])
+        self.n_rows = int(self.info["rows_traced"])
+
+    def fill(self, row_off, cols, counts) -> None:
+        """The block's CSR into tensors: device to device, or through the
+        host for a gloo group's cpu tensors."""
+        import ctypes as C
+
+        from ._lib import check, load
+
+        if row_off.device.type == "cpu":
+            import torch
+
+            rp, c, v = self.res.csr()  # (over all N rows; the block's are begin, begin + stride, ...)
+            lens = np.diff(rp)[self.begin::self.stride]
+            row_off[0] = 0
+            row_off[1:len(lens) + 1] = torch.from_numpy(np.cumsum(lens))
+            cols[:self.nnz] = torch.from_numpy(c[:self.nnz])
+            counts[:self.nnz] = torch.from_numpy(v[:self.nnz].view(np.int32))
+            return
+        check(load().rthx_result_copy_csr_device(self.res.handle, 0, C.c_void_p(row_off.data_ptr()),
+                                                 C.c_void_p(cols.data_ptr()), C.c_void_p(counts.data_ptr())))
+
+    def done(self) -> None:
+        self._free.put(self.res)
+
+
+def merge_row_shards_device(row_offs, cols, counts, n_rows: int, sizes=None, stream=None):
+    """Merge W strided row blocks (block k: rows k, k + W, ...; local row
+    offsets) that lie on one GPU into one CSR in row order with the HIP
+    kernels of rthx_merge_row_shards.  sizes: the blocks' entry counts when
+    known (else read from their offsets).  Returns (row_ptr int64
+    [n_rows + 1], cols int32, counts int32 holding the uint32 bits),
+    enqueued on `stream` (default: torch's current stream)."""
+    import ctypes as C
+
+    import torch
+
+    from ._lib import check, load
+
+    W = len(row_offs)
+    dev = row_offs[0].device
+    if sizes is None:
+        sizes = []
+        for k in range(W):
+            n_k = len(range(k, n_rows, W))
+            sizes.append(int(row_offs[k][n_k].item()) - int(row_offs[k][0].item()))
+    total = int(sum(sizes))
+    row_ptr = torch.empty(n_rows + 1, dtype=torch.int64, device=dev)
+    out_c = torch.empty(max(total, 1), dtype=torch.int32, device=dev)
+    out_n = torch.empty(max(total, 1), dtype=torch.int32, device=dev)
+    arr = C.c_void_p * W
+    ro = arr(*[C.c_void_p(t.data_ptr()) for t in row_offs])
+    cc = arr(*[C.c_void_p(t.data_ptr()) for t in cols])
+    nn = arr(*[C.c_void_p(t.data_ptr()) for t in counts])
+    st = stream if stream is not None else torch.cuda.current_stream(dev)
+    check(load().rthx_merge_row_shards(dev.index, W, n_rows, ro, cc, nn, C.c_void_p(row_ptr.data_ptr()),
+                                       C.c_void_p(out_c.data_ptr()), C.c_void_p(out_n.data_ptr()),
+                                       C.c_void_p(st.cuda_stream)))
+    return row_ptr, out_c[:total], out_n[:total]
+
+
+def merge_row_shards_host(row_offs, cols, counts, n_rows: int):
+    """The same merge on the host (numpy; a gloo group's blocks)."""
+    W = len(row_offs)
+    lens = np.zeros(n_rows, dtype=np.int64)
+    for k in range(W):
+        n_k = len(range(k, n_rows, W))
+        ro = np.asarray(row_offs[k][:n_k + 1], dtype=np.int64)
+        lens[k::W] = np.diff(ro)
+    row_ptr = np.zeros(n_rows + 1, dtype=np.int64)
+    np.cumsum(lens, out=row_ptr[1:])
+    total = int(row_ptr[-1])
+    out_c = np.zeros(total, dtype=np.int32)
+    out_n = np.zeros(total, dtype=np.uint32)
+    for k in range(W):
+        rows = np.arange(k, n_rows, W)
+        ro = np.asarray(row_offs[k][:len(rows) + 1], dtype=np.int64)
+        lk = np.diff(ro)
+        tot = int(lk.sum())
+        if tot == 0:
+            continue
+        dst = np.repeat(row_ptr[rows] - (ro[:-1] - ro[0]), lk) + np.arange(tot)
+        out_c[dst] = np.asarray(cols[k])[ro[0]:ro[0] + tot]
+        out_n[dst] = np.asarray(counts[k]).view(np.uint32)[ro[0]:ro[0] + tot]
+    return row_ptr, out_c, out_n
+
+
+def _assemble_band(comm, band: int, shard, owner: int, n_rows: int, stream):
+    """Band `band`'s block copied out of this rank's trace, gathered to its
+    owner and merged there (runs on the pipeline's second thread).  Returns
+    the owner's (row_ptr, cols, counts) or None on the other ranks."""
+    import torch
+
+    W = comm.world
+    sizes = comm.all_sizes(band, shard.nnz)
+    cap = max(max(sizes), 1)
+    nmax = (n_rows + W - 1) // W
+    dev = comm.device
+    ctx = torch.cuda.stream(stream) if stream is not None else _nullctx()
+    with ctx:
+        row_off = torch.zeros(nmax + 1, dtype=torch.int64, device=dev)
+        pairs = torch.zeros((2, cap), dtype=torch.int32, device=dev)
+        if stream is not None:
+            stream.synchronize()  # (the buffers exist before the library's stream writes them)
+        shard.fill(row_off, pairs[0], pairs[1])
+        shard.done()
+        ros = comm.gather(band, row_off, owner)
+        prs = comm.gather(band, pairs, owner)
+        if ros is None:
+            if stream is not None:
+                stream.synchronize()  # (the gather has read this rank's buffers)
+            return None
+        if dev.type == "cuda":
+            out = merge_row_shards_device(ros, [p[0] for p in prs], [p[1] for p in prs], n_rows, sizes, stream)
+            stream.synchronize()
+            return out
+        return merge_row_shards_host([r.numpy() for r in ros], [p[0].numpy() for p in prs],
+                                     [p[1].numpy() for p in prs], n_rows)
+
+
+class _nullctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
+def trace_bands_row_sharded(dom, rays: int, group=None, seed: int = 1, nudge: float = None, device: int = 0,
+                            faithful: bool = False, overlap: bool = True, tracer=None, comm=None):
+    """C5 (:spectral_variable) over W ranks, row-sharded and pipelined (see the
+    section comment above).  rays: per band, as mesh() (R = rays // N rays
+    per emitter).  Every rank traces its rows of every traced band
+    (traced_bands order); traced band i is assembled on rank i mod W.
+
+    Returns (owned, info): owned maps each traced bin this rank owns
+    (1-based, as traced_bands) to its count matrix in row order (row_ptr,
+    cols, counts) -- tensors on the rank's GPU on an NCCL group (counts:
+    int32 holding the uint32 bits), numpy on gloo -- and info holds each
+    band's trace info and the host-clock timeline (trace and assembly
+    intervals, seconds from the start).  overlap=False assembles each band
+    before the next traces (the sequential form, for comparison).
+    tracer / comm: stand-ins for tests and the one-GPU emulation
+    (tools/bench_c5_bands.py); the product uses HipShardTracer and
+    TorchBandComm."""
+    import threading
+    import time
+    from concurrent.futures import ThreadPoolExecutor
+
+    comm = comm or TorchBandComm(group)
+    W, rank = comm.world, comm.rank
+    if nudge is None:
+        nudge = 10_000 * np.finfo(np.float64).eps
+    traced = traced_bands(dom)
+    N = dom.flat().n_emitters
+    R = rays // N
+    own_tracer = tracer is None
+    tracer = tracer or HipShardTracer(dom, device)
+    stream = None
+    if comm.device.type == "cuda":
+        import torch
+
+        stream = torch.cuda.Stream(device=comm.device)
+    t0 = time.perf_counter()
+    timeline = []
+    lock = threading.Lock()
+
+    def assemble(i, b, shard):
+        import torch
+
+        if comm.device.type == "cuda":
+            torch.cuda.set_device(comm.device)
+        ta = time.perf_counter() - t0
+        out = _assemble_band(comm, i, shard, i % W, N, stream)
+        with lock:
+            timeline.append({"band": b, "what": "assemble", "owner": i % W, "start_s": ta,
+                             "end_s": time.perf_counter() - t0})
+        return out
+
+    owned, infos, futs = {}, [], []
+    ex = ThreadPoolExecutor(max_workers=1) if overlap else None
+    try:
+        for i, (b, _bins) in enumerate(traced):
+            ts = time.perf_counter() - t0
+            shard = tracer(b - 1, R, nudge, seed, rank, W, faithful)
+            te = time.perf_counter() - t0
+            inf = dict(shard.info, bin=b)
+            infos.append(inf)
+            with lock:
+                timeline.append({"band": b, "what": "trace", "start_s": ts, "end_s": te,
+                                 "kernel_ms": inf.get("trace_ms"), "pack_ms": inf.get("pack_ms")})
+            if ex is not None:
+                futs.append((b, ex.submit(assemble, i, b, shard)))
+            else:
+                out = assemble(i, b, shard)
+                if out is not None:
+                    owned[b] = out
+        for b, f in futs:
+            out = f.result()
+            if out is not None:
+                owned[b] = out
+    finally:
+        if ex is not None:
+            ex.shutdown(wait=True)
+        if own_tracer:
+            tracer.close()
+    total = time.perf_counter() - t0
+    timeline.sort(key=lambda e: (e["start_s"], e["what"]))
+    return owned, {"world": W, "rank": rank, "rays_per_emitter": R, "traces": infos, "timeline": timeline,
+                   "wall_s": total, "owner": {b: i % W for i, (b, _) in enumerate(traced)}}

@@ -159,3 +159,112 @@ def test_two_rank_bands_equal_single_process(tmp_path):
         assert np.array_equal(m[f"b{b}_0"], rp)
         assert np.array_equal(m[f"b{b}_1"], cols)
         assert np.array_equal(m[f"b{b}_2"], cnt)
+
+
+class _OracleShards:
+    """Test stand-in for rthx.distributed.HipShardTracer on a CPU-only host:
+    the CPU restatement (oracle, test infrastructure) traces the rank's rows."""
+
+    def __init__(self, flat, threads=2):
+        self.flat, self.threads = flat, threads
+
+    def __call__(self, bin0, R, nudge, seed, begin, stride, faithful):
+        from oracle import oracle
+        from rthx import _lib
+
+        args, _k = _lib.make_args(bin0, R, nudge, seed, begin, self.flat.n_emitters, stride)
+        rp, cols, cnt, info, _ = oracle.trace_exchange(self.flat, args, self.threads)
+        return _HostShard(rp, cols, cnt, info, begin, stride)
+
+
+class _HostShard:
+    def __init__(self, rp, cols, cnt, info, begin, stride):
+        self.rp, self.cols, self.cnt, self.info = rp, cols, cnt, dict(info)
+        self.lens = np.diff(rp)[begin::stride]
+        self.nnz = int(self.lens.sum())
+
+    def fill(self, row_off, cols, counts):
+        row_off[0] = 0
+        row_off[1:len(self.lens) + 1] = torch.from_numpy(np.cumsum(self.lens))
+        cols[:self.nnz] = torch.from_numpy(np.ascontiguousarray(self.cols[:self.nnz], dtype=np.int32))
+        counts[:self.nnz] = torch.from_numpy(np.ascontiguousarray(self.cnt[:self.nnz], dtype=np.uint32).view(np.int32))
+
+    def done(self):
+        pass
+
+
+def _row_sharded_worker(rank, world, port, out_path, overlap):
+    """C5's row-sharded band pipeline over processes (rthx.distributed
+    trace_bands_row_sharded): every rank traces its rows of all 8 bands,
+    band i is gathered to rank i mod W and merged there."""
+    sys.path[:0] = [H.PKG, H.ROOT, os.path.join(H.ROOT, "tests")]
+    import torch.distributed as dist
+
+    from rthx.distributed import trace_bands_row_sharded
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    dom = H.greenhouse_domain(n_layers=4, nx=5, ny=2, n_bins=8)
+    flat = dom.flat()
+    owned, info = trace_bands_row_sharded(dom, 300 * flat.n_emitters, seed=12, nudge=H.NUDGE, overlap=overlap,
+                                          tracer=_OracleShards(flat))
+    assert set(owned) == {b for b, o in info["owner"].items() if o == rank}
+    assert {e["band"] for e in info["timeline"] if e["what"] == "assemble"} == set(info["owner"])
+    np.savez(out_path + f".{rank}.npz", **{f"b{b}_{i}": np.asarray(a) for b, t in owned.items()
+                                           for i, a in enumerate(t)})
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,overlap", [(2, True), (3, False)])
+def test_row_sharded_band_pipeline_equals_single_process(tmp_path, world, overlap):
+    """All 8 bands, each assembled on its owner rank from the ranks' row
+    blocks, bit-identical to the one-process trace of the whole band."""
+    out = str(tmp_path / "rows")
+    mp.spawn(_row_sharded_worker, args=(world, _free_port(), out, overlap), nprocs=world, join=True)
+    from oracle import oracle
+    from rthx import _lib
+    from rthx.distributed import traced_bands
+
+    dom = H.greenhouse_domain(n_layers=4, nx=5, ny=2, n_bins=8)
+    flat = dom.flat()
+    traced = traced_bands(dom)
+    assert len(traced) == 8
+    got = {}
+    for r in range(world):
+        m = np.load(out + f".{r}.npz")
+        for b, _ in traced:
+            if f"b{b}_0" in m:
+                assert b not in got
+                got[b] = (m[f"b{b}_0"], m[f"b{b}_1"], m[f"b{b}_2"])
+    assert set(got) == {b for b, _ in traced}
+    for k, (b, _aliases) in enumerate(traced):
+        args, _k = _lib.make_args(b - 1, 300, H.NUDGE, 12, 0, flat.n_emitters, 1)
+        rp, cols, cnt, _i, _ = oracle.trace_exchange(flat, args, 4)
+        assert np.array_equal(got[b][0], rp)
+        assert np.array_equal(got[b][1], cols)
+        assert np.array_equal(got[b][2].view(np.uint32), cnt)
+
+
+def test_merge_row_shards_host_matches_merge_csr():
+    """The host merge of strided row blocks (the gloo branch) against the
+    general disjoint-block merge, including empty rows and blocks."""
+    from rthx.distributed import merge_csr, merge_row_shards_host
+
+    rng = np.random.default_rng(3)
+    n = 23
+    lens = rng.integers(0, 5, n)
+    lens[[0, 7, 8]] = 0
+    rp = np.concatenate(([0], np.cumsum(lens)))
+    cols = rng.integers(0, n, rp[-1]).astype(np.int32)
+    cnt = rng.integers(1, 2**32 - 1, rp[-1], dtype=np.uint64).astype(np.uint32)
+    for W in (1, 2, 5, 30):
+        ros, cs, ns = [], [], []
+        for k in range(W):
+            rows = np.arange(k, n, W)
+            ro = np.concatenate(([0], np.cumsum(lens[rows])))
+            ros.append(ro)
+            cs.append(np.concatenate([cols[rp[r]:rp[r + 1]] for r in rows]) if rows.size else np.zeros(0, np.int32))
+            ns.append(np.concatenate([cnt[rp[r]:rp[r + 1]] for r in rows]).view(np.int32) if rows.size
+                      else np.zeros(0, np.int32))
+        m = merge_row_shards_host(ros, cs, ns, n)
+        assert np.array_equal(m[0], rp) and np.array_equal(m[1], cols) and np.array_equal(m[2], cnt)

@@ -3,12 +3,18 @@ F_smooth from a 1e8-ray trace within RMS 1e-3 of F_smooth from a 1e9-ray
 reference trace, and the Crosbie & Schrenker centreline after
 solveEquilibrium! on the fine mesh.
 
-The 1e9-ray reference is traced on the device: every row of the device trace
-equals the CPU restatement's row bit for bit (tests/test_gpu_parity.py), and
-this test re-checks that on a strided sample of the 1e9-ray rows, so it is
-the CPU reference's F_raw without the CPU's ~25 s.  Both traces use
-independent seeds, so the RMS measures the Monte Carlo error of the 1e8-ray
-F_smooth.
+The 1e9-ray reference uses the reference's own sampling
+(RTHX_FLAG_FAITHFUL_SAMPLING: acos/sin/cos of the Lambert and volume
+directions and the ABC/CDA triangle split of a cell, as
+emitVolumeRay2D.jl:6-31, emitSurfaceRay2D.jl and lambertSample2D.jl:1-10),
+traced on the device: every row of the device trace equals the CPU
+restatement's row bit for bit (tests/test_gpu_parity.py), and this test
+re-checks that on a strided sample of the 1e9-ray rows in faithful mode, so
+it is the CPU reference's F_raw without the CPU's minutes.  Two 1e8-ray
+traces are held against it: the default (optimized) sampling the bench
+measures, and faithful sampling.  All three use independent seeds, so the
+RMS measures the Monte Carlo error of the 1e8-ray F_smooth (and, for the
+optimized trace, any bias of its sampling against the reference's).
 
 Tolerances: RMS over all N^2 entries of F_smooth <= 1e-3 (north_star); the
 C&S centreline within the reference's rtol 0.05 (test/test_2d_grey.jl:216)
@@ -33,47 +39,59 @@ def traced(hip):
     from rthx.equilibrium import solve_equilibrium
 
     out = {}
-    for rays, seed in ((100_000_000, 21), (1_000_000_000, 22)):
+    # (key: rays, sampling) -> (domain, F_smooth, T after the grey solve)
+    for rays, seed, faithful in ((100_000_000, 21, False), (100_000_000, 23, True), (1_000_000_000, 22, True)):
         dom = H.square_domain(ND)
-        dom(rays, seed=seed, verbose=False)
+        dom(rays, seed=seed, verbose=False, faithful=faithful)
         Fs = np.asarray(dom.F_smooth)
         T, _, _, _ = solve_equilibrium(dom)
-        out[rays] = (dom, Fs, T)
+        out[(rays, "faithful" if faithful else "optimized")] = (dom, Fs, T)
     return out
 
 
+REFERENCE = (1_000_000_000, "faithful")
+
+
 def test_f_smooth_rms_vs_1e9_ray_reference(traced):
-    _, Fa, _ = traced[100_000_000]
-    _, Fb, _ = traced[1_000_000_000]
-    n = Fa.shape[0]
-    assert Fa.shape == Fb.shape == (n, n) and n == 4 * ND + ND * ND
-    d = Fa - Fb
-    rms = float(np.sqrt(np.mean(d * d)))
-    nz = Fb > 0
-    rms_nz = float(np.sqrt(np.mean(d[nz] ** 2)))
-    rel = float(np.linalg.norm(d) / np.linalg.norm(Fb))
-    print(f"F_smooth RMS vs 1e9 rays: all entries {rms:.3e}, nonzero entries {rms_nz:.3e}, "
-          f"relative (Frobenius) {rel:.3e}, max |dF| {np.abs(d).max():.3e}")
+    _, Fb, _ = traced[REFERENCE]
+    n = Fb.shape[0]
+    record = {"config": "101x101 grey kappa=1: F_smooth of 1e8 rays vs F_smooth of the 1e9-ray reference traced "
+                        "with the reference's own sampling (RTHX_FLAG_FAITHFUL_SAMPLING), independent seeds",
+              "n": int(n), "bar": "RMS <= 1e-3 (north_star)", "reference": "1e9 rays, faithful sampling, seed 22"}
+    for sampling in ("optimized", "faithful"):
+        _, Fa, _ = traced[(100_000_000, sampling)]
+        assert Fa.shape == Fb.shape == (n, n) and n == 4 * ND + ND * ND
+        d = Fa - Fb
+        rms = float(np.sqrt(np.mean(d * d)))
+        nz = Fb > 0
+        rms_nz = float(np.sqrt(np.mean(d[nz] ** 2)))
+        rel = float(np.linalg.norm(d) / np.linalg.norm(Fb))
+        print(f"1e8 rays ({sampling}) F_smooth RMS vs the faithful 1e9-ray reference: all entries {rms:.3e}, "
+              f"nonzero entries {rms_nz:.3e}, relative (Frobenius) {rel:.3e}, max |dF| {np.abs(d).max():.3e}")
+        record[f"1e8_{sampling}"] = {"rms_all_entries": rms, "rms_nonzero_entries": rms_nz,
+                                     "nonzero_fraction": float(nz.mean()), "relative_frobenius": rel,
+                                     "max_abs_dF": float(np.abs(d).max())}
+        assert rms <= 1e-3
+        assert rms_nz <= 1e-3
+        assert np.allclose(Fa.sum(axis=1), 1.0, atol=1e-9)
+    assert np.allclose(Fb.sum(axis=1), 1.0, atol=1e-9)
     rec = os.environ.get("RTHX_ACCURACY_RECORD")  # (measurement runs: the numbers as JSON)
     if rec:
+        for key, (dom, _F, T) in traced.items():
+            record.setdefault("crosbie_schrenker_rel_err", {})[f"{key[0]:.0e}_{key[1]}"] = _cs_error(dom, T)
         with open(rec, "w") as f:
-            json.dump({"config": "101x101 grey kappa=1, F_smooth of 1e8 rays vs 1e9 rays (independent seeds)",
-                       "n": int(n), "rms_all_entries": rms, "rms_nonzero_entries": rms_nz,
-                       "nonzero_fraction": float(nz.mean()), "relative_frobenius": rel,
-                       "max_abs_dF": float(np.abs(d).max()), "bar": "RMS <= 1e-3 (north_star)"}, f, indent=1)
-    assert rms <= 1e-3
-    assert rms_nz <= 1e-3
-    assert np.allclose(Fa.sum(axis=1), 1.0, atol=1e-9) and np.allclose(Fb.sum(axis=1), 1.0, atol=1e-9)
+            json.dump(record, f, indent=1)
 
 
 def test_reference_rows_equal_cpu_restatement(hip):
-    """The 1e9-ray reference rows (R = 94295) equal the CPU restatement's on a
-    strided sample of rows (surface and volume emitters)."""
+    """The 1e9-ray reference rows (R = 94295, faithful sampling) equal the
+    CPU restatement's (faithful mode) on a strided sample of rows (surface
+    and volume emitters)."""
     dom = H.square_domain(ND)
     flat = dom.flat()
     N = flat.n_emitters
     R = 1_000_000_000 // N
-    args, _k = hip.make_args(0, R, H.NUDGE, 22, 0, N, 1013)
+    args, _k = hip.make_args(0, R, H.NUDGE, 22, 0, N, 1013, flags=hip.abi.RTHX_FLAG_FAITHFUL_SAMPLING)
     dd = hip.DeviceDomain(flat, 0)
     res = hip.DeviceResult()
     try:
@@ -89,15 +107,20 @@ def test_reference_rows_equal_cpu_restatement(hip):
     assert int(np.sum(g[2] != ocnt)) <= 1e-6 * oinfo["rays_traced"]
 
 
-@pytest.mark.parametrize("rays", [100_000_000, 1_000_000_000])
-def test_crosbie_schrenker_centreline_101(traced, rays):
-    dom, _, T = traced[rays]
+def _cs_error(dom, T):
     cs = H.golden("reference_tables.json")["crosbie_schrenker"]
     tau = np.linspace(1 / (2 * ND), 1 - 1 / (2 * ND), ND)
     ana = H.line_interpolation(cs["relative_tau_z"], cs["source_func_center"], tau)
     Tg = T[dom.num_surfaces:]
     sf = (Tg.reshape(ND, ND)[:, (ND + 1) // 2 - 1] / 1000.0) ** 4
-    err = np.linalg.norm(sf - ana) / max(np.linalg.norm(sf), np.linalg.norm(ana))
-    print(f"{rays:.0e} rays: C&S centreline relative error {err:.4f}")
+    return float(np.linalg.norm(sf - ana) / max(np.linalg.norm(sf), np.linalg.norm(ana)))
+
+
+@pytest.mark.parametrize("key", [(100_000_000, "optimized"), (100_000_000, "faithful"), REFERENCE])
+def test_crosbie_schrenker_centreline_101(traced, key):
+    dom, _, T = traced[key]
+    cs = H.golden("reference_tables.json")["crosbie_schrenker"]
+    err = _cs_error(dom, T)
+    print(f"{key[0]:.0e} rays ({key[1]} sampling): C&S centreline relative error {err:.4f}")
     assert err <= cs["rtol"]
     assert abs(dom.energy_error) < 1e-4

@@ -67,6 +67,56 @@ def test_c1_exact(hip, flags):
     assert_same(gpu_trace(hip, flat, args), oracle.trace_exchange(flat, args, 16))
 
 
+@pytest.mark.parametrize("ndim,flags", [(11, 0), (11, 1), (51, 0)])
+def test_philox10_build_exact(hip, ndim, flags):
+    """The 10-round-Philox build of the exchange tracer (csrc/_build/philox10,
+    the bench's `philox10` leg) equals the restatement built with
+    EMIT_ROUNDS=10 exactly, and differs from the 7-round product."""
+    import ctypes as C
+
+    import bench
+
+    lib = C.CDLL(bench.PHILOX10_LIB, mode=C.RTLD_LOCAL)
+    lib.rthx_last_error.restype = C.c_char_p
+    lib.rthx_domain_create.argtypes = [C.POINTER(hip.abi.DomainDesc), C.c_int32, C.POINTER(C.c_void_p)]
+    lib.rthx_domain_destroy.argtypes = [C.c_void_p]
+    lib.rthx_result_create.argtypes = [C.POINTER(C.c_void_p)]
+    lib.rthx_result_destroy.argtypes = [C.c_void_p]
+    lib.rthx_trace_exchange.argtypes = [C.c_void_p, C.POINTER(hip.abi.TraceArgs), C.c_void_p]
+    lib.rthx_result_get_info.argtypes = [C.c_void_p, C.POINTER(hip.abi.ResultInfo)]
+    lib.rthx_result_copy_csr.argtypes = [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int32),
+                                         C.POINTER(C.c_uint32)]
+    lib.rthx_build_id.restype = C.c_char_p
+    assert lib.rthx_build_id().decode() == hip.source_build_id()
+    flat = H.square_domain(ndim).flat()
+    args, _k = _args(hip, flat, 400_000 // flat.n_emitters + 1, seed=4, flags=flags)
+    h, r = C.c_void_p(), C.c_void_p()
+    assert lib.rthx_domain_create(C.byref(flat.desc), 0, C.byref(h)) == 0, lib.rthx_last_error()
+    assert lib.rthx_result_create(C.byref(r)) == 0
+    try:
+        assert lib.rthx_trace_exchange(h, C.byref(args), r) == 0, lib.rthx_last_error()
+        inf = hip.abi.ResultInfo()
+        assert lib.rthx_result_get_info(r, C.byref(inf)) == 0
+        info = inf.as_dict()
+        rp = np.empty(flat.n_emitters + 1, np.int64)
+        cols = np.empty(max(info["nnz"], 1), np.int32)
+        cnt = np.empty(max(info["nnz"], 1), np.uint32)
+        assert lib.rthx_result_copy_csr(r, hip.abi.ptr(rp, C.c_int64), hip.abi.ptr(cols, C.c_int32),
+                                        hip.abi.ptr(cnt, C.c_uint32)) == 0
+    finally:
+        lib.rthx_result_destroy(r)
+        lib.rthx_domain_destroy(h)
+    g10 = (rp, cols[:info["nnz"]], cnt[:info["nnz"]], info)
+    oracle.use_emit_rounds(10)
+    try:
+        o10 = oracle.trace_exchange(flat, args, 16)
+    finally:
+        oracle.use_emit_rounds(7)
+    assert_same(g10, o10)
+    g7 = gpu_trace(hip, flat, args)
+    assert not (np.array_equal(g7[1], g10[1]) and np.array_equal(g7[2], g10[2]))
+
+
 @pytest.mark.parametrize("ndim", [11, 51])
 def test_axis_rect_kernels_match_general_polygon_kernels(hip, ndim, monkeypatch):
     """Square meshes take the axis-aligned-rectangle kernels (dist_to_rect);
