@@ -428,7 +428,10 @@ def main():
     # device (rthx_result_info superseded / superseded_faults).
     steps_checked = info["superseded"] + 1
     step_faults = int(info["superseded_faults"])
-    bad = step_faults != 0 or (not args.blocking and args.mode != "threads" and steps_checked != args.steps)
+    # (the last step itself: completed by info() after `elapsed` was taken, so
+    # a look-back fallback it needed -- its re-trace untimed -- counts too)
+    bad = (step_faults != 0 or info["lookback_fallbacks"] > 0
+           or (not args.blocking and args.mode != "threads" and steps_checked != args.steps))
     if dist is not None:  # (one decision for every rank: the fallback below has its own barriers)
         import torch
 

@@ -531,8 +531,13 @@ int rthx_scene3d_stats(const rthx_scene3d* scene, int64_t* n_tri, int64_t* n_nod
  * hits are then found from the lattice (the same Moeller-Trumbore test on the
  * candidate cells), the BVH walk covers the interior triangles only, and
  * with 2 a ray leaving an interior polygon away from its edges walks nothing;
- * the counts are those of the plain walk.  hull_tris / interior_tris: the
- * triangles of each kind. */
+ * the counts are those of the plain walk.  *hull = 3: no box hull, but the
+ * scene is one convex enclosure seen from inside (every vertex on or in
+ * front of every emitting plane, e.g. the readme's icosphere with inward
+ * normals): a ray's exit triangle is found from a cube map of exit
+ * directions about the centroid (rthx_trace3d.h CvxPlane), again with the
+ * same test and counts.  hull_tris / interior_tris: the triangles of each
+ * kind (box hull). */
 int rthx_scene3d_hull(const rthx_scene3d* scene, int32_t* hull, int64_t* hull_tris, int64_t* interior_tris);
 int rthx_trace_exchange_3d(rthx_scene3d* scene, const rthx_trace_args* args, rthx_result* res);
 

@@ -832,10 +832,8 @@ int plan_trace_split(const rthx_domain* dom, const rthx_trace_args* a, TracePlan
   int64_t slots = 0;
   rthx::LaunchCfg L = launch_of(dom, a, p);
   L.slots = &slots;
-  if (rthx::launch_trace(L) != hipSuccess || slots <= 0) {  // (occupancy unknown: the plan without a slot split)
-    (void)hipGetLastError();
-    return RTHX_OK;
-  }
+  HIP_TRY(rthx::launch_trace(L), "trace kernel occupancy query");  // (a failed query is a real HIP error)
+  if (slots <= 0) return RTHX_OK;  // (no resident slot reported: the plan without a slot split)
   return plan_trace(dom, a, p, slots);
 }
 

@@ -37,12 +37,14 @@ struct rthx_scene3d {
   int device = 0;
   hipStream_t stream = nullptr;
   hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
-  DevBuf polys, tris, nodes, tables, scene, faces, lines, hull_tris;
+  DevBuf polys, tris, nodes, tables, scene, faces, lines, hull_tris, cvx_planes, cvx_start, cvx_items;
   rthx::DevScene3D S{};
   int64_t n_poly = 0;
   int64_t n_hull_tris = 0, n_in_tris = 0;  // box hull: hull / interior triangles
   bool convex_interior = false;             // box hull: the interior is one convex set (Emit3::convex)
-  int top_choice[16] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};  // LDS node-cache size per kernel variant (launch_trace3d)
+  int top_choice[24] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1,
+                        -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};  // LDS node-cache size per kernel variant (launch_trace3d)
+  int64_t cvx_list_items = 0;  // convex enclosure: entries of the cube map's lists
   int ghist_choice[4] = {-1, -1, -1, -1};  // per (faithful, pack16, N, R): global-histogram form chosen (1) or not (0)
   int64_t ghist_key[4] = {-1, -1, -1, -1};
   ~rthx_scene3d() {
@@ -420,6 +422,117 @@ bool detect_box_hull(const std::vector<rthx::Emit3>& P, int64_t n, const double*
   return hb.lines.size() <= 4096;  // (the kernel stages the lines in LDS: at most 16 KB)
 }
 
+// Convex enclosure seen from inside (rthx_trace3d.h CvxPlane): every vertex
+// on or in front of every polygon's emitting plane (within 1e-12 of the
+// scene scale) and the vertices' centroid strictly inside.  Fills the
+// centroid, the inscribed / circumscribed radii (padded outward), one plane
+// per triangle of `tris` and the cube map's lists; false when the scene is
+// not such an enclosure.
+struct CvxBuild {
+  double c[3] = {0.0, 0.0, 0.0};
+  double rin = 0.0, rout = 0.0;
+  int res = 0;
+  std::vector<rthx::CvxPlane> planes;
+  std::vector<int32_t> start, items;
+};
+
+double angle_between(V a, V b) {  // unit vectors; robust near 0 and pi
+  return std::atan2(norm(cross(a, b)), dot(a, b));
+}
+
+// The unit direction of cube-map face f at (u, v) in [-1, 1]^2 (the inverse
+// of rthx::cvx_cell's mapping).
+V cvx_dir(int f, double u, double v) {
+  const double s = (f & 1) ? -1.0 : 1.0;
+  V m = f < 2 ? V{s, u, v} : f < 4 ? V{v, s, u} : V{u, v, s};
+  return scale(m, 1.0 / norm(m));
+}
+
+bool detect_convex_enclosure(const std::vector<rthx::Emit3>& P, const std::vector<rthx::Tri3>& tris, double scale_,
+                             CvxBuild& cb) {
+  std::vector<V> verts;
+  for (const rthx::Emit3& E : P)
+    for (int i = 0; i < E.nv; ++i) verts.push_back({E.v[i][0], E.v[i][1], E.v[i][2]});
+  std::sort(verts.begin(), verts.end(), [](const V& a, const V& b) {
+    return a.x < b.x || (a.x == b.x && (a.y < b.y || (a.y == b.y && a.z < b.z)));
+  });
+  verts.erase(std::unique(verts.begin(), verts.end(),
+                          [](const V& a, const V& b) { return a.x == b.x && a.y == b.y && a.z == b.z; }),
+              verts.end());
+  const double tol = 1e-12 * scale_;
+  for (const rthx::Emit3& E : P) {
+    const V nn{E.n[0], E.n[1], E.n[2]}, p0{E.v[0][0], E.v[0][1], E.v[0][2]};
+    for (const V& q : verts)
+      if (dot(nn, sub(q, p0)) < -tol) return false;
+  }
+  V c{0.0, 0.0, 0.0};
+  for (const V& q : verts) c = {c.x + q.x, c.y + q.y, c.z + q.z};
+  c = scale(c, 1.0 / (double)verts.size());
+  double rin = 1e300, rout = 0.0;
+  for (const rthx::Emit3& E : P) {
+    const V nn{E.n[0], E.n[1], E.n[2]}, p0{E.v[0][0], E.v[0][1], E.v[0][2]};
+    rin = std::min(rin, dot(nn, sub(c, p0)));
+  }
+  for (const V& q : verts) rout = std::max(rout, norm(sub(q, c)));
+  if (!(rin > 1e-6 * scale_)) return false;  // (the centroid must lie well inside)
+  cb.c[0] = c.x;
+  cb.c[1] = c.y;
+  cb.c[2] = c.z;
+  cb.rin = rin * (1.0 - 1e-9);
+  cb.rout = rout * (1.0 + 1e-9) + 1e-12 * scale_;
+  // one plane per triangle (its polygon's emitting normal)
+  cb.planes.resize(tris.size());
+  std::vector<V> tcen(tris.size());
+  std::vector<double> tha(tris.size());
+  for (size_t t = 0; t < tris.size(); ++t) {
+    const rthx::Tri3& T = tris[t];
+    const rthx::Emit3& E = P[(size_t)T.poly];
+    rthx::CvxPlane& pl = cb.planes[t];
+    for (int k = 0; k < 3; ++k) pl.n[k] = E.n[k];
+    pl.h = E.n[0] * T.v0[0] + E.n[1] * T.v0[1] + E.n[2] * T.v0[2];
+    const V a{T.v0[0], T.v0[1], T.v0[2]};
+    const V b{a.x + T.e1[0], a.y + T.e1[1], a.z + T.e1[2]}, d{a.x + T.e2[0], a.y + T.e2[1], a.z + T.e2[2]};
+    V w[3] = {sub(a, c), sub(b, c), sub(d, c)};
+    for (V& x : w) x = scale(x, 1.0 / norm(x));
+    V m = {w[0].x + w[1].x + w[2].x, w[0].y + w[1].y + w[2].y, w[0].z + w[1].z + w[2].z};
+    m = scale(m, 1.0 / norm(m));
+    tcen[t] = m;
+    // (the spherical triangle lies in the cap through its corners: a cap
+    // under 90 degrees is convex on the sphere)
+    tha[t] = std::max({angle_between(m, w[0]), angle_between(m, w[1]), angle_between(m, w[2])});
+    if (!(tha[t] < 1.4)) return false;  // (a triangle too wide for the cone bound)
+  }
+  std::vector<double> tcos(tris.size()), tsin(tris.size());
+  for (size_t t = 0; t < tris.size(); ++t) {
+    tcos[t] = std::cos(tha[t]);
+    tsin[t] = std::sin(tha[t]);
+  }
+  // cube-map resolution: about two cells per triangle edge across
+  const double per_face = std::sqrt((double)tris.size() / 6.0);
+  cb.res = (int)std::min(64.0, std::max(4.0, std::ceil(2.0 * per_face)));
+  const int res = cb.res;
+  const size_t n_cells = (size_t)6 * res * res;
+  cb.start.assign(n_cells + 1, 0);
+  cb.items.clear();
+  for (int f = 0; f < 6; ++f)
+    for (int j = 0; j < res; ++j)
+      for (int i = 0; i < res; ++i) {
+        const double u0 = -1.0 + 2.0 * i / res, u1 = -1.0 + 2.0 * (i + 1) / res;
+        const double v0 = -1.0 + 2.0 * j / res, v1 = -1.0 + 2.0 * (j + 1) / res;
+        const V cc = cvx_dir(f, 0.5 * (u0 + u1), 0.5 * (v0 + v1));
+        const double ha = std::max({angle_between(cc, cvx_dir(f, u0, v0)), angle_between(cc, cvx_dir(f, u1, v0)),
+                                    angle_between(cc, cvx_dir(f, u0, v1)), angle_between(cc, cvx_dir(f, u1, v1))});
+        const size_t cell = ((size_t)f * res + j) * res + i;
+        // angle(cc, tcen) <= a + tha  <=>  cc . tcen >= cos(a) cos(tha) - sin(a) sin(tha)
+        // (a + tha < pi; the cosine falls on [0, pi])
+        const double a = ha + rthx::kCvxMaxArc + rthx::kCvxPad, ca = std::cos(a), sa = std::sin(a);
+        for (size_t t = 0; t < tris.size(); ++t)
+          if (dot(cc, tcen[t]) >= ca * tcos[t] - sa * tsin[t] - 1e-12) cb.items.push_back((int32_t)t);
+        cb.start[cell + 1] = (int32_t)cb.items.size();
+      }
+  return true;
+}
+
 // Leaf references of `nodes` shifted by `tri_off` triangles and inner
 // references by `node_off` nodes (a BVH appended behind another).
 void shift_bvh(std::vector<rthx::Bvh2Node>& nodes, int32_t node_off, int32_t tri_off) {
@@ -563,6 +676,7 @@ RTHX_EXPORT int rthx_scene3d_create_grouped(const double* xyz, const int32_t* nv
   const char* no_hull = rthx::knob("RTHX_T3_NO_HULL");
   const bool hull = group && !(no_hull && no_hull[0] == '1') && detect_box_hull(polys, n, slo, shi, hb);
   std::vector<rthx::Tri3> hull_tris;
+  bool interior_convex = false;  // (box hull: the interior pass's finding, whatever the polygon order)
   int32_t full_root = 0, n_in_nodes = (int32_t)nodes.size();
   int64_t n_in_tris = (int64_t)tris.size();
   if (hull) {
@@ -622,6 +736,7 @@ RTHX_EXPORT int rthx_scene3d_create_grouped(const double* xyz, const int32_t* nv
       if (convex)
         for (int64_t k = 0; k < n; ++k)
           if (!hb.in_hull[(size_t)k]) polys[(size_t)k].convex = 1;
+      interior_convex = convex;
       // the interior's bounding ball: centre the vertices' mean, radius the
       // farthest vertex, padded by 1e-9 relative plus 1e-12 of the scene
       // (every interior triangle lies within it: convex combinations)
@@ -643,6 +758,11 @@ RTHX_EXPORT int rthx_scene3d_create_grouped(const double* xyz, const int32_t* nv
     all_tris.insert(all_tris.end(), tris_sorted.begin(), tris_sorted.end());
     tris_sorted.swap(all_tris);
   }
+  // Convex enclosure seen from inside (no box hull): the cube map of exit
+  // directions (rthx_trace3d.h CvxPlane)
+  CvxBuild cvb;
+  const char* no_cvx = rthx::knob("RTHX_T3_NO_CVX");
+  const bool cvx = !hull && !(no_cvx && no_cvx[0] == '1') && detect_convex_enclosure(polys, tris_sorted, scale, cvb);
   std::vector<double> tables(rthx::kTableDoubles);
   rthx::fill_tables(tables.data());
 
@@ -656,7 +776,7 @@ RTHX_EXPORT int rthx_scene3d_create_grouped(const double* xyz, const int32_t* nv
   s->device = device;
   s->n_poly = n;
   s->n_hull_tris = (int64_t)hull_tris.size();
-  s->convex_interior = hull && n_in_tris > 0 && polys[(size_t)(n - 1)].convex == 1;
+  s->convex_interior = hull && n_in_tris > 0 && interior_convex;
   s->n_in_tris = n_in_tris;
   auto bail = [&](int code) {
     delete s;
@@ -678,6 +798,10 @@ RTHX_EXPORT int rthx_scene3d_create_grouped(const double* xyz, const int32_t* nv
                !up(s->lines, hb.lines.data(), hb.lines.size() * sizeof(float)) ||
                !up(s->hull_tris, hull_tris.data(), hull_tris.size() * sizeof(rthx::Tri3))))
     return bail(fail(RTHX_ENOMEM, "uploading the 3D scene's box hull"));
+  if (cvx && (!up(s->cvx_planes, cvb.planes.data(), cvb.planes.size() * sizeof(rthx::CvxPlane)) ||
+              !up(s->cvx_start, cvb.start.data(), cvb.start.size() * 4) ||
+              !up(s->cvx_items, cvb.items.data(), std::max<size_t>(cvb.items.size(), 1) * 4)))
+    return bail(fail(RTHX_ENOMEM, "uploading the 3D scene's exit-direction map"));
   s->S.n_poly = (int32_t)n;
   s->S.n_tri = (int32_t)tris.size();
   s->S.n_nodes = (int32_t)nodes.size();
@@ -699,6 +823,17 @@ RTHX_EXPORT int rthx_scene3d_create_grouped(const double* xyz, const int32_t* nv
   s->S.faces = hull ? s->faces.as<rthx::HullFace>() : nullptr;
   s->S.hull_lines = hull ? s->lines.as<float>() : nullptr;
   s->S.hull_tris = hull ? s->hull_tris.as<rthx::Tri3>() : nullptr;
+  s->S.cvx = cvx ? 1 : 0;
+  s->S.cvx_res = cvx ? cvb.res : 0;
+  s->S.cvx_cos_arc = (float)std::cos(2.0 * rthx::kCvxMaxArc);
+  s->S.cvx_tpad = (float)(1e-9 * scale);
+  for (int k = 0; k < 3; ++k) s->S.cvx_c[k] = cvb.c[k];
+  s->S.cvx_rin2 = cvb.rin * cvb.rin;
+  s->S.cvx_rout2 = cvb.rout * cvb.rout;
+  s->S.cvx_planes = cvx ? s->cvx_planes.as<rthx::CvxPlane>() : nullptr;
+  s->S.cvx_start = cvx ? s->cvx_start.as<int32_t>() : nullptr;
+  s->S.cvx_items = cvx ? s->cvx_items.as<int32_t>() : nullptr;
+  s->cvx_list_items = cvx ? (int64_t)cvb.items.size() : 0;
   if (!up(s->scene, &s->S, sizeof(s->S))) return bail(fail(RTHX_ENOMEM, "uploading the 3D scene"));
   if (rthx::knob("RTHX_VERBOSE"))
     std::fprintf(stderr, "rthx_scene3d_create: host geometry + BVH %.2f ms, device setup + upload %.2f ms\n",
@@ -721,7 +856,7 @@ RTHX_EXPORT int rthx_scene3d_stats(const rthx_scene3d* sc, int64_t* n_tri, int64
 
 RTHX_EXPORT int rthx_scene3d_hull(const rthx_scene3d* sc, int32_t* hull, int64_t* hull_tris, int64_t* interior_tris) {
   if (!sc) return fail(RTHX_EINVAL, "null scene");
-  if (hull) *hull = sc->S.hull ? (sc->convex_interior ? 2 : 1) : 0;
+  if (hull) *hull = sc->S.hull ? (sc->convex_interior ? 2 : 1) : sc->S.cvx ? 3 : 0;
   if (hull_tris) *hull_tris = sc->n_hull_tris;
   if (interior_tris) *interior_tris = sc->n_in_tris;
   return RTHX_OK;
@@ -752,7 +887,15 @@ RTHX_EXPORT int rthx_trace_exchange_3d(rthx_scene3d* sc, const rthx_trace_args* 
   if (n_rows > 0 && R >= 2 * kSplitMinRays)
     split = std::max<int64_t>(1, std::min<int64_t>((split_target + n_rows - 1) / n_rows, R / kSplitMinRays));
   const bool pack16 = (R + split - 1) / split < 65536;
-  const size_t lds_bytes = rthx::trace3d_dynamic_lds(pack16 ? (N + 1) / 2 : N, sc->S.stack, sc->S.n_hull_lines);
+  // A box hull's face records and lattice lines sit in LDS beside the row
+  // histogram and the stacks; when they do not fit, the plain walk of the
+  // whole scene's BVH (root full_root) traces the scene instead.
+  bool use_hull = sc->S.hull != 0;
+  size_t lds_bytes = rthx::trace3d_dynamic_lds(pack16 ? (N + 1) / 2 : N, sc->S.stack, use_hull ? sc->S.n_hull_lines : -1);
+  if (use_hull && lds_bytes + rthx::kTrace3dStaticLds > rthx::kMaxLdsBytes) {
+    use_hull = false;
+    lds_bytes = rthx::trace3d_dynamic_lds(pack16 ? (N + 1) / 2 : N, sc->S.stack, -1);
+  }
   if (lds_bytes + rthx::kTrace3dStaticLds > rthx::kMaxLdsBytes)
     return fail(RTHX_ERANGE, "N too large for the LDS row histogram and walk stacks of the 3D tracer");
   if (n_rows * split >= (int64_t(1) << 31)) return fail(RTHX_ERANGE, "too many rows in one call");
@@ -821,7 +964,8 @@ RTHX_EXPORT int rthx_trace_exchange_3d(rthx_scene3d* sc, const rthx_trace_args* 
     L.faithful = (a->flags & RTHX_FLAG_FAITHFUL_SAMPLING) != 0;
     L.pack16 = pack16;
     L.top_choice = sc->top_choice;
-    L.hull = sc->S.hull != 0;
+    L.hull = use_hull;
+    L.cvx = sc->S.cvx != 0;
     // The global-histogram form when its LDS (the stacks alone) keeps more
     // workgroups resident than the LDS histogram's (RTHX_T3_GHIST=0/1 forces).
     const char* gh = rthx::knob("RTHX_T3_GHIST");
@@ -832,7 +976,7 @@ RTHX_EXPORT int rthx_trace_exchange_3d(rthx_scene3d* sc, const rthx_trace_args* 
       const int64_t key = N * 2 + (pack16 ? 1 : 0);
       if (sc->ghist_key[slot_k] != key) {
         int wh = 0, wg = 0;
-        HIP_TRY(rthx::trace3d_occupancy(L, lds_bytes, rthx::trace3d_dynamic_lds(0, sc->S.stack, sc->S.n_hull_lines), &wh, &wg),
+        HIP_TRY(rthx::trace3d_occupancy(L, lds_bytes, rthx::trace3d_dynamic_lds(0, sc->S.stack, use_hull ? sc->S.n_hull_lines : -1), &wh, &wg),
                 "3D tracer occupancy");
         // (more than a quarter more workgroups: at config 4 L3 the GH form's
         // 6 against the histogram's 5 measured 4 % slower -- a returnless
@@ -842,7 +986,7 @@ RTHX_EXPORT int rthx_trace_exchange_3d(rthx_scene3d* sc, const rthx_trace_args* 
       }
       L.ghist = sc->ghist_choice[slot_k] == 1;
     }
-    if (L.ghist) L.lds_bytes = rthx::trace3d_dynamic_lds(0, sc->S.stack, sc->S.n_hull_lines);
+    if (L.ghist) L.lds_bytes = rthx::trace3d_dynamic_lds(0, sc->S.stack, use_hull ? sc->S.n_hull_lines : -1);
     HIP_TRY(rthx::launch_trace3d(L), "trace_exchange_3d_kernel launch");
   }
   HIP_TRY(hipEventRecord(sc->ev[1], st), "hipEventRecord");

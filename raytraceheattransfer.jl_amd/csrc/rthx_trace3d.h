@@ -85,6 +85,65 @@ constexpr int kHullFaceWords = 6 * 12;  // the six face records, as the kernel s
 constexpr float kHullMargin = 1e-4f;  // candidate margin, relative to the box's largest extent
 constexpr float kHullMinDir = 1e-6f;  // smallest |direction component| the hull path takes
 
+// Convex enclosure seen from inside (rthx_trace3d.cpp detect_convex_enclosure,
+// e.g. the readme's icosphere with its inward normals): every vertex lies on
+// or in front of every polygon's emitting plane, so the scene is one convex
+// body whose polygons all emit into it, and a ray leaves it exactly once.
+// Its exit point p lies on the boundary, so between the inscribed ball (the
+// smallest plane distance from the vertices' centroid c) and the
+// circumscribed one (the largest vertex distance): on the part of the ray
+// from where it leaves the inscribed ball (or its origin, when it misses
+// that ball) to where it leaves the circumscribed one.  The directions from
+// c of that part lie in a cap about m (the sum of its two end directions);
+// a cube map of directions about c lists, for each of its cells, every
+// triangle whose central projection could meet a cap of radius kCvxMaxArc
+// about a direction in the cell (cones of the cell and the triangle, padded
+// by kCvxPad).  A ray (a deep one, as Emit3::convex) whose cap is within
+// kCvxMaxArc tests the triangles of m's cell only: their exit-plane
+// distances first (the nearest, t_min), then the fp64 Moeller-Trumbore test
+// with the walk's (t, id) rule on those whose plane lies within
+// kCvxTRel of t_min -- any triangle that Moeller-Trumbore can accept lies
+// at the exit point, within rounding.  Rays with a longer cap, a grazing
+// exit (|cos| < kCvxMinExitCos) or no hit walk the BVH as before.
+struct alignas(16) CvxPlane {
+  double n[3];  // the polygon's emitting (inward) unit normal
+  double h;     // n . v0: inside is n . x >= h
+};
+constexpr double kCvxMaxArc = 0.02;      // largest half-arc (radians) the fast path takes
+constexpr double kCvxPad = 2e-3;         // list padding (radians): fp32 direction arithmetic
+constexpr float kCvxTRel = 1e-5f;        // relative window above t_min for the fp64 test
+constexpr double kCvxMinExitCos = 1e-3;  // |n . d| of the exit plane below this: walk
+
+// Cube-map cell of direction m (need not be unit): face 2 * axis + (m_axis < 0)
+// of the dominant axis, u / v the other two coordinates over it, as
+// (x: y, z), (y: z, x), (z: x, y).  Shared by the host's lists and the kernel.
+__host__ __device__ inline int cvx_cell(float m0, float m1, float m2, int res) {
+  const float a0 = fabsf(m0), a1 = fabsf(m1), a2 = fabsf(m2);
+  int f;
+  float u, v, a;
+  if (a0 >= a1 && a0 >= a2) {
+    f = m0 < 0.0f ? 1 : 0;
+    a = a0;
+    u = m1;
+    v = m2;
+  } else if (a1 >= a2) {
+    f = m1 < 0.0f ? 3 : 2;
+    a = a1;
+    u = m2;
+    v = m0;
+  } else {
+    f = m2 < 0.0f ? 5 : 4;
+    a = a2;
+    u = m0;
+    v = m1;
+  }
+  const float s = 0.5f * (float)res / a;
+  int i = (int)((u + a) * s), j = (int)((v + a) * s);
+  i = i < 0 ? 0 : i > res - 1 ? res - 1 : i;
+  j = j < 0 ? 0 : j > res - 1 ? res - 1 : j;
+  return (f * res + j) * res + i;
+}
+
 struct DevScene3D {
   int32_t n_poly, n_tri, n_nodes;
   int32_t stack;  // walk stack entries a lane needs (inner-node depth of the BVHs)
@@ -107,6 +166,16 @@ struct DevScene3D {
   const HullFace RTHX_GLOBAL* faces;       // [6]
   const float RTHX_GLOBAL* hull_lines;     // lattice lines relative to the box corner
   const Tri3 RTHX_GLOBAL* hull_tris;       // [2 x cells], cell order, (v0 v1 v2), (v2 v3 v0)
+  // convex enclosure seen from inside (CvxPlane): 1 = the fast path
+  int32_t cvx;
+  int32_t cvx_res;           // cube-map cells per face edge
+  float cvx_cos_arc;         // cos(2 kCvxMaxArc): the longest arc (between the cap's ends) taken
+  float cvx_tpad;            // absolute window above t_min (1e-9 of the scene scale)
+  double cvx_c[3];           // the vertices' centroid
+  double cvx_rin2, cvx_rout2;  // squared inscribed (shrunk 1e-9) and circumscribed (grown 1e-9) radii
+  const CvxPlane RTHX_GLOBAL* cvx_planes;  // per triangle of `tris` (BVH order)
+  const int32_t RTHX_GLOBAL* cvx_start;    // [6 res^2 + 1] list offsets per cell
+  const int32_t RTHX_GLOBAL* cvx_items;    // triangle indices into `tris`
 };
 
 constexpr uint32_t kTrace3dTag = 0x40000000u;  // Philox counter word 3 of the 3D tracer
@@ -143,7 +212,8 @@ struct Trace3dLaunch {
   bool pack16;  // < 65536 rays per workgroup: u16 row-histogram counters
   bool ghist;   // counts straight to the dense rows (no LDS histogram)
   bool hull;    // box hull fast path (DevScene3D::hull)
-  int* top_choice;  // [hull * 8 + ghist * 4 + faithful * 2 + pack16]: LDS node-cache size (64 / 128), -1 = not chosen yet
+  bool cvx;     // convex-enclosure fast path (DevScene3D::cvx)
+  int* top_choice;  // [mode * 8 + ghist * 4 + faithful * 2 + pack16] (mode 0 plain, 1 hull, 2 cvx): LDS node-cache size (64 / 128), -1 = not chosen yet
 };
 
 hipError_t launch_trace3d(const Trace3dLaunch& L);

@@ -234,6 +234,61 @@ struct Walk {
     return c < 0.0 || (b < 0.0 && b * b > c);
   }
 
+  // Convex enclosure seen from inside (rthx_trace3d.h CvxPlane, DevScene3D::cvx):
+  // the nearest hit among the triangles listed for the cube-map cell of the
+  // ray's exit cap, into best_*; false when the fast path does not apply
+  // (a long cap, a grazing exit) or finds no hit -- the ray then walks the
+  // BVH, and best_* are untouched unless a hit was found.
+  __device__ __forceinline__ bool convex_exit(const DevScene3D& S) {
+    const double q0 = o[0] - S.cvx_c[0], q1 = o[1] - S.cvx_c[1], q2 = o[2] - S.cvx_c[2];
+    const double b = __builtin_fma(q0, d[0], __builtin_fma(q1, d[1], q2 * d[2]));  // q . d (|d| = 1)
+    const double qq = __builtin_fma(q0, q0, __builtin_fma(q1, q1, q2 * q2));
+    const double bb = b * b;
+    // leaving the circumscribed ball (the origin lies inside it), and the
+    // inscribed one (its far root; none, or behind: from the origin)
+    const double t_out = -b + sqrt(fmax(bb - (qq - S.cvx_rout2), 0.0));
+    const double din = bb - (qq - S.cvx_rin2);
+    const double t_lo = din > 0.0 ? fmax(-b + sqrt(din), 0.0) : 0.0;
+    float A0 = (float)__builtin_fma(t_lo, d[0], q0), A1 = (float)__builtin_fma(t_lo, d[1], q1),
+          A2 = (float)__builtin_fma(t_lo, d[2], q2);
+    float B0 = (float)__builtin_fma(t_out, d[0], q0), B1 = (float)__builtin_fma(t_out, d[1], q1),
+          B2 = (float)__builtin_fma(t_out, d[2], q2);
+    const float ia = __builtin_amdgcn_rsqf(__builtin_fmaf(A0, A0, __builtin_fmaf(A1, A1, A2 * A2)));
+    const float ib = __builtin_amdgcn_rsqf(__builtin_fmaf(B0, B0, __builtin_fmaf(B1, B1, B2 * B2)));
+    A0 *= ia; A1 *= ia; A2 *= ia;
+    B0 *= ib; B1 *= ib; B2 *= ib;
+    // (NaN fails: a degenerate end falls back to the walk)
+    if (!(__builtin_fmaf(A0, B0, __builtin_fmaf(A1, B1, A2 * B2)) >= S.cvx_cos_arc)) return false;
+    const int cell = cvx_cell(A0 + B0, A1 + B1, A2 + B2, S.cvx_res);
+    const int k0 = S.cvx_start[cell], k1 = S.cvx_start[cell + 1];
+    // pass 1: the nearest exit plane among the cell's triangles (fp64 plane
+    // distance and slope, their quotient in fp32)
+    float t_min = __builtin_inff();
+    double nd_min = 0.0;
+    for (int k = k0; k < k1; ++k) {
+      const CvxPlane P = S.cvx_planes[S.cvx_items[k]];
+      const double nd = __builtin_fma(P.n[0], d[0], __builtin_fma(P.n[1], d[1], P.n[2] * d[2]));
+      const double num = P.h - __builtin_fma(P.n[0], o[0], __builtin_fma(P.n[1], o[1], P.n[2] * o[2]));
+      const float t = (float)num / (float)nd;
+      if (nd < 0.0 && t < t_min) {
+        t_min = t;
+        nd_min = nd;
+      }
+    }
+    if (!(t_min < __builtin_inff()) || !(-nd_min >= kCvxMinExitCos)) return false;
+    // pass 2: Moeller-Trumbore on the triangles whose plane the ray meets
+    // at the exit point (within kCvxTRel)
+    const float lim = __builtin_fmaf(t_min, kCvxTRel, t_min) + S.cvx_tpad;
+    for (int k = k0; k < k1; ++k) {
+      const int idx = S.cvx_items[k];
+      const CvxPlane P = S.cvx_planes[idx];
+      const double nd = __builtin_fma(P.n[0], d[0], __builtin_fma(P.n[1], d[1], P.n[2] * d[2]));
+      const double num = P.h - __builtin_fma(P.n[0], o[0], __builtin_fma(P.n[1], o[1], P.n[2] * o[2]));
+      if (nd < 0.0 && (float)num / (float)nd <= lim) consider(S.tris[idx]);
+    }
+    return best_poly >= 0;
+  }
+
   // Lattice cells [lo, hi] of the lines [0, n] within margin m of p
   // (first guess from the uniform spacing, then corrected).
   static __device__ __forceinline__ void cell_range(const float RTHX_LDS* L, int n, float inv, float p, float m,
@@ -356,9 +411,13 @@ __device__ __forceinline__ void emit_ray(const Emit3& E, const double* tab, uint
 // from the face lattices and the walk covers the interior BVH (root 0; its
 // top is the LDS cache), or the whole scene's (full_root) when the hull path
 // does not apply.
-template <bool FAITHFUL, bool PACK16, int TOP, bool GH = false, bool HULL = false>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(HULL ? kHullWaves : GH ? kGhWaves : kHistWaves))) void trace_exchange_3d_kernel(const DevScene3D* __restrict__ Sp,
+// MODE: 0 the BVH walk alone, 1 box hull (HULL), 2 convex enclosure seen
+// from inside (CVX: DevScene3D::cvx; rays the fast path does not take walk
+// the whole scene's BVH, root 0).
+template <bool FAITHFUL, bool PACK16, int TOP, bool GH = false, int MODE = 0>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(MODE == 1 ? kHullWaves : GH ? kGhWaves : kHistWaves))) void trace_exchange_3d_kernel(const DevScene3D* __restrict__ Sp,
                                                                                   TraceParams P, TallyParams T) {
+  constexpr bool HULL = MODE == 1, CVX = MODE == 2;
   // dynamic LDS: [row histogram][walk stacks] (GH: the stacks only)
   extern __shared__ uint32_t hist[];
   __shared__ Bvh2Node s_top[TOP];
@@ -443,10 +502,12 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(HULL ?
           emit_ray<FAITHFUL>(*(const Emit3*)em, s_tab, (uint32_t)g, r, P.key0, P.key1,
                              o, d, deep);
           w.init(o, d);
+          if (MODE == 0) w.node = S.full_root;  // (a box-hull scene whose hull records did not fit in LDS: the whole BVH)
           if (HULL)  // (a convex interior emitter's deep ray, or one that misses the interior's ball, meets no interior triangle: no walk)
             w.node = w.hull_hit(S, grp, hf, hl)
                          ? (S.n_in_nodes > 0 && !(convex && deep) && w.meets_ball(S) ? 0 : kWalkDone)
                          : S.full_root;
+          if (CVX && deep && w.convex_exit(S)) w.node = kWalkDone;
           live = true;
         }
       }
@@ -466,10 +527,12 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(HULL ?
                        P.key1, o, d, deep);
     Walk w;
     w.init(o, d);
+    if (MODE == 0) w.node = S.full_root;
     if (HULL)
       w.node = w.hull_hit(S, grp, hf, hl)
                    ? (S.n_in_nodes > 0 && !(convex && deep) && w.meets_ball(S) ? 0 : kWalkDone)
                    : S.full_root;
+    if (CVX && deep && w.convex_exit(S)) w.node = kWalkDone;
     while (w.step(S, topo, n_top, grp, glo, glen, stk)) {
     }
     tally(w.best_poly);
@@ -490,24 +553,24 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(HULL ?
 
 namespace {
 
-template <bool FAITHFUL, bool PACK16, bool GH, bool HULL>
+template <bool FAITHFUL, bool PACK16, bool GH, int MODE>
 hipError_t launch_variant(const Trace3dLaunch& L) {
   // The 128-node cache when it costs no workgroup per CU against the 64-node
   // one (occupancy queries are slow host calls: the choice is kept per scene
   // and kernel variant in L.top_choice).
-  int& top = L.top_choice[(HULL ? 8 : 0) + (GH ? 4 : 0) + (FAITHFUL ? 2 : 0) + (PACK16 ? 1 : 0)];
+  int& top = L.top_choice[MODE * 8 + (GH ? 4 : 0) + (FAITHFUL ? 2 : 0) + (PACK16 ? 1 : 0)];
   if (top < 0) {
     int pc64 = 0, pc128 = 0;
     hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &pc64, (const void*)t3::trace_exchange_3d_kernel<FAITHFUL, PACK16, 64, GH, HULL>, t3::kThreads, L.lds_bytes);
+        &pc64, (const void*)t3::trace_exchange_3d_kernel<FAITHFUL, PACK16, 64, GH, MODE>, t3::kThreads, L.lds_bytes);
     if (e != hipSuccess) return e;
     e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &pc128, (const void*)t3::trace_exchange_3d_kernel<FAITHFUL, PACK16, 128, GH, HULL>, t3::kThreads, L.lds_bytes);
+        &pc128, (const void*)t3::trace_exchange_3d_kernel<FAITHFUL, PACK16, 128, GH, MODE>, t3::kThreads, L.lds_bytes);
     if (e != hipSuccess) return e;
     top = pc128 > 0 && pc128 >= pc64 ? 128 : 64;
   }
-  auto kern = top == 128 ? t3::trace_exchange_3d_kernel<FAITHFUL, PACK16, 128, GH, HULL>
-                         : t3::trace_exchange_3d_kernel<FAITHFUL, PACK16, 64, GH, HULL>;
+  auto kern = top == 128 ? t3::trace_exchange_3d_kernel<FAITHFUL, PACK16, 128, GH, MODE>
+                         : t3::trace_exchange_3d_kernel<FAITHFUL, PACK16, 64, GH, MODE>;
   if (L.lds_bytes > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.lds_bytes);
     if (e != hipSuccess) return e;
@@ -519,32 +582,34 @@ hipError_t launch_variant(const Trace3dLaunch& L) {
 
 }  // namespace
 
-template <bool HULL>
+template <int MODE>
 hipError_t launch_trace3d_h(const Trace3dLaunch& L) {
-  if (L.ghist) return L.faithful ? launch_variant<true, false, true, HULL>(L) : launch_variant<false, false, true, HULL>(L);
-  if (L.faithful) return L.pack16 ? launch_variant<true, true, false, HULL>(L) : launch_variant<true, false, false, HULL>(L);
-  return L.pack16 ? launch_variant<false, true, false, HULL>(L) : launch_variant<false, false, false, HULL>(L);
+  if (L.ghist) return L.faithful ? launch_variant<true, false, true, MODE>(L) : launch_variant<false, false, true, MODE>(L);
+  if (L.faithful) return L.pack16 ? launch_variant<true, true, false, MODE>(L) : launch_variant<true, false, false, MODE>(L);
+  return L.pack16 ? launch_variant<false, true, false, MODE>(L) : launch_variant<false, false, false, MODE>(L);
 }
 
 hipError_t launch_trace3d(const Trace3dLaunch& L) {
-  return L.hull ? launch_trace3d_h<true>(L) : launch_trace3d_h<false>(L);
+  return L.hull ? launch_trace3d_h<1>(L) : L.cvx ? launch_trace3d_h<2>(L) : launch_trace3d_h<0>(L);
 }
 
 // Resident workgroups per CU of the LDS-histogram and the global-histogram
 // forms (the host keeps the global one when it fits more).
+template <int MODE>
+void occupancy_kernels(const Trace3dLaunch& L, const void** kh, const void** kg) {
+  *kh = L.faithful ? (L.pack16 ? (const void*)t3::trace_exchange_3d_kernel<true, true, 64, false, MODE>
+                               : (const void*)t3::trace_exchange_3d_kernel<true, false, 64, false, MODE>)
+                   : (L.pack16 ? (const void*)t3::trace_exchange_3d_kernel<false, true, 64, false, MODE>
+                               : (const void*)t3::trace_exchange_3d_kernel<false, false, 64, false, MODE>);
+  *kg = L.faithful ? (const void*)t3::trace_exchange_3d_kernel<true, false, 64, true, MODE>
+                   : (const void*)t3::trace_exchange_3d_kernel<false, false, 64, true, MODE>;
+}
+
 hipError_t trace3d_occupancy(const Trace3dLaunch& L, size_t lds_hist, size_t lds_gh, int* wg_hist, int* wg_gh) {
-  const void* kh = L.hull ? (L.faithful ? (L.pack16 ? (const void*)t3::trace_exchange_3d_kernel<true, true, 64, false, true>
-                                                     : (const void*)t3::trace_exchange_3d_kernel<true, false, 64, false, true>)
-                                         : (L.pack16 ? (const void*)t3::trace_exchange_3d_kernel<false, true, 64, false, true>
-                                                     : (const void*)t3::trace_exchange_3d_kernel<false, false, 64, false, true>))
-                          : (L.faithful ? (L.pack16 ? (const void*)t3::trace_exchange_3d_kernel<true, true, 64, false>
-                                                     : (const void*)t3::trace_exchange_3d_kernel<true, false, 64, false>)
-                                         : (L.pack16 ? (const void*)t3::trace_exchange_3d_kernel<false, true, 64, false>
-                                                     : (const void*)t3::trace_exchange_3d_kernel<false, false, 64, false>));
-  const void* kg = L.hull ? (L.faithful ? (const void*)t3::trace_exchange_3d_kernel<true, false, 64, true, true>
-                                         : (const void*)t3::trace_exchange_3d_kernel<false, false, 64, true, true>)
-                          : (L.faithful ? (const void*)t3::trace_exchange_3d_kernel<true, false, 64, true>
-                                         : (const void*)t3::trace_exchange_3d_kernel<false, false, 64, true>);
+  const void *kh = nullptr, *kg = nullptr;
+  if (L.hull) occupancy_kernels<1>(L, &kh, &kg);
+  else if (L.cvx) occupancy_kernels<2>(L, &kh, &kg);
+  else occupancy_kernels<0>(L, &kh, &kg);
   hipError_t e = hipSuccess;
   if (lds_hist > 64 * 1024) e = hipFuncSetAttribute(kh, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_hist);
   if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(wg_hist, kh, t3::kThreads, lds_hist);

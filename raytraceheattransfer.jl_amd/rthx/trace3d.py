@@ -74,7 +74,9 @@ class Scene3D:
         if hasattr(self._lib, "rthx_scene3d_hull"):  # rthx_scene3d_hull: the box-hull fast path
             h, ht, it = C.c_int32(), C.c_int64(), C.c_int64()
             check(self._lib.rthx_scene3d_hull(self.handle, C.byref(h), C.byref(ht), C.byref(it)))
-            out.update(hull=h.value > 0, convex_interior=h.value == 2, hull_tris=ht.value, interior_tris=it.value)
+            # (0 none, 1 box hull, 2 box hull + convex interior, 3 convex enclosure seen from inside)
+            out.update(hull=h.value in (1, 2), convex_interior=h.value == 2, convex_enclosure=h.value == 3,
+                       hull_mode=h.value, hull_tris=ht.value, interior_tris=it.value)
         return out
 
     def close(self) -> None:

@@ -317,3 +317,68 @@ def test_box_hull_not_taken(hip, monkeypatch):
     assert not st["hull"]
     C, lost = oracle.trace_exchange_3d(xyz, nv, nrm, 2000, seed=16, nthreads=16, groups=g)
     assert np.array_equal(D, C)
+
+
+def _icosphere_inside(level):
+    """The readme's icosphere enclosure seen from inside (readme.md:532-704):
+    its triangles with their inward normals (ViewFactorDomain3D)."""
+    from test_gpu_known_answers import _icosphere_domain
+
+    dom, _eq = _icosphere_domain(level)
+    xyz, nv = dom.polygon_arrays()
+    normals = np.array([s.inwardNormal for s in dom.subfaces()])
+    return xyz, nv, normals
+
+
+@pytest.mark.parametrize("level,faithful", [(1, False), (2, False), (2, True), (3, False), (3, True)])
+def test_convex_enclosure_fast_path_exact(hip, level, faithful, monkeypatch):
+    """A convex enclosure seen from inside (the icosphere) takes the exit-
+    direction map (rthx_scene3d_hull = 3): every row equals the plain BVH
+    walk's (RTHX_T3_NO_CVX=1) bit for bit, and sampled rows the brute-force
+    CPU restatement's."""
+    from rthx.trace3d import Scene3D
+
+    xyz, nv, nrm = _icosphere_inside(level)
+    n = len(nv)
+    R = 20_000
+    s = Scene3D(xyz, nv, nrm)
+    try:
+        assert s.stats()["hull_mode"] == 3
+    finally:
+        s.close()
+    D, info = gpu_dense(xyz, nv, nrm, R, seed=17, faithful=faithful)
+    monkeypatch.setenv("RTHX_T3_NO_CVX", "1")
+    s = Scene3D(xyz, nv, nrm)
+    try:
+        assert s.stats()["hull_mode"] == 0
+    finally:
+        s.close()
+    W, winfo = gpu_dense(xyz, nv, nrm, R, seed=17, faithful=faithful)
+    monkeypatch.delenv("RTHX_T3_NO_CVX")
+    bad = int(np.count_nonzero(D != W))
+    assert bad == 0, f"{bad} counts differ from the plain walk"
+    assert info["lost_total"] == winfo["lost_total"]
+    rows = np.unique(np.linspace(0, n - 1, 5).astype(int))
+    for g in rows:
+        C, _lost = oracle.trace_exchange_3d(xyz, nv, nrm, R, seed=17, begin=int(g), end=int(g) + 1, nthreads=16)
+        assert np.array_equal(D[g], C[0]), f"row {g}"
+
+
+def test_convex_enclosure_detection(hip):
+    """The fast path needs every vertex on or in front of every emitting
+    plane: the icosphere with outward normals (rays leave the body), and a
+    box hull scene, do not take it."""
+    from rthx.trace3d import Scene3D
+
+    xyz, nv, nrm = _icosphere_inside(1)
+    s = Scene3D(xyz, nv, -nrm)
+    try:
+        assert s.stats()["hull_mode"] == 0
+    finally:
+        s.close()
+    xyz, nv, nrm, _nc = H.cube_icosphere_scene(ndim=2, level=1)
+    s = Scene3D(xyz, nv, nrm)
+    try:
+        assert s.stats()["hull_mode"] != 3
+    finally:
+        s.close()

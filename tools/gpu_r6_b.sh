@@ -16,3 +16,12 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r6/prof_pipe -o
   python3 tools/bench_c5_bands.py --emulate-world 8 --pipeline --rays 1e9 --ranks 7 --reps 1 \
   > gpurun_out/r6/c5_pipeline_prof.log 2>&1 || { tail -30 gpurun_out/r6/c5_pipeline_prof.log; exit 1; }
 find gpurun_out/r6/prof_pipe -name "*.csv" | head
+timeout -k 10 600 python -u -m pytest -x -v --timeout 400 --timeout-method thread -m gpu tests/test_gpu_accuracy.py \
+  "tests/test_gpu_parity.py::test_philox10_build_exact" > gpurun_out/r6/pytest_acc.log 2>&1 || { tail -30 gpurun_out/r6/pytest_acc.log; exit 1; }
+grep -E "RMS|C&S|passed|failed" gpurun_out/r6/pytest_acc.log
+RTHX_ACCURACY_RECORD=gpurun_out/r6/accuracy.json timeout -k 10 600 python -u -m pytest -x -q -s --timeout 400 --timeout-method thread -m gpu \
+  "tests/test_gpu_accuracy.py::test_f_smooth_rms_vs_1e9_ray_reference" > gpurun_out/r6/pytest_acc_rec.log 2>&1 || exit 1
+timeout -k 10 300 python bench.py --no-cpu --steps 20 --warmup 10 > gpurun_out/r6/bench_a.json 2> gpurun_out/r6/bench_a.err || { tail gpurun_out/r6/bench_a.err; exit 1; }
+python -c "
+import json; d = json.load(open('gpurun_out/r6/bench_a.json'))
+print('value', d['value'], 'kernel', d['roofline']['avg_kernel_ms'], 'philox10', d['philox10'])"
