@@ -218,6 +218,16 @@ int rthx_result_copy_csr(const rthx_result* res, int64_t* row_ptr,
  * with no tallied ray are empty).  Any pointer may be NULL. */
 int rthx_result_copy_F(const rthx_result* res, int64_t* row_ptr, int32_t* cols, double* vals);
 
+/* F_raw as above, in compressed sparse columns -- the layout of Julia's
+ * SparseMatrixCSC{Float64,Int64}, so the seam returns the reference's
+ * matrix without a host transpose (parallelRayTracing.jl:154-158):
+ * colptr[N+1], rowval[nnz] (each column's rows ascending) and nzval[nnz],
+ * indices counted from index_base (0, or 1 for Julia).  One-device results
+ * are transposed on the device (radix sort of (column, row) keys); several
+ * devices' results on the host.  Any pointer may be NULL. */
+int rthx_result_copy_F_csc(const rthx_result* res, int32_t index_base, int64_t* colptr, int64_t* rowval,
+                           double* nzval);
+
 /* Pin (page-lock) caller memory for direct device DMA, e.g. the cols/counts
  * arrays a caller reuses across traces; unregister before freeing it. */
 int rthx_host_register(void* ptr, size_t bytes);

@@ -105,3 +105,99 @@ hipError_t merge_row_shards(const ShardSet& S, int64_t* row_ptr, uint32_t* cols,
 
 }  // namespace asmb
 }  // namespace rthx
+
+// ---------------------------------------------------------------------------
+// F_raw as CSC (rthx_result_copy_F_csc): Julia's SparseMatrixCSC{Float64,Int64}
+// layout, so that the seam hands the reference a matrix it need not
+// transpose (RTHX.jl builds F from the CSC arrays; the reference's own
+// sparse(I, J, V) + row_normalize!, parallelRayTracing.jl:154-169).
+// Traffic per nonzero: key + count written and sorted (the radix sort reads
+// and writes them once per 8-bit digit: 4 passes for u32 keys), then 16 B of
+// (rowval, nzval) written.
+// ---------------------------------------------------------------------------
+#include <hipcub/device/device_radix_sort.hpp>
+
+namespace rthx {
+namespace asmb {
+
+// One wave per local row: the row's tallied rays (the sum of its counts) and
+// its entries' keys.
+template <class K>
+__global__ __launch_bounds__(256) void k_csc_keys(CscJob J, K* __restrict__ keys, uint32_t* __restrict__ vals,
+                                                  double* __restrict__ rowsum) {
+  const int64_t k = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (k >= J.n_rows) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t b = J.row_off[k] - J.row_off[0], e = J.row_off[k + 1] - J.row_off[0];
+  uint64_t t = 0;
+  for (int64_t i = b + lane; i < e; i += 64) {
+    const uint32_t c = J.cols[i], n = J.counts[i];
+    keys[i] = ((K)c << J.row_bits) | (K)k;
+    vals[i] = n;
+    t += n;
+  }
+  for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off);
+  if (lane == 0) rowsum[k] = (double)t;
+}
+
+template <class K>
+__global__ __launch_bounds__(256) void k_csc_finish(CscJob J, const K* __restrict__ keys,
+                                                    const uint32_t* __restrict__ vals,
+                                                    const double* __restrict__ rowsum, int64_t* __restrict__ colptr,
+                                                    int64_t* __restrict__ rowval, double* __restrict__ nzval) {
+  const K mask = ((K)1 << J.row_bits) - 1;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i <= J.nnz; i += (int64_t)gridDim.x * 256) {
+    // columns (prev, c] start at entry i (the last entry closes the rest)
+    const int64_t c = i < J.nnz ? (int64_t)(keys[i] >> J.row_bits) : J.n_cols;
+    const int64_t prev = i > 0 ? (int64_t)(keys[i - 1] >> J.row_bits) : -1;
+    for (int64_t q = prev + 1; q <= c; ++q) colptr[q] = i + J.base;
+    if (i < J.nnz) {
+      const int64_t k = (int64_t)(keys[i] & mask);
+      rowval[i] = J.begin + k * J.stride + J.base;
+      nzval[i] = (double)vals[i] / rowsum[k];  // (count / tallied: rthx_result_copy_F's quotient)
+    }
+  }
+}
+
+hipError_t csc_keys(const CscJob& J, void* keys, uint32_t* vals, double* rowsum, hipStream_t st) {
+  if (J.n_rows <= 0) return hipSuccess;
+  const dim3 grid((unsigned)((J.n_rows + 3) / 4));
+  if (J.key_bits <= 32)
+    hipLaunchKernelGGL(k_csc_keys<uint32_t>, grid, dim3(256), 0, st, J, (uint32_t*)keys, vals, rowsum);
+  else
+    hipLaunchKernelGGL(k_csc_keys<uint64_t>, grid, dim3(256), 0, st, J, (uint64_t*)keys, vals, rowsum);
+  return hipGetLastError();
+}
+
+hipError_t csc_sort(const CscJob& J, void* tmp, size_t* tmp_bytes, void* keys0, void* keys1, uint32_t* vals0,
+                    uint32_t* vals1, int* which, hipStream_t st) {
+  hipError_t e;
+  if (J.key_bits <= 32) {
+    hipcub::DoubleBuffer<uint32_t> kb((uint32_t*)keys0, (uint32_t*)keys1);
+    hipcub::DoubleBuffer<uint32_t> vb(vals0, vals1);
+    e = hipcub::DeviceRadixSort::SortPairs(tmp, *tmp_bytes, kb, vb, (int)J.nnz, 0, J.key_bits, st);
+    if (which) *which = kb.selector;
+  } else {
+    hipcub::DoubleBuffer<uint64_t> kb((uint64_t*)keys0, (uint64_t*)keys1);
+    hipcub::DoubleBuffer<uint32_t> vb(vals0, vals1);
+    e = hipcub::DeviceRadixSort::SortPairs(tmp, *tmp_bytes, kb, vb, (int)J.nnz, 0, J.key_bits, st);
+    if (which) *which = kb.selector;
+  }
+  return e;
+}
+
+hipError_t csc_finish(const CscJob& J, const void* keys, const uint32_t* vals, const double* rowsum, int64_t* colptr,
+                      int64_t* rowval, double* nzval, hipStream_t st) {
+  const int64_t work = J.nnz + 1;
+  const unsigned grid = (unsigned)(work < 65536 * 256 ? (work + 255) / 256 : 65536);
+  if (J.key_bits <= 32)
+    hipLaunchKernelGGL(k_csc_finish<uint32_t>, dim3(grid), dim3(256), 0, st, J, (const uint32_t*)keys, vals, rowsum,
+                       colptr, rowval, nzval);
+  else
+    hipLaunchKernelGGL(k_csc_finish<uint64_t>, dim3(grid), dim3(256), 0, st, J, (const uint64_t*)keys, vals, rowsum,
+                       colptr, rowval, nzval);
+  return hipGetLastError();
+}
+
+}  // namespace asmb
+}  // namespace rthx

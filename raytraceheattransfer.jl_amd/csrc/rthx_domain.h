@@ -72,6 +72,9 @@ struct rthx_result {
   int64_t lb_hint_shape[3] = {0, 0, 0};  // its (N, rows, R)
   rthx::HostBuf h_totals;  // pinned copy of a look-back launch's totals
   rthx::DevBuf fvals;      // F_raw values (rthx_result_copy_F)
+  // rthx_result_copy_F_csc: radix-sort keys / counts (double-buffered), the
+  // sort's scratch, row sums, and the CSC arrays before their host copy
+  rthx::DevBuf csc_keys[2], csc_vals[2], csc_tmp, csc_rowsum, csc_colptr, csc_rowval, csc_nz;
   bool valid = false;
   bool host_row_off = false;
   int64_t N = 0, R = 0, n_rows = 0, begin = 0, stride = 1, split = 1;
@@ -104,7 +107,9 @@ struct rthx_result {
     for (auto& e : pend_ev)
       if (e) (void)hipEventDestroy(e);
     rthx::DevBuf* all[] = {&stage_cols, &stage_cnt, &row_nnz,  &row_tallied, &row_off,  &totals, &cols,
-                     &cnt,        &dense,     &rec_ids,  &rec_ok,      &rec_orig, &rec_end, &lb_status, &lb_totals, &fvals, &arrive};
+                     &cnt,        &dense,     &rec_ids,  &rec_ok,      &rec_orig, &rec_end, &lb_status, &lb_totals, &fvals, &arrive,
+                     &csc_keys[0], &csc_keys[1], &csc_vals[0], &csc_vals[1], &csc_tmp, &csc_rowsum, &csc_colptr,
+                     &csc_rowval, &csc_nz};
     for (rthx::DevBuf* b : all) b->release();
     h_cols.release();
     h_cnt.release();

@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cstdio>
 #include <cstdlib>
 #include <cmath>
@@ -431,13 +432,40 @@ bool detect_box_hull(const std::vector<rthx::Emit3>& P, int64_t n, const double*
 struct CvxBuild {
   double c[3] = {0.0, 0.0, 0.0};
   double rin = 0.0, rout = 0.0;
+  double max_arc = 0.0;  // the largest half-arc the fast path takes (radians)
   int res = 0;
-  std::vector<rthx::CvxPlane> planes;
+  std::vector<rthx::CvxPlane> list_planes;  // per list entry (inline)
   std::vector<int32_t> start, items;
 };
 
 double angle_between(V a, V b) {  // unit vectors; robust near 0 and pi
   return std::atan2(norm(cross(a, b)), dot(a, b));
+}
+
+// Angular distance from unit direction x to the spherical triangle with unit
+// corners w[0..2] (0 inside): the nearest of its three great-circle arcs,
+// or corner.
+double sph_tri_dist(V x, const V w[3]) {
+  const V n01 = cross(w[0], w[1]), n12 = cross(w[1], w[2]), n20 = cross(w[2], w[0]);
+  const double s = dot(cross(sub(w[1], w[0]), sub(w[2], w[0])), w[0]) >= 0.0 ? 1.0 : -1.0;  // orientation
+  if (s * dot(x, n01) >= 0.0 && s * dot(x, n12) >= 0.0 && s * dot(x, n20) >= 0.0) return 0.0;
+  double best = 1e300;
+  for (int e = 0; e < 3; ++e) {
+    const V a = w[e], b = w[(e + 1) % 3];
+    const V nn = cross(a, b);
+    const double ln = norm(nn);
+    best = std::min({best, angle_between(x, a), angle_between(x, b)});
+    if (!(ln > 0.0)) continue;
+    const V u = scale(nn, 1.0 / ln);
+    const double xn = dot(x, u);
+    V p = sub(x, scale(u, xn));
+    const double lp = norm(p);
+    if (!(lp > 0.0)) continue;
+    p = scale(p, 1.0 / lp);
+    // p within the arc a -> b
+    if (dot(cross(a, p), u) >= 0.0 && dot(cross(p, b), u) >= 0.0) best = std::min(best, std::asin(std::min(1.0, std::fabs(xn))));
+  }
+  return best;
 }
 
 // The unit direction of cube-map face f at (u, v) in [-1, 1]^2 (the inverse
@@ -480,14 +508,20 @@ bool detect_convex_enclosure(const std::vector<rthx::Emit3>& P, const std::vecto
   cb.c[2] = c.z;
   cb.rin = rin * (1.0 - 1e-9);
   cb.rout = rout * (1.0 + 1e-9) + 1e-12 * scale_;
+  {
+    const double q = rin / rout;
+    cb.max_arc = std::min(rthx::kCvxArcMax, std::max(rthx::kCvxArcMin, 0.25 * std::sqrt(std::max(0.0, 1.0 - q * q))));
+    if (const char* e = rthx::knob("RTHX_T3_CVX_ARC")) cb.max_arc = std::max(1e-4, std::atof(e));
+  }
   // one plane per triangle (its polygon's emitting normal)
-  cb.planes.resize(tris.size());
+  std::vector<rthx::CvxPlane> planes(tris.size());
   std::vector<V> tcen(tris.size());
+  std::vector<std::array<V, 3>> tw(tris.size());  // corner directions
   std::vector<double> tha(tris.size());
   for (size_t t = 0; t < tris.size(); ++t) {
     const rthx::Tri3& T = tris[t];
     const rthx::Emit3& E = P[(size_t)T.poly];
-    rthx::CvxPlane& pl = cb.planes[t];
+    rthx::CvxPlane& pl = planes[t];
     for (int k = 0; k < 3; ++k) pl.n[k] = E.n[k];
     pl.h = E.n[0] * T.v0[0] + E.n[1] * T.v0[1] + E.n[2] * T.v0[2];
     const V a{T.v0[0], T.v0[1], T.v0[2]};
@@ -497,6 +531,9 @@ bool detect_convex_enclosure(const std::vector<rthx::Emit3>& P, const std::vecto
     V m = {w[0].x + w[1].x + w[2].x, w[0].y + w[1].y + w[2].y, w[0].z + w[1].z + w[2].z};
     m = scale(m, 1.0 / norm(m));
     tcen[t] = m;
+    tw[t][0] = w[0];
+    tw[t][1] = w[1];
+    tw[t][2] = w[2];
     // (the spherical triangle lies in the cap through its corners: a cap
     // under 90 degrees is convex on the sphere)
     tha[t] = std::max({angle_between(m, w[0]), angle_between(m, w[1]), angle_between(m, w[2])});
@@ -507,13 +544,18 @@ bool detect_convex_enclosure(const std::vector<rthx::Emit3>& P, const std::vecto
     tcos[t] = std::cos(tha[t]);
     tsin[t] = std::sin(tha[t]);
   }
-  // cube-map resolution: about two cells per triangle edge across
+  // cube-map resolution: cells about a quarter of a triangle across
+  // (RTHX_T3_CVX_RES: cells per triangle edge; 2 / 3 / 4 / 6 measured,
+  // profiles/round6/ab/cvx_res_arc.log)
   const double per_face = std::sqrt((double)tris.size() / 6.0);
-  cb.res = (int)std::min(64.0, std::max(4.0, std::ceil(2.0 * per_face)));
+  double cells_per_tri = 4.0;
+  if (const char* e = rthx::knob("RTHX_T3_CVX_RES")) cells_per_tri = std::max(0.5, std::atof(e));
+  cb.res = (int)std::min(96.0, std::max(4.0, std::ceil(cells_per_tri * per_face)));
   const int res = cb.res;
   const size_t n_cells = (size_t)6 * res * res;
   cb.start.assign(n_cells + 1, 0);
   cb.items.clear();
+  cb.list_planes.clear();
   for (int f = 0; f < 6; ++f)
     for (int j = 0; j < res; ++j)
       for (int i = 0; i < res; ++i) {
@@ -525,9 +567,20 @@ bool detect_convex_enclosure(const std::vector<rthx::Emit3>& P, const std::vecto
         const size_t cell = ((size_t)f * res + j) * res + i;
         // angle(cc, tcen) <= a + tha  <=>  cc . tcen >= cos(a) cos(tha) - sin(a) sin(tha)
         // (a + tha < pi; the cosine falls on [0, pi])
-        const double a = ha + rthx::kCvxMaxArc + rthx::kCvxPad, ca = std::cos(a), sa = std::sin(a);
-        for (size_t t = 0; t < tris.size(); ++t)
-          if (dot(cc, tcen[t]) >= ca * tcos[t] - sa * tsin[t] - 1e-12) cb.items.push_back((int32_t)t);
+        const double a = ha + cb.max_arc + rthx::kCvxPad, ca = std::cos(a), sa = std::sin(a);
+        std::vector<std::pair<double, int32_t>> in_cell;  // (distance from the cell's centre, triangle)
+        // a triangle is listed when its spherical triangle comes within
+        // a of the cell's centre (cones first, then the exact distance)
+        for (size_t t = 0; t < tris.size(); ++t) {
+          const double ct = dot(cc, tcen[t]);
+          if (ct >= ca * tcos[t] - sa * tsin[t] - 1e-12 && sph_tri_dist(cc, tw[t].data()) <= a + 1e-9)
+            in_cell.push_back({-ct, (int32_t)t});
+        }
+        std::sort(in_cell.begin(), in_cell.end());
+        for (const auto& e : in_cell) {
+          cb.items.push_back(e.second);
+          cb.list_planes.push_back(planes[(size_t)e.second]);
+        }
         cb.start[cell + 1] = (int32_t)cb.items.size();
       }
   return true;
@@ -798,7 +851,7 @@ RTHX_EXPORT int rthx_scene3d_create_grouped(const double* xyz, const int32_t* nv
                !up(s->lines, hb.lines.data(), hb.lines.size() * sizeof(float)) ||
                !up(s->hull_tris, hull_tris.data(), hull_tris.size() * sizeof(rthx::Tri3))))
     return bail(fail(RTHX_ENOMEM, "uploading the 3D scene's box hull"));
-  if (cvx && (!up(s->cvx_planes, cvb.planes.data(), cvb.planes.size() * sizeof(rthx::CvxPlane)) ||
+  if (cvx && (!up(s->cvx_planes, cvb.list_planes.data(), std::max<size_t>(cvb.list_planes.size(), 1) * sizeof(rthx::CvxPlane)) ||
               !up(s->cvx_start, cvb.start.data(), cvb.start.size() * 4) ||
               !up(s->cvx_items, cvb.items.data(), std::max<size_t>(cvb.items.size(), 1) * 4)))
     return bail(fail(RTHX_ENOMEM, "uploading the 3D scene's exit-direction map"));
@@ -825,7 +878,7 @@ RTHX_EXPORT int rthx_scene3d_create_grouped(const double* xyz, const int32_t* nv
   s->S.hull_tris = hull ? s->hull_tris.as<rthx::Tri3>() : nullptr;
   s->S.cvx = cvx ? 1 : 0;
   s->S.cvx_res = cvx ? cvb.res : 0;
-  s->S.cvx_cos_arc = (float)std::cos(2.0 * rthx::kCvxMaxArc);
+  s->S.cvx_cos_arc = (float)std::cos(2.0 * cvb.max_arc);
   s->S.cvx_tpad = (float)(1e-9 * scale);
   for (int k = 0; k < 3; ++k) s->S.cvx_c[k] = cvb.c[k];
   s->S.cvx_rin2 = cvb.rin * cvb.rin;

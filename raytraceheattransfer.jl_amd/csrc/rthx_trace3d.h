@@ -96,20 +96,26 @@ constexpr float kHullMinDir = 1e-6f;  // smallest |direction component| the hull
 // that ball) to where it leaves the circumscribed one.  The directions from
 // c of that part lie in a cap about m (the sum of its two end directions);
 // a cube map of directions about c lists, for each of its cells, every
-// triangle whose central projection could meet a cap of radius kCvxMaxArc
-// about a direction in the cell (cones of the cell and the triangle, padded
-// by kCvxPad).  A ray (a deep one, as Emit3::convex) whose cap is within
-// kCvxMaxArc tests the triangles of m's cell only: their exit-plane
-// distances first (the nearest, t_min), then the fp64 Moeller-Trumbore test
-// with the walk's (t, id) rule on those whose plane lies within
-// kCvxTRel of t_min -- any triangle that Moeller-Trumbore can accept lies
-// at the exit point, within rounding.  Rays with a longer cap, a grazing
+// triangle whose central projection could meet a cap of the largest half-arc
+// about a direction in the cell (the spherical triangle within that radius
+// plus the cell's own and kCvxPad of the cell's centre).  A ray (a deep one,
+// as Emit3::convex) whose cap is within that half-arc tests the triangles of
+// m's cell only: where it meets their
+// planes, and the fp64 Moeller-Trumbore test with the walk's (t, id) rule on
+// those whose plane it meets within kCvxTRel of the nearest exit plane --
+// any triangle that Moeller-Trumbore can accept lies at the exit point,
+// within rounding.  Rays with a longer cap, a grazing
 // exit (|cos| < kCvxMinExitCos) or no hit walk the BVH as before.
 struct alignas(16) CvxPlane {
   double n[3];  // the polygon's emitting (inward) unit normal
   double h;     // n . v0: inside is n . x >= h
 };
-constexpr double kCvxMaxArc = 0.02;      // largest half-arc (radians) the fast path takes
+// Largest half-arc (radians) the fast path takes: the scene's
+// sqrt(1 - (r_in / r_out)^2) / 4 -- half the half-arc of a ray that just
+// touches the inscribed ball (the icosphere: L2 0.04, L3 0.02; longer caps
+// walk; the lists of longer ones cost more than their walks save,
+// profiles/round6/ab/cvx_res_arc.log) -- within [kCvxArcMin, kCvxArcMax].
+constexpr double kCvxArcMin = 0.005, kCvxArcMax = 0.1;
 constexpr double kCvxPad = 2e-3;         // list padding (radians): fp32 direction arithmetic
 constexpr float kCvxTRel = 1e-5f;        // relative window above t_min for the fp64 test
 constexpr double kCvxMinExitCos = 1e-3;  // |n . d| of the exit plane below this: walk
@@ -169,13 +175,13 @@ struct DevScene3D {
   // convex enclosure seen from inside (CvxPlane): 1 = the fast path
   int32_t cvx;
   int32_t cvx_res;           // cube-map cells per face edge
-  float cvx_cos_arc;         // cos(2 kCvxMaxArc): the longest arc (between the cap's ends) taken
+  float cvx_cos_arc;         // cos(2 x the largest half-arc): the longest arc (between the cap's ends) taken
   float cvx_tpad;            // absolute window above t_min (1e-9 of the scene scale)
   double cvx_c[3];           // the vertices' centroid
   double cvx_rin2, cvx_rout2;  // squared inscribed (shrunk 1e-9) and circumscribed (grown 1e-9) radii
-  const CvxPlane RTHX_GLOBAL* cvx_planes;  // per triangle of `tris` (BVH order)
   const int32_t RTHX_GLOBAL* cvx_start;    // [6 res^2 + 1] list offsets per cell
-  const int32_t RTHX_GLOBAL* cvx_items;    // triangle indices into `tris`
+  const CvxPlane RTHX_GLOBAL* cvx_planes;  // per list entry: its triangle's plane (inline)
+  const int32_t RTHX_GLOBAL* cvx_items;    // per list entry: its triangle's index into `tris`
 };
 
 constexpr uint32_t kTrace3dTag = 0x40000000u;  // Philox counter word 3 of the 3D tracer

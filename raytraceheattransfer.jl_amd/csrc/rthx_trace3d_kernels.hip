@@ -261,30 +261,35 @@ struct Walk {
     if (!(__builtin_fmaf(A0, B0, __builtin_fmaf(A1, B1, A2 * B2)) >= S.cvx_cos_arc)) return false;
     const int cell = cvx_cell(A0 + B0, A1 + B1, A2 + B2, S.cvx_res);
     const int k0 = S.cvx_start[cell], k1 = S.cvx_start[cell + 1];
-    // pass 1: the nearest exit plane among the cell's triangles (fp64 plane
-    // distance and slope, their quotient in fp32)
-    float t_min = __builtin_inff();
+    // One pass over the cell's triangles (their planes stored inline, in
+    // order of their distance from the cell's centre: the exit triangle
+    // usually comes first).  t_k: where the ray meets triangle k's plane
+    // (fp64 distance and slope, their quotient in fp32); the fp64
+    // Moeller-Trumbore test runs on every triangle whose t_k lies within
+    // kCvxTRel of the smallest t_k seen so far -- a superset of those
+    // within kCvxTRel of the final smallest, the exit plane's.
+    float t_min = __builtin_inff(), lim = __builtin_inff();
     double nd_min = 0.0;
     for (int k = k0; k < k1; ++k) {
-      const CvxPlane P = S.cvx_planes[S.cvx_items[k]];
+      const CvxPlane P = S.cvx_planes[k];
       const double nd = __builtin_fma(P.n[0], d[0], __builtin_fma(P.n[1], d[1], P.n[2] * d[2]));
+      if (!(nd < 0.0)) continue;
       const double num = P.h - __builtin_fma(P.n[0], o[0], __builtin_fma(P.n[1], o[1], P.n[2] * o[2]));
-      const float t = (float)num / (float)nd;
-      if (nd < 0.0 && t < t_min) {
+      const float t = (float)num * __builtin_amdgcn_rcpf((float)nd);
+      if (t < t_min) {
         t_min = t;
         nd_min = nd;
+        lim = __builtin_fmaf(t_min, kCvxTRel, t_min) + S.cvx_tpad;
       }
+      if (t <= lim) consider(S.tris[S.cvx_items[k]]);
     }
-    if (!(t_min < __builtin_inff()) || !(-nd_min >= kCvxMinExitCos)) return false;
-    // pass 2: Moeller-Trumbore on the triangles whose plane the ray meets
-    // at the exit point (within kCvxTRel)
-    const float lim = __builtin_fmaf(t_min, kCvxTRel, t_min) + S.cvx_tpad;
-    for (int k = k0; k < k1; ++k) {
-      const int idx = S.cvx_items[k];
-      const CvxPlane P = S.cvx_planes[idx];
-      const double nd = __builtin_fma(P.n[0], d[0], __builtin_fma(P.n[1], d[1], P.n[2] * d[2]));
-      const double num = P.h - __builtin_fma(P.n[0], o[0], __builtin_fma(P.n[1], o[1], P.n[2] * o[2]));
-      if (nd < 0.0 && (float)num / (float)nd <= lim) consider(S.tris[idx]);
+    // (no exit plane, or a grazing exit: the walk decides, from scratch)
+    if (!(-nd_min >= kCvxMinExitCos) || best_poly < 0) {
+      best_t = __builtin_inf();
+      best_tf = __builtin_inff();
+      best_id = 0x7FFFFFFF;
+      best_poly = -1;
+      return false;
     }
     return best_poly >= 0;
   }

@@ -341,27 +341,13 @@ end
 device_domain(rtm) = uploaded(rtm, false)
 multi_domain(rtm) = uploaded(rtm, true)
 
-# Page-locked cols / counts buffers reused across traces (rthx_host_register):
-# the library DMAs the device CSR straight into them.
-const PINNED = Dict{Symbol, Any}()
-
-function pinned(name::Symbol, ::Type{T}, n::Integer) where T
-    a = get(PINNED, name, nothing)
-    if a === nothing || length(a) < n
-        a === nothing || check(ccall((:rthx_host_unregister, LIB[]), Cint, (Ptr{Cvoid},), a))
-        a = zeros(T, max(cld(5n, 4), 1024))
-        check(ccall((:rthx_host_register, LIB[]), Cint, (Ptr{Cvoid}, Csize_t), a, sizeof(a)))
-        PINNED[name] = a
-    end
-    return a::Vector{T}
-end
-
 """
     computeExchangeFactorsBin(rtm, rays_per_emitter, nudge, spectral_bin, surface_mapping,
                               volume_mapping, num_surfaces, num_volumes, num_emitters, verbose, rec)
 
 Drop-in for parallelRayTracing.jl:64-159: one `rthx_trace_exchange` call,
-then `sparse` + `row_normalize!` exactly as the reference (:154-158).
+then F_raw (the reference's `sparse` + `row_normalize!`, :154-169) formed
+and laid out as SparseMatrixCSC on the device (`rthx_result_copy_F_csc`).
 """
 function computeExchangeFactorsBin(rtm, rays_per_emitter::Integer, nudge, spectral_bin::Integer,
                                    surface_mapping, volume_mapping, num_surfaces, num_volumes, num_emitters,
@@ -383,11 +369,13 @@ function computeExchangeFactorsBin(rtm, rays_per_emitter::Integer, nudge, spectr
         info = Ref{ResultInfo}()
         check(ccall((:rthx_result_get_info, LIB[]), Cint, (Ptr{Cvoid}, Ptr{ResultInfo}), res[], info))
         N, nnz = info[].n_emitters, info[].nnz
-        rowptr = Vector{Int64}(undef, N + 1)
-        cols = pinned(:cols, Int32, max(nnz, 1))
-        counts = pinned(:counts, UInt32, max(nnz, 1))
-        check(ccall((:rthx_result_copy_csr, LIB[]), Cint, (Ptr{Cvoid}, Ptr{Int64}, Ptr{Int32}, Ptr{UInt32}),
-                    res[], rowptr, cols, counts))
+        # F_raw in Julia's own CSC layout (1-based), formed and transposed on
+        # the device: no host transpose of the CSR (at C2, 3e7 nonzeros)
+        colptr = Vector{Int64}(undef, N + 1)
+        rowval = Vector{Int64}(undef, nnz)
+        nzval = Vector{Float64}(undef, nnz)
+        check(ccall((:rthx_result_copy_F_csc, LIB[]), Cint, (Ptr{Cvoid}, Int32, Ptr{Int64}, Ptr{Int64}, Ptr{Float64}),
+                    res[], Int32(1), colptr, rowval, nzval))
         verbose && println("  rthx: $(info[].rays_traced) rays on $(info[].n_devices) device(s), nnz $nnz, ",
                            "trace $(round(info[].trace_ms; digits=3)) ms")
         if rec !== nothing && info[].n_recorded > 0
@@ -402,11 +390,12 @@ function computeExchangeFactorsBin(rtm, rays_per_emitter::Integer, nudge, spectr
                 push!(rec.endpoints[1], eltype(rec.endpoints[1])(e[2k-1], e[2k]))
             end
         end
-        # CSR of F (rows = emitters) is the CSC of F^T
-        inv_rays = 1.0 / rays_per_emitter
-        Ft = SparseMatrixCSC(N, N, rowptr .+ 1, Int64.(cols[1:nnz]) .+ 1, Float64.(counts[1:nnz]) .* inv_rays)
-        F = SparseMatrixCSC(transpose(Ft))
-        return parentmodule(@__MODULE__).RayTraceHeatTransfer.row_normalize!(F, rays_per_emitter)
+        # The reference's sparse(I, J, V) + row_normalize! (parallelRayTracing.jl:154-169):
+        # every row divided by its sum, here count / (rays the row tallied) on the
+        # device, and row_normalize!'s loss line from the trace's lost-ray count
+        # (R * max|1 - row sum| = the most rays one row lost, :163)
+        println("Maximum ray tracing ray loss per emitter: $(info[].lost_max_row)/$rays_per_emitter")
+        return SparseMatrixCSC(N, N, colptr, rowval, nzval)
     finally
         ccall((:rthx_result_destroy, LIB[]), Cvoid, (Ptr{Cvoid},), res[])
     end

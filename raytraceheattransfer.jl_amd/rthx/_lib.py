@@ -67,6 +67,9 @@ def load(path: Optional[str] = None) -> C.CDLL:
                                           C.POINTER(C.c_int64), C.c_int64, C.POINTER(C.c_int64)]
     lib.rthx_result_get_device_csr.argtypes = [C.c_void_p, C.c_int32, C.POINTER(abi.DeviceCsr)]
     lib.rthx_result_copy_csr_device.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p]
+    if hasattr(lib, "rthx_result_copy_F_csc"):  # (older A/B variant libraries lack it)
+        lib.rthx_result_copy_F_csc.argtypes = [C.c_void_p, C.c_int32, C.POINTER(C.c_int64), C.POINTER(C.c_int64),
+                                               C.POINTER(C.c_double)]
     if hasattr(lib, "rthx_merge_row_shards"):  # (older A/B variant libraries lack it)
         pp = C.POINTER(C.c_void_p)
         lib.rthx_merge_row_shards.argtypes = [C.c_int32, C.c_int32, C.c_int64, pp, pp, pp, C.c_void_p, C.c_void_p,
@@ -369,6 +372,20 @@ class DeviceResult:
         check(self._lib.rthx_result_copy_F(self.handle, abi.ptr(row_ptr, C.c_int64), abi.ptr(cols, C.c_int32),
                                            abi.ptr(vals, C.c_double)))
         return row_ptr, cols[:nnz], vals[:nnz]
+
+    def F_csc(self, index_base: int = 0):
+        """F_raw in compressed sparse columns (rthx_result_copy_F_csc): (colptr,
+        rowval, nzval), indices from index_base -- the arrays of Julia's
+        SparseMatrixCSC with index_base = 1; scipy.sparse.csc_matrix((nzval,
+        rowval, colptr)) with 0."""
+        inf = self.info()
+        n, nnz = inf["n_emitters"], inf["nnz"]
+        colptr = np.empty(n + 1, dtype=np.int64)
+        rowval = np.empty(max(nnz, 1), dtype=np.int64)
+        nzval = np.empty(max(nnz, 1), dtype=np.float64)
+        check(self._lib.rthx_result_copy_F_csc(self.handle, int(index_base), abi.ptr(colptr, C.c_int64),
+                                               abi.ptr(rowval, C.c_int64), abi.ptr(nzval, C.c_double)))
+        return colptr, rowval[:nnz], nzval[:nnz]
 
     def rays(self):
         inf = self.info()

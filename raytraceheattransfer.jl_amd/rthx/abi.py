@@ -255,6 +255,7 @@ EXPORTED_SYMBOLS = (
     "rthx_result_copy_csr",
     "rthx_result_copy_rays",
     "rthx_result_copy_F",
+    "rthx_result_copy_F_csc",
     "rthx_result_get_device_csr",
     "rthx_result_copy_csr_device",
     "rthx_merge_row_shards",

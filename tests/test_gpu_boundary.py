@@ -596,3 +596,32 @@ def test_superseded_async_faults_are_counted(hip, monkeypatch):
             res.close()
     finally:
         dd.close()
+
+
+@pytest.mark.parametrize("shape", ["full", "shard", "multi"])
+def test_F_csc_equals_host_transpose(hip, shape):
+    """rthx_result_copy_F_csc (F_raw as Julia's SparseMatrixCSC layout,
+    transposed on the device by a radix sort of (column, row) keys; several
+    devices' results on the host) equals the host transpose of
+    rthx_result_copy_F's CSR exactly, indices counted from 0 and from 1."""
+    import scipy.sparse as sp
+
+    flat = H.square_domain(21, kappa=0.7).flat()
+    N = flat.n_emitters
+    begin, stride = (1, 3) if shape == "shard" else (0, 1)
+    args, _k = hip.make_args(0, 3001, H.NUDGE, 4, begin, N, stride)
+    dd = hip.MultiDeviceDomain(flat, [0, 0]) if shape == "multi" else hip.DeviceDomain(flat, 0)
+    res = hip.DeviceResult()
+    try:
+        res.trace(dd, args)
+        rp, cols, vals = res.F()
+        ref = sp.csr_matrix((vals, cols, rp), shape=(N, N)).tocsc()
+        ref.sort_indices()
+        for base in (0, 1):
+            cp, rv, nz = res.F_csc(base)
+            assert np.array_equal(cp - base, ref.indptr)
+            assert np.array_equal(rv - base, ref.indices)
+            assert np.array_equal(nz, ref.data)
+    finally:
+        res.close()
+        dd.close()
