@@ -324,9 +324,10 @@ class EmulatedBandComm:
 
     @classmethod
     def for_rank(cls, dom, rays: int, rank: int, world: int, device: int = 0, seed: int = 1, nudge: float = None,
-                 faithful: bool = False):
+                 faithful: bool = False, last_parts: int = 2):
         """The stand-in for `rank`, its peers' blocks of the bands it owns
-        (traced band i is owned by rank i mod W) traced now, on `device`."""
+        (traced band i is owned by rank i mod W; pieces as band_pieces)
+        traced now, on `device`."""
         import torch
 
         if nudge is None:
@@ -337,21 +338,23 @@ class EmulatedBandComm:
         tracer = HipShardTracer(dom, device, n_results=1)
         peers = {}
         try:
-            for i, (b, _bins) in enumerate(traced):
+            for tag, i, _begin, stride, _parts in band_pieces(len(traced), rank, world, last_parts):
+                b = traced[i][0]
                 if i % world != rank:
                     continue
+                h = tag[1] if isinstance(tag, tuple) else 0
                 blocks = []
                 for k in range(world):
                     if k == rank:
                         blocks.append(None)
                         continue
-                    sh = tracer(b - 1, R, nudge, seed, k, world, faithful)
+                    sh = tracer(b - 1, R, nudge, seed, k + h * world, stride, faithful)
                     ro = torch.empty(sh.n_rows + 1, dtype=torch.int64, device=torch.device("cuda", device))
                     pr = torch.empty((2, max(sh.nnz, 1)), dtype=torch.int32, device=ro.device)
                     sh.fill(ro, pr[0], pr[1])
                     sh.done()
                     blocks.append((ro, pr[:, :sh.nnz]))
-                peers[i] = blocks
+                peers[tag] = blocks
         finally:
             tracer.close()
         return cls(rank, world, device, peers)
@@ -514,16 +517,22 @@ def merge_row_shards_host(row_offs, cols, counts, n_rows: int):
     return row_ptr, out_c, out_n
 
 
-def _assemble_band(comm, band: int, shard, owner: int, n_rows: int, stream):
-    """Band `band`'s block copied out of this rank's trace, gathered to its
-    owner and merged there (runs on the pipeline's second thread).  Returns
-    the owner's (row_ptr, cols, counts) or None on the other ranks."""
+def _assemble_piece(comm, tag, shard, owner: int, n_rows: int, parts: int, held: dict, stream):
+    """One traced piece of a band -- the whole band (parts = 1), or piece h
+    of `parts` (rows rank + h W, stride parts W) -- copied out of this
+    rank's trace and gathered to the band's owner (runs on the pipeline's
+    second thread).  The owner merges once the band's last piece has
+    arrived: block h W + k of the merge is rank k's piece h, the rows
+    congruent to h W + k modulo parts W.  Returns the owner's (row_ptr,
+    cols, counts) after the last piece, None otherwise."""
     import torch
 
     W = comm.world
-    sizes = comm.all_sizes(band, shard.nnz)
+    band, h = tag if isinstance(tag, tuple) else (tag, 0)
+    n_sh = parts * W
+    sizes = comm.all_sizes(tag, shard.nnz)
     cap = max(max(sizes), 1)
-    nmax = (n_rows + W - 1) // W
+    nmax = (n_rows + n_sh - 1) // n_sh
     dev = comm.device
     ctx = torch.cuda.stream(stream) if stream is not None else _nullctx()
     with ctx:
@@ -533,18 +542,41 @@ def _assemble_band(comm, band: int, shard, owner: int, n_rows: int, stream):
             stream.synchronize()  # (the buffers exist before the library's stream writes them)
         shard.fill(row_off, pairs[0], pairs[1])
         shard.done()
-        ros = comm.gather(band, row_off, owner)
-        prs = comm.gather(band, pairs, owner)
+        ros = comm.gather(tag, row_off, owner)
+        prs = comm.gather(tag, pairs, owner)
         if ros is None:
             if stream is not None:
                 stream.synchronize()  # (the gather has read this rank's buffers)
             return None
+        got = held.setdefault(band, {})
+        got[h] = (ros, prs, sizes)
+        if len(got) < parts:
+            return None
+        del held[band]
+        blocks = [(got[hh][0][k], got[hh][1][k], got[hh][2][k]) for hh in range(parts) for k in range(W)]
         if dev.type == "cuda":
-            out = merge_row_shards_device(ros, [p[0] for p in prs], [p[1] for p in prs], n_rows, sizes, stream)
+            out = merge_row_shards_device([x[0] for x in blocks], [x[1][0] for x in blocks],
+                                          [x[1][1] for x in blocks], n_rows, [x[2] for x in blocks], stream)
             stream.synchronize()
             return out
-        return merge_row_shards_host([r.numpy() for r in ros], [p[0].numpy() for p in prs],
-                                     [p[1].numpy() for p in prs], n_rows)
+        return merge_row_shards_host([x[0].numpy() for x in blocks], [x[1][0].numpy() for x in blocks],
+                                     [x[1][1].numpy() for x in blocks], n_rows)
+
+
+def band_pieces(n_traced: int, rank: int, world: int, last_parts: int = 1):
+    """The traces one rank runs, in order: (tag, traced-band index, emitter
+    begin, stride, parts).  Every band whole (rows rank, rank + W, ...) but
+    the last, which is traced in last_parts pieces (rows rank + h W,
+    stride last_parts W) so that its first pieces' gathers run while its
+    last one traces."""
+    out = []
+    for i in range(n_traced):
+        P = last_parts if i == n_traced - 1 else 1
+        if P == 1:
+            out.append((i, i, rank, world, 1))
+        else:
+            out.extend(((i, h), i, rank + h * world, P * world, P) for h in range(P))
+    return out
 
 
 class _nullctx:
@@ -556,7 +588,8 @@ class _nullctx:
 
 
 def trace_bands_row_sharded(dom, rays: int, group=None, seed: int = 1, nudge: float = None, device: int = 0,
-                            faithful: bool = False, overlap: bool = True, tracer=None, comm=None):
+                            faithful: bool = False, overlap: bool = True, tracer=None, comm=None,
+                            last_parts: int = 2):
     """C5 (:spectral_variable) over W ranks, row-sharded and pipelined (see the
     section comment above).  rays: per band, as mesh() (R = rays // N rays
     per emitter).  Every rank traces its rows of every traced band
@@ -567,8 +600,12 @@ def trace_bands_row_sharded(dom, rays: int, group=None, seed: int = 1, nudge: fl
     cols, counts) -- tensors on the rank's GPU on an NCCL group (counts:
     int32 holding the uint32 bits), numpy on gloo -- and info holds each
     band's trace info and the host-clock timeline (trace and assembly
-    intervals, seconds from the start).  overlap=False assembles each band
-    before the next traces (the sequential form, for comparison).
+    intervals, seconds from the start; wall_s: from the first trace to the
+    last assembly, call_s: the whole call).  overlap=False assembles each
+    band before the next traces (the sequential form, for comparison).
+    last_parts: the last band is traced in that many pieces, so that only
+    its last piece's gather and the merge follow the last trace
+    (band_pieces).
     tracer / comm: stand-ins for tests and the one-GPU emulation
     (tools/bench_c5_bands.py); the product uses HipShardTracer and
     TorchBandComm."""
@@ -594,34 +631,38 @@ def trace_bands_row_sharded(dom, rays: int, group=None, seed: int = 1, nudge: fl
     timeline = []
     lock = threading.Lock()
 
-    def assemble(i, b, shard):
+    held = {}  # (owner) pieces of a band gathered so far
+
+    def assemble(tag, i, b, shard, parts):
         import torch
 
         if comm.device.type == "cuda":
             torch.cuda.set_device(comm.device)
         ta = time.perf_counter() - t0
-        out = _assemble_band(comm, i, shard, i % W, N, stream)
+        out = _assemble_piece(comm, tag, shard, i % W, N, parts, held, stream)
         with lock:
             timeline.append({"band": b, "what": "assemble", "owner": i % W, "start_s": ta,
-                             "end_s": time.perf_counter() - t0})
+                             "end_s": time.perf_counter() - t0, "piece": tag[1] if isinstance(tag, tuple) else None})
         return out
 
     owned, infos, futs = {}, [], []
     ex = ThreadPoolExecutor(max_workers=1) if overlap else None
     try:
-        for i, (b, _bins) in enumerate(traced):
+        for tag, i, begin, stride, parts in band_pieces(len(traced), rank, W, last_parts):
+            b = traced[i][0]
             ts = time.perf_counter() - t0
-            shard = tracer(b - 1, R, nudge, seed, rank, W, faithful)
+            shard = tracer(b - 1, R, nudge, seed, begin, stride, faithful)
             te = time.perf_counter() - t0
             inf = dict(shard.info, bin=b)
             infos.append(inf)
             with lock:
                 timeline.append({"band": b, "what": "trace", "start_s": ts, "end_s": te,
-                                 "kernel_ms": inf.get("trace_ms"), "pack_ms": inf.get("pack_ms")})
+                                 "kernel_ms": inf.get("trace_ms"), "pack_ms": inf.get("pack_ms"),
+                                 "piece": tag[1] if isinstance(tag, tuple) else None})
             if ex is not None:
-                futs.append((b, ex.submit(assemble, i, b, shard)))
+                futs.append((b, ex.submit(assemble, tag, i, b, shard, parts)))
             else:
-                out = assemble(i, b, shard)
+                out = assemble(tag, i, b, shard, parts)
                 if out is not None:
                     owned[b] = out
         for b, f in futs:
@@ -635,5 +676,7 @@ def trace_bands_row_sharded(dom, rays: int, group=None, seed: int = 1, nudge: fl
             tracer.close()
     total = time.perf_counter() - t0
     timeline.sort(key=lambda e: (e["start_s"], e["what"]))
+    wall = max(e["end_s"] for e in timeline) - min(e["start_s"] for e in timeline) if timeline else 0.0
     return owned, {"world": W, "rank": rank, "rays_per_emitter": R, "traces": infos, "timeline": timeline,
-                   "wall_s": total, "owner": {b: i % W for i, (b, _) in enumerate(traced)}}
+                   "wall_s": wall, "call_s": total, "last_parts": last_parts,
+                   "owner": {b: i % W for i, (b, _) in enumerate(traced)}}

@@ -193,7 +193,7 @@ class _HostShard:
         pass
 
 
-def _row_sharded_worker(rank, world, port, out_path, overlap):
+def _row_sharded_worker(rank, world, port, out_path, overlap, last_parts):
     """C5's row-sharded band pipeline over processes (rthx.distributed
     trace_bands_row_sharded): every rank traces its rows of all 8 bands,
     band i is gathered to rank i mod W and merged there."""
@@ -206,7 +206,8 @@ def _row_sharded_worker(rank, world, port, out_path, overlap):
     dom = H.greenhouse_domain(n_layers=4, nx=5, ny=2, n_bins=8)
     flat = dom.flat()
     owned, info = trace_bands_row_sharded(dom, 300 * flat.n_emitters, seed=12, nudge=H.NUDGE, overlap=overlap,
-                                          tracer=_OracleShards(flat))
+                                          tracer=_OracleShards(flat), last_parts=last_parts)
+    assert len(info["traces"]) == 7 + last_parts
     assert set(owned) == {b for b, o in info["owner"].items() if o == rank}
     assert {e["band"] for e in info["timeline"] if e["what"] == "assemble"} == set(info["owner"])
     np.savez(out_path + f".{rank}.npz", **{f"b{b}_{i}": np.asarray(a) for b, t in owned.items()
@@ -215,12 +216,13 @@ def _row_sharded_worker(rank, world, port, out_path, overlap):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,overlap", [(2, True), (3, False)])
-def test_row_sharded_band_pipeline_equals_single_process(tmp_path, world, overlap):
+@pytest.mark.parametrize("world,overlap,last_parts", [(2, True, 2), (3, False, 1), (2, True, 3)])
+def test_row_sharded_band_pipeline_equals_single_process(tmp_path, world, overlap, last_parts):
     """All 8 bands, each assembled on its owner rank from the ranks' row
-    blocks, bit-identical to the one-process trace of the whole band."""
+    blocks (the last band from last_parts pieces per rank), bit-identical to
+    the one-process trace of the whole band."""
     out = str(tmp_path / "rows")
-    mp.spawn(_row_sharded_worker, args=(world, _free_port(), out, overlap), nprocs=world, join=True)
+    mp.spawn(_row_sharded_worker, args=(world, _free_port(), out, overlap, last_parts), nprocs=world, join=True)
     from oracle import oracle
     from rthx import _lib
     from rthx.distributed import traced_bands
@@ -248,7 +250,7 @@ def test_row_sharded_band_pipeline_equals_single_process(tmp_path, world, overla
 def test_merge_row_shards_host_matches_merge_csr():
     """The host merge of strided row blocks (the gloo branch) against the
     general disjoint-block merge, including empty rows and blocks."""
-    from rthx.distributed import merge_csr, merge_row_shards_host
+    from rthx.distributed import merge_row_shards_host
 
     rng = np.random.default_rng(3)
     n = 23

@@ -78,8 +78,8 @@ def _check_owned(hip, dom, owned, info, R, seed, rank):
         dd.close()
 
 
-@pytest.mark.parametrize("W,overlap", [(3, True), (2, False)])
-def test_row_sharded_pipeline_emulated_ranks_exact(hip, W, overlap):
+@pytest.mark.parametrize("W,overlap,last_parts", [(3, True, 2), (2, False, 1), (2, True, 3)])
+def test_row_sharded_pipeline_emulated_ranks_exact(hip, W, overlap, last_parts):
     """Every emulated rank of W runs the whole pipeline (its rows of all 8
     bands traced, its bands' blocks gathered and merged on the GPU): each
     merged band equals the one-device trace."""
@@ -90,10 +90,12 @@ def test_row_sharded_pipeline_emulated_ranks_exact(hip, W, overlap):
     R, seed = 1200, 7
     seen = set()
     for q in range(W):
-        comm = EmulatedBandComm.for_rank(dom, R * N, q, W, 0, seed=seed, nudge=H.NUDGE)
-        owned, info = trace_bands_row_sharded(dom, R * N, seed=seed, nudge=H.NUDGE, overlap=overlap, comm=comm)
-        assert len(info["traces"]) == 8
-        assert all(t["rows_traced"] == len(range(q, N, W)) for t in info["traces"])
+        comm = EmulatedBandComm.for_rank(dom, R * N, q, W, 0, seed=seed, nudge=H.NUDGE, last_parts=last_parts)
+        owned, info = trace_bands_row_sharded(dom, R * N, seed=seed, nudge=H.NUDGE, overlap=overlap, comm=comm,
+                                              last_parts=last_parts)
+        assert len(info["traces"]) == 7 + last_parts
+        assert sum(t["rows_traced"] for t in info["traces"][7:]) == len(range(q, N, W))
+        assert all(t["rows_traced"] == len(range(q, N, W)) for t in info["traces"][:7])
         _check_owned(hip, dom, owned, info, R, seed, q)
         seen |= set(owned)
     assert len(seen) == 8

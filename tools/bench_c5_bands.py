@@ -40,6 +40,7 @@ def main():
     ap.add_argument("--ranks", default="", help="--pipeline: emulated ranks (default: all)")
     ap.add_argument("--xgmi-gbs", type=float, default=50.0, help="--pipeline: one xGMI link's achieved GB/s (model)")
     ap.add_argument("--reps", type=int, default=2, help="--pipeline: timed pipeline runs per rank (after one warm-up)")
+    ap.add_argument("--last-parts", type=int, default=2, help="--pipeline: pieces the last band is traced in")
     a = ap.parse_args()
     if a.emulate_world > 0 and a.pipeline:
         return emulate_pipeline(a)
@@ -125,13 +126,14 @@ def emulate_pipeline(a):
     rows of every band on this GPU while a second thread and stream copy out,
     'gather' (its peers' blocks, traced beforehand, copied into receive
     buffers on this GPU: the receive's HBM writes, not the xGMI transfer) and
-    merge (rthx_merge_row_shards) the band it owns.  The wall time is the
-    rank's whole pipeline; the xGMI transfer of a band's blocks is modelled
-    (largest peer block / --xgmi-gbs, every sender on its own link) and added
-    where it cannot hide behind the next band's trace: after the last band."""
+    merge (rthx_merge_row_shards) the band it owns.  The critical path is the
+    rank's pipeline from its first trace to its last assembly; the xGMI
+    transfer of a piece's blocks is modelled (largest peer block /
+    --xgmi-gbs, every sender on its own link) and added where it cannot hide
+    behind the next trace: for the last piece traced."""
     import torch
 
-    from rthx.distributed import EmulatedBandComm, trace_bands_row_sharded, traced_bands
+    from rthx.distributed import EmulatedBandComm, HipShardTracer, trace_bands_row_sharded, traced_bands
 
     W = a.emulate_world
     dom = H.greenhouse_domain()
@@ -140,52 +142,64 @@ def emulate_pipeline(a):
     rays = R * N
     traced = traced_bands(dom)
     ranks = [int(x) for x in a.ranks.split(",")] if a.ranks else list(range(W))
-    print(f"C5 pipeline, W={W} emulated on one GPU, {rays:.3e} rays per band, {len(traced)} band traces; "
-          f"xGMI model {a.xgmi_gbs:.0f} GB/s per link", flush=True)
+    P = a.last_parts
+    print(f"C5 pipeline, W={W} emulated on one GPU, {rays:.3e} rays per band, {len(traced)} band traces "
+          f"(the last in {P} pieces); xGMI model {a.xgmi_gbs:.0f} GB/s per link", flush=True)
     worst = 0.0
-    for q in ranks:
-        comm = EmulatedBandComm.for_rank(dom, rays, q, W, 0, seed=1)
-        peer_bytes = {i: max(8 * int(b[1].shape[1]) + 8 * int(b[0].shape[0]) for b in blocks if b is not None)
-                      for i, blocks in comm.peers.items()}
-        res = {}
-        for overlap in (True, False):
-            trace_bands_row_sharded(dom, rays, seed=1, overlap=overlap, comm=comm)  # warm-up
-            best = None
-            for _ in range(a.reps):
-                torch.cuda.synchronize()
-                owned, info = trace_bands_row_sharded(dom, rays, seed=1, overlap=overlap, comm=comm)
-                if best is None or info["wall_s"] < best[1]["wall_s"]:
-                    best = (owned, info)
-                del owned
-            res[overlap] = best[1]
-        info = res[True]
-        tl = info["timeline"]
-        tr = [e for e in tl if e["what"] == "trace"]
-        asm = [e for e in tl if e["what"] == "assemble"]
-        kern = sum(e["kernel_ms"] + e["pack_ms"] for e in tr)
-        last_i = len(traced) - 1
-        xgmi_last = peer_bytes.get(last_i, 0) / (a.xgmi_gbs * 1e9) * 1e3
-        own_last = [e for e in asm if e["band"] == traced[last_i][0]][0]
-        local_gather_ms = 0.0  # (the emulated gather's copies are inside the measured assembly)
-        extra = max(0.0, xgmi_last - local_gather_ms) if last_i in peer_bytes else 0.0
-        # a band's modelled xGMI time also has to fit under the next band's trace
-        hid = all(peer_bytes[i] / (a.xgmi_gbs * 1e9) * 1e3 <= tr[i + 1]["end_s"] * 1e3 - tr[i + 1]["start_s"] * 1e3
-                  for i in peer_bytes if i < last_i)
-        crit = info["wall_s"] * 1e3 + extra
-        worst = max(worst, crit)
-        print(f"rank {q}: owns bands {[b for b, o in info['owner'].items() if o == q]}; "
-              f"pipelined wall {info['wall_s'] * 1e3:.1f} ms (trace kernels {kern:.1f} ms, last band's assembly "
-              f"ends {(own_last['end_s'] - tr[-1]['end_s']) * 1e3:.1f} ms after the last trace) + modelled xGMI of "
-              f"the last band {extra:.1f} ms = {crit:.1f} ms; earlier bands' xGMI hidden under the next trace: {hid}; "
-              f"sequential (assembly after each trace) {res[False]['wall_s'] * 1e3:.1f} ms", flush=True)
-        for e in tl:
-            print(f"    {e['what']:8s} band {e['band']}  {e['start_s'] * 1e3:8.2f} -> {e['end_s'] * 1e3:8.2f} ms"
-                  + (f"  kernel {e['kernel_ms']:.2f} + pack {e['pack_ms']:.2f}" if e["what"] == "trace" else
-                     f"  (owner rank {e['owner']})"), flush=True)
-        del comm
-        torch.cuda.empty_cache()
+    tracer = HipShardTracer(dom, 0)
+    try:
+        for q in ranks:
+            comm = EmulatedBandComm.for_rank(dom, rays, q, W, 0, seed=1, last_parts=P)
+            peer_bytes = {t: max(8 * int(b[1].shape[1]) + 8 * int(b[0].shape[0]) for b in blocks if b is not None)
+                          for t, blocks in comm.peers.items()}
+            res = {}
+            for overlap in (True, False):
+                trace_bands_row_sharded(dom, rays, seed=1, overlap=overlap, comm=comm, tracer=tracer,
+                                        last_parts=P)  # warm-up
+                best = None
+                for _ in range(a.reps):
+                    torch.cuda.synchronize()
+                    owned, info = trace_bands_row_sharded(dom, rays, seed=1, overlap=overlap, comm=comm,
+                                                          tracer=tracer, last_parts=P)
+                    if best is None or info["wall_s"] < best[1]["wall_s"]:
+                        best = (owned, info)
+                    del owned
+                res[overlap] = best[1]
+            info = res[True]
+            tl = info["timeline"]
+            tr = [e for e in tl if e["what"] == "trace"]
+            kern = sum(e["kernel_ms"] + e["pack_ms"] for e in tr)
+            last_tag = (len(traced) - 1, P - 1) if P > 1 else len(traced) - 1
+            xgmi_last = peer_bytes.get(last_tag, 0) / (a.xgmi_gbs * 1e9) * 1e3
+            # every earlier piece's modelled transfer must fit under the trace that follows it
+            hid = all(peer_bytes[t] / (a.xgmi_gbs * 1e9) * 1e3 <= (tr[j + 1]["end_s"] - tr[j + 1]["start_s"]) * 1e3
+                      for j, t in enumerate(_tags(len(traced), P)) if t in peer_bytes and t != last_tag)
+            crit = info["wall_s"] * 1e3 + xgmi_last
+            worst = max(worst, crit)
+            nnz = "/".join(f"{t['nnz'] / 1e6:.1f}" for t in info["traces"])
+            print(f"rank {q}: owns bands {[b for b, o in info['owner'].items() if o == q]}; pipelined "
+                  f"{info['wall_s'] * 1e3:.1f} ms first trace -> last assembly (trace kernels + packs {kern:.1f} ms, "
+                  f"the last assembly ends {(tl[-1]['end_s'] - tr[-1]['end_s']) * 1e3:.1f} ms after the last trace) + "
+                  f"modelled xGMI of the last piece {xgmi_last:.1f} ms = {crit:.1f} ms; earlier pieces' xGMI hidden "
+                  f"under the next trace: {hid}; sequential (assembly after each trace) {res[False]['wall_s'] * 1e3:.1f} ms; "
+                  f"shard nnz per trace (M) {nnz}", flush=True)
+            for e in tl:
+                pc = "" if e.get("piece") is None else f" piece {e['piece']}"
+                print(f"    {e['what']:8s} band {e['band']}{pc}  {e['start_s'] * 1e3:8.2f} -> {e['end_s'] * 1e3:8.2f} ms"
+                      + (f"  kernel {e['kernel_ms']:.2f} + pack {e['pack_ms']:.2f}" if e["what"] == "trace" else
+                         f"  (owner rank {e['owner']})"), flush=True)
+            del comm
+            torch.cuda.empty_cache()
+    finally:
+        tracer.close()
     print(f"W={W} pipelined row shards: critical path {worst:.1f} ms over ranks {ranks} "
           f"({len(traced) * rays / (worst * 1e-3) / 1e9:.1f} Grays/s whole node, projected)", flush=True)
+
+
+def _tags(n, P):
+    from rthx.distributed import band_pieces
+
+    return [t for t, *_ in band_pieces(n, 0, 1, P)]
 
 
 if __name__ == "__main__":
