@@ -66,9 +66,11 @@ void fill_tables(double* t) {
 }
 
 
-hipError_t device_stream(int device, hipStream_t* out) {
+namespace {
+hipError_t lib_stream(int device, hipStream_t* out, int which) {
   static std::mutex mu;
-  static std::vector<hipStream_t> streams;
+  static std::vector<hipStream_t> all[2];
+  std::vector<hipStream_t>& streams = all[which];
   std::lock_guard<std::mutex> lock(mu);
   if (device < 0) return hipErrorInvalidDevice;
   if ((size_t)device >= streams.size()) streams.resize(device + 1, nullptr);
@@ -83,6 +85,10 @@ hipError_t device_stream(int device, hipStream_t* out) {
   *out = streams[device];
   return hipSuccess;
 }
+}  // namespace
+
+hipError_t device_stream(int device, hipStream_t* out) { return lib_stream(device, out, 0); }
+hipError_t copy_stream(int device, hipStream_t* out) { return lib_stream(device, out, 1); }
 }  // namespace rthx
 
 namespace rthx {
@@ -1478,8 +1484,10 @@ RTHX_EXPORT int rthx_result_copy_csr_device(const rthx_result* cres, int32_t par
   if (rc) return rc;
   rthx::DeviceGuard keep_device;  // (the caller's current device, e.g. torch's, is restored)
   HIP_TRY(hipSetDevice(q->device), "hipSetDevice");
+  // (the library's copy stream: the trace is complete -- device_block waited
+  // for it -- and the next trace, on the device stream, need not wait for this copy)
   hipStream_t st = nullptr;
-  HIP_TRY(rthx::device_stream(q->device, &st), "device stream");
+  HIP_TRY(rthx::copy_stream(q->device, &st), "copy stream");
   const size_t nnz = (size_t)q->info.nnz;
   if (row_off && q->n_rows >= 0)
     HIP_TRY(hipMemcpyAsync(row_off, q->row_off.p, (size_t)(q->n_rows + 1) * 8, hipMemcpyDeviceToDevice, st),

@@ -123,5 +123,9 @@ inline double now_ms() {
 // stream creates a hardware queue (~0.1 s on MI355X), so domains, scenes,
 // smoothing results and solves share it instead of creating their own.
 hipError_t device_stream(int device, hipStream_t* out);
+// A second such stream per device for device-to-device copies out of a
+// finished result (rthx_result_copy_csr_device), so that the next trace on
+// the device stream does not queue behind them.
+hipError_t copy_stream(int device, hipStream_t* out);
 
 }  // namespace rthx

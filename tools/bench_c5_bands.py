@@ -133,7 +133,8 @@ def emulate_pipeline(a):
     behind the next trace: for the last piece traced."""
     import torch
 
-    from rthx.distributed import EmulatedBandComm, HipShardTracer, trace_bands_row_sharded, traced_bands
+    from rthx.distributed import (EmulatedBandComm, HipShardTracer, assembly_order, trace_bands_row_sharded,
+                                  traced_bands)
 
     W = a.emulate_world
     dom = H.greenhouse_domain()
@@ -143,6 +144,7 @@ def emulate_pipeline(a):
     traced = traced_bands(dom)
     ranks = [int(x) for x in a.ranks.split(",")] if a.ranks else list(range(W))
     P = a.last_parts
+    print("pipeline order (rthx.distributed.assembly_order):", [b for b, _ in assembly_order(dom, traced)])
     print(f"C5 pipeline, W={W} emulated on one GPU, {rays:.3e} rays per band, {len(traced)} band traces "
           f"(the last in {P} pieces); xGMI model {a.xgmi_gbs:.0f} GB/s per link", flush=True)
     worst = 0.0
