@@ -270,3 +270,31 @@ def test_merge_row_shards_host_matches_merge_csr():
                       else np.zeros(0, np.int32))
         m = merge_row_shards_host(ros, cs, ns, n)
         assert np.array_equal(m[0], rp) and np.array_equal(m[1], cols) and np.array_equal(m[2], cnt)
+
+
+def test_band_pieces_and_assembly_order():
+    """band_pieces: every band whole but the last, whose pieces cover the
+    rank's rows exactly once; assembly_order: a permutation of the traced
+    bands with the most transparent one last."""
+    from rthx.distributed import assembly_order, band_pieces, traced_bands
+
+    N, W = 103, 4
+    for P in (1, 2, 3):
+        for rank in range(W):
+            pcs = band_pieces(8, rank, W, P)
+            assert [i for _t, i, *_ in pcs[:7]] == list(range(7))
+            assert all(s == W and b == rank and p == 1 for _t, _i, b, s, p in pcs[:7])
+            last = pcs[7:]
+            assert len(last) == P and all(i == 7 and p == P for _t, i, _b, _s, p in last)
+            rows = sorted(r for _t, _i, b, s, _p in last for r in range(b, N, s))
+            assert rows == list(range(rank, N, W))
+    dom = H.greenhouse_domain(n_layers=4, nx=5, ny=2, n_bins=8)
+    traced = traced_bands(dom)
+    order = assembly_order(dom, traced)
+    assert sorted(b for b, _ in order) == sorted(b for b, _ in traced)
+    flat = dom.flat()
+    nf = len(flat.fine_volume)
+    beta = np.asarray(flat.beta).reshape(-1, nf)
+    tau = {b: float(np.dot(beta[b - 1], np.abs(flat.fine_volume))) for b, _ in traced}
+    assert tau[order[-1][0]] == min(tau.values())
+    assert [b for b, _ in order[:-1]] == [b for b, _ in traced if b != order[-1][0]]
