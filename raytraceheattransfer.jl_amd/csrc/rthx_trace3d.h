@@ -196,9 +196,9 @@ constexpr int kTrace3dThreads = RTHX_T3_THREADS;  // lanes per workgroup
 // Breadth-first top of the node array (rthx_trace3d.cpp layout_nodes): the
 // kernel stages the first 64 or 128 nodes in LDS (launch_trace3d).
 constexpr int kTopNodes = 128;
-// static LDS of the 3D kernel: emitter, counters and (at least) the 64-node
-// cache
-constexpr size_t kTrace3dStaticLds = 512 + 64 * 64;
+// static LDS of the 3D kernel: emitter, counters, (at least) the 64-node
+// cache and the fast-path kernels' deferred-walk rings (128 ray indices per wave)
+constexpr size_t kTrace3dStaticLds = 512 + 64 * 64 + (size_t)(kTrace3dThreads / 64) * 128 * 4;
 // dynamic LDS: the row histogram (`words` = N, or (N + 1) / 2 packed u16,
 // padded to 64), then the stacks, then (box hull) the face records and lines
 __host__ __device__ constexpr size_t trace3d_stack_offset(int64_t words) { return (size_t)((words + 63) & ~int64_t(63)); }

@@ -35,6 +35,9 @@ constexpr int kThreads = kTrace3dThreads;
 #ifndef RTHX_T3_REFILL
 #define RTHX_T3_REFILL 16  // ray regeneration: refill batch (lanes); 0 = one ray per lane per pass
 #endif
+#ifndef RTHX_T3_DEFER
+#define RTHX_T3_DEFER 1  // fast-path kernels: rays that need a walk are deferred and walked a wave at a time
+#endif
 #ifndef RTHX_T3_WAVES
 #define RTHX_T3_WAVES 6  // waves per SIMD the LDS-histogram kernels are built for (1 = compiler's choice; 6 with the table in global memory: L3 9.43 -> 9.53 Grays/s)
 #endif
@@ -496,28 +499,76 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(MODE =
   constexpr int kRefill = RTHX_T3_REFILL;
   Walk w;
   bool live = false;
+  // The fast paths (HULL, CVX) settle most rays at emission; the few that
+  // need a BVH walk are deferred (DEFER): their ray index goes to a per-wave
+  // ring in LDS, and once the ring holds a wave's worth (or the slice has no
+  // rays left) the wave walks them together, every idle lane taking the
+  // next deferred ray and repeating its emission and fast path (the same
+  // arithmetic, so the same hit).  Walks then run with the wave's lanes
+  // busy instead of beside lanes that finish a fast ray every trip.
+  constexpr bool DEFER = (HULL || CVX) && RTHX_T3_DEFER;
+  constexpr uint32_t kRing = 128;  // ring entries per wave (a full ring: walk at once)
+  __shared__ uint32_t s_ring[DEFER ? kThreads / 64 : 1][DEFER ? kRing : 1];
+  uint32_t RTHX_LDS* ring = (uint32_t RTHX_LDS*)&s_ring[DEFER ? tid >> 6 : 0][0];
+  uint32_t q_head = 0, q_cnt = 0;  // wave-uniform
+  bool walking = false, drained = false;  // wave-uniform: the walk phase; the slice has no new rays
+  // (lanes below this one among those of mask m: v_mbcnt)
+  auto below = [](uint64_t m) {
+    return (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+  };
   while (true) {
     if (__popcll(__ballot(!live)) >= kRefill || __ballot(live) == 0ull) {
-      if (!live) {
-        const uint32_t r = atomicAdd(&s_next, 1u);
-        if (r < (uint32_t)r_end) {
-          const Emit3 RTHX_LDS* em = lds_opaque(&s_emit);
-          double o[3], d[3];
-          bool deep;
-          emit_ray<FAITHFUL>(*(const Emit3*)em, s_tab, (uint32_t)g, r, P.key0, P.key1,
-                             o, d, deep);
-          w.init(o, d);
-          if (MODE == 0) w.node = S.full_root;  // (a box-hull scene whose hull records did not fit in LDS: the whole BVH)
-          if (HULL)  // (a convex interior emitter's deep ray, or one that misses the interior's ball, meets no interior triangle: no walk)
-            w.node = w.hull_hit(S, grp, hf, hl)
-                         ? (S.n_in_nodes > 0 && !(convex && deep) && w.meets_ball(S) ? 0 : kWalkDone)
-                         : S.full_root;
-          if (CVX && deep && w.convex_exit(S)) w.node = kWalkDone;
-          live = true;
+      const bool wphase = DEFER && walking;
+      uint32_t r = 0;
+      bool got = false;
+      if (wphase) {  // walk phase: idle lanes take deferred rays
+        const uint64_t idle = __ballot(!live);
+        const uint32_t n_idle = (uint32_t)__popcll(idle);
+        const uint32_t take = q_cnt < n_idle ? q_cnt : n_idle;
+        const uint32_t rank = below(idle);
+        if (!live && rank < take) {
+          r = ring[(q_head + rank) & (kRing - 1)];
+          got = true;
         }
+        q_head = (q_head + take) & (kRing - 1);
+        q_cnt -= take;
+        walking = q_cnt != 0;
+      } else if (!drained) {
+        if (!live) {
+          r = atomicAdd(&s_next, 1u);
+          got = r < (uint32_t)r_end;
+        }
+        if (DEFER) drained = __ballot(!live && !got) != 0ull;
+      }
+      // A ray's emission and fast path (its walk's start in w.node,
+      // kWalkDone when it needs none); a deferred ray's CVX map is known to
+      // have found nothing.
+      if (got) {
+        const Emit3 RTHX_LDS* em = lds_opaque(&s_emit);
+        double o[3], d[3];
+        bool deep;
+        emit_ray<FAITHFUL>(*(const Emit3*)em, s_tab, (uint32_t)g, r, P.key0, P.key1, o, d, deep);
+        w.init(o, d);
+        if (MODE == 0) w.node = S.full_root;  // (a box-hull scene whose hull records did not fit in LDS: the whole BVH)
+        if (HULL)  // (a convex interior emitter's deep ray, or one that misses the interior's ball, meets no interior triangle: no walk)
+          w.node = w.hull_hit(S, grp, hf, hl)
+                       ? (S.n_in_nodes > 0 && !(convex && deep) && w.meets_ball(S) ? 0 : kWalkDone)
+                       : S.full_root;
+        if (CVX && !wphase && deep && w.convex_exit(S)) w.node = kWalkDone;
+        live = true;
+      }
+      if (DEFER && !wphase) {  // rays that need a walk go to the ring
+        const bool defer = got && w.node != kWalkDone;
+        const uint64_t dm = __ballot(defer);
+        if (defer) {
+          ring[(q_head + q_cnt + below(dm)) & (kRing - 1)] = r;
+          live = false;
+        }
+        q_cnt += (uint32_t)__popcll(dm);  // (q_cnt < 64 before: never more than kRing)
+        walking = q_cnt >= 64 || (drained && q_cnt > 0);
       }
     }
-    if (__ballot(live) == 0ull) break;
+    if (__ballot(live) == 0ull && (!DEFER || (drained && q_cnt == 0))) break;
     if (live && !w.step(S, topo, n_top, grp, glo, glen, stk)) {
       tally(w.best_poly);
       live = false;
