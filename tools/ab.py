@@ -46,6 +46,11 @@ def main():
     ap.add_argument("--env", default="",
                     help="NAME=v1,v2,...: every library is also timed with each value of that knob "
                          "(RTHX_DEV_KNOBS is set; 'auto' leaves the knob unset)")
+    ap.add_argument("--with-pack", action="store_true",
+                    help="time trace + pack (staged rows: row scan, part merge, CSR pack) instead of the trace kernel alone")
+    ap.add_argument("--sets", default="",
+                    help="knob sets separated by '|', each 'NAME=v:NAME2=v2' ('none' = no knobs): every library is "
+                         "also timed with each set (replaces --env)")
     args = ap.parse_args()
     import bench
 
@@ -63,9 +68,22 @@ def main():
     targs, _k = _lib.make_args(max(args.c5_bin, 0), R, nudge, 1, 0, N, args.stride, flags=abi.RTHX_FLAG_DEVICE_ONLY)
     os.environ["RTHX_DEV_KNOBS"] = "1"
     knob, vals = (args.env.split("=", 1)[0], args.env.split("=", 1)[1].split(",")) if args.env else (None, [None])
+    if args.sets:
+        knob, vals = "sets", args.sets.split("|")
+    set_names = set()
+    for v in (vals if knob == "sets" else []):
+        set_names |= {kv.split("=", 1)[0] for kv in v.split(":") if "=" in kv}
 
     def set_knob(v):
         if knob is None:
+            return
+        if knob == "sets":
+            for k in set_names:
+                os.environ.pop(k, None)
+            for kv in v.split(":"):
+                if "=" in kv:
+                    k, x = kv.split("=", 1)
+                    os.environ[k] = x
             return
         if v in (None, "auto"):
             os.environ.pop(knob, None)
@@ -83,7 +101,8 @@ def main():
             for _ in range(2):
                 assert lib.rthx_trace_exchange(h, C.byref(targs), r) == 0, lib.rthx_last_error()
             tag = os.path.basename(os.path.dirname(p)) or p
-            runs.append((tag + (f" {knob}={v}" if knob else ""), lib, h, r, [], v))
+            label = f" [{v}]" if knob == "sets" else (f" {knob}={v}" if knob else "")
+            runs.append((tag + label, lib, h, r, [], v))
     for _ in range(args.rounds):
         for p, lib, h, r, ts, v in runs:
             set_knob(v)
@@ -91,7 +110,7 @@ def main():
                 assert lib.rthx_trace_exchange(h, C.byref(targs), r) == 0
                 inf = abi.ResultInfo()
                 lib.rthx_result_get_info(r, C.byref(inf))
-                ts.append(inf.trace_ms)
+                ts.append(inf.trace_ms + (inf.pack_ms if args.with_pack else 0.0))
     rays = len(range(0, N, args.stride)) * R
     for p, lib, h, r, ts, v in runs:
         t = np.array(ts)
