@@ -277,6 +277,40 @@ def greenhouse_domain(n_layers=67, nx=201, ny=3, n_bins=8, scale_height=15_900.0
     return RayTracingDomain2D(faces, [(nx, ny)] * n_layers)
 
 
+def layered_slab_domain(kappas, W=100.0, nx=21):
+    """A W x 1 slab between two black plates cut into len(kappas) horizontal
+    layers of equal height, layer j with extinction kappas[j] (a coarse
+    rectangle each, meshed nx x 2; side walls solid, interfaces open): the
+    traceRayVariable walk (traceRay.jl:73-147) across every layer.  Plate
+    to plate, a cold non-scattering slab transmits 2 E3(tau) of a Lambert
+    emitter's rays, tau = sum(kappas) / len(kappas) (slab_transmission)."""
+    L = len(kappas)
+    faces = []
+    for j, k in enumerate(kappas):
+        y0, y1 = j / L, (j + 1) / L
+        f = PolyVolume2D([(0.0, y0), (W, y0), (W, y1), (0.0, y1)], [j == 0, True, j == L - 1, True], 1, float(k), 0.0)
+        f.epsilon = [1.0] * 4
+        f.T_in_g = -1.0
+        faces.append(f)
+    return RayTracingDomain2D(faces, [(nx, 2)] * L)
+
+
+def slab_transmission(dom, row_ptr, cols, counts, n_central=5):
+    """(mean, standard error) over the n_central middle bottom-plate elements
+    of the fraction of each row's tallied rays absorbed by the top plate."""
+    L, nx = len(dom.fine_mesh), len(dom.fine_mesh[0]) // 2  # (fine faces x fastest: row 1 then row 2)
+    top = np.array(sorted(dom.surface_mapping[(L, f, 3)] - 1 for f in range(nx + 1, 2 * nx + 1)))
+    lo = (nx - n_central) // 2 + 1
+    fr = []
+    for f in range(lo, lo + n_central):
+        g = dom.surface_mapping[(1, f, 1)] - 1
+        c = cols[row_ptr[g]:row_ptr[g + 1]]
+        n = counts[row_ptr[g]:row_ptr[g + 1]].astype(np.float64)
+        fr.append(n[np.isin(c, top)].sum() / n.sum())
+    fr = np.array(fr)
+    return float(fr.mean()), float(fr.std(ddof=1) / math.sqrt(len(fr)))
+
+
 def quad_lattice_domain(ncx=2, ncy=3, nxf=4, nyf=3, kappa=0.8):
     """A unit square cut into an ncx x ncy lattice of coarse squares (outer
     walls solid, interior walls open), each meshed nxf x nyf: a multi-polygon

@@ -241,3 +241,62 @@ def test_icosphere_enclosure_montecarlo(hip, level):
     T_eq = dom.facesMesh[eq].subFaces[0].T_w
     assert abs(T_eq - ico["T_limit"]) < 2.0, T_eq
     assert abs(dom.energy_error) < H.golden("reference_3d.json")["energy_tolerance_W"] * 100
+
+
+# --- traceRayVariable against an analytic answer (layered slab) ------------
+@pytest.mark.parametrize("kappas,tau", [([0.2, 0.5, 1.5, 2.0, 0.8], 1.0), ([0.05, 0.05, 2.4], 0.8333333333333334),
+                                        ([4.0, 0.0, 0.0, 0.0], 1.0)])
+def test_layered_slab_transmission_is_2E3(hip, kappas, tau):
+    """A cold non-scattering slab between black plates, cut into layers of
+    different extinction (the layered-lattice walk of C5's kernels), and its
+    one-layer twin of the same optical thickness (traceRayUniform): the
+    central bottom-plate elements send 2 E3(tau) of their rays to the top
+    plate (within 4.5 standard errors at 2e6 rays per element + 0.05 %),
+    and the layered slab's counts equal the CPU restatement exactly at 2e4
+    rays per element (test_oracle_known_answers.py pins the restatement to
+    the same value).
+
+    Transparent (kappa = 0) layers are the one place where DESIGN.md §5's
+    rounding-level difference (fp64 FMA contraction of p + t d on the
+    device) was seen to change a ray: a nearly out-of-plane ray (|dy| =
+    3.3e-5) crosses the empty top layer and ends 7e-17 below the top wall;
+    the restatement's two roundings put its end point on the wall (outside
+    every cell: lost, as the reference's would), the fused one inside (the
+    top wall).  For such profiles the test bounds the difference to exactly
+    that: rays the restatement loses and the device tallies to a wall,
+    at most 1 in 1e6."""
+    from scipy.special import expn
+
+    exact = 2.0 * expn(3, tau)
+    for ks in (kappas, [tau]):
+        dom = H.layered_slab_domain(ks)
+        flat = dom.flat()
+        dd = hip.DeviceDomain(flat, 0)
+        res = hip.DeviceResult()
+        try:
+            args, _k = hip.make_args(0, 2_000_000, H.NUDGE, 7, 0, flat.n_emitters, 1)
+            res.trace(dd, args)
+            info = res.info()
+            rp, cols, cnt = res.csr()
+            assert info["lost_total"] <= 1e-6 * info["rays_traced"]
+            mean, se = H.slab_transmission(dom, rp, cols, cnt)
+            assert abs(mean - exact) < 4.5 * se + 5e-4 * exact, (ks, mean, se, exact)
+            args, _k = hip.make_args(0, 20_000, H.NUDGE, 11, 0, flat.n_emitters, 1)
+            res.trace(dd, args)
+            rp, cols, cnt = res.csr()
+            info = res.info()
+            orp, ocols, ocnt, oi, _ = oracle.trace_exchange(flat, args, 16)
+            if min(ks) > 0.0:
+                assert np.array_equal(rp, orp) and np.array_equal(cols, ocols) and np.array_equal(cnt, ocnt), ks
+            else:
+                n = flat.n_emitters
+                dev = sp.csr_matrix((cnt.astype(np.int64), cols, rp), shape=(n, n))
+                ora = sp.csr_matrix((ocnt.astype(np.int64), ocols, orp), shape=(n, n))
+                diff = (dev - ora).tocoo()
+                extra = int(oi["lost_total"] - info["lost_total"])
+                assert diff.nnz == 0 or (diff.data > 0).all(), ks  # the device only gains rays
+                assert int(diff.data.sum()) == extra <= 1e-6 * info["rays_traced"], (ks, extra)
+                assert (diff.col < dom.num_surfaces).all(), ks  # ... tallied to walls
+        finally:
+            res.close()
+            dd.close()
