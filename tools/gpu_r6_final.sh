@@ -26,3 +26,8 @@ for L in 2 3; do
   timeout -k 10 300 python tools/bench_trace3d.py --interior --level $L >> $OUT/trace3d_$TAG.log 2>&1 || exit 1
 done
 grep config4 $OUT/trace3d_$TAG.log | cut -c1-90,300-480
+# the driver's multi-GPU launch shape rehearsed on this one GPU (2 ranks share
+# device 0: a code-path check, no scaling claim)
+timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 \
+  bench.py --gpus 2 --steps 5 --warmup 2 --philox10-steps 0 --faithful-steps 0 > $OUT/bench2_$TAG.log 2>&1 || { tail -20 $OUT/bench2_$TAG.log; exit 1; }
+grep '"metric"' $OUT/bench2_$TAG.log | cut -c1-200
