@@ -600,14 +600,6 @@ RTHX_EXPORT int rthx_domain_create(const rthx_domain_desc* desc, int32_t device,
       size_t off = a16(8 * xs.size());
       L.off_ys = (int32_t)off;
       off = a16(off + 8 * ys.size());
-      L.off_bot = (int32_t)off;
-      off = a16(off + 4 * lnx);
-      L.off_right = (int32_t)off;
-      off = a16(off + 4 * lny);
-      L.off_top = (int32_t)off;
-      off = a16(off + 4 * lnx);
-      L.off_left = (int32_t)off;
-      off = a16(off + 4 * lny);
       L.bytes = (int32_t)off;
       L.inv_x = (double)lnx / (xs[lnx] - xs[0]);
       L.inv_y = (double)lny / (ys[lny] - ys[0]);
@@ -616,18 +608,6 @@ RTHX_EXPORT int rthx_domain_create(const rthx_domain_desc* desc, int32_t device,
       std::memset(b, 0, off);
       std::memcpy(b, xs.data(), 8 * xs.size());
       std::memcpy(b + L.off_ys, ys.data(), 8 * ys.size());
-      int32_t* bot = reinterpret_cast<int32_t*>(b + L.off_bot);
-      int32_t* right = reinterpret_cast<int32_t*>(b + L.off_right);
-      int32_t* top = reinterpret_cast<int32_t*>(b + L.off_top);
-      int32_t* left = reinterpret_cast<int32_t*>(b + L.off_left);
-      for (int64_t i = 0; i < lnx; ++i) {
-        bot[i] = s.fine_surface[4 * (size_t)map[i] + 0];
-        top[i] = s.fine_surface[4 * (size_t)map[(lny - 1) * lnx + i] + 2];
-      }
-      for (int64_t j = 0; j < lny; ++j) {
-        right[j] = s.fine_surface[4 * (size_t)map[j * lnx + lnx - 1] + 1];
-        left[j] = s.fine_surface[4 * (size_t)map[j * lnx] + 3];
-      }
       UP(blob.data(), blob.size(), D.lat_blob);
       if (!identity) UP(map.data(), map.size(), D.lat_map);
       D.lat = L;

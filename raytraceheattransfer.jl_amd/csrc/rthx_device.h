@@ -81,16 +81,16 @@ struct CoarseLayout {
 // Lattice form of a single axis-aligned coarse rectangle whose fine cells
 // are the nx x ny rectangles [xs[i], xs[i+1]) x [ys[j], ys[j+1]) (meshQuad
 // on a rectangle, meshQuad.jl:139-179).  LAT kernels stage the blob in LDS:
-// xs[nx+1], ys[ny+1] (f64), then the surface index of the boundary walls
-// bottom[nx], right[ny], top[nx], left[ny] (i32, -1 where not solid; every
-// interior fine wall is open).  Fine cell (i, j) is polygon j nx + i when
-// `identity`, else lat_map[j nx + i].  bytes == 0: not a lattice.
+// xs[nx+1], ys[ny+1] (f64; every interior fine wall is open, the boundary
+// walls' surface indices come from f_surf).  Fine cell (i, j) is polygon
+// j nx + i when `identity`, else lat_map[j nx + i].  bytes == 0: not a
+// lattice.
 struct LatticeLayout {
   int32_t bytes;             // blob bytes (multiple of 16)
   int32_t nx, ny;
   int32_t identity;
-  int32_t off_ys, off_bot, off_right, off_top, off_left;
-  int32_t reserved;
+  int32_t off_ys;
+  int32_t reserved[5];
   double inv_x, inv_y;       // nx / (xs[nx] - xs[0]), ny / (ys[ny] - ys[0]): first guess of the cell
 };
 
@@ -989,20 +989,12 @@ __device__ __forceinline__ int lattice_index(const double RTHX_LDS* b, int n, do
 struct LatticeLds {
   const double RTHX_LDS* xs;
   const double RTHX_LDS* ys;
-  const int32_t RTHX_LDS* bot;
-  const int32_t RTHX_LDS* right;
-  const int32_t RTHX_LDS* top;
-  const int32_t RTHX_LDS* left;
 };
 
 __device__ __forceinline__ LatticeLds lattice_lds_view(const char RTHX_LDS* base, const LatticeLayout& L) {
   LatticeLds v;
   v.xs = (const double RTHX_LDS*)base;
   v.ys = (const double RTHX_LDS*)(base + L.off_ys);
-  v.bot = (const int32_t RTHX_LDS*)(base + L.off_bot);
-  v.right = (const int32_t RTHX_LDS*)(base + L.off_right);
-  v.top = (const int32_t RTHX_LDS*)(base + L.off_top);
-  v.left = (const int32_t RTHX_LDS*)(base + L.off_left);
   return v;
 }
 
@@ -1055,20 +1047,12 @@ __device__ __forceinline__ int segment_lat(const DevDomain& D, const TraceParams
   // four-wall test of dist_to_rect would find it (w = 0 when none qualifies,
   // distToSurface2D's findmin)
   const int w = box_hit_in(px, py, dx, dy, dx < 0.0 ? L.xs[i] : L.xs[i + 1], dy < 0.0 ? L.ys[j] : L.ys[j + 1]).wall;
-  // w 0 / 1 / 2 / 3: bot[i] if j = 0, right[j] if i = nx - 1, top[i] if
-  // j = ny - 1, left[j] if i = 0, else an interior wall (-1); one read at a
-  // selected address instead of a branch per wall
-  // (the array is picked by its byte offset in the blob: selecting among the
-  // four LDS pointers made the compiler index a scratch copy of them)
-  const bool wy = (w & 1) == 0;  // bottom or top: indexed by i
-  // (the four offsets are uniform: read into scalars, then selected per lane,
-  // not a per-lane load from a selected address)
-  const int o_bot = __builtin_amdgcn_readfirstlane(G.off_bot), o_right = __builtin_amdgcn_readfirstlane(G.off_right);
-  const int o_top = __builtin_amdgcn_readfirstlane(G.off_top), o_left = __builtin_amdgcn_readfirstlane(G.off_left);
-  const int off = w == 0 ? o_bot : w == 1 ? o_right : w == 2 ? o_top : o_left;
-  const int edge = w == 0 ? j : w == 1 ? G.nx - 1 - i : w == 2 ? G.ny - 1 - j : i;
-  const char RTHX_LDS* base = (const char RTHX_LDS*)L.xs;  // (xs opens the blob)
-  return edge == 0 ? *(const int32_t RTHX_LDS*)(base + off + 4 * (wy ? i : j)) : -1;
+  // the wall's surface index (-1 where not solid: every interior wall) from
+  // the domain's table, one L2-resident load at the ray's end (round 6: the
+  // same index as the boundary arrays the lattice blob held, without the
+  // per-lane selects of array and edge; headline 0.7722 -> 0.7658 ms, D2
+  // 19.92 -> 19.58 ms, profiles/round6/ab/lat_fsurf.log)
+  return D.f_surf[4 * (G.identity ? j * G.nx + i : D.lat_map[j * G.nx + i]) + w];
 }
 
 // ---------------------------------------------------------------------------
