@@ -311,6 +311,17 @@ struct RayDraws {
 __host__ __device__ __forceinline__ uint64_t dbits(double x) { return __builtin_bit_cast(uint64_t, x); }
 __host__ __device__ __forceinline__ double bitsd(uint64_t b) { return __builtin_bit_cast(double, b); }
 
+// A polynomial coefficient held in an SGPR pair at its point of use (device
+// code): an fma whose addend is a scalar register is the non-destructive
+// VOP3 form, where a coefficient kept in a VGPR pair was copied into the
+// destructive v_fmac's accumulator for every ray.  The value is unchanged.
+__host__ __device__ __forceinline__ double sconst(double c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __asm__ volatile("" : "+s"(c));
+#endif
+  return c;
+}
+
 // -ln(u) for u in (0, 1] from a 128-entry table (the free path
 // S = -ln(u)/beta, traceRay.jl:25,79).  u = 2^k z with z in [0.6875, 1.375)
 // (so u near 1 keeps k = 0), table entry i = 7 bits of z below the exponent:
@@ -331,9 +342,9 @@ __host__ __device__ __forceinline__ double neg_log_tab(double u, const double* t
   const double invc = tab[4 * i], t_hi = tab[4 * i + 1], t_lo = tab[4 * i + 2];
   const double r = __builtin_fma(z, invc, -1.0);
   double q = __builtin_fma(r, 1.0 / 7.0, -1.0 / 6.0);
-  q = __builtin_fma(r, q, 1.0 / 5.0);
+  q = __builtin_fma(r, q, sconst(1.0 / 5.0));
   q = __builtin_fma(r, q, -1.0 / 4.0);
-  q = __builtin_fma(r, q, 1.0 / 3.0);
+  q = __builtin_fma(r, q, sconst(1.0 / 3.0));
   q = __builtin_fma(r, q, -0.5);
   const double l1p = __builtin_fma(r * r, q, r);
   const double kd = (double)k;
@@ -356,9 +367,9 @@ __host__ __device__ __forceinline__ double neg_log_u32(uint32_t w, const double*
   const double invc = tab[4 * i], t_hi = tab[4 * i + 1], t_lo = tab[4 * i + 2];
   const double r = __builtin_fma(z, invc, -1.0);
   double q = __builtin_fma(r, 1.0 / 7.0, -1.0 / 6.0);
-  q = __builtin_fma(r, q, 1.0 / 5.0);
+  q = __builtin_fma(r, q, sconst(1.0 / 5.0));
   q = __builtin_fma(r, q, -1.0 / 4.0);
-  q = __builtin_fma(r, q, 1.0 / 3.0);
+  q = __builtin_fma(r, q, sconst(1.0 / 3.0));
   q = __builtin_fma(r, q, -0.5);
   const double l1p = __builtin_fma(r * r, q, r);
   const double kd = (double)k;
@@ -413,7 +424,7 @@ __device__ __forceinline__ double cos_2pi_u32(uint32_t w, const double* tab) {
   const double d = (double)(w & 0xFFFFFFu) * (RTHX_TWO_PI * 0x1.0p-32);
   const double z = d * d;
   const double cd = __builtin_fma(z, __builtin_fma(z, __builtin_fma(z, -1.0 / 720.0, 1.0 / 24.0), -0.5), 1.0);
-  const double ps = __builtin_fma(z, __builtin_fma(z, -1.0 / 5040.0, 1.0 / 120.0), -1.0 / 6.0);
+  const double ps = __builtin_fma(z, __builtin_fma(z, -1.0 / 5040.0, 1.0 / 120.0), sconst(-1.0 / 6.0));
   const double sd = __builtin_fma(d * z, ps, d);
   const double C = tab[2 * j], S = tab[2 * j + 1];
   return __builtin_fma(C, cd, -(S * sd));
@@ -867,10 +878,13 @@ __device__ __forceinline__ void emit_volume(const Emitter& e, double eta, const 
   } else {
     // u4 = u32(a2) without forming it: ct = 1 - 2 u4 = fma(w, -2^-31, 1) and
     // u4 (1 - u4) = w ((1 - u4) 2^-32), the factor an exact power-of-two
-    // scaling of RN(1 - u4) -- the same values as from u4
+    // scaling of RN(1 - u4) -- the same values as from u4.  (RN(1 - u4) is
+    // formed against the inline constant 1.0 and then scaled by a literal:
+    // fma(w, -2^-64, 2^-32) needed the addend 2^-32 moved into a VGPR pair
+    // for every ray.)
     const double w4 = (double)rw.a[2];
     ct = __builtin_fma(w4, -0x1.0p-31, 1.0);           // cos(acos(x)) = x
-    const double om = __builtin_fma(w4, -0x1.0p-64, 0x1.0p-32);
+    const double om = __builtin_fma(w4, -0x1.0p-32, 1.0) * 0x1.0p-32;
     st = 2.0 * sqrt_unit(w4 * om);                      // sin(acos(x)) = sqrt((1-x)(1+x))
     cphi = cos_2pi_u32(rw.a[3], cos_tab);
   }

@@ -49,6 +49,9 @@ namespace rthx {
 #endif
 constexpr int kBufferRsrcWord3 = 0x00020000;
 constexpr int kSc1 = 16;
+#ifndef RTHX_PW_ROTATE
+#define RTHX_PW_ROTATE 1  // SINGLE group rounds: free-path words by rotation (0: per-lane selects on r & 3)
+#endif
 #ifndef RTHX_GTAB
 // 1: the cos / log tables (and 1 / beta_uniform) read from the domain's
 // per-bin copy in global memory (L1 / L2) instead of LDS: 8 KB less LDS per
@@ -559,11 +562,26 @@ __global__ __launch_bounds__(kMaxTraceThreads) RTHX_TRACE_WAVES void trace_excha
         uint32_t b[4];
         philox_words(r >> 2, (uint32_t)g, 1u, (uint32_t)P.bin, P.key0, P.key1, b);
         b0 = b[0]; b1 = b[1]; b2 = b[2]; b3 = b[3];
+#if RTHX_PW_ROTATE
+        if (!grp) {
+          // (a tail ray's own block: word r & 3 by bit selects -- a compare
+          // chain becomes a branchy switch)
+          const uint32_t k = r & 3u;
+          b0 = (k & 2u) ? ((k & 1u) ? b3 : b2) : ((k & 1u) ? b1 : b0);
+        }
+#endif
       }
-      // (word r & 3 of the block by bit selects: a compare chain becomes a
-      // branchy switch)
+#if RTHX_PW_ROTATE
+      // the group rounds' rays take the block's words in order: b0, then the
+      // words move down (three moves instead of per-lane selects on r & 3)
+      const uint32_t pw = b0;
+      b0 = b1;
+      b1 = b2;
+      b2 = b3;
+#else
       const uint32_t k = r & 3u;
       const uint32_t pw = (k & 2u) ? ((k & 1u) ? b3 : b2) : ((k & 1u) ? b1 : b0);
+#endif
       if (r >= rb && r < re) one_ray(r, true, pw, ek);
     }
     };
