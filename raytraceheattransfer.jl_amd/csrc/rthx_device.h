@@ -399,9 +399,12 @@ __device__ __forceinline__ double div_pos(double n, double d) {
 
 // sqrt(x) for x in {0} U [2^-60, 1]: the rsq + Newton sequence of the
 // correctly rounded IEEE sqrt without its subnormal/overflow rescaling
-// (the operands here are unit draws, far from either).
+// (the operands here are unit draws, far from either).  x = 0 takes
+// rsq(2^-1000) = 2^500, a finite estimate, and the sequence then yields 0
+// itself (g = 0 x 2^500, every correction 0), so no select on x > 0 is
+// needed; every x in [2^-60, 1] is its own max.
 __device__ __forceinline__ double sqrt_unit(double x) {
-  const double y = __builtin_amdgcn_rsq(x);
+  const double y = __builtin_amdgcn_rsq(__builtin_fmax(x, 0x1.0p-1000));
   double g = x * y, h = 0.5 * y;
   const double r = __builtin_fma(-h, g, 0.5);
   g = __builtin_fma(g, r, g);
@@ -410,7 +413,7 @@ __device__ __forceinline__ double sqrt_unit(double x) {
   g = __builtin_fma(d, h, g);
   d = __builtin_fma(-g, g, x);
   g = __builtin_fma(d, h, g);
-  return x > 0.0 ? g : x;
+  return g;
 }
 
 // cos(2 pi w / 2^32) for a 32-bit draw w (emitVolumeRay2D.jl:28-31: phi = 2 pi u,
@@ -504,26 +507,28 @@ __device__ __forceinline__ double dist_to_box(double px, double py, double dx, d
 // compared in wall order as the four-wall loop does.  Two bounds are read
 // instead of four and two walls tested instead of four.
 struct BoxHit {
-  double num, den;  // the winning wall's |num|, |den| (parameter num / den)
+  double num, den;  // the winning wall's num, den, signed (parameter |num| / |den|)
   int wall;         // its index (0 when no wall qualifies)
   bool any;
 };
 
 __device__ __forceinline__ BoxHit box_hit_in(double px, double py, double dx, double dy, double xb, double yb) {
   const bool xdn = dx < 0.0, ydn = dy < 0.0;
-  const double nx = fabs(xb - px), ny = fabs(yb - py), ax = fabs(dx), ay = fabs(dy);
+  // (the magnitudes enter every product as operand modifiers; the winner's
+  // num and den are selected signed, so no |x| is formed in a register)
+  const double sx = xb - px, sy = yb - py;
   // (num den > 0: den = |d| on the chosen side, > 0 unless d is 0 there)
-  const bool vx = ax >= 1e-10 && __dmul_rn(nx, ax) > 0.0;
-  const bool vy = ay >= 1e-10 && __dmul_rn(ny, ay) > 0.0;
+  const bool vx = fabs(dx) >= 1e-10 && __dmul_rn(fabs(sx), fabs(dx)) > 0.0;
+  const bool vy = fabs(dy) >= 1e-10 && __dmul_rn(fabs(sy), fabs(dy)) > 0.0;
   // wall order: the y wall comes first unless it is the top wall (2) and the
   // x wall the right one (1); the later wall wins only if strictly closer
   const bool y_first = ydn || xdn;
-  const double cx = __dmul_rn(nx, ay), cy = __dmul_rn(ny, ax);
+  const double cx = __dmul_rn(fabs(sx), fabs(dy)), cy = __dmul_rn(fabs(sy), fabs(dx));
   const bool xw = vx && (!vy || (y_first ? cx < cy : !(cy < cx)));
   BoxHit h;
   h.any = vx || vy;
-  h.num = xw ? nx : ny;
-  h.den = xw ? ax : ay;
+  h.num = xw ? sx : sy;
+  h.den = xw ? dx : dy;
   h.wall = h.any ? (xw ? (xdn ? 3 : 1) : (ydn ? 0 : 2)) : 0;
   return h;
 }
@@ -533,8 +538,11 @@ __device__ __forceinline__ double dist_in_box(double px, double py, double dx, d
   const BoxHit h = box_hit_in(px, py, dx, dy, xb, yb);
   widx = h.wall;
   if (!h.any) return __builtin_inf();
-  const double u = div_pos(h.num, h.den);  // (num in [0, domain size], den >= 1e-10)
-  return u > 0.0 ? u : __builtin_inf();
+  // (a candidate has |num| > 0 and 1e-10 <= |den| <= 1 -- a direction is a
+  // unit 3D vector's projection -- so |num| / |den| >= |num| > 0 even for the
+  // least subnormal |num|: the reference's test u <= 0 -> Inf,
+  // distToSurface2D.jl:12, never fires for it)
+  return div_pos(fabs(h.num), fabs(h.den));
 }
 
 template <class Poly>
