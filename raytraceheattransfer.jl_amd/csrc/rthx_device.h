@@ -483,20 +483,25 @@ __device__ __forceinline__ double dist_to_box(double px, double py, double dx, d
                                               double y0, double y1, int& widx) {
   const double num[4] = {py - y0, x1 - px, y1 - py, px - x0};
   const double den[4] = {-dy, dx, dy, -dx};
+  // (the best wall's num and den are kept signed and their magnitudes taken
+  // as operand modifiers where they are used, so no |x| is formed in a
+  // register for the selects)
   double bn = 1.0, bd = 0.0;
   int bi = 0;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    double an = fabs(num[i]), ad = fabs(den[i]);
-    bool better = (ad >= 1e-10) && (__dmul_rn(num[i], den[i]) > 0.0) && (__dmul_rn(an, bd) < __dmul_rn(bn, ad));
-    bn = better ? an : bn;
-    bd = better ? ad : bd;
+    bool better = (fabs(den[i]) >= 1e-10) && (__dmul_rn(num[i], den[i]) > 0.0) &&
+                  (__dmul_rn(fabs(num[i]), fabs(bd)) < __dmul_rn(fabs(bn), fabs(den[i])));
+    bn = better ? num[i] : bn;
+    bd = better ? den[i] : bd;
     bi = better ? i : bi;
   }
   widx = bi;
   if (bd == 0.0) return __builtin_inf();
-  double u = div_pos(bn, bd);  // (bd >= 1e-10)
-  return u > 0.0 ? u : __builtin_inf();
+  // (a candidate has num den > 0, so |num| > 0, and 1e-10 <= |den| <= 1:
+  // |num| / |den| >= |num| > 0, and the reference's u <= 0 -> Inf,
+  // distToSurface2D.jl:12, never fires for it)
+  return div_pos(fabs(bn), fabs(bd));
 }
 
 // dist_to_box for a point in the half-open box [x0, x1) x [y0, y1) (MLAT
