@@ -163,8 +163,13 @@ RTHX_EXPORT int rthx_trace_direct(rthx_domain* dom, const double* weights, const
   HIP_TRY(Wk.n_lost.reserve(4), "hipMalloc lost counter");
   HIP_TRY(Wk.lost.reserve(chunk * 4), "hipMalloc lost list");
   if (!Wk.have_frames) {
-    HIP_TRY(Wk.sgeo.reserve(std::max<int64_t>(ns, 1) * sizeof(rthx::SurfGeo)), "hipMalloc surface frames");
+    // (entry ns: the gas's frame, t = (1, 0), which the kernel reads for a
+    // scattering lane from the same load a wall lane makes)
+    static const rthx::SurfGeo kGasFrame{1.0, 0.0, 0.0, 0.0};
+    HIP_TRY(Wk.sgeo.reserve((ns + 1) * sizeof(rthx::SurfGeo)), "hipMalloc surface frames");
     HIP_TRY(rthx::launch_surface_frames(dom->d_dom, ns, Wk.sgeo.as<rthx::SurfGeo>(), st), "surface_frames launch");
+    HIP_TRY(hipMemcpyAsync(Wk.sgeo.as<rthx::SurfGeo>() + ns, &kGasFrame, sizeof(kGasFrame), hipMemcpyHostToDevice, st),
+            "hipMemcpy gas frame");
     HIP_TRY(Wk.emit.reserve(n * sizeof(rthx::Emitter)), "hipMalloc emitter records");
     HIP_TRY(rthx::launch_emitter_table(dom->d_dom, n, Wk.emit.as<rthx::Emitter>(), st), "emitter_table launch");
     Wk.have_frames = true;

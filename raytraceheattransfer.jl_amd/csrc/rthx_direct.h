@@ -41,7 +41,7 @@ struct DirectParams {
   unsigned long long* next;       // item claim counter (zeroed before each launch)
   const uint64_t* alias;          // [n_elem] (alias index << 32) | acceptance threshold
   const DirectElem* el;           // [n_elem]
-  const SurfGeo* sgeo;            // [Ns]
+  const SurfGeo* sgeo;            // [Ns + 1]: the walls' frames, then the gas's ((1, 0), no midpoint)
   const Emitter* emitters;        // [n_elem] emission records (load_emitter, built once per domain)
   unsigned long long* counts;     // [3][n_elem] emitted, absorbed, redirected
   uint32_t* lost;                 // first pass: items of lost rays that committed path events

@@ -238,9 +238,10 @@ __global__ __launch_bounds__(FAITHFUL ? kDirectThreads : kDirectMaxThreads) RTHX
             dirty = true;
             ++ev;
             const double* tab = (const double*)lds_opaque(&s_tab[0]);
-            // the wall's frame (tangent, midpoint); the gas scatters in (1, 0)
-            SurfGeo sg{1.0, 0.0, 0.0, 0.0};
-            if (wall) sg = Q.sgeo[a];
+            // the wall's frame (tangent, midpoint); the gas scatters in (1, 0),
+            // the frame after the walls' (one load for every lane, no
+            // defaults to form and no branch)
+            const SurfGeo sg = Q.sgeo[wall ? a : Ns];
             if (wall && !redirect) {  // re-emission point nudged toward the fine midpoint (traceSingleRay.jl:40)
               px = px + __dmul_rn(sg.mx - px, eta);
               py = py + __dmul_rn(sg.my - py, eta);
