@@ -234,6 +234,9 @@ RTHX_EXPORT int rthx_trace_direct(rthx_domain* dom, const double* weights, const
     uint32_t nl = 0;
     HIP_TRY(hipMemcpyAsync(&nl, Wk.n_lost.p, 4, hipMemcpyDeviceToHost, st), "hipMemcpy lost count");
     HIP_TRY(hipStreamSynchronize(st), "direct kernels");
+#if RTHX_DIRECT_PROF
+    rthx::direct_prof_dump();  // (diagnostic builds: per-region lane counts of the first pass)
+#endif
     if (nl > 0) {
       // replay: roll back the path events of the lost rays
       Q.replay = Wk.lost.as<uint32_t>();

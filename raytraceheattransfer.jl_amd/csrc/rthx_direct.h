@@ -76,4 +76,7 @@ hipError_t launch_counter_reduce(const uint32_t* partial, int32_t n_blocks, int6
 hipError_t launch_surface_frames(const DevDomain* D, int32_t n_surfaces, SurfGeo* out, hipStream_t stream);
 hipError_t launch_emitter_table(const DevDomain* D, int64_t n, Emitter* out, hipStream_t stream);
 
+#if RTHX_DIRECT_PROF
+void direct_prof_dump();
+#endif
 }  // namespace rthx

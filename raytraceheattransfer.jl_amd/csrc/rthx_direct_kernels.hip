@@ -44,6 +44,28 @@ constexpr uint32_t kPoolClaim = 256;  // rays per global claim (one atomic per 2
 #endif
 constexpr int kDirectRefill = RTHX_DIRECT_REFILL;  // refill once this many lanes of a wave are idle
 
+// RTHX_DIRECT_PROF (diagnostic builds only): per region, the wave executions
+// and the lanes active in them, flushed to g_dprof at exit and printed by
+// the host after the launch (direct_prof_dump).  Regions: 0 emission lanes,
+// 1 leg (segment), 2 leg ended, 3 absorbed, 4 redirected, 5 fate, 6 refill;
+// 7 and 8: s_memtime ticks of the loop's refill part (emission included) and
+// of its leg part (segment and interaction), summed over waves.
+#ifndef RTHX_DIRECT_PROF
+#define RTHX_DIRECT_PROF 0
+#endif
+#if RTHX_DIRECT_PROF
+constexpr int kProfRegions = 9;
+__device__ unsigned long long g_dprof[2 * kProfRegions];
+#define DPROF(k)                                   \
+  do {                                             \
+    const uint64_t m_ = __ballot(1);               \
+    dpe[k] += 1u;                                  \
+    dpl[k] += (uint32_t)__popcll(m_);              \
+  } while (0)
+#else
+#define DPROF(k)
+#endif
+
 __device__ __forceinline__ void philox_block(uint32_t w[4], uint32_t r0, uint32_t r1, uint32_t blk, uint32_t tag,
                                              uint32_t k0, uint32_t k1) {
   w[0] = r0; w[1] = r1; w[2] = blk; w[3] = tag;
@@ -126,11 +148,19 @@ __global__ __launch_bounds__(FAITHFUL ? kDirectThreads : kDirectMaxThreads) RTHX
   int c = 0, seg = 0, it = 0;
   uint32_t ev = 0;
   uint32_t n_absorbed = 0, n_escaped = 0, n_roulette = 0, n_capped = 0, n_events = 0;
+#if RTHX_DIRECT_PROF
+  uint32_t dpe[kProfRegions] = {}, dpl[kProfRegions] = {};
+  uint64_t dpt_refill = 0, dpt_leg = 0;
+#endif
 
   while (true) {
+#if RTHX_DIRECT_PROF
+    const uint64_t t0_ = __builtin_amdgcn_s_memtime();
+#endif
     if (more) {
       const uint64_t idle = __ballot(!live);
       if (__popcll(idle) >= kDirectRefill || __ballot(live) == 0ull) {
+        DPROF(6);
         const uint32_t need = (uint32_t)__popcll(idle);
         const uint64_t avail = pool_end - pool;
         uint64_t fresh = 0;
@@ -149,6 +179,7 @@ __global__ __launch_bounds__(FAITHFUL ? kDirectThreads : kDirectMaxThreads) RTHX
         }
         bool got = false;
         if (!live && (int64_t)mine < n_items) {
+          DPROF(0);
           got = true;
           item = (uint32_t)mine;
           const uint64_t ray = (uint64_t)Q.ray_begin + (replay ? (uint64_t)Q.replay[item] : (uint64_t)item);
@@ -192,8 +223,13 @@ __global__ __launch_bounds__(FAITHFUL ? kDirectThreads : kDirectMaxThreads) RTHX
     }
     // (no ray in flight: done once nothing is left to emit; else a batch
     // that roulette ended at emission -- the next trip emits again)
+#if RTHX_DIRECT_PROF
+    const uint64_t t1_ = __builtin_amdgcn_s_memtime();
+    dpt_refill += t1_ - t0_;
+#endif
     if (!more && __ballot(live) == 0ull) break;
     if (live) {
+      DPROF(1);
       // traceRay (traceRay.jl:20-147) one coarse segment at a time, 10,000 per call
       int a;
       if (LAT) {
@@ -211,6 +247,7 @@ __global__ __launch_bounds__(FAITHFUL ? kDirectThreads : kDirectMaxThreads) RTHX
       }
       ++seg;
       if (a != kRayContinue) {
+        DPROF(2);
         int fate = -1;  // -1: next iteration; else a DirectStat
         if (a < 0) {
           fate = kStatEscaped;  // traceRay returned nothing (traceSingleRay.jl:20-22)
@@ -226,9 +263,11 @@ __global__ __launch_bounds__(FAITHFUL ? kDirectThreads : kDirectMaxThreads) RTHX
           // gas: rand() < omega scatters (:58-62), else absorbs (:63-75)
           const bool redirect = wall ? !lt : lt;
           if (!redirect && !E.reemit) {
+            DPROF(3);
             if (!replay) add(1, a, 1u);  // true absorption: wall_absorbed / absorbed (directRayTracing.jl:104-108)
             fate = kStatAbsorbed;
           } else {
+            DPROF(4);
             if (redirect) {
               add(2, a, sign);  // reflected / scattered (:112-115)
             } else {
@@ -268,6 +307,7 @@ __global__ __launch_bounds__(FAITHFUL ? kDirectThreads : kDirectMaxThreads) RTHX
           }
         }
         if (fate >= 0) {
+          DPROF(5);
           live = false;
           if (!replay) {
             n_absorbed += fate == kStatAbsorbed ? 1u : 0u;
@@ -280,8 +320,21 @@ __global__ __launch_bounds__(FAITHFUL ? kDirectThreads : kDirectMaxThreads) RTHX
         }
       }
     }
+#if RTHX_DIRECT_PROF
+    dpt_leg += __builtin_amdgcn_s_memtime() - t1_;
+#endif
   }
 
+#if RTHX_DIRECT_PROF
+  dpe[7] = 1u;
+  dpe[8] = 1u;
+  if (lane == 0)
+    for (int k = 0; k < kProfRegions; ++k) {
+      atomicAdd(&g_dprof[2 * k], (unsigned long long)dpe[k]);
+      atomicAdd(&g_dprof[2 * k + 1], k == 7 ? (unsigned long long)dpt_refill
+                                      : k == 8 ? (unsigned long long)dpt_leg : (unsigned long long)dpl[k]);
+    }
+#endif
   if (!replay) {
     const uint32_t st[kDirectStats] = {n_absorbed, n_escaped, n_roulette, n_capped, n_events};
 #pragma unroll
@@ -447,5 +500,19 @@ hipError_t launch_surface_frames(const DevDomain* D, int32_t n_surfaces, SurfGeo
                      n_surfaces, out);
   return hipGetLastError();
 }
+
+#if RTHX_DIRECT_PROF
+void direct_prof_dump() {
+  unsigned long long h[2 * kProfRegions] = {};
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_dprof), sizeof(h)) != hipSuccess) return;
+  static const char* names[kProfRegions] = {"emission", "leg", "leg ended", "absorbed", "redirected", "fate",
+                                            "refill", "t_refill", "t_leg"};
+  for (int k = 0; k < kProfRegions; ++k)
+    fprintf(stderr, "DPROF %-11s executions %14llu lanes %16llu lanes/exec %6.2f\n", names[k], h[2 * k],
+            h[2 * k + 1], h[2 * k] ? (double)h[2 * k + 1] / (double)h[2 * k] : 0.0);
+  unsigned long long z[2 * kProfRegions] = {};
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_dprof), z, sizeof(z));
+}
+#endif
 
 }  // namespace rthx
